@@ -1,0 +1,451 @@
+"""numpy fp32 restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+
+Every function names the reference lines it restates (paths relative to the
+reference repository root).  Layouts are point-major: a cloud batch is
+``(B, N, C)`` with channels contiguous, which is the transpose of the
+reference's ``B x C x N`` Conv1d layout; weights keep the reference's
+``[out, in(, 1)]`` state-dict shapes.
+
+The max-pool backward is the sparse form (gradient routed to the first argmax
+point of each channel), which equals torch's dense ``MaxBackward`` whenever
+the maximum is unique (``models/pointnet.py:129``).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+
+F32 = np.float32
+
+# --------------------------------------------------------------------------
+# parameter specs: reference state_dict names and shapes
+# --------------------------------------------------------------------------
+
+# models/pointnet.py:186-195 (PointNetCls(k=40, feature_transform=False)) +
+# :81-94 (PointNetfeat); cls factory utils/model_utils.py:68-70.
+def cls_spec(k: int = 40):
+    return [
+        ("feat.conv1.weight", (64, 3, 1)), ("feat.conv1.bias", (64,)),
+        ("feat.conv2.weight", (64, 64, 1)), ("feat.conv2.bias", (64,)),
+        ("feat.conv3.weight", (128, 64, 1)), ("feat.conv3.bias", (128,)),
+        ("feat.conv4.weight", (1024, 128, 1)), ("feat.conv4.bias", (1024,)),
+        ("fc1.weight", (512, 1024)), ("fc1.bias", (512,)),
+        ("fc2.weight", (256, 512)), ("fc2.bias", (256,)),
+        ("fc3.weight", (k, 256)), ("fc3.bias", (k,)),
+    ]
+
+
+# models/pointnet.py:46-57 (STNkd); STN3d is stnkd_spec(3) with fc3 -> 9.
+def stnkd_spec(prefix: str, k: int):
+    return [
+        (prefix + "conv1.weight", (64, k, 1)), (prefix + "conv1.bias", (64,)),
+        (prefix + "conv2.weight", (128, 64, 1)), (prefix + "conv2.bias", (128,)),
+        (prefix + "conv3.weight", (1024, 128, 1)), (prefix + "conv3.bias", (1024,)),
+        (prefix + "fc1.weight", (512, 1024)), (prefix + "fc1.bias", (512,)),
+        (prefix + "fc2.weight", (256, 512)), (prefix + "fc2.bias", (256,)),
+        (prefix + "fc3.weight", (k * k, 256)), (prefix + "fc3.bias", (k * k,)),
+    ]
+
+
+def cls_ft_spec(k: int = 40):
+    """PointNetCls(k, feature_transform=True): feat.fstn = STNkd(64) is
+    registered after feat.conv1..conv4 (models/pointnet.py:86-94)."""
+    s = cls_spec(k)
+    return s[:8] + stnkd_spec("feat.fstn.", 64) + s[8:]
+
+
+# models/discriminator.py:30-39 (DeepConvDiscNet(input_dim, output_dim)).
+def disc_spec(input_dim: int = 40, output_dim: int = 1):
+    return [
+        ("conv1.weight", (512, input_dim, 1)), ("conv1.bias", (512,)),
+        ("conv2.weight", (256, 512, 1)), ("conv2.bias", (256,)),
+        ("conv3.weight", (256, 256, 1)), ("conv3.bias", (256,)),
+        ("conv4.weight", (64, 256, 1)), ("conv4.bias", (64,)),
+        ("conv5.weight", (64, 64, 1)), ("conv5.bias", (64,)),
+        ("fc.weight", (output_dim, 64)), ("fc.bias", (output_dim,)),
+    ]
+
+
+# models/pointnet.py:261-278 (PointNetSeg(NUM_SEG_CLASSES)).
+def seg_spec(num_seg_classes: int = 50):
+    dims = [(64, 3), (128, 64), (128, 128), (128, 128), (512, 128), (2048, 512)]
+    s = []
+    for i, (o, c) in enumerate(dims, 1):
+        s += [(f"conv{i}.weight", (o, c, 1)), (f"conv{i}.bias", (o,))]
+    s += [("fc1.weight", (256, 3024)), ("fc1.bias", (256,)),
+          ("fc2.weight", (256, 256)), ("fc2.bias", (256,)),
+          ("fc3.weight", (128, 256)), ("fc3.bias", (128,)),
+          ("fc4.weight", (num_seg_classes, 128)), ("fc4.bias", (num_seg_classes,))]
+    return s
+
+
+def _fans(shape):
+    fan_in = int(np.prod(shape[1:]))
+    return fan_in, int(shape[0]) * int(np.prod(shape[2:]))
+
+
+def make_params(spec, seed: int, init: str = "default") -> "OrderedDict[str, np.ndarray]":
+    """Deterministic weights from numpy PCG64 (stable across numpy versions).
+
+    ``init="default"`` mirrors the bounds of torch's default Conv1d/Linear init
+    (U(+-1/sqrt(fan_in)) for weight and bias; PointNetCls is built with it,
+    utils/model_utils.py:68-70).  ``init="xavier"`` mirrors
+    utils/model_utils.py:27-58 with init_type='xavier' (xavier_normal gain 1,
+    bias 0), used for the discriminator (:104-106).
+    """
+    rng = np.random.default_rng(seed)
+    out = OrderedDict()
+    last_fan_in = None
+    for name, shape in spec:
+        if name.endswith("weight"):
+            fan_in, fan_out = _fans(shape)
+            last_fan_in = fan_in
+            if init == "xavier":
+                std = math.sqrt(2.0 / (fan_in + fan_out))
+                out[name] = rng.normal(0.0, std, shape).astype(F32)
+            else:
+                b = 1.0 / math.sqrt(fan_in)
+                out[name] = rng.uniform(-b, b, shape).astype(F32)
+        else:
+            if init == "xavier":
+                out[name] = np.zeros(shape, F32)
+            else:
+                b = 1.0 / math.sqrt(last_fan_in)
+                out[name] = rng.uniform(-b, b, shape).astype(F32)
+    return out
+
+
+def _w(p, name):
+    w = p[name]
+    return w.reshape(w.shape[0], -1) if w.ndim == 3 else w
+
+
+def relu(x):
+    return np.maximum(x, F32(0))
+
+
+# --------------------------------------------------------------------------
+# generator: PointNetCls
+# --------------------------------------------------------------------------
+
+def point_mlp_fwd(pts, p, prefix="feat."):
+    """relu(conv1), relu(conv2), relu(conv3) as per-point matvecs
+    (models/pointnet.py:115-116,127).  pts: (B, N, 3)."""
+    x1 = relu(pts @ _w(p, prefix + "conv1.weight").T + p[prefix + "conv1.bias"])
+    x2 = relu(x1 @ _w(p, prefix + "conv2.weight").T + p[prefix + "conv2.bias"])
+    x3 = relu(x2 @ _w(p, prefix + "conv3.weight").T + p[prefix + "conv3.bias"])
+    return x1.astype(F32), x2.astype(F32), x3.astype(F32)
+
+
+def conv_max_fwd(x, w, b, relu_before_max=False):
+    """conv (1x1) then max over points, first index on ties
+    (models/pointnet.py:128-130; torch.max(dim) returns the first maximal index
+    on CPU).  x: (B, N, K), w: (O, K).  Returns (gmax (B, O), argmax (B, O))."""
+    B = x.shape[0]
+    O = w.shape[0]
+    gmax = np.empty((B, O), F32)
+    am = np.empty((B, O), np.int32)
+    for bi in range(B):
+        y = x[bi] @ w.T + b
+        if relu_before_max:
+            y = relu(y)
+        a = np.argmax(y, axis=0)
+        am[bi] = a
+        gmax[bi] = y[a, np.arange(O)]
+    return gmax, am
+
+
+def head_fwd(g, p, mask=None, p_drop=0.3):
+    """relu(fc1) -> relu(dropout(fc2)) -> fc3 (models/pointnet.py:200-202).
+    ``mask`` (B, 256) of {0,1} replaces nn.Dropout's Bernoulli draw; eval mode
+    passes None."""
+    h1 = relu(g @ p["fc1.weight"].T + p["fc1.bias"]).astype(F32)
+    z2 = (h1 @ p["fc2.weight"].T + p["fc2.bias"]).astype(F32)
+    scale = None
+    if mask is not None:
+        scale = (mask.astype(F32) * (F32(1.0) / F32(1.0 - p_drop))).astype(F32)
+        z2 = z2 * scale
+    h2 = relu(z2).astype(F32)
+    logits = (h2 @ p["fc3.weight"].T + p["fc3.bias"]).astype(F32)
+    return logits, (h1, h2, scale)
+
+
+def cls_forward(p, pts, mask=None):
+    """PointNetCls.forward (models/pointnet.py:197-203), feature_transform=False.
+    Returns logits (B, k), global (B, 1024) and a cache for cls_backward."""
+    pts = np.ascontiguousarray(pts, F32)
+    x1, x2, x3 = point_mlp_fwd(pts, p)
+    gmax, am = conv_max_fwd(x3, _w(p, "feat.conv4.weight"), p["feat.conv4.bias"])
+    logits, hc = head_fwd(gmax, p, mask)
+    cache = dict(pts=pts, x1=x1, x2=x2, x3=x3, gmax=gmax, am=am, head=hc)
+    return logits, gmax, cache
+
+
+def conv_max_bwd(dg, am, x, w):
+    """Sparse MaxBackward + conv backward (models/pointnet.py:128-129):
+    dW[o,:] = sum_b dg[b,o] x[b, am[b,o], :], db = sum_b dg, and
+    dX[b, am[b,o], :] += dg[b,o] * W[o,:]."""
+    B, N, K = x.shape
+    dW = np.zeros(w.shape, np.float64)
+    dX = np.zeros((B, N, K), F32)
+    for bi in range(B):
+        rows = x[bi][am[bi]]                       # (O, K)
+        dW += dg[bi][:, None].astype(np.float64) * rows
+        np.add.at(dX[bi], am[bi], dg[bi][:, None] * w)
+    return dW.astype(F32), dg.sum(0).astype(F32), dX
+
+
+def cls_backward(p, cache, dlogits):
+    """Autograd of cls_forward given dL/dlogits; returns grads keyed like the
+    reference state_dict (conv weights shaped [out, in, 1])."""
+    pts, x1, x2, x3 = cache["pts"], cache["x1"], cache["x2"], cache["x3"]
+    gmax, am = cache["gmax"], cache["am"]
+    h1, h2, scale = cache["head"]
+    g = OrderedDict()
+    dlogits = dlogits.astype(F32)
+    g["fc3.weight"] = dlogits.T @ h2
+    g["fc3.bias"] = dlogits.sum(0)
+    dz2 = (dlogits @ p["fc3.weight"]) * (h2 > 0)
+    if scale is not None:
+        dz2 = dz2 * scale
+    g["fc2.weight"] = dz2.T @ h1
+    g["fc2.bias"] = dz2.sum(0)
+    dz1 = (dz2 @ p["fc2.weight"]) * (h1 > 0)
+    g["fc1.weight"] = dz1.T @ gmax
+    g["fc1.bias"] = dz1.sum(0)
+    dgl = (dz1 @ p["fc1.weight"]).astype(F32)
+    W4 = _w(p, "feat.conv4.weight")
+    dW4, db4, dX3 = conv_max_bwd(dgl, am, x3, W4)
+    B, N, _ = x3.shape
+    dz3 = (dX3 * (x3 > 0)).reshape(B * N, -1)
+    dz2p = (dz3 @ _w(p, "feat.conv3.weight")) * (x2.reshape(B * N, -1) > 0)
+    dz1p = (dz2p @ _w(p, "feat.conv2.weight")) * (x1.reshape(B * N, -1) > 0)
+    feat = OrderedDict()
+    feat["feat.conv1.weight"] = (dz1p.T @ pts.reshape(B * N, 3))[:, :, None]
+    feat["feat.conv1.bias"] = dz1p.sum(0)
+    feat["feat.conv2.weight"] = (dz2p.T @ x1.reshape(B * N, -1))[:, :, None]
+    feat["feat.conv2.bias"] = dz2p.sum(0)
+    feat["feat.conv3.weight"] = (dz3.T @ x2.reshape(B * N, -1))[:, :, None]
+    feat["feat.conv3.bias"] = dz3.sum(0)
+    feat["feat.conv4.weight"] = dW4[:, :, None]
+    feat["feat.conv4.bias"] = db4
+    out = OrderedDict()
+    for k in list(feat) + ["fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias",
+                           "fc3.weight", "fc3.bias"]:
+        out[k] = (feat[k] if k in feat else g[k]).astype(F32)
+    out["_dglobal"] = dgl
+    return out
+
+
+# --------------------------------------------------------------------------
+# discriminator: DeepConvDiscNet
+# --------------------------------------------------------------------------
+
+_DLAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5"]
+
+
+def lrelu(x, s=F32(0.2)):
+    return np.where(x > 0, x, x * s).astype(F32)
+
+
+def disc_forward(d, x):
+    """DeepConvDiscNet.forward (models/discriminator.py:42-51): five 1x1 convs
+    with LeakyReLU(0.2) then Linear(64, out).  x: (M, C) -> (M, out)."""
+    acts = [x.astype(F32)]
+    h = acts[0]
+    for l in _DLAYERS:
+        h = lrelu(h @ _w(d, l + ".weight").T + d[l + ".bias"])
+        acts.append(h)
+    out = (h @ d["fc.weight"].T + d["fc.bias"]).astype(F32)
+    return out, acts
+
+
+def disc_backward(d, acts, dout, need_params=True, need_input=True):
+    """Autograd of disc_forward.  LeakyReLU backward uses the (in-place) output
+    sign, which equals the input sign (discriminator.py:39)."""
+    g = OrderedDict()
+    dout = dout.astype(F32)
+    if need_params:
+        g["fc.weight"] = dout.T @ acts[5]
+        g["fc.bias"] = dout.sum(0)
+    dh = dout @ d["fc.weight"]
+    for i in range(5, 0, -1):
+        l = _DLAYERS[i - 1]
+        dz = np.where(acts[i] > 0, dh, dh * F32(0.2)).astype(F32)
+        if need_params:
+            g[l + ".weight"] = (dz.T @ acts[i - 1])[:, :, None]
+            g[l + ".bias"] = dz.sum(0)
+        if i > 1 or need_input:
+            dh = dz @ _w(d, l + ".weight")
+    out = OrderedDict((k, g[k].astype(F32)) for k, _ in disc_spec(acts[0].shape[1],
+                                                                  dout.shape[1])) if need_params else None
+    return out, (dh.astype(F32) if need_input else None)
+
+
+# --------------------------------------------------------------------------
+# losses (torch.nn.CrossEntropyLoss / BCEWithLogitsLoss, mean reduction)
+# --------------------------------------------------------------------------
+
+def log_softmax(x):
+    """F.log_softmax(x, dim=1) (utils/trainer.py:472,492)."""
+    m = x.max(1, keepdims=True)
+    s = x - m
+    return (s - np.log(np.exp(s).sum(1, keepdims=True))).astype(F32)
+
+
+def log_softmax_bwd(lsm, dy):
+    return (dy - np.exp(lsm) * dy.sum(1, keepdims=True)).astype(F32)
+
+
+def cross_entropy(logits, labels):
+    """CrossEntropyLoss() (train_classification.py:199) used at trainer.py:469.
+    Returns (loss, dloss/dlogits)."""
+    B = logits.shape[0]
+    lsm = log_softmax(logits)
+    loss = -float(np.mean(lsm[np.arange(B), labels]))
+    grad = np.exp(lsm)
+    grad[np.arange(B), labels] -= 1.0
+    return loss, (grad / F32(B)).astype(F32)
+
+
+def bce_with_logits(x, y):
+    """BCEWithLogitsLoss() (train_classification.py:200) used at
+    trainer.py:507,537,553.  Returns (loss, dloss/dx)."""
+    x = x.astype(np.float64)
+    y = y.astype(np.float64)
+    l = np.maximum(x, 0) - x * y + np.log1p(np.exp(-np.abs(x)))
+    sig = 1.0 / (1.0 + np.exp(-x))
+    return float(l.mean()), ((sig - y) / x.size).astype(F32)
+
+
+# --------------------------------------------------------------------------
+# Adam (torch.optim.Adam, single-tensor path; train_classification.py:110-122)
+# --------------------------------------------------------------------------
+
+class Adam:
+    def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8):
+        self.p = params
+        self.lr, (self.b1, self.b2), self.eps = lr, betas, eps
+        self.m = OrderedDict((k, np.zeros_like(v)) for k, v in params.items())
+        self.v = OrderedDict((k, np.zeros_like(v)) for k, v in params.items())
+        self.t = 0
+
+    def step(self, grads):
+        """exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+        p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, value=-lr/bc1)."""
+        self.t += 1
+        bc1 = 1.0 - self.b1 ** self.t
+        bc2s = math.sqrt(1.0 - self.b2 ** self.t)
+        w1 = F32(1.0 - self.b1)
+        for k in self.p:
+            g = grads[k].astype(F32)
+            m, v = self.m[k], self.v[k]
+            m += w1 * (g - m)
+            v *= F32(self.b2)
+            v += F32(1.0 - self.b2) * g * g
+            denom = np.sqrt(v) / F32(bc2s) + F32(self.eps)
+            self.p[k] -= F32(self.lr / bc1) * (m / denom)
+
+
+# --------------------------------------------------------------------------
+# the adversarial step (utils/trainer.py:426-559)
+# --------------------------------------------------------------------------
+
+def adv_step(G, D, optG, optD, pts_gt, labels, pts_nogt, mask_gt, mask_nogt,
+             y_gt, y_nogt, lambda_cls=1.0, lambda_adv=0.001, apply_adam=True):
+    """One run_training iteration.  The stochastic parts are inputs: dropout
+    masks (B, 256) for the two G passes and the U(0.7,1.05) / U(0,0.305) soft
+    D labels drawn by make_D_label(random=True) (utils/utils.py:22-31).
+    ImagePool(0).query is the identity (utils/image_pool.py:35-36)."""
+    logits_gt, _, c_gt = cls_forward(G, pts_gt, mask_gt)             # :468
+    l, dce = cross_entropy(logits_gt, labels)                          # :469
+    lsm_gt = log_softmax(logits_gt)                                    # :472
+    logits_ng, _, c_ng = cls_forward(G, pts_nogt, mask_nogt)           # :490
+    lsm_ng = log_softmax(logits_ng)                                    # :492
+    d_ng, acts_ng = disc_forward(D, lsm_ng)                            # :499
+    loss_adv, dadv = bce_with_logits(d_ng, np.ones_like(d_ng))         # :500-508
+    # G backward (:510-520); D frozen -> only the input gradient
+    _, dlsm = disc_backward(D, acts_ng, F32(lambda_adv) * dadv, need_params=False)
+    dlog_ng = log_softmax_bwd(lsm_ng, dlsm)
+    ga = cls_backward(G, c_gt, F32(lambda_cls) * dce)
+    gb = cls_backward(G, c_ng, dlog_ng)
+    gG = OrderedDict((k, (ga[k] + gb[k]).astype(F32)) for k in G)
+    # D backward (:526-556)
+    d_gt, acts_gt = disc_forward(D, lsm_gt)
+    lD1, d1 = bce_with_logits(d_gt, y_gt)
+    lD2, d2 = bce_with_logits(d_ng, y_nogt)
+    g1, _ = disc_backward(D, acts_gt, F32(0.5) * d1, need_input=False)
+    g2, _ = disc_backward(D, acts_ng, F32(0.5) * d2, need_input=False)
+    gD = OrderedDict((k, (g1[k] + g2[k]).astype(F32)) for k in D)
+    if apply_adam:
+        optG.step(gG)                                                   # :558
+        optD.step(gD)                                                   # :559
+    losses = dict(loss_cls=l, loss_adv=loss_adv, loss_D=0.5 * lD1 + 0.5 * lD2,
+                  loss_D_gt=0.5 * lD1, loss_D_nogt=0.5 * lD2)
+    aux = dict(logits_gt=logits_gt, logits_nogt=logits_ng, d_nogt=d_ng, d_gt=d_gt,
+               am_gt=c_gt["am"], am_nogt=c_ng["am"], gmax_gt=c_gt["gmax"],
+               gmax_nogt=c_ng["gmax"])
+    return losses, gG, gD, aux
+
+
+# --------------------------------------------------------------------------
+# T-Net path (models/pointnet.py:14-79,118-122,345-353) - forward only
+# --------------------------------------------------------------------------
+
+def stn_forward(p, x, prefix, k):
+    """STNkd/STN3d forward on point-major x (B, N, k) -> (B, k, k)."""
+    h = relu(x @ _w(p, prefix + "conv1.weight").T + p[prefix + "conv1.bias"])
+    h = relu(h @ _w(p, prefix + "conv2.weight").T + p[prefix + "conv2.bias"]).astype(F32)
+    g, _ = conv_max_fwd(h, _w(p, prefix + "conv3.weight"), p[prefix + "conv3.bias"],
+                        relu_before_max=True)
+    h = relu(g @ p[prefix + "fc1.weight"].T + p[prefix + "fc1.bias"])
+    h = relu(h @ p[prefix + "fc2.weight"].T + p[prefix + "fc2.bias"])
+    t = h @ p[prefix + "fc3.weight"].T + p[prefix + "fc3.bias"]
+    t = t + np.eye(k, dtype=F32).reshape(1, k * k)
+    return t.reshape(-1, k, k).astype(F32)
+
+
+def cls_ft_forward(p, pts, mask=None):
+    """PointNetCls(feature_transform=True).forward (pointnet.py:109-137,197-203)."""
+    pts = np.ascontiguousarray(pts, F32)
+    x1 = relu(pts @ _w(p, "feat.conv1.weight").T + p["feat.conv1.bias"])
+    x2 = relu(x1 @ _w(p, "feat.conv2.weight").T + p["feat.conv2.bias"]).astype(F32)
+    trans = stn_forward(p, x2, "feat.fstn.", 64)
+    x2t = np.matmul(x2, trans).astype(F32)
+    x3 = relu(x2t @ _w(p, "feat.conv3.weight").T + p["feat.conv3.bias"]).astype(F32)
+    gmax, am = conv_max_fwd(x3, _w(p, "feat.conv4.weight"), p["feat.conv4.bias"])
+    logits, _ = head_fwd(gmax, p, mask)
+    return logits, gmax, trans
+
+
+def feature_transform_regularizer(trans):
+    """mean_b ||T T^T - I||_F (models/pointnet.py:345-353)."""
+    d = trans.shape[1]
+    r = np.matmul(trans, trans.transpose(0, 2, 1)) - np.eye(d, dtype=F32)[None]
+    return float(np.mean(np.sqrt((r.astype(np.float64) ** 2).sum((1, 2)))))
+
+
+# --------------------------------------------------------------------------
+# segmentation net (models/pointnet.py:261-317) - forward only
+# --------------------------------------------------------------------------
+
+def seg_forward(p, pts, cls):
+    """PointNetSeg.forward: pts (B, N, 3), cls (B, 1, 16) -> (B, 50, N), (B, 2048, 1)."""
+    pts = np.ascontiguousarray(pts, F32)
+    xs = []
+    h = pts
+    for i in range(1, 7):
+        h = relu(h @ _w(p, f"conv{i}.weight").T + p[f"conv{i}.bias"]).astype(F32)
+        xs.append(h)
+    B, N, _ = pts.shape
+    g = xs[5].max(1)                                        # (B, 2048)
+    feat = np.concatenate(xs[:5] + [np.broadcast_to(g[:, None, :], (B, N, 2048)),
+                                    np.broadcast_to(cls.reshape(B, 1, -1), (B, N, cls.shape[-1]))],
+                          axis=2)
+    h = relu(feat @ p["fc1.weight"].T + p["fc1.bias"])
+    h = relu(h @ p["fc2.weight"].T + p["fc2.bias"])
+    h = relu(h @ p["fc3.weight"].T + p["fc3.bias"])
+    out = h @ p["fc4.weight"].T + p["fc4.bias"]
+    return out.transpose(0, 2, 1).astype(F32), g[:, :, None].astype(F32)

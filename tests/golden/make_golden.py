@@ -1,0 +1,263 @@
+"""Capture golden vectors from the reference (run in the build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+Imports the reference's own modules from /root/reference (read-only; nothing is
+copied) and runs them on CPU with deterministic inputs:
+
+* weights come from ``oracle.pointnet_np.make_params`` (numpy PCG64, seeded),
+  loaded into the reference models with ``load_state_dict`` - so only seeds are
+  stored, never weights;
+* stochastic parts are injected: the dropout mask replaces ``model.dropout``
+  (models/pointnet.py:194,201) and the soft D labels replace
+  ``utils.trainer.make_D_label``'s uniform_ draw (utils/utils.py:28);
+* ``run_training`` (utils/trainer.py:403-608) is driven with in-memory loaders.
+
+Outputs small ``.npz`` fixtures next to this script.  The GPU box never sees
+the reference; it only sees these fixtures.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle import pointnet_np as onp  # noqa: E402
+
+B_SMALL = 4
+N_PTS = 1024
+SAMPLES = 512
+FULL_LIMIT = 16384
+
+
+def summarize(prefix, arr, out, rng_seed=1234):
+    """Full tensor when small; sum / l2 / absmax + fixed-index samples else."""
+    a = np.asarray(arr, np.float32)
+    if a.size <= FULL_LIMIT:
+        out[prefix] = a
+        return
+    flat = a.reshape(-1)
+    idx = np.random.default_rng(rng_seed).choice(flat.size, SAMPLES, replace=False)
+    idx.sort()
+    out[prefix + ".sum"] = np.float64(flat.astype(np.float64).sum())
+    out[prefix + ".l2"] = np.float64(np.sqrt((flat.astype(np.float64) ** 2).sum()))
+    out[prefix + ".absmax"] = np.float32(np.abs(flat).max())
+    out[prefix + ".idx"] = idx.astype(np.int64)
+    out[prefix + ".val"] = flat[idx]
+
+
+def make_pts(seed, B, N):
+    return np.random.default_rng(seed).uniform(-1, 1, (B, N, 3)).astype(np.float32)
+
+
+def make_mask(rng, B, width=256, p=0.3):
+    return (rng.random((B, width)) >= p).astype(np.float32)
+
+
+def main(ref_root):
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, ref_root)
+    import torch
+    import torch.nn as nn
+    from models.pointnet import PointNetCls, PointNetSeg
+    from models.discriminator import DeepConvDiscNet
+    import utils.trainer as rtrainer
+    from utils.image_pool import ImagePool
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+    def load(model, params):
+        sd = {k: torch.from_numpy(v.copy()) for k, v in params.items()}
+        model.load_state_dict(sd)
+        return model
+
+    class MaskDropout(nn.Module):
+        """Stands in for nn.Dropout(p=0.3) with masks taken from a queue:
+        torch computes input * (bernoulli(1-p) / (1-p))."""
+
+        def __init__(self, masks, p=0.3):
+            super().__init__()
+            self.masks, self.p = masks, p
+
+        def forward(self, x):
+            if not self.training:
+                return x
+            m = torch.from_numpy(self.masks.pop(0))
+            return x * (m / (1.0 - self.p))
+
+    # ---------------- G1: cls forward (eval) ----------------
+    G = onp.make_params(onp.cls_spec(40), seed=1)
+    model = load(PointNetCls(k=40, feature_transform=False), G).eval()
+    pts = make_pts(11, B_SMALL, N_PTS)
+    am_holder = {}
+
+    def hook(mod, inp, out):
+        am_holder["am"] = torch.max(out, 2)[1].detach().numpy().astype(np.int32)
+
+    h = model.feat.conv4.register_forward_hook(hook)
+    with torch.no_grad():
+        logits, glob, tf = model(torch.from_numpy(pts))
+    h.remove()
+    np.savez_compressed(os.path.join(HERE, "g1_cls_fwd.npz"), g_seed=1, pts_seed=11,
+                        B=B_SMALL, N=N_PTS, logits=logits.numpy(),
+                        gmax=glob.numpy()[:, :, 0], argmax=am_holder["am"])
+
+    # ---------------- G2: cls forward+backward (train, injected dropout) ----
+    rng = np.random.default_rng(21)
+    mask = make_mask(rng, B_SMALL)
+    labels = rng.integers(0, 40, B_SMALL)
+    model = load(PointNetCls(k=40, feature_transform=False), G).train()
+    model.dropout = MaskDropout([mask.copy()])
+    logits, glob, _ = model(torch.from_numpy(pts))
+    loss = nn.CrossEntropyLoss()(logits, torch.from_numpy(labels).long())
+    loss.backward()
+    out = dict(g_seed=1, pts_seed=11, mask=mask, labels=labels.astype(np.int64),
+               loss=np.float64(loss.item()), logits=logits.detach().numpy())
+    for name, p in model.named_parameters():
+        summarize("grad." + name, p.grad.numpy(), out)
+    np.savez_compressed(os.path.join(HERE, "g2_cls_bwd.npz"), **out)
+
+    # ---------------- G3: run_training (adversarial step) ----------------
+    def run_adv(iters, seed):
+        Gp = onp.make_params(onp.cls_spec(40), seed=1)
+        Dp = onp.make_params(onp.disc_spec(40, 1), seed=2, init="xavier")
+        rng = np.random.default_rng(seed)
+        B = B_SMALL
+        batches_gt, batches_ng, masks, soft = [], [], [], []
+        for _ in range(iters):
+            batches_gt.append((rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32),
+                               rng.integers(0, 40, B).astype(np.int64)))
+            batches_ng.append(rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32))
+            masks.append(make_mask(rng, B))   # GT pass  (trainer.py:468)
+            masks.append(make_mask(rng, B))   # noGT pass (trainer.py:490)
+            soft.append(rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32))   # :530-535
+            soft.append(rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32))  # :546-551
+        model = load(PointNetCls(k=40, feature_transform=False), Gp)
+        model.dropout = MaskDropout([m.copy() for m in masks])
+        model_D = load(DeepConvDiscNet(40, 1), Dp)
+        soft_q = [s.copy() for s in soft]
+        orig = rtrainer.make_D_label
+
+        def make_D_label(input, value, device, random=False):
+            if random:
+                return torch.from_numpy(soft_q.pop(0)).to(device)
+            return orig(input, value, device, random=False)
+
+        rec = {"cls": [], "gan": []}
+
+        class Rec(nn.Module):
+            def __init__(self, inner, key):
+                super().__init__()
+                self.inner, self.key = inner, key
+
+            def forward(self, a, b):
+                r = self.inner(a, b)
+                rec[self.key].append(float(r.item()))
+                return r
+
+        optimizer = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        optimizer_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        tmp = tempfile.mkdtemp(prefix="golden_")
+        args = argparse.Namespace(device=torch.device("cpu"), total_iterations=iters,
+                                  lambda_cls=1.0, lambda_adv=0.001,
+                                  iter_save_epoch=10 ** 9, iter_test_epoch=10 ** 9,
+                                  exp_dir=tmp, tensorboard=False, batch_size=B)
+        tl = [(torch.from_numpy(batches_gt[0][0]), torch.from_numpy(batches_gt[0][1]))]
+        logger = logging.getLogger("golden")
+        logger.addHandler(logging.NullHandler())
+        logger.propagate = False
+        rtrainer.make_D_label = make_D_label
+        try:
+            rtrainer.run_training(
+                trainloader_gt=[(torch.from_numpy(a), torch.from_numpy(b)) for a, b in batches_gt],
+                trainloader_nogt=[torch.from_numpy(a) for a in batches_ng],
+                trainloader_gt_iter=enumerate([(torch.from_numpy(a), torch.from_numpy(b))
+                                               for a, b in batches_gt]),
+                targetloader_nogt_iter=enumerate([torch.from_numpy(a) for a in batches_ng]),
+                testloader=tl, model=model, model_D=model_D,
+                gan_loss=Rec(nn.BCEWithLogitsLoss(), "gan"),
+                cls_loss=Rec(nn.CrossEntropyLoss(), "cls"),
+                optimizer=optimizer, optimizer_D=optimizer_D,
+                history_pool_gt=ImagePool(0), history_pool_nogt=ImagePool(0),
+                train_logger=logger, test_logger=logger, writer=None, args=args)
+        finally:
+            rtrainer.make_D_label = orig
+        return dict(batches_gt=batches_gt, batches_ng=batches_ng, masks=masks, soft=soft,
+                    rec=rec, model=model, model_D=model_D)
+
+    for iters, fname in ((1, "g3_adv_step1.npz"), (3, "g3_adv_step3.npz")):
+        r = run_adv(iters, seed=31)
+        out = dict(iters=iters, data_seed=31, g_seed=1, d_seed=2, B=B_SMALL, N=N_PTS)
+        # cls criterion: index 0 is the train step, index 1 the iter-0 test pass
+        cls_train = [r["rec"]["cls"][0]] + r["rec"]["cls"][2:]
+        gan = np.array(r["rec"]["gan"]).reshape(iters, 3)
+        out["loss_cls"] = np.array(cls_train)
+        out["loss_adv"] = gan[:, 0]
+        out["loss_D_gt"] = gan[:, 1] * 0.5
+        out["loss_D_nogt"] = gan[:, 2] * 0.5
+        if iters == 1:
+            for name, p in r["model"].named_parameters():
+                summarize("gradG." + name, p.grad.numpy(), out)
+            for name, p in r["model_D"].named_parameters():
+                summarize("gradD." + name, p.grad.numpy(), out)
+        for name, p in r["model"].named_parameters():
+            summarize("paramG." + name, p.detach().numpy(), out)
+        for name, p in r["model_D"].named_parameters():
+            summarize("paramD." + name, p.detach().numpy(), out)
+        np.savez_compressed(os.path.join(HERE, fname), **out)
+
+    # ---------------- G4: discriminator fwd/bwd ----------------
+    Dp = onp.make_params(onp.disc_spec(40, 1), seed=2, init="xavier")
+    rng = np.random.default_rng(41)
+    x = onp.log_softmax(rng.normal(0, 3, (32, 40)).astype(np.float32))
+    dout = rng.normal(0, 1, (32, 1)).astype(np.float32)
+    md = load(DeepConvDiscNet(40, 1), Dp)
+    xt = torch.from_numpy(x).requires_grad_(True)
+    o = md(xt)
+    o.backward(torch.from_numpy(dout))
+    out = dict(d_seed=2, x=x, dout=dout, out=o.detach().numpy(), dx=xt.grad.numpy())
+    for name, p in md.named_parameters():
+        summarize("grad." + name, p.grad.numpy(), out)
+    np.savez_compressed(os.path.join(HERE, "g4_disc.npz"), **out)
+
+    # ---------------- G5: T-Net feature transform (eval) ----------------
+    Gf = onp.make_params(onp.cls_ft_spec(40), seed=5)
+    mf = load(PointNetCls(k=40, feature_transform=True), Gf).eval()
+    pts5 = make_pts(51, 2, N_PTS)
+    with torch.no_grad():
+        lg, gl, trans = mf(torch.from_numpy(pts5))
+        d = trans.size(1)
+        reg = torch.mean(torch.norm(torch.bmm(trans, trans.transpose(2, 1)) -
+                                    torch.eye(d)[None], dim=(1, 2)))
+    np.savez_compressed(os.path.join(HERE, "g5_tnet.npz"), g_seed=5, pts_seed=51,
+                        logits=lg.numpy(), gmax=gl.numpy()[:, :, 0], trans=trans.numpy(),
+                        reg=np.float64(reg.item()))
+
+    # ---------------- G6: segmentation forward ----------------
+    Sp = onp.make_params(onp.seg_spec(50), seed=6)
+    ms = load(PointNetSeg(50), Sp).eval()
+    pts6 = make_pts(61, 2, 2048)
+    cls = np.zeros((2, 1, 16), np.float32)
+    cls[0, 0, 3] = 1
+    cls[1, 0, 11] = 1
+    with torch.no_grad():
+        so, sg = ms(torch.from_numpy(pts6), torch.from_numpy(cls))
+    out = dict(s_seed=6, pts_seed=61, cls=cls, gmax=sg.numpy()[:, :, 0])
+    summarize("out", so.numpy(), out)
+    np.savez_compressed(os.path.join(HERE, "g6_seg_fwd.npz"), **out)
+
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")

@@ -1,0 +1,38 @@
+"""Helpers to compare against the golden fixtures written by make_golden.py."""
+import os
+
+import numpy as np
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return dict(np.load(os.path.join(HERE, name), allow_pickle=False))
+
+
+def rel_err(a, ref):
+    """max|a-ref| / max(1, max|ref|)  (SURVEY.md 8c tolerance form)."""
+    a = np.asarray(a, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return float(np.max(np.abs(a - ref)) / max(1.0, float(np.max(np.abs(ref)))))
+
+
+def check_tensor(fx, prefix, arr, tol=1e-3):
+    """Compare a tensor against a fixture entry (full, or summary + samples)."""
+    arr = np.asarray(arr, np.float32)
+    if prefix in fx:
+        ref = fx[prefix]
+        assert arr.shape == ref.shape, (prefix, arr.shape, ref.shape)
+        e = rel_err(arr, ref)
+        assert e <= tol, f"{prefix}: rel err {e:.3e} > {tol}"
+        return e
+    flat = arr.reshape(-1).astype(np.float64)
+    scale = max(1.0, float(fx[prefix + ".absmax"]))
+    e_val = float(np.max(np.abs(flat[fx[prefix + ".idx"]] - fx[prefix + ".val"]))) / scale
+    e_sum = abs(flat.sum() - float(fx[prefix + ".sum"])) / max(scale, abs(float(fx[prefix + ".sum"])))
+    e_l2 = abs(np.sqrt((flat ** 2).sum()) - float(fx[prefix + ".l2"])) / max(1.0, float(fx[prefix + ".l2"]))
+    e_max = abs(np.abs(flat).max() - float(fx[prefix + ".absmax"])) / scale
+    e = max(e_val, e_l2, e_max)
+    assert e <= tol, f"{prefix}: sample/l2/absmax err {e:.3e} > {tol}"
+    assert e_sum <= max(tol, 1e-3), f"{prefix}: sum err {e_sum:.3e}"
+    return e

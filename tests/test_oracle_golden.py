@@ -1,0 +1,107 @@
+"""Pin the numpy oracle against golden vectors captured from the reference.
+
+CPU only.  The fixtures come from tests/golden/make_golden.py, which ran the
+reference's own modules (models/pointnet.py, models/discriminator.py,
+utils/trainer.py:run_training) on the same seeded inputs.
+"""
+import numpy as np
+import pytest
+
+from oracle import pointnet_np as onp
+from golden_util import load, rel_err, check_tensor
+
+
+def _pts(seed, B, N):
+    return np.random.default_rng(seed).uniform(-1, 1, (B, N, 3)).astype(np.float32)
+
+
+def test_g1_cls_forward():
+    fx = load("g1_cls_fwd.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    pts = _pts(int(fx["pts_seed"]), int(fx["B"]), int(fx["N"]))
+    logits, gmax, cache = onp.cls_forward(G, pts, None)
+    assert rel_err(logits, fx["logits"]) < 1e-4
+    assert rel_err(gmax, fx["gmax"]) < 1e-4
+    assert (cache["am"] == fx["argmax"]).mean() > 0.999
+
+
+def test_g2_cls_backward():
+    fx = load("g2_cls_bwd.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    pts = _pts(int(fx["pts_seed"]), 4, 1024)
+    logits, _, cache = onp.cls_forward(G, pts, fx["mask"])
+    loss, dlog = onp.cross_entropy(logits, fx["labels"])
+    assert abs(loss - float(fx["loss"])) < 1e-5
+    grads = onp.cls_backward(G, cache, dlog)
+    for k in G:
+        check_tensor(fx, "grad." + k, grads[k], tol=1e-4)
+
+
+def _adv_inputs(fx):
+    rng = np.random.default_rng(int(fx["data_seed"]))
+    B, N, iters = int(fx["B"]), int(fx["N"]), int(fx["iters"])
+    steps = []
+    for _ in range(iters):
+        pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+        lab = rng.integers(0, 40, B)
+        pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+        m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+        m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+        y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+        y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+        steps.append((pg, lab, pn, m1, m2, y1, y2))
+    return steps
+
+
+@pytest.mark.parametrize("name", ["g3_adv_step1.npz", "g3_adv_step3.npz"])
+def test_g3_adv_step(name):
+    fx = load(name)
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    D = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
+    oG, oD = onp.Adam(G), onp.Adam(D)
+    for i, (pg, lab, pn, m1, m2, y1, y2) in enumerate(_adv_inputs(fx)):
+        losses, gG, gD, _ = onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2)
+        assert abs(losses["loss_cls"] - fx["loss_cls"][i]) < 1e-4
+        assert abs(losses["loss_adv"] - fx["loss_adv"][i]) < 1e-4
+        assert abs(losses["loss_D_gt"] - fx["loss_D_gt"][i]) < 1e-4
+        assert abs(losses["loss_D_nogt"] - fx["loss_D_nogt"][i]) < 1e-4
+        if int(fx["iters"]) == 1:
+            for k in G:
+                check_tensor(fx, "gradG." + k, gG[k], tol=1e-4)
+            for k in D:
+                check_tensor(fx, "gradD." + k, gD[k], tol=1e-4)
+    for k in G:
+        check_tensor(fx, "paramG." + k, G[k], tol=1e-5)
+    for k in D:
+        check_tensor(fx, "paramD." + k, D[k], tol=1e-5)
+
+
+def test_g4_disc():
+    fx = load("g4_disc.npz")
+    D = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
+    out, acts = onp.disc_forward(D, fx["x"])
+    assert rel_err(out, fx["out"]) < 1e-5
+    g, dx = onp.disc_backward(D, acts, fx["dout"])
+    assert rel_err(dx, fx["dx"]) < 1e-5
+    for k in D:
+        check_tensor(fx, "grad." + k, g[k], tol=1e-5)
+
+
+def test_g5_tnet():
+    fx = load("g5_tnet.npz")
+    G = onp.make_params(onp.cls_ft_spec(40), seed=int(fx["g_seed"]))
+    pts = _pts(int(fx["pts_seed"]), 2, 1024)
+    logits, gmax, trans = onp.cls_ft_forward(G, pts)
+    assert rel_err(trans, fx["trans"]) < 1e-4
+    assert rel_err(gmax, fx["gmax"]) < 1e-4
+    assert rel_err(logits, fx["logits"]) < 1e-4
+    assert abs(onp.feature_transform_regularizer(trans) - float(fx["reg"])) < 1e-3
+
+
+def test_g6_seg():
+    fx = load("g6_seg_fwd.npz")
+    S = onp.make_params(onp.seg_spec(50), seed=int(fx["s_seed"]))
+    pts = _pts(int(fx["pts_seed"]), 2, 2048)
+    out, g = onp.seg_forward(S, pts, fx["cls"])
+    assert rel_err(g[:, :, 0], fx["gmax"]) < 1e-4
+    check_tensor(fx, "out", out, tol=1e-4)
