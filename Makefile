@@ -1,0 +1,30 @@
+# Builds the MI355X (gfx950) library and the CPU oracle.
+#   make            -> adversarial_learning_on_pointclouds_amd/lib/libpcadv.so
+#   make asm        -> kernel assembly + resource usage under build/
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := adversarial_learning_on_pointclouds_amd
+SRC := $(wildcard $(PKG)/csrc/*.hip)
+OBJ := $(patsubst $(PKG)/csrc/%.hip,build/obj/%.o,$(SRC))
+HDR := $(wildcard $(PKG)/csrc/*.h) include/pcadv.h
+LIB := $(PKG)/lib/libpcadv.so
+HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
+
+all: $(LIB)
+
+build/obj/%.o: $(PKG)/csrc/%.hip $(HDR)
+	@mkdir -p build/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	@mkdir -p $(PKG)/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+
+asm: $(SRC)
+	@mkdir -p build/asm
+	for f in $(SRC); do $(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage --cuda-device-only -S $$f -o build/asm/$$(basename $$f .hip).s 2> build/asm/$$(basename $$f .hip).usage; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all asm clean

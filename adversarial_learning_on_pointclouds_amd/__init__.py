@@ -1,0 +1,18 @@
+"""MI355X-native PointNet adversarial-training hot path (gfx950 HIP kernels).
+
+Drop-in counterparts of the reference's models and training loop
+(YiruS/Adversarial_Learning_on_PointClouds): PointNetCls / PointNetfeat
+(models/pointnet.py), DeepConvDiscNet (models/discriminator.py), load_models
+(utils/model_utils.py), make_D_label (utils/utils.py), ImagePool
+(utils/image_pool.py), run_training / run_testing (utils/trainer.py), plus the
+fused native step AdvTrainStep.  All compute runs in libpcadv.so (C ABI in
+include/pcadv.h); there is no CPU fallback.
+"""
+from . import _lib
+from .discriminator import DeepConvDiscNet
+from .pointnet import PointNetCls, PointNetfeat, STN3d, STNkd, feature_transform_regularizer
+from .step import AdvTrainStep
+
+__all__ = ["PointNetCls", "PointNetfeat", "STN3d", "STNkd", "DeepConvDiscNet",
+           "feature_transform_regularizer", "AdvTrainStep"]
+__version__ = "0.1.0"

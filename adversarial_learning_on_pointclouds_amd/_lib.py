@@ -1,0 +1,124 @@
+"""ctypes binding of libpcadv.so (the C ABI declared in include/pcadv.h).
+
+torch is imported first on purpose: the wheel ships its own libamdhip64.so.7,
+and loading it before libpcadv.so makes the dynamic loader reuse that HIP
+runtime (same soname), so torch's streams and allocations are valid handles
+for the library.
+
+There is no fallback: if the shared library is missing every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PCADV_LIB", os.path.join(_HERE, "lib", "libpcadv.so"))
+
+PCADV_OK = 0
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+
+# state_dict-order flat layouts (must equal the enums in include/pcadv.h)
+G_LAYOUT = {
+    "feat.conv1.weight": 0, "feat.conv1.bias": 192,
+    "feat.conv2.weight": 256, "feat.conv2.bias": 4352,
+    "feat.conv3.weight": 4416, "feat.conv3.bias": 12608,
+    "feat.conv4.weight": 12736, "feat.conv4.bias": 143808,
+    "fc1.weight": 144832, "fc1.bias": 669120,
+    "fc2.weight": 669632, "fc2.bias": 800704,
+    "fc3.weight": 800960, "fc3.bias": 811200,
+}
+G_NUMEL = 811240
+D_LAYOUT = {
+    "conv1.weight": 0, "conv1.bias": 20480,
+    "conv2.weight": 20992, "conv2.bias": 152064,
+    "conv3.weight": 152320, "conv3.bias": 217856,
+    "conv4.weight": 218112, "conv4.bias": 234496,
+    "conv5.weight": 234560, "conv5.bias": 238656,
+    "fc.weight": 238720, "fc.bias": 238784,
+}
+D_NUMEL = 238785
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+
+
+class AdvArgs(ctypes.Structure):
+    """Mirror of pcadv_adv_args (include/pcadv.h)."""
+
+    _fields_ = [
+        ("B", _i), ("N", _i),
+        ("pts_gt", _vp), ("labels", _vp), ("pts_nogt", _vp),
+        ("drop_mask_gt", _vp), ("drop_mask_nogt", _vp),
+        ("soft_gt", _vp), ("soft_nogt", _vp),
+        ("g_param", _vp), ("g_grad", _vp), ("g_m", _vp), ("g_v", _vp),
+        ("d_param", _vp), ("d_grad", _vp), ("d_m", _vp), ("d_v", _vp),
+        ("step_count", _vp),
+        ("lr_g", _f), ("lr_d", _f), ("beta1", _f), ("beta2", _f), ("eps", _f),
+        ("lambda_cls", _f), ("lambda_adv", _f), ("drop_p", _f),
+        ("rng_seed", _u64),
+        ("apply_adam", _i),
+        ("losses", _vp), ("logits", _vp),
+        ("workspace", _vp), ("workspace_bytes", _sz),
+    ]
+
+
+# name -> (restype, argtypes); every symbol of include/pcadv.h
+SIGNATURES = {
+    "pcadv_last_error": (ctypes.c_char_p, []),
+    "pcadv_abi_version": (_i, []),
+    "pcadv_feat_fwd": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 5 + [_vp]),
+    "pcadv_feat_bwd_workspace_bytes": (_sz, [_i, _i]),
+    "pcadv_feat_bwd": (_i, [_vp, _vp, _vp, _i, _i] + [_vp] * 6 + [_vp] * 8 + [_vp, _sz, _vp]),
+    "pcadv_conv_max_fwd": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "pcadv_linear_fwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _u64, _f, _vp]),
+    "pcadv_linear_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _u64, _f, _vp, _vp, _vp, _vp, _vp,
+                              _i, _i, _i, _i, _vp]),
+    "pcadv_adam": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _vp]),
+    "pcadv_adv_step_workspace_bytes": (_sz, [_i, _i]),
+    "pcadv_adv_step": (_i, [ctypes.POINTER(AdvArgs), _vp]),
+    "pcadv_adv_step_adam": (_i, [ctypes.POINTER(AdvArgs), _vp]),
+}
+
+_lib = None
+
+
+class PcadvError(RuntimeError):
+    pass
+
+
+def load():
+    """dlopen libpcadv.so once; raise if it is missing (no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PcadvError(
+                f"libpcadv.so not found at {LIB_PATH}: build it with `make` (hipcc, gfx950). "
+                "There is no CPU fallback for the pcadv ops.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != PCADV_OK:
+        msg = load().pcadv_last_error().decode(errors="replace")
+        raise PcadvError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

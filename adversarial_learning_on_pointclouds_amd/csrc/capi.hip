@@ -1,0 +1,287 @@
+// extern "C" entry points of libpcadv.so (include/pcadv.h) and the fused
+// adversarial step, which enqueues the whole iteration of
+// utils/trainer.py:run_training (:426-559) on one stream.
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+
+namespace pcadv {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int launch_point_mlp3(const float*, const float*, int, int, int, const float*, const float*,
+                      const float*, const float*, const float*, const float*, float*, float*,
+                      float*, int32_t*, hipStream_t);
+int launch_conv_max128(const float*, int, int, const float*, const float*, int, bool, float*,
+                       int32_t*, hipStream_t);
+size_t feat_bwd_workspace_bytes(int C, int N);
+int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
+                    const float*, const float*, const float*, const float*, const float*,
+                    const float*, float*, float*, float*, float*, float*, float*, float*, float*,
+                    void*, size_t, hipStream_t);
+int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
+                      const float*, const int32_t*, uint64_t, float, hipStream_t);
+int launch_linear_bwd(const float*, const float*, int, const float*, const int32_t*, uint64_t,
+                      float, const float*, const float*, float*, float*, float*, int, int, int,
+                      int, hipStream_t);
+int launch_cls_loss(const float*, const int64_t*, int, int, float, float*, float*, float*,
+                    hipStream_t);
+int launch_disc_loss(const float*, int, const float*, const float*, const int32_t*, uint64_t,
+                     float, float*, float*, hipStream_t);
+int launch_lsm_bwd(const float*, const float*, int, int, float*, hipStream_t);
+int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, const float*,
+                 float*, float*, int64_t, float, const int32_t*, int, float, float, float,
+                 hipStream_t);
+int launch_inc(int32_t*, hipStream_t);
+
+// ---- workspace carve for the fused step ------------------------------------
+struct StepWs {
+  float *x1, *x2, *x3, *gmax, *h1, *h2, *logits, *dlogits, *dh2, *dh1, *dgmax;
+  float *din, *d1, *d2, *d3, *d4, *d5, *dout;
+  float *ddout, *dd5, *dd4, *dd3, *dd2, *dd1, *ddin;
+  float *mask;
+  int32_t* gidx;
+  void* feat_ws;
+  size_t feat_ws_bytes;
+  size_t total;
+};
+
+static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+static StepWs carve(int B, int N, char* base) {
+  StepWs w{};
+  const size_t C = 2 * (size_t)B, R = 3 * (size_t)B;
+  size_t off = 0;
+  auto take = [&](size_t nfloat) {
+    char* p = base ? base + off : nullptr;
+    off += align_up(nfloat * sizeof(float));
+    return reinterpret_cast<float*>(p);
+  };
+  w.x1 = take(C * N * 64);
+  w.x2 = take(C * N * 64);
+  w.x3 = take(C * N * 128);
+  w.gmax = take(C * 1024);
+  w.gidx = reinterpret_cast<int32_t*>(take(C * 1024));
+  w.h1 = take(C * 512);
+  w.h2 = take(C * 256);
+  w.logits = take(C * 40);
+  w.dlogits = take(C * 40);
+  w.dh2 = take(C * 256);
+  w.dh1 = take(C * 512);
+  w.dgmax = take(C * 1024);
+  w.din = take(R * 40);
+  w.d1 = take(R * 512);
+  w.d2 = take(R * 256);
+  w.d3 = take(R * 256);
+  w.d4 = take(R * 64);
+  w.d5 = take(R * 64);
+  w.dout = take(R);
+  w.ddout = take(R);
+  w.dd5 = take(R * 64);
+  w.dd4 = take(R * 64);
+  w.dd3 = take(R * 256);
+  w.dd2 = take(R * 256);
+  w.dd1 = take(R * 512);
+  w.ddin = take(R * 40);
+  w.mask = take(C * 256);
+  w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
+  w.feat_ws = take(w.feat_ws_bytes / sizeof(float) + 1);
+  w.total = off;
+  return w;
+}
+
+#define PC_TRY(call)            \
+  do {                          \
+    int rc_ = (call);           \
+    if (rc_ != PCADV_OK) return rc_; \
+  } while (0)
+
+static int adv_adam(const pcadv_adv_args* a, hipStream_t s) {
+  PC_REQUIRE(a && a->g_param && a->d_param && a->step_count, "adv_step_adam: bad arguments");
+  return launch_adam2(a->g_param, a->g_grad, a->g_m, a->g_v, PCADV_G_NUMEL, a->lr_g, a->d_param,
+                      a->d_grad, a->d_m, a->d_v, PCADV_D_NUMEL, a->lr_d, a->step_count, 0,
+                      a->beta1, a->beta2, a->eps, s);
+}
+
+static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
+  PC_REQUIRE(a && a->B > 0 && a->B <= 256 && a->N > 0, "adv_step: bad B/N");
+  const int B = a->B, N = a->N, C = 2 * B, R = 3 * B;
+  PC_REQUIRE(a->workspace && a->workspace_bytes >= carve(B, N, nullptr).total,
+             "adv_step: workspace too small (need %zu bytes)", carve(B, N, nullptr).total);
+  StepWs w = carve(B, N, static_cast<char*>(a->workspace));
+  const float* G = a->g_param;
+  float* gG = a->g_grad;
+  const float* D = a->d_param;
+  float* gD = a->d_grad;
+  const int32_t* st = a->step_count;
+  float* logits = a->logits ? a->logits : w.logits;
+
+  // dropout: explicit masks (parity mode) are staged as one [2B][256] array
+  const float* mask = nullptr;
+  if (a->drop_mask_gt || a->drop_mask_nogt) {
+    PC_REQUIRE(a->drop_mask_gt && a->drop_mask_nogt, "adv_step: give both dropout masks or none");
+    if (hipMemcpyAsync(w.mask, a->drop_mask_gt, sizeof(float) * B * 256, hipMemcpyDeviceToDevice,
+                       s) != hipSuccess ||
+        hipMemcpyAsync(w.mask + (size_t)B * 256, a->drop_mask_nogt, sizeof(float) * B * 256,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess) {
+      set_error("adv_step: mask staging copy failed");
+      return PCADV_EHIP;
+    }
+    mask = w.mask;
+  }
+  const int32_t* rstep = mask ? nullptr : st;
+
+  // ---- generator forward, both loaders in one launch (:468, :490) ----------
+  PC_TRY(launch_point_mlp3(a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
+                           G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                           G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, w.x1, w.x2, w.x3,
+                           a->step_count, s));
+  PC_TRY(launch_conv_max128(w.x3, C, N, G + PCADV_G_CONV4_W, G + PCADV_G_CONV4_B, 1024, false,
+                            w.gmax, w.gidx, s));
+  PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
+                           PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
+                           PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s));
+  PC_TRY(launch_linear_fwd(w.h2, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, logits, C, 40, 256,
+                           PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, s));
+  // ---- losses on the logits; D input rows [lsm_gt; lsm_nogt; lsm_nogt] -----
+  PC_TRY(launch_cls_loss(logits, a->labels, B, 40, a->lambda_cls, w.din, w.dlogits, a->losses, s));
+  // ---- discriminator forward (:499, :530, :546 share parameters) -----------
+  PC_TRY(launch_linear_fwd(w.din, D + PCADV_D_CONV1_W, D + PCADV_D_CONV1_B, w.d1, R, 512, 40,
+                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.d1, D + PCADV_D_CONV2_W, D + PCADV_D_CONV2_B, w.d2, R, 256, 512,
+                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.d2, D + PCADV_D_CONV3_W, D + PCADV_D_CONV3_B, w.d3, R, 256, 256,
+                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.d3, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, w.d4, R, 64, 256,
+                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.d4, D + PCADV_D_CONV5_W, D + PCADV_D_CONV5_B, w.d5, R, 64, 64,
+                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.d5, D + PCADV_D_FC_W, D + PCADV_D_FC_B, w.dout, R, 1, 64,
+                           PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_disc_loss(w.dout, B, a->soft_gt, a->soft_nogt, st, a->rng_seed, a->lambda_adv,
+                          w.ddout, a->losses, s));
+  // ---- discriminator backward: param grads from rows [0,2B) (D loss), input
+  //      grad of rows [2B,3B) (generator's adversarial loss, D frozen) --------
+  const int MW = 2 * B;
+  PC_TRY(launch_linear_bwd(w.ddout, w.dout, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.d5,
+                           D + PCADV_D_FC_W, w.dd5, gD + PCADV_D_FC_W, gD + PCADV_D_FC_B, R, MW,
+                           1, 64, s));
+  PC_TRY(launch_linear_bwd(w.dd5, w.d5, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d4,
+                           D + PCADV_D_CONV5_W, w.dd4, gD + PCADV_D_CONV5_W, gD + PCADV_D_CONV5_B,
+                           R, MW, 64, 64, s));
+  PC_TRY(launch_linear_bwd(w.dd4, w.d4, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d3,
+                           D + PCADV_D_CONV4_W, w.dd3, gD + PCADV_D_CONV4_W, gD + PCADV_D_CONV4_B,
+                           R, MW, 64, 256, s));
+  PC_TRY(launch_linear_bwd(w.dd3, w.d3, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d2,
+                           D + PCADV_D_CONV3_W, w.dd2, gD + PCADV_D_CONV3_W, gD + PCADV_D_CONV3_B,
+                           R, MW, 256, 256, s));
+  PC_TRY(launch_linear_bwd(w.dd2, w.d2, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d1,
+                           D + PCADV_D_CONV2_W, w.dd1, gD + PCADV_D_CONV2_W, gD + PCADV_D_CONV2_B,
+                           R, MW, 256, 512, s));
+  PC_TRY(launch_linear_bwd(w.dd1, w.d1, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.din,
+                           D + PCADV_D_CONV1_W, w.ddin, gD + PCADV_D_CONV1_W, gD + PCADV_D_CONV1_B,
+                           R, MW, 512, 40, s));
+  PC_TRY(launch_lsm_bwd(w.din, w.ddin, B, 40, w.dlogits, s));
+  // ---- generator head backward (:520) --------------------------------------
+  PC_TRY(launch_linear_bwd(w.dlogits, logits, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h2,
+                           G + PCADV_G_FC3_W, w.dh2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, C,
+                           40, 256, s));
+  PC_TRY(launch_linear_bwd(w.dh2, w.h2, PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, w.h1,
+                           G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C, C,
+                           256, 512, s));
+  PC_TRY(launch_linear_bwd(w.dh1, w.h1, PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, w.gmax,
+                           G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
+                           C, 512, 1024, s));
+  // ---- PointNetfeat backward (sparse max-pool) -----------------------------
+  PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV2_W,
+                         G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x1, w.x2, w.x3,
+                         gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
+                         gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
+                         gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
+                         s));
+  // ---- optimizer.step(); optimizer_D.step() (:558-559) ----------------------
+  if (a->apply_adam) return adv_adam(a, s);
+  return PCADV_OK;
+}
+
+}  // namespace pcadv
+
+using namespace pcadv;
+
+extern "C" {
+
+const char* pcadv_last_error(void) { return g_err; }
+int pcadv_abi_version(void) { return 1; }
+
+int pcadv_feat_fwd(const float* pts, int C, int N, const float* w1, const float* b1,
+                   const float* w2, const float* b2, const float* w3, const float* b3,
+                   const float* w4, const float* b4, float* x1, float* x2, float* x3,
+                   float* gmax, int32_t* gidx, hipStream_t stream) {
+  PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
+  PC_TRY(launch_point_mlp3(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, x1, x2, x3, nullptr,
+                           stream));
+  return launch_conv_max128(x3, C, N, w4, b4, PCADV_C4, false, gmax, gidx, stream);
+}
+
+size_t pcadv_feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_workspace_bytes(C, N); }
+
+int pcadv_feat_bwd(const float* dgmax, const int32_t* gidx, const float* pts, int C, int N,
+                   const float* w2, const float* w3, const float* w4, const float* x1,
+                   const float* x2, const float* x3, float* dw1, float* db1, float* dw2,
+                   float* db2, float* dw3, float* db3, float* dw4, float* db4, void* workspace,
+                   size_t workspace_bytes, hipStream_t stream) {
+  PC_REQUIRE(C > 0 && N > 0, "feat_bwd: bad shape C=%d N=%d", C, N);
+  return launch_feat_bwd(dgmax, gidx, pts, pts, C, C, N, w2, w3, w4, x1, x2, x3, dw1, db1, dw2,
+                         db2, dw3, db3, dw4, db4, workspace, workspace_bytes, stream);
+}
+
+int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, const float* b, int O,
+                       int relu_before_max, float* gmax, int32_t* gidx, hipStream_t stream) {
+  PC_REQUIRE(K == 128, "conv_max_fwd: only K=128 is implemented (got %d)", K);
+  PC_REQUIRE(C > 0 && N > 0 && O > 0 && O % 128 == 0, "conv_max_fwd: bad shape C=%d N=%d O=%d", C,
+             N, O);
+  return launch_conv_max128(x, C, N, w, b, O, relu_before_max != 0, gmax, gidx, stream);
+}
+
+int pcadv_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int Nout,
+                     int K, int act, const float* drop_mask, const int32_t* rng_step,
+                     uint64_t rng_seed, float drop_p, hipStream_t stream) {
+  return launch_linear_fwd(x, w, b, y, M, Nout, K, act, drop_mask, rng_step, rng_seed, drop_p,
+                           stream);
+}
+
+int pcadv_linear_bwd(const float* dy, const float* y, int act, const float* drop_mask,
+                     const int32_t* rng_step, uint64_t rng_seed, float drop_p, const float* x,
+                     const float* w, float* dx, float* dw, float* db, int M, int m_w, int Nout,
+                     int K, hipStream_t stream) {
+  return launch_linear_bwd(dy, y, act, drop_mask, rng_step, rng_seed, drop_p, x, w, dx, dw, db, M,
+                           m_w, Nout, K, stream);
+}
+
+int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+               int32_t* step_count, float lr, float beta1, float beta2, float eps,
+               hipStream_t stream) {
+  PC_REQUIRE(n > 0 && step_count, "adam: bad arguments");
+  PC_TRY(launch_adam2(param, grad, exp_avg, exp_avg_sq, n, lr, nullptr, nullptr, nullptr, nullptr,
+                      0, 0.f, step_count, 1, beta1, beta2, eps, stream));
+  return launch_inc(step_count, stream);
+}
+
+size_t pcadv_adv_step_workspace_bytes(int B, int N) { return carve(B, N, nullptr).total; }
+
+int pcadv_adv_step(const pcadv_adv_args* args, hipStream_t stream) { return adv_step(args, stream); }
+
+int pcadv_adv_step_adam(const pcadv_adv_args* args, hipStream_t stream) {
+  return adv_adam(args, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// Shared helpers for the pcadv HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+#include "../../include/pcadv.h"
+
+namespace pcadv {
+
+// thread-local last-error text (pcadv_last_error)
+void set_error(const char* fmt, ...);
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 32x32x2 f32 MFMA: exact f32 (k-ordered fma chain), 64 cycles / SIMD.
+// lane l supplies A[i=l&31][k=l>>5], B[k=l>>5][j=l&31];
+// D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5).
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int acc_row(int r, int lane) {
+  return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+
+// activation codes shared with the C ABI (include/pcadv.h)
+enum Act { ACT_NONE = PCADV_ACT_NONE, ACT_RELU = PCADV_ACT_RELU, ACT_LRELU = PCADV_ACT_LRELU };
+
+__device__ __forceinline__ float act_fwd(float x, int act) {
+  if (act == ACT_RELU) return x > 0.f ? x : 0.f;
+  if (act == ACT_LRELU) return x > 0.f ? x : x * 0.2f;
+  return x;
+}
+// derivative from the activation OUTPUT (sign preserved by relu/leaky relu)
+__device__ __forceinline__ float act_bwd(float y, int act) {
+  if (act == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (act == ACT_LRELU) return y > 0.f ? 1.f : 0.2f;
+  return 1.f;
+}
+
+// ---------------------------------------------------------------------------
+// counter-based RNG (Philox-4x32-10) for dropout masks and soft D labels.
+// Keyed by (seed, step counter read on device) so graph replays draw fresh
+// numbers each step without host involvement.
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                        uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += W0; k1 += W1;
+  }
+  return {c0, c1, c2, c3};
+}
+
+// uniform in [0,1) with 24 random bits
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// stream ids keep the different random draws of one step independent
+enum RngStream : uint32_t { RNG_DROPOUT = 1, RNG_LABEL_GT = 2, RNG_LABEL_NOGT = 3 };
+
+__device__ __forceinline__ float rng_uniform(uint64_t seed, uint32_t step, uint32_t stream,
+                                             uint32_t index) {
+  u32x4 r = philox(index, step, stream, 0x5043u, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return u01(r.x);
+}
+
+}  // namespace pcadv
+
+#define PC_HIP_CHECK_LAUNCH(what)                                              \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess) {                                                    \
+      pcadv::set_error("%s: %s", what, hipGetErrorString(e_));                 \
+      return PCADV_EHIP;                                                       \
+    }                                                                          \
+  } while (0)
+
+#define PC_REQUIRE(cond, ...)                                                  \
+  do {                                                                         \
+    if (!(cond)) {                                                             \
+      pcadv::set_error(__VA_ARGS__);                                           \
+      return PCADV_EINVAL;                                                     \
+    }                                                                          \
+  } while (0)

@@ -1,0 +1,201 @@
+"""Tensor-level wrappers of the pcadv HIP kernels + autograd.Functions.
+
+Every wrapper validates shapes, dtypes, devices and contiguity on the host
+before launching (a kernel never sees a shape its grid does not assume), then
+enqueues on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, check, ptr, stream_ptr
+
+__all__ = ["ACT_NONE", "ACT_RELU", "ACT_LRELU", "feat_fwd", "feat_bwd", "conv_max_fwd",
+           "linear_fwd", "linear_bwd", "adam_", "PointFeatFunction", "LinearFunction"]
+
+
+def _req(t, name, shape=None, dtype=torch.float32):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: pcadv ops run on the HIP device only (got {t.device})")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    return t
+
+
+def _mat(w):
+    """Conv1d [out,in,1] or Linear [out,in] weight as a contiguous [out][in]."""
+    return w.reshape(w.shape[0], -1)
+
+
+# ---------------------------------------------------------------------------
+# PointNetfeat (feature_transform=False)
+# ---------------------------------------------------------------------------
+
+def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4):
+    """pts (C, N, 3) -> gmax (C, 1024), gidx (C, 1024) int32, saved (x1, x2, x3)."""
+    lib = _lib.load()
+    _req(pts, "pts")
+    if pts.dim() != 3 or pts.shape[2] != 3:
+        raise ValueError(f"pts: expected (C, N, 3), got {tuple(pts.shape)}")
+    C, N, _ = pts.shape
+    ws = [_req(_mat(w1), "conv1.weight", (64, 3)), _req(b1, "conv1.bias", (64,)),
+          _req(_mat(w2), "conv2.weight", (64, 64)), _req(b2, "conv2.bias", (64,)),
+          _req(_mat(w3), "conv3.weight", (128, 64)), _req(b3, "conv3.bias", (128,)),
+          _req(_mat(w4), "conv4.weight", (1024, 128)), _req(b4, "conv4.bias", (1024,))]
+    dev = pts.device
+    x1 = torch.empty(C, N, 64, device=dev)
+    x2 = torch.empty(C, N, 64, device=dev)
+    x3 = torch.empty(C, N, 128, device=dev)
+    gmax = torch.empty(C, 1024, device=dev)
+    gidx = torch.empty(C, 1024, device=dev, dtype=torch.int32)
+    check(lib.pcadv_feat_fwd(ptr(pts), C, N, *[ptr(t) for t in ws], ptr(x1), ptr(x2), ptr(x3),
+                             ptr(gmax), ptr(gidx), stream_ptr()), "pcadv_feat_fwd")
+    return gmax, gidx, (x1, x2, x3)
+
+
+def feat_bwd(dgmax, gidx, pts, w2, w3, w4, x1, x2, x3):
+    """Gradients of (conv1..conv4) weights and biases given dL/dgmax."""
+    lib = _lib.load()
+    C, N, _ = pts.shape
+    _req(dgmax, "dgmax", (C, 1024))
+    _req(gidx, "gidx", (C, 1024), torch.int32)
+    _req(pts, "pts")
+    _req(x1, "x1", (C, N, 64))
+    _req(x2, "x2", (C, N, 64))
+    _req(x3, "x3", (C, N, 128))
+    w2m, w3m, w4m = _mat(w2), _mat(w3), _mat(w4)
+    _req(w2m, "conv2.weight", (64, 64))
+    _req(w3m, "conv3.weight", (128, 64))
+    _req(w4m, "conv4.weight", (1024, 128))
+    dev = pts.device
+    grads = [torch.empty(64, 3, 1, device=dev), torch.empty(64, device=dev),
+             torch.empty(64, 64, 1, device=dev), torch.empty(64, device=dev),
+             torch.empty(128, 64, 1, device=dev), torch.empty(128, device=dev),
+             torch.empty(1024, 128, 1, device=dev), torch.empty(1024, device=dev)]
+    nbytes = lib.pcadv_feat_bwd_workspace_bytes(C, N)
+    ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+    check(lib.pcadv_feat_bwd(ptr(dgmax), ptr(gidx), ptr(pts), C, N, ptr(w2m), ptr(w3m), ptr(w4m),
+                             ptr(x1), ptr(x2), ptr(x3), *[ptr(g) for g in grads], ptr(ws),
+                             nbytes, stream_ptr()), "pcadv_feat_bwd")
+    return grads
+
+
+def conv_max_fwd(x, w, b, relu_before_max=False):
+    """x (C, N, 128) point-major; w (O, 128[,1]); -> gmax (C, O), gidx (C, O)."""
+    lib = _lib.load()
+    _req(x, "x")
+    C, N, K = x.shape
+    wm = _req(_mat(w), "w")
+    O = wm.shape[0]
+    _req(b, "b", (O,))
+    if wm.shape[1] != K:
+        raise ValueError("conv_max_fwd: weight/input width mismatch")
+    gmax = torch.empty(C, O, device=x.device)
+    gidx = torch.empty(C, O, device=x.device, dtype=torch.int32)
+    check(lib.pcadv_conv_max_fwd(ptr(x), C, N, K, ptr(wm), ptr(b), O, int(bool(relu_before_max)),
+                                 ptr(gmax), ptr(gidx), stream_ptr()), "pcadv_conv_max_fwd")
+    return gmax, gidx
+
+
+# ---------------------------------------------------------------------------
+# linear / 1x1 conv on B x C x 1
+# ---------------------------------------------------------------------------
+
+def linear_fwd(x, w, b, act=ACT_NONE, mask=None, p=0.0):
+    lib = _lib.load()
+    _req(x, "x")
+    M, K = x.shape
+    wm = _req(_mat(w), "weight")
+    Nout = wm.shape[0]
+    if wm.shape[1] != K:
+        raise ValueError(f"linear: weight {tuple(wm.shape)} does not match input width {K}")
+    _req(b, "bias", (Nout,))
+    if mask is not None:
+        _req(mask, "dropout mask", (M, Nout))
+    y = torch.empty(M, Nout, device=x.device)
+    check(lib.pcadv_linear_fwd(ptr(x), ptr(wm), ptr(b), ptr(y), M, Nout, K, act, ptr(mask), None,
+                               0, float(p), stream_ptr()), "pcadv_linear_fwd")
+    return y
+
+
+def linear_bwd(dy, y, act, mask, p, x, w, need_dx=True, need_dw=True, m_w=None):
+    lib = _lib.load()
+    M, K = x.shape
+    wm = _mat(w)
+    Nout = wm.shape[0]
+    _req(dy, "grad_output", (M, Nout))
+    _req(y, "output", (M, Nout))
+    _req(x, "x", (M, K))
+    _req(wm, "weight", (Nout, K))
+    if mask is not None:
+        _req(mask, "dropout mask", (M, Nout))
+    m_w = M if m_w is None else m_w
+    dx = torch.empty(M, K, device=x.device) if need_dx else None
+    dw = torch.empty_like(w) if need_dw else None
+    db = torch.empty(Nout, device=x.device) if need_dw else None
+    check(lib.pcadv_linear_bwd(ptr(dy), ptr(y), act, ptr(mask), None, 0, float(p), ptr(x), ptr(wm),
+                               ptr(dx), ptr(dw), ptr(db), M, m_w, Nout, K, stream_ptr()),
+          "pcadv_linear_bwd")
+    return dx, dw, db
+
+
+def adam_(param, grad, exp_avg, exp_avg_sq, step_count, lr, beta1, beta2, eps):
+    """In-place torch.optim.Adam step on flat fp32 buffers; step_count is a
+    device int32 tensor advanced by the call."""
+    lib = _lib.load()
+    n = param.numel()
+    for t, nm in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _req(t, nm)
+        if t.numel() != n:
+            raise ValueError(f"adam: {nm} has {t.numel()} elements, expected {n}")
+    _req(step_count, "step_count", (1,), torch.int32)
+    check(lib.pcadv_adam(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), n, ptr(step_count),
+                         lr, beta1, beta2, eps, stream_ptr()), "pcadv_adam")
+
+
+# ---------------------------------------------------------------------------
+# autograd
+# ---------------------------------------------------------------------------
+
+class PointFeatFunction(torch.autograd.Function):
+    """PointNetfeat.forward (models/pointnet.py:109-132) as one fused pass:
+    returns the global feature (C, 1024); the max-pool backward is sparse."""
+
+    @staticmethod
+    def forward(ctx, pts, w1, b1, w2, b2, w3, b3, w4, b4):
+        gmax, gidx, (x1, x2, x3) = feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4)
+        ctx.save_for_backward(pts, w2, w3, w4, x1, x2, x3, gidx)
+        ctx.mark_non_differentiable(gidx)
+        return gmax, gidx
+
+    @staticmethod
+    def backward(ctx, dgmax, _dgidx):
+        pts, w2, w3, w4, x1, x2, x3, gidx = ctx.saved_tensors
+        g = feat_bwd(dgmax.contiguous(), gidx, pts, w2, w3, w4, x1, x2, x3)
+        return (None, *g)
+
+
+class LinearFunction(torch.autograd.Function):
+    """act(mask/(1-p) * (x w^T + b)) for nn.Linear / 1x1 Conv1d layers."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act, mask, p):
+        y = linear_fwd(x, w, b, act, mask, p)
+        ctx.save_for_backward(x, w, y, mask if mask is not None else torch.empty(0))
+        ctx.act, ctx.p, ctx.has_mask = act, p, mask is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y, mask = ctx.saved_tensors
+        dx, dw, db = linear_bwd(dy.contiguous(), y, ctx.act, mask if ctx.has_mask else None, ctx.p,
+                                x, w, need_dx=ctx.needs_input_grad[0],
+                                need_dw=ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        return dx, dw, db, None, None, None

@@ -1,0 +1,116 @@
+"""Drop-in PointNet modules backed by the pcadv HIP kernels.
+
+Same class names, constructor arguments, forward signatures, return tuples and
+state_dict keys/shapes as the reference's models/pointnet.py, so checkpoints
+load in either direction and utils/trainer.py-style loops run unchanged.
+The compute runs in libpcadv.so; there is no eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .ops import ACT_NONE, ACT_RELU, LinearFunction, PointFeatFunction
+
+__all__ = ["PointNetfeat", "PointNetCls", "STN3d", "STNkd", "feature_transform_regularizer"]
+
+
+class STNkd(nn.Module):
+    """k x k transform regressor (models/pointnet.py:46-79).  Parameters only in
+    this round; its HIP forward is a later §8 row (a7)."""
+
+    def __init__(self, k=64):
+        super().__init__()
+        self.conv1 = nn.Conv1d(k, 64, 1)
+        self.conv2 = nn.Conv1d(64, 128, 1)
+        self.conv3 = nn.Conv1d(128, 1024, 1)
+        self.fc1 = nn.Linear(1024, 512)
+        self.fc2 = nn.Linear(512, 256)
+        self.fc3 = nn.Linear(256, k * k)
+        self.relu = nn.ReLU()
+        self.k = k
+
+    def forward(self, x):
+        raise NotImplementedError("STNkd HIP forward is not built yet (feature_transform=True)")
+
+
+class STN3d(STNkd):
+    """3 x 3 input transform (models/pointnet.py:14-43)."""
+
+    def __init__(self):
+        super().__init__(k=3)
+
+
+class PointNetfeat(nn.Module):
+    """models/pointnet.py:81-137.  forward(x: B x 3 x N) -> (global B x 1024, trans_feat)."""
+
+    def __init__(self, global_feat=True, feature_transform=False):
+        super().__init__()
+        self.conv1 = nn.Conv1d(3, 64, 1)
+        self.conv2 = nn.Conv1d(64, 64, 1)
+        self.conv3 = nn.Conv1d(64, 128, 1)
+        self.conv4 = nn.Conv1d(128, 1024, 1)
+        self.global_feat = global_feat
+        self.feature_transform = feature_transform
+        if self.feature_transform:
+            self.fstn = STNkd(k=64)
+
+    def forward_points(self, pts):
+        """pts: C x N x 3 (point-major, as PointNetCls receives it)."""
+        if self.feature_transform:
+            raise NotImplementedError("feature_transform=True: STNkd HIP path not built yet")
+        gmax, gidx = PointFeatFunction.apply(
+            pts.contiguous(), self.conv1.weight, self.conv1.bias, self.conv2.weight,
+            self.conv2.bias, self.conv3.weight, self.conv3.bias, self.conv4.weight,
+            self.conv4.bias)
+        self.last_argmax = gidx
+        return gmax
+
+    def forward(self, x):
+        # the reference receives B x C x N; the kernels read the point-major
+        # B x N x 3 layout, which is a free view when x came from a transpose.
+        g = self.forward_points(x.transpose(1, 2))
+        if self.global_feat:
+            return g, None
+        n_pts = x.size(2)
+        raise NotImplementedError("global_feat=False (per-point concat) is not on the hot path")
+
+
+class PointNetCls(nn.Module):
+    """models/pointnet.py:186-203.  forward(x: B x N x 3) ->
+    (logits B x k, x_global B x 1024 x 1, trans_feat)."""
+
+    def __init__(self, k=3, feature_transform=False):
+        super().__init__()
+        self.feature_transform = feature_transform
+        self.feat = PointNetfeat(global_feat=True, feature_transform=feature_transform)
+        self.fc1 = nn.Linear(1024, 512)
+        self.fc2 = nn.Linear(512, 256)
+        self.fc3 = nn.Linear(256, k)
+        self.dropout = nn.Dropout(p=0.3)
+        self.relu = nn.ReLU()
+        # optional queue of explicit dropout masks (B x 256 {0,1}) for parity runs
+        self.dropout_masks = []
+
+    def _dropout_mask(self, B, device):
+        if not self.training or self.dropout.p == 0.0:
+            return None
+        if self.dropout_masks:
+            return self.dropout_masks.pop(0).to(device=device, dtype=torch.float32).contiguous()
+        return (torch.rand(B, 256, device=device) >= self.dropout.p).float()
+
+    def forward(self, x):
+        x_global = self.feat.forward_points(x)
+        h = LinearFunction.apply(x_global, self.fc1.weight, self.fc1.bias, ACT_RELU, None, 0.0)
+        mask = self._dropout_mask(x.shape[0], x.device)
+        h = LinearFunction.apply(h, self.fc2.weight, self.fc2.bias, ACT_RELU, mask,
+                                 float(self.dropout.p))
+        out = LinearFunction.apply(h, self.fc3.weight, self.fc3.bias, ACT_NONE, None, 0.0)
+        return out, x_global.unsqueeze(2), None
+
+
+def feature_transform_regularizer(trans):
+    """mean_b ||T T^T - I||_F (models/pointnet.py:345-353), on trans's device."""
+    d = trans.size(1)
+    eye = torch.eye(d, device=trans.device, dtype=trans.dtype)[None]
+    return torch.mean(torch.norm(torch.bmm(trans, trans.transpose(2, 1)) - eye, dim=(1, 2)))

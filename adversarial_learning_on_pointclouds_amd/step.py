@@ -1,0 +1,229 @@
+"""The fused adversarial train step (one iteration of utils/trainer.py:run_training,
+:426-559) as a single native call, optionally captured into a HIP graph.
+
+Parameters of both networks are moved into one flat fp32 buffer each (state_dict
+order, offsets = include/pcadv.h); the modules' Parameters become views of it,
+so checkpoints, eval passes and torch optimizers keep working on the same
+memory.  Both networks' gradients share ONE flat buffer (generator first), so a
+data-parallel run averages them with a single all-reduce.  Adam moments are
+flat too and are handed to a torch Adam optimizer's state as views
+(exp_avg / exp_avg_sq), so optimizer.state_dict() stays meaningful.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import AdvArgs, D_LAYOUT, D_NUMEL, G_LAYOUT, G_NUMEL, check, stream_ptr
+
+D_GRAD_OFFSET = (G_NUMEL + 63) // 64 * 64  # D grads start 256-B aligned
+
+
+def flatten_params(module, layout, numel, device):
+    """Copy a module's parameters into one flat buffer and rebind them as views."""
+    flat = torch.zeros(numel, device=device, dtype=torch.float32)
+    named = dict(module.named_parameters())
+    if set(named) != set(layout):
+        raise ValueError(f"{type(module).__name__}: parameters {sorted(set(named) ^ set(layout))} "
+                         "do not match the fused-step layout")
+    for name, off in layout.items():
+        p = named[name]
+        n = p.numel()
+        flat[off:off + n].copy_(p.detach().reshape(-1))
+        p.data = flat[off:off + n].view_as(p)
+    return flat
+
+
+def _views(flat, module, layout):
+    named = dict(module.named_parameters())
+    return {name: flat[off:off + named[name].numel()].view_as(named[name])
+            for name, off in layout.items()}
+
+
+def _align(nbytes):
+    return (nbytes + 255) // 256 * 256
+
+
+class AdvTrainStep:
+    """run_training's iteration body for PointNetCls(k=40) + DeepConvDiscNet(40, 1).
+
+    Call with device tensors pts_gt (B, N, 3) f32, labels (B,) int64, pts_nogt
+    (B, N, 3) f32.  Dropout masks and soft D labels are drawn on device from
+    Philox keyed by (seed, step) unless given explicitly (parity mode:
+    masks=(gt, nogt) each (B, 256) {0,1}; soft=(gt, nogt) each (B,)).
+    Returns the device tensor [loss_cls, loss_adv, loss_D_gt, loss_D_nogt]
+    (no host sync: read it when you log, trainer.py:561-572).
+    """
+
+    def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
+                 lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
+                 seed=0, device="cuda"):
+        self.lib = _lib.load()
+        self.model, self.model_D = model, model_D
+        self.B, self.N = int(B), int(N)
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("AdvTrainStep runs on the HIP device only")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        if optimizer is not None:
+            g = optimizer.param_groups[0]
+            lr, betas, eps = g["lr"], tuple(g["betas"]), g["eps"]
+        if optimizer_D is not None:
+            lr_D = optimizer_D.param_groups[0]["lr"]
+        self.hp = dict(lr=float(lr), lr_D=float(lr_D), betas=betas, eps=float(eps),
+                       lambda_cls=float(lambda_cls), lambda_adv=float(lambda_adv),
+                       p=float(model.dropout.p))
+        self.g_param = flatten_params(model, G_LAYOUT, G_NUMEL, dev)
+        self.d_param = flatten_params(model_D, D_LAYOUT, D_NUMEL, dev)
+        self.grad_flat = torch.zeros(D_GRAD_OFFSET + D_NUMEL, device=dev)
+        self.g_grad = self.grad_flat[:G_NUMEL]
+        self.d_grad = self.grad_flat[D_GRAD_OFFSET:]
+        self.g_m = torch.zeros_like(self.g_param)
+        self.g_v = torch.zeros_like(self.g_param)
+        self.d_m = torch.zeros_like(self.d_param)
+        self.d_v = torch.zeros_like(self.d_param)
+        self.step_count = torch.zeros(1, device=dev, dtype=torch.int32)
+        for opt, mod, layout, m, v, gr in (
+                (optimizer, model, G_LAYOUT, self.g_m, self.g_v, self.g_grad),
+                (optimizer_D, model_D, D_LAYOUT, self.d_m, self.d_v, self.d_grad)):
+            mv, vv, gv = _views(m, mod, layout), _views(v, mod, layout), _views(gr, mod, layout)
+            for name, p in mod.named_parameters():
+                p.grad = gv[name]
+                if opt is not None:
+                    opt.state[p] = {"step": torch.zeros((), dtype=torch.float32),
+                                    "exp_avg": mv[name], "exp_avg_sq": vv[name]}
+        self.optimizers = (optimizer, optimizer_D)
+        self.losses = torch.zeros(4, device=dev)
+        self.logits = torch.zeros(2 * self.B, 40, device=dev)
+        nbytes = self.lib.pcadv_adv_step_workspace_bytes(self.B, self.N)
+        self.workspace = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.graph = None
+        self._keep = []
+
+    # ------------------------------------------------------------------
+    def _args(self, pts_gt, labels, pts_nogt, masks, soft, apply_adam):
+        B, N = int(pts_gt.shape[0]), self.N
+        if not 0 < B <= self.B:
+            raise ValueError(f"batch of {B} clouds; this step was built for at most {self.B}")
+        for t, nm, shape, dt in ((pts_gt, "pts_gt", (B, N, 3), torch.float32),
+                                 (pts_nogt, "pts_nogt", (B, N, 3), torch.float32),
+                                 (labels, "labels", (B,), torch.int64)):
+            if (tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous()
+                    or t.device != self.device):
+                raise ValueError(f"{nm}: expected contiguous {dt} {shape} on {self.device}, "
+                                 f"got {t.dtype} {tuple(t.shape)} on {t.device}")
+        a = AdvArgs()
+        a.B, a.N = B, N
+        a.pts_gt, a.labels, a.pts_nogt = pts_gt.data_ptr(), labels.data_ptr(), pts_nogt.data_ptr()
+        if masks is not None:
+            for m in masks:
+                if tuple(m.shape) != (B, 256) or m.dtype != torch.float32 or not m.is_contiguous():
+                    raise ValueError("dropout masks must be contiguous float32 (B, 256)")
+            a.drop_mask_gt, a.drop_mask_nogt = masks[0].data_ptr(), masks[1].data_ptr()
+        if soft is not None:
+            for s in soft:
+                if s.numel() != B or s.dtype != torch.float32 or not s.is_contiguous():
+                    raise ValueError("soft labels must be contiguous float32 with B elements")
+            a.soft_gt, a.soft_nogt = soft[0].data_ptr(), soft[1].data_ptr()
+        a.g_param, a.g_grad = self.g_param.data_ptr(), self.g_grad.data_ptr()
+        a.g_m, a.g_v = self.g_m.data_ptr(), self.g_v.data_ptr()
+        a.d_param, a.d_grad = self.d_param.data_ptr(), self.d_grad.data_ptr()
+        a.d_m, a.d_v = self.d_m.data_ptr(), self.d_v.data_ptr()
+        a.step_count = self.step_count.data_ptr()
+        hp = self.hp
+        a.lr_g, a.lr_d = hp["lr"], hp["lr_D"]
+        a.beta1, a.beta2, a.eps = hp["betas"][0], hp["betas"][1], hp["eps"]
+        a.lambda_cls, a.lambda_adv, a.drop_p = hp["lambda_cls"], hp["lambda_adv"], hp["p"]
+        a.rng_seed = self.seed
+        a.apply_adam = int(bool(apply_adam))
+        a.losses = self.losses.data_ptr()
+        a.logits = self.logits.data_ptr()
+        a.workspace = self.workspace.data_ptr()
+        a.workspace_bytes = self.workspace.numel()
+        return a
+
+    def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, apply_adam=True):
+        """Whole iteration: forward, losses, backward, both Adam steps."""
+        a = self._args(pts_gt, labels, pts_nogt, masks, soft, apply_adam)
+        check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step")
+        return self.losses
+
+    def grads(self, pts_gt, labels, pts_nogt, masks=None, soft=None):
+        """Forward + backward only (gradients in grad_flat; step counter advanced)."""
+        return self(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False)
+
+    def adam(self):
+        """optimizer.step(); optimizer_D.step() on the current gradients."""
+        a = AdvArgs()
+        a.g_param, a.g_grad = self.g_param.data_ptr(), self.g_grad.data_ptr()
+        a.g_m, a.g_v = self.g_m.data_ptr(), self.g_v.data_ptr()
+        a.d_param, a.d_grad = self.d_param.data_ptr(), self.d_grad.data_ptr()
+        a.d_m, a.d_v = self.d_m.data_ptr(), self.d_v.data_ptr()
+        a.step_count = self.step_count.data_ptr()
+        a.lr_g, a.lr_d = self.hp["lr"], self.hp["lr_D"]
+        a.beta1, a.beta2, a.eps = self.hp["betas"][0], self.hp["betas"][1], self.hp["eps"]
+        check(self.lib.pcadv_adv_step_adam(ctypes.byref(a), stream_ptr()), "pcadv_adv_step_adam")
+
+    # ------------------------------------------------------------------
+    def _snapshot(self):
+        return [t.clone() for t in (self.g_param, self.g_m, self.g_v, self.d_param, self.d_m,
+                                    self.d_v, self.step_count)]
+
+    def _restore(self, saved):
+        for dst, src in zip((self.g_param, self.g_m, self.g_v, self.d_param, self.d_m, self.d_v,
+                             self.step_count), saved):
+            dst.copy_(src)
+
+    def capture_on(self, pts_gt, labels, pts_nogt, apply_adam=True):
+        """Capture one step reading the given (resident) input buffers into a
+        HIP graph; state is left as it was before the capture."""
+        saved = self._snapshot()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam)  # warm-up outside capture
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        a = self._args(pts_gt, labels, pts_nogt, None, None, apply_adam)
+        self._keep.append(a)
+        with torch.cuda.graph(g):
+            check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (capture)")
+        torch.cuda.synchronize()
+        self._restore(saved)
+        return g
+
+    def capture(self):
+        """Capture one step over static input buffers; returns the buffers
+        (pts_gt, labels, pts_nogt) to fill before replay()."""
+        B, N, dev = self.B, self.N, self.device
+        st = (torch.zeros(B, N, 3, device=dev), torch.zeros(B, device=dev, dtype=torch.int64),
+              torch.zeros(B, N, 3, device=dev))
+        self._static = st
+        self.graph = self.capture_on(*st)
+        return st
+
+    def replay(self):
+        self.graph.replay()
+        return self.losses
+
+    # ------------------------------------------------------------------
+    def saved_x3(self):
+        """conv3 activations of the last step, (2B, N, 128) view of the workspace
+        (carve order of csrc/capi.hip: x1, x2, x3, ...)."""
+        C, N = 2 * self.B, self.N
+        off = 2 * _align(C * N * 64 * 4)
+        n = C * N * 128
+        return self.workspace[off:off + 4 * n].view(torch.float32).view(C, N, 128)
+
+    def sync_optimizer_state(self):
+        """Copy the device step counter into the torch optimizers' 'step'."""
+        t = float(self.step_count.item())
+        for opt in self.optimizers:
+            if opt is not None:
+                for st in opt.state.values():
+                    st["step"] = torch.tensor(t)

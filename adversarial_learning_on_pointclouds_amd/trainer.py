@@ -1,0 +1,207 @@
+"""Training / evaluation loops with the reference's signatures
+(utils/trainer.py:30-69 run_testing, :222-308 run_training_pointnet_cls,
+:403-608 run_training).
+
+run_training runs each iteration through the fused native step
+(AdvTrainStep: one C-ABI call, no per-op Python) whenever the configuration is
+the hot path's (PointNetCls(k=40) + DeepConvDiscNet(40,1), Adam, CE/BCE losses,
+ImagePool(0), equal GT/noGT batch sizes); otherwise it runs the reference's
+loop body op by op over the same HIP kernels through autograd.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .discriminator import DeepConvDiscNet
+from .pointnet import PointNetCls
+from .step import AdvTrainStep
+from .utils import make_D_label
+
+
+def run_testing(dataloader, model, criterion, logger, test_iter, writer, args):
+    """utils/trainer.py:30-69 (accuracy normalised by batch_size * len(loader),
+    as the reference does)."""
+    model.eval()
+    total_accuracy = 0.0
+    total_loss = 0.0
+    for batch_idx, data in enumerate(dataloader):
+        pts, cls = data
+        pts, cls = pts.float().to(args.device), cls.long().to(args.device)
+        with torch.set_grad_enabled(False):
+            pred, _, _ = model(pts)
+            loss = criterion(pred, cls)
+        cls = cls.detach().cpu().numpy()
+        pred = np.argmax(pred.detach().cpu().numpy(), axis=1)
+        total_accuracy += int(np.sum(np.equal(pred, cls)))
+        total_loss += loss.item()
+    denom = float(args.batch_size * len(dataloader))
+    logger.info("Test accuracy: {:.4f} loss: {:.3f}".format(total_accuracy / denom, total_loss / denom))
+    if getattr(args, "tensorboard", False) and writer is not None:
+        writer.add_scalar("Loss/test_cls", total_loss / denom, test_iter)
+        writer.add_scalar("Accuracy/test", total_accuracy / denom, test_iter)
+    return total_accuracy / denom, total_loss / denom
+
+
+def _next(loader, it):
+    try:
+        _, batch = next(it)
+    except StopIteration:
+        it = enumerate(loader)
+        _, batch = next(it)
+    return batch, it
+
+
+def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pools, args):
+    if not (isinstance(model, PointNetCls) and isinstance(model_D, DeepConvDiscNet)):
+        return False
+    if model.feature_transform or model.fc3.out_features != 40:
+        return False
+    if model_D.conv1.in_channels != 40 or model_D.fc.out_features != 1:
+        return False
+    if str(args.device).split(":")[0] != "cuda":
+        return False
+    for opt in (optimizer, optimizer_D):
+        if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1:
+            return False
+        g = opt.param_groups[0]
+        if g.get("weight_decay", 0) or g.get("amsgrad") or g.get("maximize"):
+            return False
+    if type(gan_loss) is not torch.nn.BCEWithLogitsLoss or gan_loss.weight is not None \
+            or gan_loss.pos_weight is not None or gan_loss.reduction != "mean":
+        return False
+    if type(cls_loss) is not torch.nn.CrossEntropyLoss or cls_loss.weight is not None \
+            or cls_loss.reduction != "mean" or cls_loss.label_smoothing != 0.0:
+        return False
+    return all(p.pool_size == 0 for p in pools)
+
+
+def _save(model, model_D, args, tag):
+    torch.save(model.state_dict(), os.path.join(args.exp_dir, "model_{}.pth".format(tag)))
+    torch.save(model_D.state_dict(), os.path.join(args.exp_dir, "modelD_{}.pth".format(tag)))
+
+
+def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloader_nogt_iter,
+                 testloader, model, model_D, gan_loss, cls_loss, optimizer, optimizer_D,
+                 history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args):
+    """utils/trainer.py:403-608."""
+    gt_label, nogt_label = 1, 0
+    max_test_accu = float("-inf")
+    max_train_epoch = 0
+    fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss,
+                     (history_pool_gt, history_pool_nogt), args)
+    step = None
+    log_every = int(getattr(args, "log_every", 1))
+
+    for i_iter in range(args.total_iterations):
+        model.train()
+        model_D.train()
+        batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
+        pts, cls = batch
+        pts_nogt, targetloader_nogt_iter = _next(trainloader_nogt, targetloader_nogt_iter)
+        pts = pts.float().to(args.device).contiguous()
+        cls = cls.long().to(args.device).contiguous()
+        pts_nogt = pts_nogt.float().to(args.device).contiguous()
+
+        if fused and pts.shape == pts_nogt.shape:
+            if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
+                step = AdvTrainStep(model, model_D, pts.shape[0], pts.shape[1],
+                                    optimizer=optimizer, optimizer_D=optimizer_D,
+                                    lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
+                                    seed=int(getattr(args, "seed", 0)) + i_iter,
+                                    device=args.device)
+            losses = step(pts, cls, pts_nogt)
+            vals = losses.tolist() if (i_iter % log_every == 0) else None
+            if vals is not None:
+                loss_cls_value, loss_adv_value = vals[0], vals[1]
+                loss_D_value = vals[2] + vals[3]
+        else:
+            optimizer.zero_grad()
+            optimizer_D.zero_grad()
+            for param in model_D.parameters():
+                param.requires_grad = False
+            pred, global_gt, high_feat = model(pts)
+            l = cls_loss(pred, cls)
+            pred_gt_softmax = F.log_softmax(pred, dim=1)
+            pred_nogt, global_nogt, high_feat = model(pts_nogt)
+            pred_nogt_softmax = F.log_softmax(pred_nogt, dim=1)
+            D_out = model_D(pred_nogt_softmax)
+            loss_adv = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=False))
+            loss = args.lambda_cls * l + args.lambda_adv * loss_adv
+            loss.backward()
+            for param in model_D.parameters():
+                param.requires_grad = True
+            D_out = model_D(history_pool_gt.query(pred_gt_softmax.detach()))
+            loss_D1 = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=True)) * 0.5
+            loss_D1.backward()
+            D_out = model_D(history_pool_nogt.query(pred_nogt_softmax.detach()))
+            loss_D2 = gan_loss(D_out, make_D_label(D_out, nogt_label, args.device, random=True)) * 0.5
+            loss_D2.backward()
+            optimizer.step()
+            optimizer_D.step()
+            vals = True
+            loss_cls_value, loss_adv_value = l.item(), loss_adv.item()
+            loss_D_value = loss_D1.item() + loss_D2.item()
+
+        if vals is not None:
+            train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss_adv = {3:.3f} "
+                              "loss_D = {4:.3f}".format(i_iter, args.total_iterations,
+                                                        loss_cls_value, loss_adv_value,
+                                                        loss_D_value))
+            if getattr(args, "tensorboard", False) and writer is not None:
+                writer.add_scalar("Loss/train_cls", loss_cls_value, i_iter)
+                writer.add_scalar("Loss/train_adv", loss_adv_value, i_iter)
+                writer.add_scalar("Loss/train_disc", loss_D_value, i_iter)
+
+        if i_iter % args.iter_save_epoch == 0:
+            if step is not None:
+                step.sync_optimizer_state()
+            _save(model, model_D, args, "train_epoch_{}".format(i_iter // args.iter_save_epoch))
+        if i_iter % args.iter_test_epoch == 0:
+            curr_accu, _ = run_testing(testloader, model, cls_loss, test_logger, i_iter, writer, args)
+            if max_test_accu < curr_accu:
+                max_test_accu = curr_accu
+                max_train_epoch = i_iter // args.iter_test_epoch
+                _save(model, model_D, args, "train_best")
+
+    if step is not None:
+        step.sync_optimizer_state()
+    if getattr(args, "tensorboard", False) and writer is not None:
+        writer.close()
+    train_logger.info("Max test accuracy: {:.4f}".format(max_test_accu))
+    train_logger.info("Train model is at epoch: {}".format(max_train_epoch))
+    return max_test_accu
+
+
+def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, model, cls_loss,
+                              optimizer, train_logger, test_logger, writer, args):
+    """utils/trainer.py:222-308 (supervised baseline, no discriminator)."""
+    max_test_accu = float("-inf")
+    max_train_epoch = 0
+    for i_iter in range(args.total_iterations):
+        model.train()
+        optimizer.zero_grad()
+        batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
+        pts, cls = batch
+        pts, cls = pts.float().to(args.device), cls.long().to(args.device)
+        pred, global_gt, high_feat = model(pts)
+        l = cls_loss(pred, cls)
+        (args.lambda_cls * l).backward()
+        optimizer.step()
+        train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
+            i_iter, args.total_iterations, l.item(), 0.0))
+        if i_iter % args.iter_save_epoch == 0:
+            torch.save(model.state_dict(), os.path.join(
+                args.exp_dir, "model_train_epoch_{}.pth".format(i_iter // len(trainloader_gt))))
+        if i_iter % args.iter_test_epoch == 0:
+            curr_accu, _ = run_testing(testloader, model, cls_loss, test_logger, i_iter, writer, args)
+            if max_test_accu < curr_accu:
+                max_test_accu = curr_accu
+                max_train_epoch = i_iter // args.iter_test_epoch
+                torch.save(model.state_dict(), os.path.join(args.exp_dir, "model_train_best.pth"))
+    train_logger.info("Max test accuracy: {:.4f}".format(max_test_accu))
+    train_logger.info("Train model is at epoch: {}".format(max_train_epoch))
+    return max_test_accu

@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Throughput of the adversarial train step (utils/trainer.py:run_training, one
+iteration = :426-559) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-graph] [--no-cpu]
+
+Workload (BASELINE.json configs[2]): PointNetCls(k=40) + DeepConvDiscNet(40,1),
+B=32 labelled + B=32 unlabelled ModelNet40-shaped clouds of N=1024 points per
+GPU per step, fp32, Adam on both networks.  Synthetic seeded inputs
+(U(-1,1) points, labels in [0,40)), resident in HBM before timing starts.
+metric value = whole-job clouds/s counting 2B clouds per step per rank.
+For --gpus N > 1 run under torch.distributed.run: one process per GPU, each
+rank takes its own shard of the global batch and gradients are averaged with
+an RCCL all-reduce (multi-GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+B, N = 32, 1024
+POOL = 4  # distinct resident input batches cycled by the timed loop
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def make_models(dev, seed=0):
+    import adversarial_learning_on_pointclouds_amd as pc
+    torch.manual_seed(seed)
+    model = pc.PointNetCls(k=40).to(dev)
+    model_D = pc.DeepConvDiscNet(40, 1).to(dev)
+    from adversarial_learning_on_pointclouds_amd.model_utils import init_weights
+    init_weights(model_D, "xavier", verbose=False)
+    return model, model_D
+
+
+def cpu_baseline(seconds):
+    """The numpy oracle's adversarial step on a bounded sample of the same
+    workload (B=32, N=1024), timed on this host's cores."""
+    from oracle import pointnet_np as onp
+    G = onp.make_params(onp.cls_spec(40), seed=3)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=4, init="xavier")
+    oG, oD = onp.Adam(G), onp.Adam(D)
+    rng = np.random.default_rng(1000)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+    onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2)  # warm-up
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2)
+        steps += 1
+        if time.perf_counter() - t0 >= seconds and steps >= 2:
+            break
+    dt = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"value": round(2 * B * steps / dt, 2), "unit": "clouds/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N=1024, fp32) in {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=dev)
+        dist = tdist
+
+    from adversarial_learning_on_pointclouds_amd import ops
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+    from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
+
+    model, model_D = make_models(dev, seed=0)
+    step = AdvTrainStep(model, model_D, B, N, seed=1234 + rank, device=dev)
+    runner = DataParallelAdvStep(step) if dist is not None else None
+
+    # resident synthetic inputs: rank-specific shards of the global batch
+    pool = []
+    for k in range(POOL):
+        rng = np.random.default_rng(1000 + k * 64 + rank)
+        pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
+                     torch.from_numpy(rng.integers(0, 40, B)).to(dev),
+                     torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev)))
+    use_graph = not args.no_graph
+    graphs = []
+    if use_graph:
+        if runner is not None:
+            graphs = [runner.capture(*pool[k]) for k in range(POOL)]
+        else:
+            graphs = [step.capture_on(*pool[k]) for k in range(POOL)]
+
+    def one(k):
+        if use_graph:
+            graphs[k % POOL].replay()
+        elif runner is not None:
+            runner(*pool[k % POOL])
+        else:
+            step(*pool[k % POOL])
+
+    for k in range(args.warmup):
+        one(k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one(k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    losses = step.losses.cpu().numpy().tolist()
+    finite = all(np.isfinite(losses))
+
+    # dominant kernel (conv4 + max, k_conv_max128): HIP events on the stream it
+    # is launched on, same inputs as the step (x3 of the last step)
+    x3 = step.saved_x3()
+    w4, b4 = model.feat.conv4.weight, model.feat.conv4.bias
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        ops.conv_max_fwd(x3, w4, b4)
+    reps = 50
+    ev0.record()
+    for _ in range(reps):
+        ops.conv_max_fwd(x3, w4, b4)
+    ev1.record()
+    torch.cuda.synchronize()
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
+    flops = 2.0 * (2 * B) * N * 1024 * 128
+    achieved = flops / kern_s / 1e12
+
+    result = {
+        "metric": "point-clouds/sec (adv train step), B=32 N=1024 ModelNet40, 1/2/4/8 GPU",
+        "value": round(2 * B * args.steps * world / dt, 1),
+        "unit": "clouds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
+        "config": {"workload": "adversarial cls step: PointNetCls(k=40)+DeepConvDiscNet(40,1), "
+                               "B=32 GT + 32 noGT clouds/GPU, N=1024, Adam x2",
+                   "global_batch": 2 * B * world, "points": N,
+                   "parallelism": f"dp{world}", "hip_graph": use_graph},
+        "roofline": {"bound": "mfma", "kernel": "k_conv_max128 (conv4 128->1024 + max/argmax)",
+                     "achieved": round(achieved, 2), "peak": 157.3, "unit": "TFLOP/s",
+                     "frac": round(achieved / 157.3, 4), "traffic": None,
+                     "avg_launch_us": round(kern_s * 1e6, 2),
+                     "algorithmic_flops_per_launch": flops},
+        "losses_last_step": [round(v, 5) for v in losses],
+        "finite": finite,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

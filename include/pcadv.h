@@ -1,0 +1,184 @@
+/*
+ * pcadv — MI355X-native (gfx950) PointNet adversarial-training hot path.
+ *
+ * C ABI of libpcadv.so.  Plain pointers and sizes only: every pointer is HIP
+ * device memory owned by the caller (the library never allocates, frees or
+ * retains a pointer past the call), every call is enqueued on `stream` without
+ * a host sync and is safe to capture into a hipGraph.  Return value: PCADV_OK
+ * or a negative error code; pcadv_last_error() then describes it
+ * (thread-local).  No C++ exception crosses this boundary.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo root,
+ * YiruS/Adversarial_Learning_on_PointClouds):
+ *   pcadv_feat_fwd / pcadv_feat_bwd  <- PointNetfeat.forward + autograd
+ *                                       (models/pointnet.py:81-137; called from
+ *                                        PointNetCls.forward :197-203)
+ *   pcadv_conv_max_fwd               <- Conv1d(128->1024,1) + torch.max(dim=2)
+ *                                       (models/pointnet.py:89,128-130; STN3d/STNkd
+ *                                        :19,30-31 with relu before the max)
+ *   pcadv_linear_fwd / _bwd          <- nn.Linear / 1x1 Conv1d on Bx Cx1 with
+ *                                       ReLU / LeakyReLU(0.2) / Dropout
+ *                                       (models/pointnet.py:191-202,
+ *                                        models/discriminator.py:30-51)
+ *   pcadv_adam                       <- torch.optim.Adam step
+ *                                       (train_classification.py:110-122,
+ *                                        utils/trainer.py:558-559)
+ *   pcadv_adv_step                   <- one iteration of utils/trainer.py:run_training
+ *                                       (:426-559) incl. the losses of
+ *                                       train_classification.py:199-200 and
+ *                                       make_D_label (utils/utils.py:22-31)
+ *
+ * Layouts: point clouds are B x N x 3 f32 exactly as PointNetCls receives them
+ * (no transpose copy); activations are point-major [cloud][point][channel];
+ * weights are the reference's [out][in] (Conv1d [out,in,1] reinterpreted).
+ * Parameters of the fused step live in one flat f32 buffer per network in
+ * state_dict order (offsets below).
+ */
+#ifndef PCADV_H
+#define PCADV_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCADV_OK 0
+#define PCADV_EINVAL (-1)
+#define PCADV_EHIP (-2)
+
+#define PCADV_ACT_NONE 0
+#define PCADV_ACT_RELU 1
+#define PCADV_ACT_LRELU 2 /* LeakyReLU(negative_slope=0.2), discriminator.py:39 */
+
+/* channel widths of the cls generator (models/pointnet.py:86-89,191-193) */
+#define PCADV_C1 64
+#define PCADV_C2 64
+#define PCADV_C3 128
+#define PCADV_C4 1024
+
+/* flat parameter layout of PointNetCls(k=40) in state_dict order */
+enum {
+  PCADV_G_CONV1_W = 0, PCADV_G_CONV1_B = 192,
+  PCADV_G_CONV2_W = 256, PCADV_G_CONV2_B = 4352,
+  PCADV_G_CONV3_W = 4416, PCADV_G_CONV3_B = 12608,
+  PCADV_G_CONV4_W = 12736, PCADV_G_CONV4_B = 143808,
+  PCADV_G_FC1_W = 144832, PCADV_G_FC1_B = 669120,
+  PCADV_G_FC2_W = 669632, PCADV_G_FC2_B = 800704,
+  PCADV_G_FC3_W = 800960, PCADV_G_FC3_B = 811200,
+  PCADV_G_NUMEL = 811240
+};
+/* flat parameter layout of DeepConvDiscNet(40, 1) in state_dict order */
+enum {
+  PCADV_D_CONV1_W = 0, PCADV_D_CONV1_B = 20480,
+  PCADV_D_CONV2_W = 20992, PCADV_D_CONV2_B = 152064,
+  PCADV_D_CONV3_W = 152320, PCADV_D_CONV3_B = 217856,
+  PCADV_D_CONV4_W = 218112, PCADV_D_CONV4_B = 234496,
+  PCADV_D_CONV5_W = 234560, PCADV_D_CONV5_B = 238656,
+  PCADV_D_FC_W = 238720, PCADV_D_FC_B = 238784,
+  PCADV_D_NUMEL = 238785
+};
+
+const char* pcadv_last_error(void);
+int pcadv_abi_version(void);
+
+/* ---- PointNetfeat (feature_transform=False) -------------------------------
+ * pts [C][N][3]; w1 [64][3], w2 [64][64], w3 [128][64], w4 [1024][128] + biases.
+ * Saves x1,x2 [C][N][64] and x3 [C][N][128] (post-ReLU) for the backward and
+ * writes gmax [C][1024] (x_global, pointnet.py:129-130) and gidx [C][1024]
+ * (argmax over points, first index on ties as torch.max on CPU). */
+int pcadv_feat_fwd(const float* pts, int C, int N,
+                   const float* w1, const float* b1, const float* w2, const float* b2,
+                   const float* w3, const float* b3, const float* w4, const float* b4,
+                   float* x1, float* x2, float* x3, float* gmax, int32_t* gidx,
+                   hipStream_t stream);
+
+/* Bytes of workspace pcadv_feat_bwd needs for C clouds of N points. */
+size_t pcadv_feat_bwd_workspace_bytes(int C, int N);
+
+/* Autograd of pcadv_feat_fwd: dgmax [C][1024] -> dw1..db4 (overwritten).
+ * The max-pool backward is sparse (each channel's gradient goes to its argmax
+ * point), equal to torch's MaxBackward for unique maxima. */
+int pcadv_feat_bwd(const float* dgmax, const int32_t* gidx, const float* pts, int C, int N,
+                   const float* w2, const float* w3, const float* w4,
+                   const float* x1, const float* x2, const float* x3,
+                   float* dw1, float* db1, float* dw2, float* db2,
+                   float* dw3, float* db3, float* dw4, float* db4,
+                   void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* Generic 1x1-conv (K=128 -> O, O % 128 == 0) + max over points.
+ * relu_before_max=1 for the T-Nets (pointnet.py:30-31,63-64). */
+int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, const float* b,
+                       int O, int relu_before_max, float* gmax, int32_t* gidx,
+                       hipStream_t stream);
+
+/* ---- linear / 1x1 conv on B x C x 1 ----------------------------------------
+ * y[M][Nout] = act(s * (x[M][K] w[Nout][K]^T + b)), where s is the dropout
+ * scale: drop_mask[M][Nout] in {0,1} times 1/(1-drop_p) when drop_mask is
+ * non-NULL, else a device Philox draw keyed by (rng_seed, *rng_step) when
+ * rng_step is non-NULL, else 1.  K % 4 == 0. */
+int pcadv_linear_fwd(const float* x, const float* w, const float* b, float* y,
+                     int M, int Nout, int K, int act,
+                     const float* drop_mask, const int32_t* rng_step, uint64_t rng_seed,
+                     float drop_p, hipStream_t stream);
+
+/* Backward of pcadv_linear_fwd.  dz = dy * act'(y) * s (y = the forward output).
+ * dx[M][K] = dz w (skipped when dx is NULL); dw[Nout][K] = sum over the first
+ * m_w rows of dz^T x, db[Nout] likewise (skipped when dw is NULL). */
+int pcadv_linear_bwd(const float* dy, const float* y, int act,
+                     const float* drop_mask, const int32_t* rng_step, uint64_t rng_seed,
+                     float drop_p, const float* x, const float* w,
+                     float* dx, float* dw, float* db, int M, int m_w, int Nout, int K,
+                     hipStream_t stream);
+
+/* ---- Adam (torch.optim.Adam semantics, amsgrad=False, weight_decay=0) ------
+ * step_count: device int32, incremented by this call (t = *step_count + 1). */
+int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+               int64_t n, int32_t* step_count, float lr, float beta1, float beta2,
+               float eps, hipStream_t stream);
+
+/* ---- the fused adversarial step (utils/trainer.py:426-559) -------------------
+ * B clouds of N points per loader.  Stochastic inputs: when drop_mask_gt /
+ * drop_mask_nogt ([B][256] {0,1}) or soft_gt / soft_nogt ([B]) are NULL they are
+ * drawn on device from Philox keyed by (rng_seed, *step_count), so a captured
+ * graph draws fresh values each replay. */
+typedef struct pcadv_adv_args {
+  int B, N;
+  /* inputs */
+  const float* pts_gt;      /* [B][N][3] */
+  const int64_t* labels;    /* [B] class ids in [0,40) */
+  const float* pts_nogt;    /* [B][N][3] */
+  const float* drop_mask_gt, * drop_mask_nogt;
+  const float* soft_gt, * soft_nogt;
+  /* generator: flat params / grads / Adam moments (PCADV_G_NUMEL floats) */
+  float* g_param, * g_grad, * g_m, * g_v;
+  /* discriminator (PCADV_D_NUMEL floats) */
+  float* d_param, * d_grad, * d_m, * d_v;
+  int32_t* step_count;      /* device: completed steps (shared by both Adams) */
+  float lr_g, lr_d, beta1, beta2, eps;
+  float lambda_cls, lambda_adv, drop_p;
+  uint64_t rng_seed;
+  int apply_adam;           /* 0: stop after the gradients (parity tests) */
+  /* outputs */
+  float* losses;            /* [4]: loss_cls, loss_adv, loss_D_gt, loss_D_nogt */
+  float* logits;            /* [2B][40] or NULL */
+  /* scratch */
+  void* workspace;
+  size_t workspace_bytes;
+} pcadv_adv_args;
+
+size_t pcadv_adv_step_workspace_bytes(int B, int N);
+int pcadv_adv_step(const pcadv_adv_args* args, hipStream_t stream);
+
+/* The two Adam updates of pcadv_adv_step alone (optimizer.step() and
+ * optimizer_D.step(), trainer.py:558-559), for a step that ran with
+ * apply_adam = 0 and whose gradients were then all-reduced across ranks.
+ * Uses the step counter already advanced by that pcadv_adv_step. */
+int pcadv_adv_step_adam(const pcadv_adv_args* args, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCADV_H */

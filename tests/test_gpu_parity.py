@@ -1,0 +1,310 @@
+"""HIP-path parity: libpcadv.so (through its C ABI) vs the numpy oracle and the
+golden vectors captured from the reference.  Runs on an MI355X only.
+
+Tolerance (north_star): max|a - ref| / max(1, max|ref|) <= 1e-3 in fp32; the
+kernels compute in exact f32 (f32 MFMA / FMA) so most checks use 1e-4.
+argmax must match exactly except at near-ties (|v_ours - v_ref| <= 1e-5 * scale).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pointnet_np as onp
+from golden_util import check_tensor, load, rel_err
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import ops
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+
+DEV = "cuda"
+TOL = 1e-3
+
+
+def _t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def _pts(seed, B, N):
+    return np.random.default_rng(seed).uniform(-1, 1, (B, N, 3)).astype(np.float32)
+
+
+def _load(module, params):
+    module.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in params.items()})
+    return module.to(DEV)
+
+
+def _argmax_ok(am, am_ref, x3, W4, b4):
+    """Exact argmax except at near-ties (values within 1e-5 relative)."""
+    bad = np.argwhere(am != am_ref)
+    for c, o in bad:
+        v1 = x3[c, am[c, o]] @ W4[o] + b4[o]
+        v2 = x3[c, am_ref[c, o]] @ W4[o] + b4[o]
+        assert abs(v1 - v2) <= 1e-5 * max(1.0, abs(v2)), (c, o, v1, v2)
+    return len(bad)
+
+
+# ---------------------------------------------------------------------------
+# PointNetfeat forward / backward kernels
+# ---------------------------------------------------------------------------
+
+def _feat_weights(G):
+    names = ["feat.conv1.weight", "feat.conv1.bias", "feat.conv2.weight", "feat.conv2.bias",
+             "feat.conv3.weight", "feat.conv3.bias", "feat.conv4.weight", "feat.conv4.bias"]
+    return [_t(G[n]) for n in names]
+
+
+@pytest.mark.parametrize("C,N", [(4, 1024), (64, 1024), (3, 1000), (2, 2500), (1, 64), (2, 37)])
+def test_feat_fwd_vs_oracle(C, N):
+    G = onp.make_params(onp.cls_spec(40), seed=7)
+    pts = _pts(100 + C + N, C, N)
+    gmax, gidx, (x1, x2, x3) = ops.feat_fwd(_t(pts), *_feat_weights(G))
+    torch.cuda.synchronize()
+    r1, r2, r3 = onp.point_mlp_fwd(pts, G)
+    W4, b4 = G["feat.conv4.weight"][:, :, 0], G["feat.conv4.bias"]
+    rg, ra = onp.conv_max_fwd(r3, W4, b4)
+    assert rel_err(x1.cpu().numpy(), r1) < 1e-5
+    assert rel_err(x2.cpu().numpy(), r2) < 1e-5
+    assert rel_err(x3.cpu().numpy(), r3) < 1e-5
+    assert rel_err(gmax.cpu().numpy(), rg) < 1e-5
+    _argmax_ok(gidx.cpu().numpy(), ra, r3, W4, b4)
+
+
+def test_feat_fwd_golden_g1():
+    fx = load("g1_cls_fwd.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    pts = _pts(int(fx["pts_seed"]), int(fx["B"]), int(fx["N"]))
+    gmax, gidx, _ = ops.feat_fwd(_t(pts), *_feat_weights(G))
+    assert rel_err(gmax.cpu().numpy(), fx["gmax"]) < 1e-5
+    assert (gidx.cpu().numpy() == fx["argmax"]).all()
+
+
+def test_argmax_ties_first_index():
+    """Identical points tie on every channel: torch.max returns index 0."""
+    G = onp.make_params(onp.cls_spec(40), seed=8)
+    pts = np.repeat(_pts(5, 2, 1), 300, axis=1)
+    pts[1, 150:] = pts[1, 0] * 0.5  # second cloud: two distinct values, ties inside each
+    _, gidx, _ = ops.feat_fwd(_t(pts), *_feat_weights(G))
+    _, ra = onp.conv_max_fwd(onp.point_mlp_fwd(pts, G)[2], G["feat.conv4.weight"][:, :, 0],
+                             G["feat.conv4.bias"])
+    assert (gidx.cpu().numpy()[0] == 0).all()
+    assert (gidx.cpu().numpy() == ra).all()
+
+
+@pytest.mark.parametrize("C,N", [(4, 1024), (64, 1024), (3, 1000), (2, 300)])
+def test_feat_bwd_vs_oracle(C, N):
+    G = onp.make_params(onp.cls_spec(40), seed=9)
+    pts = _pts(200 + C, C, N)
+    dg = np.random.default_rng(3).normal(0, 1e-2, (C, 1024)).astype(np.float32)
+    w = _feat_weights(G)
+    gmax, gidx, (x1, x2, x3) = ops.feat_fwd(_t(pts), *w)
+    grads = ops.feat_bwd(_t(dg), gidx, _t(pts), w[2], w[4], w[6], x1, x2, x3)
+    torch.cuda.synchronize()
+    # oracle with the same (verified) argmax
+    r1, r2, r3 = onp.point_mlp_fwd(pts, G)
+    W4 = G["feat.conv4.weight"][:, :, 0]
+    _, ra = onp.conv_max_fwd(r3, W4, G["feat.conv4.bias"])
+    assert _argmax_ok(gidx.cpu().numpy(), ra, r3, W4, G["feat.conv4.bias"]) == 0
+    dW4, db4, dX3 = onp.conv_max_bwd(dg, ra, r3, W4)
+    B_, N_ = C, N
+    dz3 = (dX3 * (r3 > 0)).reshape(B_ * N_, -1)
+    dz2 = (dz3 @ G["feat.conv3.weight"][:, :, 0]) * (r2.reshape(B_ * N_, -1) > 0)
+    dz1 = (dz2 @ G["feat.conv2.weight"][:, :, 0]) * (r1.reshape(B_ * N_, -1) > 0)
+    ref = [dz1.T @ pts.reshape(-1, 3), dz1.sum(0), dz2.T @ r1.reshape(B_ * N_, -1), dz2.sum(0),
+           dz3.T @ r2.reshape(B_ * N_, -1), dz3.sum(0), dW4, db4]
+    for g, r in zip(grads, ref):
+        e = rel_err(g.cpu().numpy().reshape(r.shape), r)
+        assert e < 1e-5, e
+
+
+def test_feat_bwd_deterministic():
+    G = onp.make_params(onp.cls_spec(40), seed=10)
+    pts = _pts(11, 8, 1024)
+    dg = _t(np.random.default_rng(4).normal(0, 1, (8, 1024)).astype(np.float32))
+    w = _feat_weights(G)
+    _, gidx, xs = ops.feat_fwd(_t(pts), *w)
+    a = ops.feat_bwd(dg, gidx, _t(pts), w[2], w[4], w[6], *xs)
+    b = ops.feat_bwd(dg, gidx, _t(pts), w[2], w[4], w[6], *xs)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+# ---------------------------------------------------------------------------
+# linear kernels vs a plain torch fp32 reference
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("M,N,K,act", [(64, 512, 1024, 1), (96, 1, 64, 0), (96, 512, 40, 2),
+                                       (5, 40, 256, 0), (33, 77, 12, 2)])
+def test_linear_vs_torch(M, N, K, act):
+    g = torch.Generator().manual_seed(M * 1000 + N + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    mask = (torch.rand(M, N, generator=g) >= 0.3).float()
+    dy = torch.randn(M, N, generator=g)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    z = (xr @ wr.T + br) * (mask / 0.7)
+    yr = torch.relu(z) if act == 1 else (torch.nn.functional.leaky_relu(z, 0.2) if act == 2 else z)
+    yr.backward(dy)
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), act, mask.to(DEV), 0.3)
+    dx, dw, db = ops.linear_bwd(dy.to(DEV), y, act, mask.to(DEV), 0.3, x.to(DEV), w.to(DEV))
+    assert rel_err(y.cpu().numpy(), yr.detach().numpy()) < 1e-5
+    assert rel_err(dx.cpu().numpy(), xr.grad.numpy()) < 1e-5
+    assert rel_err(dw.cpu().numpy(), wr.grad.numpy()) < 1e-5
+    assert rel_err(db.cpu().numpy(), br.grad.numpy()) < 1e-5
+
+
+# ---------------------------------------------------------------------------
+# drop-in modules vs the reference's golden vectors
+# ---------------------------------------------------------------------------
+
+def test_cls_module_golden_g1_g2():
+    fx1 = load("g1_cls_fwd.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=1)
+    model = _load(pc.PointNetCls(k=40), G).eval()
+    pts = _t(_pts(11, 4, 1024))
+    with torch.no_grad():
+        logits, glob, tf = model(pts)
+    assert tf is None and glob.shape == (4, 1024, 1)
+    assert rel_err(logits.cpu().numpy(), fx1["logits"]) < 1e-4
+    fx2 = load("g2_cls_bwd.npz")
+    model.train()
+    model.dropout_masks = [torch.from_numpy(fx2["mask"])]
+    logits, _, _ = model(pts)
+    loss = torch.nn.CrossEntropyLoss()(logits, torch.from_numpy(fx2["labels"]).to(DEV))
+    loss.backward()
+    assert abs(loss.item() - float(fx2["loss"])) < 1e-4
+    for name, p in model.named_parameters():
+        check_tensor(fx2, "grad." + name, p.grad.cpu().numpy(), tol=1e-4)
+
+
+def test_disc_module_golden_g4():
+    fx = load("g4_disc.npz")
+    D = onp.make_params(onp.disc_spec(40, 1), seed=2, init="xavier")
+    md = _load(pc.DeepConvDiscNet(40, 1), D)
+    x = _t(fx["x"]).requires_grad_(True)
+    out = md(x)
+    out.backward(_t(fx["dout"]))
+    assert rel_err(out.detach().cpu().numpy(), fx["out"]) < 1e-5
+    assert rel_err(x.grad.cpu().numpy(), fx["dx"]) < 1e-5
+    for name, p in md.named_parameters():
+        check_tensor(fx, "grad." + name, p.grad.cpu().numpy(), tol=1e-5)
+
+
+# ---------------------------------------------------------------------------
+# the fused adversarial step
+# ---------------------------------------------------------------------------
+
+def _adv_inputs(fx):
+    rng = np.random.default_rng(int(fx["data_seed"]))
+    B, N, iters = int(fx["B"]), int(fx["N"]), int(fx["iters"])
+    out = []
+    for _ in range(iters):
+        pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+        lab = rng.integers(0, 40, B)
+        pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+        m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+        m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+        y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+        y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+        out.append((pg, lab, pn, m1, m2, y1, y2))
+    return out
+
+
+def _make_step(B, N, g_seed=1, d_seed=2, seed=0):
+    model = _load(pc.PointNetCls(k=40), onp.make_params(onp.cls_spec(40), seed=g_seed))
+    model_D = _load(pc.DeepConvDiscNet(40, 1),
+                    onp.make_params(onp.disc_spec(40, 1), seed=d_seed, init="xavier"))
+    return AdvTrainStep(model, model_D, B, N, seed=seed), model, model_D
+
+
+@pytest.mark.parametrize("name", ["g3_adv_step1.npz", "g3_adv_step3.npz"])
+def test_adv_step_golden_g3(name):
+    fx = load(name)
+    step, model, model_D = _make_step(int(fx["B"]), int(fx["N"]))
+    for i, (pg, lab, pn, m1, m2, y1, y2) in enumerate(_adv_inputs(fx)):
+        losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                      soft=(_t(y1), _t(y2))).cpu().numpy()
+        assert abs(losses[0] - fx["loss_cls"][i]) < 1e-4
+        assert abs(losses[1] - fx["loss_adv"][i]) < 1e-4
+        assert abs(losses[2] - fx["loss_D_gt"][i]) < 1e-4
+        assert abs(losses[3] - fx["loss_D_nogt"][i]) < 1e-4
+        if int(fx["iters"]) == 1:
+            for nm, p in model.named_parameters():
+                check_tensor(fx, "gradG." + nm, p.grad.cpu().numpy(), tol=1e-4)
+            for nm, p in model_D.named_parameters():
+                check_tensor(fx, "gradD." + nm, p.grad.cpu().numpy(), tol=1e-4)
+    for nm, p in model.named_parameters():
+        check_tensor(fx, "paramG." + nm, p.detach().cpu().numpy(), tol=1e-5)
+    for nm, p in model_D.named_parameters():
+        check_tensor(fx, "paramD." + nm, p.detach().cpu().numpy(), tol=1e-5)
+
+
+def test_adv_step_full_size_vs_oracle():
+    """Bench configuration (B=32, N=1024): one step, gradients vs the oracle."""
+    B, N = 32, 1024
+    step, model, model_D = _make_step(B, N, g_seed=3, d_seed=4)
+    rng = np.random.default_rng(1000)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+    G = onp.make_params(onp.cls_spec(40), seed=3)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=4, init="xavier")
+    oG, oD = onp.Adam(G), onp.Adam(D)
+    losses_ref, gG, gD, aux = onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2)
+    losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                  soft=(_t(y1), _t(y2))).cpu().numpy()
+    for i, k in enumerate(["loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt"]):
+        assert abs(losses[i] - losses_ref[k]) < 1e-4, (k, losses[i], losses_ref[k])
+    gl = step.logits.cpu().numpy()
+    assert rel_err(gl[:B], aux["logits_gt"]) < 1e-4
+    assert rel_err(gl[B:], aux["logits_nogt"]) < 1e-4
+    for nm, p in model.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), gG[nm]) < TOL, nm
+        assert rel_err(p.detach().cpu().numpy(), G[nm]) < 1e-5, nm
+    for nm, p in model_D.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), gD[nm]) < TOL, nm
+        assert rel_err(p.detach().cpu().numpy(), D[nm]) < 1e-5, nm
+
+
+def test_adv_step_graph_replay_matches_eager():
+    B, N = 8, 1024
+    s1, m1, _ = _make_step(B, N, seed=77)
+    s2, m2, _ = _make_step(B, N, seed=77)
+    rng = np.random.default_rng(5)
+    pg, pn = _t(_pts(1, B, N)), _t(_pts(2, B, N))
+    lab = _t(rng.integers(0, 40, B), torch.int64)
+    st = s2.capture()
+    for _ in range(3):
+        st[0].copy_(pg)
+        st[1].copy_(lab)
+        st[2].copy_(pn)
+        l2 = s2.replay().clone()
+        l1 = s1(pg, lab, pn).clone()
+        assert torch.equal(l1, l2)
+    assert torch.equal(s1.g_param, s2.g_param)
+    assert torch.equal(s1.d_param, s2.d_param)
+    assert int(s1.step_count.item()) == 3
+
+
+def test_device_rng_dropout_and_labels_statistics():
+    """Device Philox draws: keep rate 0.7, labels inside U(0.7,1.05) / U(0,0.305)."""
+    B, N = 32, 256
+    step, _, _ = _make_step(B, N, seed=123)
+    x = torch.ones(2 * B, 256, device=DEV)
+    w = torch.eye(256, device=DEV)
+    b = torch.zeros(256, device=DEV)
+    from adversarial_learning_on_pointclouds_amd import _lib as L
+    y = torch.empty_like(x)
+    cnt = torch.tensor([5], device=DEV, dtype=torch.int32)
+    L.check(L.load().pcadv_linear_fwd(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), 2 * B, 256, 256, 0,
+                                      None, L.ptr(cnt), 99, 0.3, L.stream_ptr()), "linear")
+    keep = (y > 0).float().mean().item()
+    assert abs(keep - 0.7) < 0.03
+    assert torch.allclose(y[y > 0], torch.full_like(y[y > 0], 1 / 0.7))
