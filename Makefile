@@ -28,3 +28,10 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all asm clean
+
+# diagnostic build with per-phase timestamps (never loaded by the product path)
+STAMPS_LIB := build/stamps/libpcadv_stamps.so
+stamps: $(SRC) $(HDR)
+	@mkdir -p build/stamps
+	$(HIPCC) $(HIPFLAGS) -DPCADV_STAMPS -shared -o $(STAMPS_LIB) $(SRC)
+.PHONY: stamps

@@ -73,9 +73,10 @@ class AdvArgs(ctypes.Structure):
 SIGNATURES = {
     "pcadv_last_error": (ctypes.c_char_p, []),
     "pcadv_abi_version": (_i, []),
-    "pcadv_feat_fwd": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 5 + [_vp]),
+    "pcadv_feat_fwd_workspace_bytes": (_sz, [_i, _i]),
+    "pcadv_feat_fwd": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 3 + [_vp, _sz, _vp]),
     "pcadv_feat_bwd_workspace_bytes": (_sz, [_i, _i]),
-    "pcadv_feat_bwd": (_i, [_vp, _vp, _vp, _i, _i] + [_vp] * 6 + [_vp] * 8 + [_vp, _sz, _vp]),
+    "pcadv_feat_bwd": (_i, [_vp, _vp, _vp, _i, _i] + [_vp] * 7 + [_vp] * 8 + [_vp, _sz, _vp]),
     "pcadv_conv_max_fwd": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_linear_fwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _u64, _f, _vp]),
     "pcadv_linear_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _u64, _f, _vp, _vp, _vp, _vp, _vp,

@@ -25,8 +25,13 @@ int launch_conv_max128(const float*, int, int, const float*, const float*, int, 
 size_t feat_bwd_workspace_bytes(int C, int N);
 int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
                     const float*, const float*, const float*, const float*, const float*,
-                    const float*, float*, float*, float*, float*, float*, float*, float*, float*,
-                    void*, size_t, hipStream_t);
+                    const float*, const float*, float*, float*, float*, float*, float*, float*,
+                    float*, float*, void*, size_t, hipStream_t);
+size_t feat_fwd_workspace_bytes(int C, int N);
+int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
+                          const float*, const float*, const float*, const float*, const float*,
+                          const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
+                          hipStream_t, uint64_t* stamps = nullptr, int stagger = 20);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t);
 int launch_linear_bwd(const float*, const float*, int, const float*, const int32_t*, uint64_t,
@@ -44,7 +49,7 @@ int launch_inc(int32_t*, hipStream_t);
 
 // ---- workspace carve for the fused step ------------------------------------
 struct StepWs {
-  float *x1, *x2, *x3, *gmax, *h1, *h2, *logits, *dlogits, *dh2, *dh1, *dgmax;
+  float *x3, *gmax, *h1, *h2, *logits, *dlogits, *dh2, *dh1, *dgmax;
   float *din, *d1, *d2, *d3, *d4, *d5, *dout;
   float *ddout, *dd5, *dd4, *dd3, *dd2, *dd1, *ddin;
   float *mask;
@@ -65,9 +70,7 @@ static StepWs carve(int B, int N, char* base) {
     off += align_up(nfloat * sizeof(float));
     return reinterpret_cast<float*>(p);
   };
-  w.x1 = take(C * N * 64);
-  w.x2 = take(C * N * 64);
-  w.x3 = take(C * N * 128);
+  w.x3 = take(C * N * 128);  // first: Python's saved_x3() views offset 0
   w.gmax = take(C * 1024);
   w.gidx = reinterpret_cast<int32_t*>(take(C * 1024));
   w.h1 = take(C * 512);
@@ -93,6 +96,8 @@ static StepWs carve(int B, int N, char* base) {
   w.ddin = take(R * 40);
   w.mask = take(C * 256);
   w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
+  if (feat_fwd_workspace_bytes((int)C, N) > w.feat_ws_bytes)
+    w.feat_ws_bytes = feat_fwd_workspace_bytes((int)C, N);
   w.feat_ws = take(w.feat_ws_bytes / sizeof(float) + 1);
   w.total = off;
   return w;
@@ -140,12 +145,11 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   const int32_t* rstep = mask ? nullptr : st;
 
   // ---- generator forward, both loaders in one launch (:468, :490) ----------
-  PC_TRY(launch_point_mlp3(a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
-                           G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
-                           G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, w.x1, w.x2, w.x3,
-                           a->step_count, s));
-  PC_TRY(launch_conv_max128(w.x3, C, N, G + PCADV_G_CONV4_W, G + PCADV_G_CONV4_B, 1024, false,
-                            w.gmax, w.gidx, s));
+  PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
+                               G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                               G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
+                               G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
+                               w.feat_ws, w.feat_ws_bytes, s));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
@@ -202,8 +206,9 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
   // ---- PointNetfeat backward (sparse max-pool) -----------------------------
-  PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV2_W,
-                         G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x1, w.x2, w.x3,
+  PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
+                         G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                         G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
@@ -222,26 +227,38 @@ extern "C" {
 const char* pcadv_last_error(void) { return g_err; }
 int pcadv_abi_version(void) { return 1; }
 
+size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
+
 int pcadv_feat_fwd(const float* pts, int C, int N, const float* w1, const float* b1,
                    const float* w2, const float* b2, const float* w3, const float* b3,
-                   const float* w4, const float* b4, float* x1, float* x2, float* x3,
-                   float* gmax, int32_t* gidx, hipStream_t stream) {
-  PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
-  PC_TRY(launch_point_mlp3(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, x1, x2, x3, nullptr,
-                           stream));
-  return launch_conv_max128(x3, C, N, w4, b4, PCADV_C4, false, gmax, gidx, stream);
+                   const float* w4, const float* b4, float* x3, float* gmax, int32_t* gidx,
+                   void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
+                               nullptr, workspace, workspace_bytes, stream);
 }
+
+#ifdef PCADV_STAMPS
+// diagnostic build only: pcadv_feat_fwd with per-workgroup phase timestamps
+int pcadv_feat_fwd_stamped(const float* pts, int C, int N, const float* w1, const float* b1,
+                           const float* w2, const float* b2, const float* w3, const float* b3,
+                           const float* w4, const float* b4, float* x3, float* gmax,
+                           int32_t* gidx, void* workspace, size_t workspace_bytes,
+                           uint64_t* stamps, int stagger, hipStream_t stream) {
+  return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
+                               nullptr, workspace, workspace_bytes, stream, stamps, stagger);
+}
+#endif
 
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_workspace_bytes(C, N); }
 
 int pcadv_feat_bwd(const float* dgmax, const int32_t* gidx, const float* pts, int C, int N,
-                   const float* w2, const float* w3, const float* w4, const float* x1,
-                   const float* x2, const float* x3, float* dw1, float* db1, float* dw2,
-                   float* db2, float* dw3, float* db3, float* dw4, float* db4, void* workspace,
-                   size_t workspace_bytes, hipStream_t stream) {
+                   const float* w1, const float* b1, const float* w2, const float* b2,
+                   const float* w3, const float* w4, const float* x3, float* dw1, float* db1,
+                   float* dw2, float* db2, float* dw3, float* db3, float* dw4, float* db4,
+                   void* workspace, size_t workspace_bytes, hipStream_t stream) {
   PC_REQUIRE(C > 0 && N > 0, "feat_bwd: bad shape C=%d N=%d", C, N);
-  return launch_feat_bwd(dgmax, gidx, pts, pts, C, C, N, w2, w3, w4, x1, x2, x3, dw1, db1, dw2,
-                         db2, dw3, db3, dw4, db4, workspace, workspace_bytes, stream);
+  return launch_feat_bwd(dgmax, gidx, pts, pts, C, C, N, w1, b1, w2, b2, w3, w4, x3, dw1, db1,
+                         dw2, db2, dw3, db3, dw4, db4, workspace, workspace_bytes, stream);
 }
 
 int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, const float* b, int O,

@@ -8,28 +8,34 @@
 // cloud) carry gradient into conv3..conv1, so k_feat_bwd_chunk compacts them
 // and runs the conv3/conv2/conv1 backward (f32 MFMA) on active rows only.
 //
-// k_feat_bwd_chunk, one workgroup per (cloud, 256-point chunk):
+// k_feat_bwd_chunk, one workgroup per (cloud, 128-point chunk), 2 per CU:
 //   1. the channels whose argmax falls in the chunk ("hits"), keyed (row, o) and
 //      sorted by rank counting, so each row's hits are contiguous and in
 //      increasing o (fixed summation order -> bitwise reproducible);
-//   2. active rows compacted; W2/W3 staged in LDS once;
-//   3. per batch of 32 active rows: gather x1/x2/x3 rows, dX3 rows from the
-//      sorted hits (loads of W4 rows issued back to back), ReLU masks, then
-//      dX2 = dZ3 W3, dX1 = dZ2 W2 and the weight gradients on v_mfma_f32_32x32x2_f32.
+//   2. active rows compacted;
+//   3. per batch of 32 active rows: recompute x1/x2 from the points, dX3 rows from the sorted
+//      hits (loads of W4 rows issued back to back) with the conv3 ReLU mask,
+//      dX2 = dZ3 W3 and dX1 = dZ2 W2 on v_mfma_f32_16x16x4_f32 (one 16x16 tile
+//      per wave), weight gradients on v_mfma_f32_32x32x2_f32.
 // Each workgroup writes its weight-gradient partials to its own slab;
 // k_reduce_slabs sums the slabs in a fixed order (no atomics).
 #include "common.h"
 
 namespace pcadv {
 
-constexpr int BW_PCH = 256;   // points per workgroup (chunk)
+constexpr int BW_PCH = 128;   // points per workgroup (chunk)
 constexpr int BW_RB = 32;     // active rows per batch
 constexpr int BW_MAXO = 1024; // channels of the pooled layer
-constexpr int BW_T = 512;     // threads per workgroup (8 waves)
+constexpr int BW_T = 512;     // threads per workgroup (8 waves), 2 workgroups per CU
 constexpr int SLAB = 12736;   // dW1 192 | db1 64 | dW2 4096 | db2 64 | dW3 8192 | db3 128
 constexpr int SL_DW1 = 0, SL_DB1 = 192, SL_DW2 = 256, SL_DB2 = 4352, SL_DW3 = 4416, SL_DB3 = 12608;
-constexpr int ST3 = 129;      // LDS stride of 128-wide rows (b32 column reads conflict-free)
-constexpr int ST2 = 65;       // LDS stride of 64-wide rows
+constexpr int SZ3 = 130;      // LDS stride of 128-wide rows (= 2 mod 32: 16x16x4 row reads
+constexpr int SZ2 = 66;       //  and 32x32x2 column reads are both conflict-free)
+
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4m mfma16(float a, float b, f32x4m c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
 struct BwdLds {
   int key[BW_MAXO];          // (row << 10) | o of each hit, generation order
@@ -40,36 +46,38 @@ struct BwdLds {
   int slot_of_row[BW_PCH];   // active flag, then compact slot (-1 if inactive)
   int rows_list[BW_PCH];     // compact slot -> row
   int hoff[BW_PCH + 4];      // first sorted hit of each compact slot
-  alignas(16) float w3[128 * 64];  // W3 [out 128][in 64]
-  alignas(16) float w2[64 * 64];   // W2 [out 64][in 64]
-  alignas(16) float dz3[BW_RB * ST3];
-  alignas(16) float x2[BW_RB * ST2];
-  alignas(16) float x1[BW_RB * ST2];
-  alignas(16) float dz2[BW_RB * ST2];
-  alignas(16) float dz1[BW_RB * ST2];
-  alignas(16) float part[4 * BW_RB * ST2];  // K-quarter partials of dX2 / dX1
+  alignas(16) float dz3[BW_RB * SZ3];
+  alignas(16) float x2[BW_RB * S64];   // recomputed conv2 output (f32, as the forward)
+  alignas(16) float x1[BW_RB * S64];   // recomputed conv1 output
+  alignas(16) float dz2[BW_RB * SZ2];
+  alignas(16) float dz1[BW_RB * SZ2];
   alignas(16) float pts[BW_RB * 4];
 };
 
-__global__ void __launch_bounds__(BW_T)
+__global__ void __launch_bounds__(BW_T, 4)
 k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx, int O,
                  const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
-                 int N, const float* __restrict__ w2, const float* __restrict__ w3,
-                 const float* __restrict__ w4, const float* __restrict__ x1,
-                 const float* __restrict__ x2, const float* __restrict__ x3,
-                 float* __restrict__ slabs) {
+                 int N, const float* __restrict__ w1, const float* __restrict__ b1,
+                 const float* __restrict__ w2, const float* __restrict__ b2,
+                 const float* __restrict__ w3, const float* __restrict__ w4,
+                 const float* __restrict__ x3, float* __restrict__ slabs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
+  const int r32 = lane & 31, h = lane >> 5, r16 = lane & 15, q = lane >> 4;
   const int c = blockIdx.y, chunk = blockIdx.x, p0 = chunk * BW_PCH;
   const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
 
-  // stage W3 / W2 (float4, coalesced); lands while the hits are scanned
-  for (int q = tid; q < 128 * 16; q += BW_T)
-    *reinterpret_cast<f32x4*>(&L.w3[4 * q]) = *reinterpret_cast<const f32x4*>(w3 + 4 * q);
-  for (int q = tid; q < 64 * 16; q += BW_T)
-    *reinterpret_cast<f32x4*>(&L.w2[4 * q]) = *reinterpret_cast<const f32x4*>(w2 + 4 * q);
+  // wave -> (row tile rt, column tile ct) of the 32 x 64 dX2 / dX1 outputs;
+  // its B fragments (16x16x4, k = 4s + q) are re-read from L2 each batch
+  const int rt = wave >> 2, ct = wave & 3;
+  // buffer loads: 32-bit lane offsets + scalar step offsets, so no 64-bit
+  // addresses are kept live across the batch loop
+  const __amdgpu_buffer_rsrc_t w3r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w3, (short)0, 128 * 64 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w2r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w2, (short)0, 64 * 64 * 4, 0x00020000);
+  const int boff = (q * 64 + 16 * ct + r16) * 4;
   if (tid < BW_PCH) L.slot_of_row[tid] = 0;
   __syncthreads();
 
@@ -94,7 +102,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   }
   __syncthreads();
 
-  // ---- 2. compact the active rows (threads 0..255 own one row each) ----------
+  // ---- 2. compact the active rows (threads 0..127 own one row each) ----------
   int nact = 0, nhits = 0;
   {
     const bool f = tid < BW_PCH && L.slot_of_row[tid] != 0;
@@ -164,24 +172,36 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 
   for (int b0 = 0; b0 < nact; b0 += BW_RB) {
     const int nb = min(BW_RB, nact - b0);
-    // ---- a. gather x1, x2, pts of the batch rows; zero dz3 ------------------
-    {
-      const int r = tid >> 4, c4 = tid & 15;  // 32 rows x 16 float4
-      f32x4 v1 = {0.f, 0.f, 0.f, 0.f}, v2 = v1;
-      if (r < nb) {
-        const size_t p = (size_t)c * N + p0 + L.rows_list[b0 + r];
-        v1 = *reinterpret_cast<const f32x4*>(x1 + p * 64 + 4 * c4);
-        v2 = *reinterpret_cast<const f32x4*>(x2 + p * 64 + 4 * c4);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        L.x1[r * ST2 + 4 * c4 + e] = v1[e];
-        L.x2[r * ST2 + 4 * c4 + e] = v2[e];
-      }
-    }
+    // ---- a. recompute x1, x2 of the batch rows from their points, with the
+    //      forward's exact operation order (bit-identical activations) --------
     if (tid < BW_RB * 3) {
       const int r = tid / 3, k = tid % 3;
       L.pts[r * 4 + k] = r < nb ? pts[(size_t)(p0 + L.rows_list[b0 + r]) * 3 + k] : 0.f;
+    }
+    __syncthreads();
+    {
+      const int ch = tid & 63, rg = tid >> 6;  // 8 groups x 4 rows
+      const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rr = 4 * rg + u;
+        L.x1[rr * S64 + ch] = conv1_point(wa, wb, wc, bb, L.pts[rr * 4 + 0], L.pts[rr * 4 + 1],
+                                          L.pts[rr * 4 + 2]);
+      }
+    }
+    __syncthreads();
+    if (wave < 2) {
+      f32x4 bf[8];
+      load_bfrag<64>(w2, 32 * wave, lane, bf);
+      f32x16 acc = {};
+      acc = mfma_rows_x_wt<64>(L.x1, S64, bf, acc, lane);
+      const int col = 32 * wave + r32;
+      const float bias = b2[col];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float v = acc[i] + bias;
+        L.x2[acc_row(i, lane) * S64 + col] = v > 0.f ? v : 0.f;
+      }
     }
 
     // ---- b. dZ3 rows: thread = (column i, 8-row group); the hits of a
@@ -189,8 +209,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     {
       const int i = tid & 127, rg = tid >> 7;
       const int s0 = b0 + 8 * rg, s1 = min(s0 + 8, b0 + nb);
-      // conv3 ReLU mask of my rows, prefetched
-      uint32_t mask = 0;
+      uint32_t mask = 0;  // conv3 ReLU mask of my rows, prefetched
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int s = s0 + u;
@@ -199,7 +218,8 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
           mask |= (x3[p * 128 + i] > 0.f ? 1u : 0u) << u;
         }
       }
-      for (int u = 0; u < 8; ++u) L.dz3[(8 * rg + u) * ST3 + i] = 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) L.dz3[(8 * rg + u) * SZ3 + i] = 0.f;
       if (s0 < s1) {
         int s = s0;
         const int j1 = L.hoff[s1];
@@ -207,17 +227,17 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
         float acc = 0.f;
         int j = L.hoff[s0];
         auto flush = [&]() {
-          L.dz3[(s - b0) * ST3 + i] = ((mask >> (s - s0)) & 1u) ? acc : 0.f;
+          L.dz3[(s - b0) * SZ3 + i] = ((mask >> (s - s0)) & 1u) ? acc : 0.f;
           acc = 0.f;
           ++s;
           jnext = L.hoff[s + 1];
         };
-        for (; j + 16 <= j1; j += 16) {
-          float wv[16];
+        for (; j + 8 <= j1; j += 8) {
+          float wv[8];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) wv[u] = w4[(size_t)L.so[j + u] * 128 + i];
+          for (int u = 0; u < 8; ++u) wv[u] = w4[(size_t)L.so[j + u] * 128 + i];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < 8; ++u) {
             while (j + u >= jnext) flush();
             acc = fmaf(L.sg[j + u], wv[u], acc);
           }
@@ -242,72 +262,66 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     }
     __syncthreads();
 
-    // ---- c. dX2 = dZ3 W3 (32 x 128 . 128 x 64): wave -> (col tile, K quarter) --
+    // ---- c. dX2 = dZ3 W3 (32 x 128 . 128 x 64), 16x16 tile per wave ---------
     {
-      const int ct = wave & 1, kq = wave >> 1;
-      f32x16 acc = {};
-      const float* ap = L.dz3 + r32 * ST3 + 32 * kq + h;
-      const float* bp = L.w3 + (32 * kq + h) * 64 + 32 * ct + r32;
+      f32x4m acc = {0.f, 0.f, 0.f, 0.f};
+      if (16 * rt < nb) {
+        const float* ap = L.dz3 + (16 * rt + r16) * SZ3 + q;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc = mfma32(ap[2 * s], bp[2 * s * 64], acc);
-      float* pp = L.part + kq * BW_RB * ST2;
+        for (int s = 0; s < 32; ++s)
+          acc = mfma16(ap[4 * s], __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w3r, boff, s * 1024, 0)), acc);
+      }
+      const int col = 16 * ct + r16;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) pp[acc_row(r, lane) * ST2 + 32 * ct + r32] = acc[r];
-    }
-    __syncthreads();
-    for (int q = tid; q < BW_RB * 64; q += BW_T) {
-      const int row = q >> 6, col = q & 63, o = row * ST2 + col;
-      const float v = ((L.part[o] + L.part[BW_RB * ST2 + o]) + L.part[2 * BW_RB * ST2 + o]) +
-                      L.part[3 * BW_RB * ST2 + o];
-      L.dz2[o] = L.x2[o] > 0.f ? v : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * rt + 4 * q + j;
+        L.dz2[row * SZ2 + col] = L.x2[row * S64 + col] > 0.f ? acc[j] : 0.f;
+      }
     }
     __syncthreads();
 
-    // ---- d. dX1 = dZ2 W2 (32 x 64 . 64 x 64): wave -> (col tile, K quarter) ----
+    // ---- d. dX1 = dZ2 W2 (32 x 64 . 64 x 64), 16x16 tile per wave -----------
     {
-      const int ct = wave & 1, kq = wave >> 1;
-      f32x16 acc = {};
-      const float* ap = L.dz2 + r32 * ST2 + 16 * kq + h;
-      const float* bp = L.w2 + (16 * kq + h) * 64 + 32 * ct + r32;
+      f32x4m acc = {0.f, 0.f, 0.f, 0.f};
+      if (16 * rt < nb) {
+        const float* ap = L.dz2 + (16 * rt + r16) * SZ2 + q;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc = mfma32(ap[2 * s], bp[2 * s * 64], acc);
-      float* pp = L.part + kq * BW_RB * ST2;
+        for (int s = 0; s < 16; ++s)
+          acc = mfma16(ap[4 * s], __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w2r, boff, s * 1024, 0)), acc);
+      }
+      const int col = 16 * ct + r16;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) pp[acc_row(r, lane) * ST2 + 32 * ct + r32] = acc[r];
-    }
-    __syncthreads();
-    for (int q = tid; q < BW_RB * 64; q += BW_T) {
-      const int row = q >> 6, col = q & 63, o = row * ST2 + col;
-      const float v = ((L.part[o] + L.part[BW_RB * ST2 + o]) + L.part[2 * BW_RB * ST2 + o]) +
-                      L.part[3 * BW_RB * ST2 + o];
-      L.dz1[o] = L.x1[o] > 0.f ? v : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * rt + 4 * q + j;
+        L.dz1[row * SZ2 + col] = L.x1[row * S64 + col] > 0.f ? acc[j] : 0.f;
+      }
     }
     __syncthreads();
 
-    // ---- e. weight / bias gradients over the batch rows ----------------------
+    // ---- e. weight / bias gradients over the batch rows (32x32x2) ------------
     {
       const int nb2 = (nb + 1) & ~1;
       // dW3[o][i] += sum_rows dz3[row][o] x2[row][i]; wave -> (o tile, i tile)
       const int ot = wave >> 1, it = wave & 1;
-      const float* ap = L.dz3 + h * ST3 + 32 * ot + r32;
-      const float* bp = L.x2 + h * ST2 + 32 * it + r32;
-      for (int s = 0; s < nb2 / 2; ++s) a_dw3 = mfma32(ap[2 * s * ST3], bp[2 * s * ST2], a_dw3);
+      const float* ap = L.dz3 + h * SZ3 + 32 * ot + r32;
+      const float* bp = L.x2 + h * S64 + 32 * it + r32;
+      for (int s = 0; s < nb2 / 2; ++s) a_dw3 = mfma32(ap[2 * s * SZ3], bp[2 * s * S64], a_dw3);
       // dW2[o][i] += sum_rows dz2[row][o] x1[row][i]; waves 0-3 rows [0,16),
       // waves 4-7 rows [16,32) of the batch, same 4 tiles
       const int t2 = wave & 3, rh = wave >> 2;
-      const float* ap2 = L.dz2 + (16 * rh + h) * ST2 + 32 * (t2 >> 1) + r32;
-      const float* bp2 = L.x1 + (16 * rh + h) * ST2 + 32 * (t2 & 1) + r32;
+      const float* ap2 = L.dz2 + (16 * rh + h) * SZ2 + 32 * (t2 >> 1) + r32;
+      const float* bp2 = L.x1 + (16 * rh + h) * S64 + 32 * (t2 & 1) + r32;
       const int n2 = max(0, min(nb2 - 16 * rh, 16)) / 2;
-      for (int s = 0; s < n2; ++s) a_dw2 = mfma32(ap2[2 * s * ST2], bp2[2 * s * ST2], a_dw2);
+      for (int s = 0; s < n2; ++s) a_dw2 = mfma32(ap2[2 * s * SZ2], bp2[2 * s * S64], a_dw2);
       if (tid < 192) {
         const int o = tid / 3, i = tid % 3;
-        for (int r = 0; r < nb; ++r) acc_w1 = fmaf(L.dz1[r * ST2 + o], L.pts[r * 4 + i], acc_w1);
+        for (int r = 0; r < nb; ++r) acc_w1 = fmaf(L.dz1[r * SZ2 + o], L.pts[r * 4 + i], acc_w1);
       } else if (tid < 320) {
-        for (int r = 0; r < nb; ++r) acc_b += L.dz3[r * ST3 + tid - 192];
+        for (int r = 0; r < nb; ++r) acc_b += L.dz3[r * SZ3 + tid - 192];
       } else if (tid < 384) {
-        for (int r = 0; r < nb; ++r) acc_b += L.dz2[r * ST2 + tid - 320];
+        for (int r = 0; r < nb; ++r) acc_b += L.dz2[r * SZ2 + tid - 320];
       } else if (tid < 448) {
-        for (int r = 0; r < nb; ++r) acc_b += L.dz1[r * ST2 + tid - 384];
+        for (int r = 0; r < nb; ++r) acc_b += L.dz1[r * SZ2 + tid - 384];
       }
     }
     __syncthreads();
@@ -321,10 +335,10 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     for (int r = 0; r < 16; ++r)
       slab[SL_DW3 + (32 * ot + acc_row(r, lane)) * 64 + 32 * it + r32] = a_dw3[r];
   }
-  // the two row halves of dW2 meet in LDS (waves 4-7 park theirs first)
+  // the two row halves of dW2 meet in LDS (waves 4-7 park theirs in dz3)
   {
     const int t2 = wave & 3;
-    float* pp = L.part;
+    float* pp = L.dz3;
     if (wave >= 4) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) pp[t2 * 1024 + r * 64 + lane] = a_dw2[r];
@@ -433,10 +447,10 @@ size_t feat_bwd_workspace_bytes(int C, int N) {
 }
 
 int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, const float* pts_b,
-                    int split, int C, int N, const float* w2, const float* w3, const float* w4,
-                    const float* x1, const float* x2, const float* x3, float* dw1, float* db1,
-                    float* dw2, float* db2, float* dw3, float* db3, float* dw4, float* db4,
-                    void* ws, size_t ws_bytes, hipStream_t s) {
+                    int split, int C, int N, const float* w1, const float* b1, const float* w2,
+                    const float* b2, const float* w3, const float* w4, const float* x3,
+                    float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
+                    float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
@@ -452,7 +466,7 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
     attr_set = true;
   }
   hipLaunchKernelGGL(k_feat_bwd_chunk, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg, gidx, O,
-                     pts_a, pts_b, split, N, w2, w3, w4, x1, x2, x3, slabs);
+                     pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   hipLaunchKernelGGL(k_reduce_slabs, dim3((SLAB + 127) / 128), dim3(1024), 0, s, slabs, C * nchunk,
                      dw1, db1, dw2, db2, dw3, db3);

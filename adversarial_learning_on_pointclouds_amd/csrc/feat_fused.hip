@@ -1,0 +1,364 @@
+// Fused PointNetfeat forward (models/pointnet.py:109-132, feature_transform=False)
+// on gfx950: conv1 -> conv2 -> conv3 -> conv4 -> max over points, one
+// workgroup per (cloud, 128-point tile), nothing but conv3's output leaves the
+// chip.
+//
+//   conv1 (3 -> 64)    VALU, exact f32
+//   conv2 (64 -> 64)   v_mfma_f32_32x32x2_f32 (exact f32)
+//   conv3 (64 -> 128)  v_mfma_f32_32x32x2_f32; x3 is written to HBM in f32 (the
+//                      backward and the exact re-evaluation below read it) and
+//                      kept in LDS split as bf16 hi + lo
+//   conv4 (128 -> 1024) + max: three bf16 MFMAs per product
+//                      (x_hi w_hi + x_hi w_lo + x_lo w_hi, f32 accumulate,
+//                      v_mfma_f32_32x32x16_bf16): relative error <= ~1.2e-5 of
+//                      sum|x w|, at 16x the per-cycle rate of the f32 MFMA.  The
+//                      epilogue keeps the top-2 (value, point) per channel.
+//
+// k_gmax_combine then merges the per-tile top-2 keys of each channel and
+// re-evaluates the winner in exact f32 (and the runner-up whenever the two are
+// within the split-product error bound), so gmax is an f32 dot product and the
+// argmax follows the f32 values, first index on ties (torch.max on CPU).
+#include "common.h"
+
+namespace pcadv {
+
+constexpr int FF_P = 128;   // points per workgroup
+constexpr int FF_T = 512;   // threads (8 waves, 1 workgroup per CU)
+constexpr int FF_SB = 136;  // bf16 row stride of the x3 hi/lo tiles (272 B)
+constexpr int FF_O = 1024;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct FwdLds {
+  alignas(16) float pts[FF_P * 4];
+  alignas(16) float x2[FF_P * S64];
+  union U {
+    float x1[FF_P * S64];          // dies after conv2
+    __bf16 x3[2][FF_P * FF_SB];    // hi, lo: born in conv3's epilogue
+  };
+  alignas(16) U u;
+};
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// split 8 floats into bf16 hi / lo parts (x ~= hi + lo to ~2^-17 relative)
+__device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, bf16x8& hi, bf16x8& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 hb = (__bf16)v[j];
+    hi[j] = hb;
+    lo[j] = (__bf16)(v[j] - (float)hb);
+  }
+}
+
+// Screening keys: the f32 value mapped to an order-preserving int32 with the
+// point's index inside the 128-point tile packed into the low 7 bits (stored
+// as 127 - idx, so equal screening values rank the lower index first).  One
+// v_max_i32 + one v_med3_i32 then keep the top-2 (value, point) pairs; the 7
+// dropped mantissa bits (2^-16 relative) sit far inside the near-tie window
+// that k_gmax_combine re-checks in exact f32.
+__device__ __forceinline__ int screen_key(float v, int idx) {
+  const int b = __float_as_int(v);
+  const int ord = b ^ ((b >> 31) & 0x7fffffff);   // int order == float order
+  return (ord & ~0x7f) | (127 - idx);
+}
+__device__ __forceinline__ float key_value(int k) {
+  const int ord = k & ~0x7f;
+  return __int_as_float(ord ^ ((ord >> 31) & 0x7fffffff));
+}
+__device__ __forceinline__ int key_index(int k) { return 127 - (k & 0x7f); }
+constexpr int KEY_NONE = (int)0x80000000;  // below every real key
+
+__device__ __forceinline__ void key_push(int k, int& k1, int& k2) {
+  k2 = max(min(k, k1), k2);  // median(k, k1, k2) for k2 <= k1: v_med3_i32
+  k1 = max(k1, k);
+}
+
+// (va, ia) ranks before (vb, ib): larger value, NaN above all, lower index on ties
+__device__ __forceinline__ bool ranks_before(float va, int ia, float vb, int ib) {
+  const bool na = va != va, nb = vb != vb;
+  if (na || nb) return na && (!nb || ia < ib);
+  return va > vb || (va == vb && ia < ib);
+}
+
+__device__ __forceinline__ void top2_merge(float v, int p, float& v1, int& i1, float& v2, int& i2) {
+  const bool a = ranks_before(v, p, v1, i1);
+  const bool b = !a && ranks_before(v, p, v2, i2);
+  const float nv2 = a ? v1 : (b ? v : v2);
+  const int ni2 = a ? i1 : (b ? p : i2);
+  v1 = a ? v : v1;
+  i1 = a ? p : i1;
+  v2 = nv2;
+  i2 = ni2;
+}
+
+__global__ void __launch_bounds__(FF_T)
+k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
+                 int N, const float* __restrict__ w1, const float* __restrict__ b1,
+                 const float* __restrict__ w2, const float* __restrict__ b2,
+                 const float* __restrict__ w3, const float* __restrict__ b3,
+                 const float* __restrict__ w4, const float* __restrict__ b4,
+                 float* __restrict__ x3g, int2* __restrict__ part, int32_t* inc_counter,
+                 uint64_t* __restrict__ stamps, int stagger) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FwdLds& L = *reinterpret_cast<FwdLds*>(smem);
+#ifdef PCADV_STAMPS
+  // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+  uint64_t* st = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+#define STAMP(k) do { if (threadIdx.x == 0) { st[k] = __builtin_amdgcn_s_memrealtime(); if ((k) == 0 || (k) == 14) st[15 - ((k) == 0 ? 0 : 2)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+  STAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int c = blockIdx.y, tile = blockIdx.x, p0 = tile * FF_P, T = gridDim.x;
+  if (inc_counter && tid == 0 && c == 0 && tile == 0) *inc_counter += 1;
+  const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
+
+  // conv2 / conv3 B fragments are fetched up front: they land during conv1
+  f32x4 bf2[8], bf3[8];
+  load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
+  load_bfrag<64>(w3, 32 * (wave & 3), lane, bf3);
+  if (tid < FF_P * 3) {
+    const int p = tid / 3, k = tid % 3;
+    L.pts[p * 4 + k] = (p0 + p < N) ? pts[(size_t)(p0 + p) * 3 + k] : 0.f;
+  }
+  __syncthreads();
+
+  STAMP(1);
+  // ---- conv1 (3 -> 64) + ReLU: thread = (channel, 16-point group) ------------
+  {
+    const int ch = tid & 63, pg = tid >> 6;
+    const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int p = pg * 16 + i;
+      L.u.x1[p * S64 + ch] =
+          conv1_point(wa, wb, wc, bb, L.pts[p * 4 + 0], L.pts[p * 4 + 1], L.pts[p * 4 + 2]);
+    }
+  }
+  __syncthreads();
+
+  STAMP(2);
+  // ---- conv2 (64 -> 64) + ReLU: wave -> (point tile, channel tile) ----------
+  {
+    const int pt = wave >> 1, ct = wave & 1;
+    f32x16 acc = {};
+    acc = mfma_rows_x_wt<64>(L.u.x1 + 32 * pt * S64, S64, bf2, acc, lane);
+    const int col = 32 * ct + r;
+    const float bias = b2[col];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[i] + bias;
+      L.x2[(32 * pt + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
+    }
+  }
+  __syncthreads();
+
+  STAMP(3);
+  // W4 fragments (f32) of this wave's first conv4 channel tile, issued before
+  // conv3's epilogue so they land during it
+  f32x4 wf[16];
+  auto wload = [&](int o0) {
+    const float* row = w4 + (size_t)(o0 + r) * 128 + 8 * h;
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      wf[2 * kb] = *reinterpret_cast<const f32x4*>(row + 16 * kb);
+      wf[2 * kb + 1] = *reinterpret_cast<const f32x4*>(row + 16 * kb + 4);
+    }
+  };
+  // ---- conv3 (64 -> 128) + ReLU: wave -> (channel tile, 2 point tiles) ------
+  {
+    const int ct = wave & 3, pp = 2 * (wave >> 2);
+    f32x16 acc0 = {}, acc1 = {};
+    acc0 = mfma_rows_x_wt<64>(L.x2 + 32 * pp * S64, S64, bf3, acc0, lane);
+    acc1 = mfma_rows_x_wt<64>(L.x2 + 32 * (pp + 1) * S64, S64, bf3, acc1, lane);
+    wload(128 * wave);
+    const int col = 32 * ct + r;
+    const float bias = b3[col];
+    float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int row = 32 * (pp + s) + acc_row(i, lane);
+        float v = (s == 0 ? acc0[i] : acc1[i]) + bias;
+        v = v > 0.f ? v : 0.f;
+        if (p0 + row < N) xg[(size_t)row * 128] = v;
+        const __bf16 hb = (__bf16)v;
+        L.u.x3[0][row * FF_SB + col] = hb;
+        L.u.x3[1][row * FF_SB + col] = (__bf16)(v - (float)hb);
+      }
+    }
+  }
+  __syncthreads();
+
+  STAMP(4);
+  // ---- conv4 (128 -> 1024) split-bf16 MFMA + top-2 over the tile's points ---
+  // wave -> channels [128*wave, 128*wave + 128) as 4 tiles of 32
+  {
+    const __bf16* xh = L.u.x3[0] + r * FF_SB + 8 * h;
+    const __bf16* xl = L.u.x3[1] + r * FF_SB + 8 * h;
+    const bool full = p0 + FF_P <= N;
+    // waves w and w+4 share a SIMD and run the same program: delay the upper
+    // half by about half a tile so one wave's epilogue (VALU) overlaps the
+    // other's MFMAs instead of both idling the matrix pipe together
+    if (__builtin_amdgcn_readfirstlane(wave) >= 4)
+      for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(1);
+    for (int ct = 0; ct < 4; ++ct) {
+      const int o0 = 128 * wave + 32 * ct;
+      bf16x8 bh[8], bl[8];
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) split8(wf[2 * kb], wf[2 * kb + 1], bh[kb], bl[kb]);
+      f32x16 acc[4] = {{}, {}, {}, {}};
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt) {
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(xh + 32 * pt * FF_SB + 16 * kb);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(xl + 32 * pt * FF_SB + 16 * kb);
+          acc[pt] = mfma_bf16(al, bh[kb], acc[pt]);
+          acc[pt] = mfma_bf16(ah, bl[kb], acc[pt]);
+          acc[pt] = mfma_bf16(ah, bh[kb], acc[pt]);
+        }
+      }
+      if (wave == 0) STAMP(5 + 2 * ct);
+      // next tile's weights are fetched only now, when bh/bl are dead, so the
+      // prefetch buffer and the split fragments never live at the same time
+      __builtin_amdgcn_sched_barrier(0);
+      if (ct < 3) wload(o0 + 32);
+      __builtin_amdgcn_sched_barrier(0);
+      // screening top-2 over the tile's 128 points (bias is added by the exact
+      // re-evaluation in k_gmax_combine; it does not change the order)
+      int k1 = KEY_NONE, k2 = KEY_NONE;
+      if (full) {
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            key_push(screen_key(acc[pt][i], 32 * pt + acc_row(i, lane)), k1, k2);
+      } else {
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int idx = 32 * pt + acc_row(i, lane);
+            if (p0 + idx < N) key_push(screen_key(acc[pt][i], idx), k1, k2);
+          }
+      }
+      // lanes l and l+32 hold the same channel over interleaved rows
+      const int o1 = __shfl_xor(k1, 32), o2 = __shfl_xor(k2, 32);
+      k2 = max(min(k1, o1), max(k2, o2));
+      k1 = max(k1, o1);
+      if (lane < 32) part[((size_t)c * T + tile) * FF_O + o0 + r] = make_int2(k1, k2);
+      if (wave == 0) STAMP(6 + 2 * ct);
+    }
+  }
+#ifdef PCADV_STAMPS
+  __syncthreads();
+#endif
+  STAMP(14);
+#undef STAMP
+}
+
+// Four lanes per (cloud, channel): merge the T tile partials (top-2 screening
+// keys), then exact f32 dot products over x3 rows (each lane 32 of the 128
+// terms) for the winner and, on near-ties, the runner-up.
+__global__ void __launch_bounds__(256)
+k_gmax_combine(const int2* __restrict__ part, int T, int C, int N,
+               const float* __restrict__ x3g, const float* __restrict__ w4,
+               const float* __restrict__ b4, float* __restrict__ gmax,
+               int32_t* __restrict__ gidx) {
+  const int q = threadIdx.x & 3;
+  const int g = blockIdx.x * 64 + (threadIdx.x >> 2);  // (cloud, channel) pair
+  const int c = g / FF_O, o = g % FF_O;
+  if (c >= C) return;  // C * FF_O is a multiple of 64: whole waves leave together
+  float v1 = -INFINITY, v2 = -INFINITY;
+  int i1 = 0x7fffffff, i2 = 0x7fffffff;
+  for (int t = q; t < T; t += 4) {
+    const int2 kk = part[((size_t)c * T + t) * FF_O + o];
+    if (kk.x != KEY_NONE) top2_merge(key_value(kk.x), t * FF_P + key_index(kk.x), v1, i1, v2, i2);
+    if (kk.y != KEY_NONE) top2_merge(key_value(kk.y), t * FF_P + key_index(kk.y), v1, i1, v2, i2);
+  }
+#pragma unroll
+  for (int m = 1; m < 4; m <<= 1) {
+    const float a1 = __shfl_xor(v1, m), a2 = __shfl_xor(v2, m);
+    const int j1 = __shfl_xor(i1, m), j2 = __shfl_xor(i2, m);
+    top2_merge(a1, j1, v1, i1, v2, i2);
+    top2_merge(a2, j2, v1, i1, v2, i2);
+  }
+  if (i1 == 0x7fffffff) i1 = 0;
+  // screening error <= ~1.2e-5 sum|x w| (+2^-16 key truncation): re-check
+  // anything within a far wider window of the winner in exact f32
+  const bool near = i2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
+  const float* wrow = w4 + (size_t)o * 128 + 32 * q;
+  auto dot = [&](int n) {
+    const float* xrow = x3g + ((size_t)c * N + n) * 128 + 32 * q;
+    f32x4 xv[8], wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xv[u] = *reinterpret_cast<const f32x4*>(xrow + 4 * u);
+      wv[u] = *reinterpret_cast<const f32x4*>(wrow + 4 * u);
+    }
+    float d = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      d = fmaf(xv[u].x, wv[u].x, d);
+      d = fmaf(xv[u].y, wv[u].y, d);
+      d = fmaf(xv[u].z, wv[u].z, d);
+      d = fmaf(xv[u].w, wv[u].w, d);
+    }
+    d += __shfl_xor(d, 1);
+    d += __shfl_xor(d, 2);
+    return d;
+  };
+  const float bias = b4[o];
+  const float e1 = dot(i1) + bias;
+  float e2 = 0.f;
+  if (near) e2 = dot(i2) + bias;
+  const bool second = near && ranks_before(e2, i2, e1, i1);
+  if (q == 0) {
+    gmax[(size_t)c * FF_O + o] = second ? e2 : e1;
+    gidx[(size_t)c * FF_O + o] = second ? i2 : i1;
+  }
+}
+
+size_t feat_fwd_workspace_bytes(int C, int N) {
+  const size_t T = (N + FF_P - 1) / FF_P;
+  return (size_t)C * T * FF_O * sizeof(int2);
+}
+
+int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int C, int N,
+                          const float* w1, const float* b1, const float* w2, const float* b2,
+                          const float* w3, const float* b3, const float* w4, const float* b4,
+                          float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
+                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int stagger) {
+  PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
+  PC_REQUIRE(ws && ws_bytes >= feat_fwd_workspace_bytes(C, N), "feat_fwd: workspace too small");
+  const int T = (N + FF_P - 1) / FF_P;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_fwd_fused),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(FwdLds)) != hipSuccess) {
+      set_error("feat_fwd: cannot reserve %zu bytes of LDS", sizeof(FwdLds));
+      return PCADV_EHIP;
+    }
+    attr_set = true;
+  }
+  int2* part = static_cast<int2*>(ws);
+  hipLaunchKernelGGL(k_feat_fwd_fused, dim3(T, C), dim3(FF_T), sizeof(FwdLds), s, pts_a, pts_b,
+                     split, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, part, inc_counter, stamps,
+                     stagger);
+  PC_HIP_CHECK_LAUNCH("k_feat_fwd_fused");
+  hipLaunchKernelGGL(k_gmax_combine, dim3(C * FF_O / 64), dim3(256), 0, s, part, T, C, N, x3, w4,
+                     b4, gmax, gidx);
+  PC_HIP_CHECK_LAUNCH("k_gmax_combine");
+  return PCADV_OK;
+}
+
+}  // namespace pcadv

@@ -13,39 +13,7 @@
 
 namespace pcadv {
 
-// LDS row strides (floats): K + 4 keeps the ds_read_b128 fragment reads of 32
-// consecutive rows conflict-free (row stride = 4 banks mod 64).
 constexpr int MLP_TILE = 64;
-constexpr int S64 = 68;
-constexpr int S128 = 132;
-
-// One 32x32 f32 MFMA tile over K (multiple of 8) with the k-permuted fragment
-// scheme: for k-group g, lane half h supplies k = 8g + 4h + j at MFMA step j, so
-// each lane reads one float4 of A (LDS) and one float4 of B per 4 MFMAs.
-template <int K>
-__device__ __forceinline__ f32x16 mfma_rows_x_wt(const float* __restrict__ a_lds, int a_stride,
-                                                 const f32x4* bfrag, f32x16 acc, int lane) {
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int g = 0; g < K / 8; ++g) {
-    f32x4 a = *reinterpret_cast<const f32x4*>(a_lds + r * a_stride + 8 * g + 4 * h);
-    acc = mfma32(a.x, bfrag[g].x, acc);
-    acc = mfma32(a.y, bfrag[g].y, acc);
-    acc = mfma32(a.z, bfrag[g].z, acc);
-    acc = mfma32(a.w, bfrag[g].w, acc);
-  }
-  return acc;
-}
-
-// B fragments for output channels [o0, o0+32) of a row-major weight W[O][K].
-template <int K>
-__device__ __forceinline__ void load_bfrag(const float* __restrict__ w, int o0, int lane,
-                                           f32x4* bfrag) {
-  const int r = lane & 31, h = lane >> 5;
-  const float* row = w + (size_t)(o0 + r) * K + 4 * h;
-#pragma unroll
-  for (int g = 0; g < K / 8; ++g) bfrag[g] = *reinterpret_cast<const f32x4*>(row + 8 * g);
-}
 
 __global__ void __launch_bounds__(256)
 k_point_mlp3(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split, int N,
@@ -128,12 +96,6 @@ k_point_mlp3(const float* __restrict__ pts_a, const float* __restrict__ pts_b, i
       if (p0 + 32 + row < N) x3[gbase + (size_t)(32 + row) * 128 + col] = v1;
     }
   }
-}
-
-// NaN-propagating "v beats best" (torch.max returns a NaN if one is present;
-// ties keep the earlier index because points arrive in increasing order).
-__device__ __forceinline__ bool beats(float v, float best) {
-  return v > best || (v != v && best == best);
 }
 
 constexpr int CM_TILE = 64;  // points per LDS tile

@@ -39,7 +39,7 @@ def _mat(w):
 # ---------------------------------------------------------------------------
 
 def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4):
-    """pts (C, N, 3) -> gmax (C, 1024), gidx (C, 1024) int32, saved (x1, x2, x3)."""
+    """pts (C, N, 3) -> gmax (C, 1024), gidx (C, 1024) int32, x3 (C, N, 128)."""
     lib = _lib.load()
     _req(pts, "pts")
     if pts.dim() != 3 or pts.shape[2] != 3:
@@ -50,30 +50,27 @@ def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4):
           _req(_mat(w3), "conv3.weight", (128, 64)), _req(b3, "conv3.bias", (128,)),
           _req(_mat(w4), "conv4.weight", (1024, 128)), _req(b4, "conv4.bias", (1024,))]
     dev = pts.device
-    x1 = torch.empty(C, N, 64, device=dev)
-    x2 = torch.empty(C, N, 64, device=dev)
     x3 = torch.empty(C, N, 128, device=dev)
     gmax = torch.empty(C, 1024, device=dev)
     gidx = torch.empty(C, 1024, device=dev, dtype=torch.int32)
-    check(lib.pcadv_feat_fwd(ptr(pts), C, N, *[ptr(t) for t in ws], ptr(x1), ptr(x2), ptr(x3),
-                             ptr(gmax), ptr(gidx), stream_ptr()), "pcadv_feat_fwd")
-    return gmax, gidx, (x1, x2, x3)
+    nbytes = lib.pcadv_feat_fwd_workspace_bytes(C, N)
+    work = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+    check(lib.pcadv_feat_fwd(ptr(pts), C, N, *[ptr(t) for t in ws], ptr(x3), ptr(gmax), ptr(gidx),
+                             ptr(work), nbytes, stream_ptr()), "pcadv_feat_fwd")
+    return gmax, gidx, x3
 
 
-def feat_bwd(dgmax, gidx, pts, w2, w3, w4, x1, x2, x3):
+def feat_bwd(dgmax, gidx, pts, w1, b1, w2, b2, w3, w4, x3):
     """Gradients of (conv1..conv4) weights and biases given dL/dgmax."""
     lib = _lib.load()
     C, N, _ = pts.shape
     _req(dgmax, "dgmax", (C, 1024))
     _req(gidx, "gidx", (C, 1024), torch.int32)
     _req(pts, "pts")
-    _req(x1, "x1", (C, N, 64))
-    _req(x2, "x2", (C, N, 64))
     _req(x3, "x3", (C, N, 128))
-    w2m, w3m, w4m = _mat(w2), _mat(w3), _mat(w4)
-    _req(w2m, "conv2.weight", (64, 64))
-    _req(w3m, "conv3.weight", (128, 64))
-    _req(w4m, "conv4.weight", (1024, 128))
+    mats = [_req(_mat(w1), "conv1.weight", (64, 3)), _req(b1, "conv1.bias", (64,)),
+            _req(_mat(w2), "conv2.weight", (64, 64)), _req(b2, "conv2.bias", (64,)),
+            _req(_mat(w3), "conv3.weight", (128, 64)), _req(_mat(w4), "conv4.weight", (1024, 128))]
     dev = pts.device
     grads = [torch.empty(64, 3, 1, device=dev), torch.empty(64, device=dev),
              torch.empty(64, 64, 1, device=dev), torch.empty(64, device=dev),
@@ -81,9 +78,9 @@ def feat_bwd(dgmax, gidx, pts, w2, w3, w4, x1, x2, x3):
              torch.empty(1024, 128, 1, device=dev), torch.empty(1024, device=dev)]
     nbytes = lib.pcadv_feat_bwd_workspace_bytes(C, N)
     ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-    check(lib.pcadv_feat_bwd(ptr(dgmax), ptr(gidx), ptr(pts), C, N, ptr(w2m), ptr(w3m), ptr(w4m),
-                             ptr(x1), ptr(x2), ptr(x3), *[ptr(g) for g in grads], ptr(ws),
-                             nbytes, stream_ptr()), "pcadv_feat_bwd")
+    check(lib.pcadv_feat_bwd(ptr(dgmax), ptr(gidx), ptr(pts), C, N, *[ptr(m) for m in mats],
+                             ptr(x3), *[ptr(g) for g in grads], ptr(ws), nbytes, stream_ptr()),
+          "pcadv_feat_bwd")
     return grads
 
 
@@ -170,15 +167,15 @@ class PointFeatFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pts, w1, b1, w2, b2, w3, b3, w4, b4):
-        gmax, gidx, (x1, x2, x3) = feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4)
-        ctx.save_for_backward(pts, w2, w3, w4, x1, x2, x3, gidx)
+        gmax, gidx, x3 = feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4)
+        ctx.save_for_backward(pts, w1, b1, w2, b2, w3, w4, x3, gidx)
         ctx.mark_non_differentiable(gidx)
         return gmax, gidx
 
     @staticmethod
     def backward(ctx, dgmax, _dgidx):
-        pts, w2, w3, w4, x1, x2, x3, gidx = ctx.saved_tensors
-        g = feat_bwd(dgmax.contiguous(), gidx, pts, w2, w3, w4, x1, x2, x3)
+        pts, w1, b1, w2, b2, w3, w4, x3, gidx = ctx.saved_tensors
+        g = feat_bwd(dgmax.contiguous(), gidx, pts, w1, b1, w2, b2, w3, w4, x3)
         return (None, *g)
 
 

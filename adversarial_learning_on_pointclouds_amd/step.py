@@ -214,11 +214,10 @@ class AdvTrainStep:
     # ------------------------------------------------------------------
     def saved_x3(self):
         """conv3 activations of the last step, (2B, N, 128) view of the workspace
-        (carve order of csrc/capi.hip: x1, x2, x3, ...)."""
+        (first region of the carve in csrc/capi.hip)."""
         C, N = 2 * self.B, self.N
-        off = 2 * _align(C * N * 64 * 4)
         n = C * N * 128
-        return self.workspace[off:off + 4 * n].view(torch.float32).view(C, N, 128)
+        return self.workspace[:4 * n].view(torch.float32).view(C, N, 128)
 
     def sync_optimizer_state(self):
         """Copy the device step counter into the torch optimizers' 'step'."""

@@ -86,24 +86,29 @@ int pcadv_abi_version(void);
 
 /* ---- PointNetfeat (feature_transform=False) -------------------------------
  * pts [C][N][3]; w1 [64][3], w2 [64][64], w3 [128][64], w4 [1024][128] + biases.
- * Saves x1,x2 [C][N][64] and x3 [C][N][128] (post-ReLU) for the backward and
- * writes gmax [C][1024] (x_global, pointnet.py:129-130) and gidx [C][1024]
- * (argmax over points, first index on ties as torch.max on CPU). */
+ * One fused pass (conv1..conv4 + max): writes x3 [C][N][128] (post-ReLU conv3
+ * output, read by the backward), gmax [C][1024] (x_global, pointnet.py:129-130,
+ * an exact f32 dot product) and gidx [C][1024] (argmax over points, first index
+ * on ties as torch.max on CPU).  conv1..conv3 are computed in f32; conv4 screens
+ * the points with three bf16 MFMAs per product (|err| <= ~1.2e-5 sum|x w|) and
+ * re-evaluates the winning point (and the runner-up on near-ties) in f32. */
+size_t pcadv_feat_fwd_workspace_bytes(int C, int N);
 int pcadv_feat_fwd(const float* pts, int C, int N,
                    const float* w1, const float* b1, const float* w2, const float* b2,
                    const float* w3, const float* b3, const float* w4, const float* b4,
-                   float* x1, float* x2, float* x3, float* gmax, int32_t* gidx,
-                   hipStream_t stream);
+                   float* x3, float* gmax, int32_t* gidx,
+                   void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Bytes of workspace pcadv_feat_bwd needs for C clouds of N points. */
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N);
 
 /* Autograd of pcadv_feat_fwd: dgmax [C][1024] -> dw1..db4 (overwritten).
  * The max-pool backward is sparse (each channel's gradient goes to its argmax
- * point), equal to torch's MaxBackward for unique maxima. */
+ * point), equal to torch's MaxBackward for unique maxima; conv1/conv2 outputs
+ * of the points that receive gradient are recomputed from pts. */
 int pcadv_feat_bwd(const float* dgmax, const int32_t* gidx, const float* pts, int C, int N,
-                   const float* w2, const float* w3, const float* w4,
-                   const float* x1, const float* x2, const float* x3,
+                   const float* w1, const float* b1, const float* w2, const float* b2,
+                   const float* w3, const float* w4, const float* x3,
                    float* dw1, float* db1, float* dw2, float* db2,
                    float* dw3, float* db3, float* dw4, float* db4,
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
