@@ -16,6 +16,7 @@ import math
 from collections import OrderedDict
 
 import numpy as np
+import scipy.sparse as _sparse
 
 F32 = np.float32
 
@@ -133,10 +134,14 @@ def relu(x):
 def point_mlp_fwd(pts, p, prefix="feat."):
     """relu(conv1), relu(conv2), relu(conv3) as per-point matvecs
     (models/pointnet.py:115-116,127).  pts: (B, N, 3)."""
-    x1 = relu(pts @ _w(p, prefix + "conv1.weight").T + p[prefix + "conv1.bias"])
-    x2 = relu(x1 @ _w(p, prefix + "conv2.weight").T + p[prefix + "conv2.bias"])
-    x3 = relu(x2 @ _w(p, prefix + "conv3.weight").T + p[prefix + "conv3.bias"])
-    return x1.astype(F32), x2.astype(F32), x3.astype(F32)
+    def layer(x, i):
+        y = x @ _w(p, f"{prefix}conv{i}.weight").T
+        y += p[f"{prefix}conv{i}.bias"]
+        return np.maximum(y, F32(0), out=y)
+    x1 = layer(pts, 1)
+    x2 = layer(x1, 2)
+    x3 = layer(x2, 3)
+    return x1, x2, x3
 
 
 def conv_max_fwd(x, w, b, relu_before_max=False):
@@ -145,15 +150,15 @@ def conv_max_fwd(x, w, b, relu_before_max=False):
     on CPU).  x: (B, N, K), w: (O, K).  Returns (gmax (B, O), argmax (B, O))."""
     B = x.shape[0]
     O = w.shape[0]
-    gmax = np.empty((B, O), F32)
-    am = np.empty((B, O), np.int32)
-    for bi in range(B):
-        y = x[bi] @ w.T + b
-        if relu_before_max:
-            y = relu(y)
-        a = np.argmax(y, axis=0)
-        am[bi] = a
-        gmax[bi] = y[a, np.arange(O)]
+    N, K = x.shape[1], x.shape[2]
+    # channel-major (O, B, N) from one GEMM, so the argmax runs along contiguous memory
+    y = w @ x.reshape(B * N, K).T
+    y += b[:, None]
+    if relu_before_max:
+        np.maximum(y, F32(0), out=y)
+    y = y.reshape(O, B, N)
+    am = np.argmax(y, axis=2).T.astype(np.int32)                 # (B, O)
+    gmax = y[np.arange(O)[None, :], np.arange(B)[:, None], am].astype(F32)
     return gmax, am
 
 
@@ -188,12 +193,14 @@ def conv_max_bwd(dg, am, x, w):
     dW[o,:] = sum_b dg[b,o] x[b, am[b,o], :], db = sum_b dg, and
     dX[b, am[b,o], :] += dg[b,o] * W[o,:]."""
     B, N, K = x.shape
-    dW = np.zeros(w.shape, np.float64)
-    dX = np.zeros((B, N, K), F32)
-    for bi in range(B):
-        rows = x[bi][am[bi]]                       # (O, K)
-        dW += dg[bi][:, None].astype(np.float64) * rows
-        np.add.at(dX[bi], am[bi], dg[bi][:, None] * w)
+    O = w.shape[0]
+    rows = x[np.arange(B)[:, None], am]                      # (B, O, K)
+    dW = np.einsum("bo,bok->ok", dg, rows)
+    # scatter-add of dg[b,o] * W[o,:] onto point am[b,o] as a sparse product
+    # (one entry per column; each row sums its entries in ascending o)
+    M = _sparse.csr_matrix((dg.reshape(-1), ((np.arange(B)[:, None] * N + am).reshape(-1),
+                                             np.arange(B * O))), shape=(B * N, B * O))
+    dX = np.asarray(M @ np.tile(w, (B, 1)), dtype=F32).reshape(B, N, K)
     return dW.astype(F32), dg.sum(0).astype(F32), dX
 
 
