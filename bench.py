@@ -16,6 +16,7 @@ an RCCL all-reduce (multi-GPU).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -169,10 +170,25 @@ def main():
     # 2 * N * (3*64 + 64*64 + 64*128 + 128*1024) per cloud
     flops = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64 + 64 * 128 + 128 * 1024)
     achieved = flops / kern_s / 1e12
-    # conv4 runs as 3 bf16 MFMAs per f32 product: its hardware ceiling for these
-    # f32-equivalent FLOPs is the dense bf16 peak / 3 (conv1..3, 7% of the FLOPs,
-    # run on the f32 MFMA); see DESIGN.md
-    peak = 2500.0 / 3.0
+    # Ceiling of this kernel pair on MI355X: conv1..conv3 (1.64 GFLOP) at the dense
+    # f32 MFMA / VALU peak (157.3 TF) plus conv4 (17.18 GFLOP), run as 3 bf16 MFMAs
+    # per f32 product, at the dense bf16 peak / 3 (2500/3 TF).  The composite peak is
+    # the total FLOPs over that minimum time (MI355X_MICROARCH.md peaks).
+    f13 = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64 + 64 * 128)
+    f4 = flops - f13
+    t_min = f13 / 157.3e12 + f4 / (2500e12 / 3.0)
+    peak = flops / t_min / 1e12
+    traffic, traffic_src = None, None
+    prof = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                         "profiles", "r*_pmc_traffic.json")))
+    if prof:
+        kern = json.load(open(prof[-1]))["kernels"]
+        names = ("pcadv::k_feat_fwd_fused", "pcadv::k_gmax_combine")
+        if all(n in kern for n in names):
+            traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
+            traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))
+    step_gflop = 22.47  # algorithmic FLOPs of one B=32 adversarial step
+    step_tf = step_gflop * world * args.steps / dt / 1e3
 
     result = {
         "metric": "point-clouds/sec (adv train step), B=32 N=1024 ModelNet40, 1/2/4/8 GPU",
@@ -194,9 +210,15 @@ def main():
         "roofline": {"bound": "mfma",
                      "kernel": "k_feat_fwd_fused + k_gmax_combine (PointNetfeat conv1..4 + max)",
                      "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": 2 * B * N * (3 + 128) * 4 + 2 * B * 1024 * 8,
                      "avg_launch_us": round(kern_s * 1e6, 2),
-                     "algorithmic_flops_per_launch": flops},
+                     "algorithmic_flops_per_launch": flops,
+                     "peak_basis": "f32 MFMA 157.3 TF for conv1-3 + bf16 2500/3 TF for conv4"},
+        "step_mfma": {"gflop_per_step": step_gflop, "achieved_tflops": round(step_tf, 2),
+                      "frac_of_f32_peak": round(step_tf / 157.3, 4)},
         "losses_last_step": [round(v, 5) for v in losses],
         "finite": finite,
     }
