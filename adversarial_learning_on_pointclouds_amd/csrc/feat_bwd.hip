@@ -446,6 +446,9 @@ size_t feat_bwd_workspace_bytes(int C, int N) {
   return (size_t)C * nchunk * SLAB * sizeof(float);
 }
 
+int launch_dw4_gather(const float* dg, const int32_t* gidx, int C, int N, const float* x3,
+                      float* dw4, float* db4, hipStream_t s);
+
 int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, const float* pts_b,
                     int split, int C, int N, const float* w1, const float* b1, const float* w2,
                     const float* b2, const float* w3, const float* w4, const float* x3,
@@ -471,6 +474,15 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
   hipLaunchKernelGGL(k_reduce_slabs, dim3((SLAB + 127) / 128), dim3(1024), 0, s, slabs, C * nchunk,
                      dw1, db1, dw2, db2, dw3, db3);
   PC_HIP_CHECK_LAUNCH("k_reduce_slabs");
+  if (dw4) return launch_dw4_gather(dg, gidx, C, N, x3, dw4, db4, s);
+  return PCADV_OK;
+}
+
+// dW4 / db4 alone (independent of k_feat_bwd_chunk: the fused step runs it on
+// a second stream)
+int launch_dw4_gather(const float* dg, const int32_t* gidx, int C, int N, const float* x3,
+                      float* dw4, float* db4, hipStream_t s) {
+  const int O = PCADV_C4;
   hipLaunchKernelGGL(k_dw4_gather, dim3((O + 3) / 4), dim3(256), 0, s, dg, gidx, C, N, O, x3,
                      dw4, db4);
   PC_HIP_CHECK_LAUNCH("k_dw4_gather");

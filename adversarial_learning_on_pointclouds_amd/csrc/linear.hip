@@ -22,30 +22,16 @@ struct DropSpec {
   float p;
 };
 
-__device__ __forceinline__ bool has_drop(const DropSpec& d) { return d.mask || d.step; }
+// dropout source, fixed per launch (a template parameter: the operand loads
+// below are then straight-line code the compiler can issue back to back)
+enum DropMode { DM_NONE = 0, DM_MASK = 1, DM_RNG = 2 };
 
-__device__ __forceinline__ float drop_scale(const DropSpec& d, int m, int n, int N) {
-  if (d.mask) return d.mask[(size_t)m * N + n] * (1.0f / (1.0f - d.p));
-  if (d.step) {
-    const float u = rng_uniform(d.seed, (uint32_t)*d.step, RNG_DROPOUT, (uint32_t)(m * N + n));
-    return u >= d.p ? 1.0f / (1.0f - d.p) : 0.f;
-  }
-  return 1.f;
-}
+static int drop_mode(const DropSpec& d) { return d.mask ? DM_MASK : (d.step ? DM_RNG : DM_NONE); }
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// dz = dy * act'(y) * s at (m, n)
-__device__ __forceinline__ float dz_at(const float* __restrict__ dy, const float* __restrict__ y,
-                                       int act, const DropSpec& drop, int m, int n, int N) {
-  float g = dy[(size_t)m * N + n];
-  if (act != ACT_NONE) g *= act_bwd(y[(size_t)m * N + n], act);
-  if (has_drop(drop)) g *= drop_scale(drop, m, n, N);
-  return g;
 }
 
 enum Op { OP_FWD = 0, OP_BWD_DATA = 1, OP_BWD_WEIGHT = 2 };
@@ -66,30 +52,61 @@ struct GemmArgs {
   int M, N, K, m_w;
 };
 
+// dropout scale s at (m, n) of an [M][N] output
+template <int DM>
+__device__ __forceinline__ float drop_scale(const GemmArgs& g, size_t i, int m, int n,
+                                            uint32_t step) {
+  const float keep = 1.0f / (1.0f - g.drop.p);
+  if (DM == DM_MASK) return g.drop.mask[i] * keep;
+  if (DM == DM_RNG)
+    return rng_uniform(g.drop.seed, step, RNG_DROPOUT, (uint32_t)(m * g.N + n)) >= g.drop.p ? keep
+                                                                                           : 0.f;
+  return 1.f;
+}
+
+// dz = dy * act'(y) * s at (m, n), 0 outside; the loads are unconditional
+// (clamped address) so a wave issues all of them before the first use
+template <int ACT, int DM>
+__device__ __forceinline__ float dz_at(const GemmArgs& g, int m, int n, bool valid,
+                                       uint32_t step) {
+  const size_t i = (size_t)(valid ? m : 0) * g.N + (valid ? n : 0);
+  float v = g.dy[i];
+  if (ACT != ACT_NONE) v *= act_bwd(g.yact[i], ACT);
+  if (DM != DM_NONE) v *= drop_scale<DM>(g, i, m, n, step);
+  return valid ? v : 0.f;
+}
+
 constexpr int MAXC = 8;  // 16-deep k chunks per wave (reduction <= 128 per wave)
 constexpr int SPLITC = 4;  // split jobs: <= 64 per wave (16 waves cover 1024)
 
 // Load the (k = kk..kk+3) A and B operand values of lane (r) for output tile
 // (r0, c0): A row r0 + r, B column c0 + r.
-template <int OP>
-__device__ __forceinline__ void load_ab(const GemmArgs& g, int r0, int c0, int r, int kk,
-                                        float* a, float* b) {
+template <int OP, int ACT, int DM>
+__device__ __forceinline__ void load_ab(const GemmArgs& g, int r0, int c0, int r, int kk, bool cv,
+                                        uint32_t step, float* a, float* b) {
   if (OP == OP_FWD) {
-    // out[m][n] = sum_k x[m][k] w[n][k]
+    // out[m][n] = sum_k x[m][k] w[n][k]  (K % 4 == 0: kk < K covers all four)
     const int m = r0 + r, n = c0 + r;
-    const f32x4v z = {0.f, 0.f, 0.f, 0.f};
-    f32x4v av = (m < g.M && kk < g.K) ? *reinterpret_cast<const f32x4v*>(g.x + (size_t)m * g.K + kk) : z;
-    f32x4v bv = (n < g.N && kk < g.K) ? *reinterpret_cast<const f32x4v*>(g.w + (size_t)n * g.K + kk) : z;
-    a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
-    b[0] = bv.x; b[1] = bv.y; b[2] = bv.z; b[3] = bv.w;
+    const bool va = cv && m < g.M && kk < g.K, vb = cv && n < g.N && kk < g.K;
+    const f32x4v av = *reinterpret_cast<const f32x4v*>(
+        g.x + (size_t)(va ? m : 0) * g.K + (va ? kk : 0));
+    const f32x4v bv = *reinterpret_cast<const f32x4v*>(
+        g.w + (size_t)(vb ? n : 0) * g.K + (vb ? kk : 0));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] = va ? av[j] : 0.f;
+      b[j] = vb ? bv[j] : 0.f;
+    }
   } else if (OP == OP_BWD_DATA) {
     // dx[m][k] = sum_n dz[m][n] w[n][k]
     const int m = r0 + r, k = c0 + r;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = kk + j;
-      a[j] = (m < g.M && n < g.N) ? dz_at(g.dy, g.yact, g.act, g.drop, m, n, g.N) : 0.f;
-      b[j] = (n < g.N && k < g.K) ? g.w[(size_t)n * g.K + k] : 0.f;
+      a[j] = dz_at<ACT, DM>(g, m, n, cv && m < g.M && n < g.N, step);
+      const bool vb = cv && n < g.N && k < g.K;
+      const float wv = g.w[(size_t)(vb ? n : 0) * g.K + (vb ? k : 0)];
+      b[j] = vb ? wv : 0.f;
     }
   } else {
     // dw[n][k] = sum_{m < m_w} dz[m][n] x[m][k]
@@ -97,37 +114,33 @@ __device__ __forceinline__ void load_ab(const GemmArgs& g, int r0, int c0, int r
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = kk + j;
-      a[j] = (m < g.m_w && n < g.N) ? dz_at(g.dy, g.yact, g.act, g.drop, m, n, g.N) : 0.f;
-      b[j] = (m < g.m_w && k < g.K) ? g.x[(size_t)m * g.K + k] : 0.f;
+      a[j] = dz_at<ACT, DM>(g, m, n, cv && m < g.m_w && n < g.N, step);
+      const bool vb = cv && m < g.m_w && k < g.K;
+      const float xv = g.x[(size_t)(vb ? m : 0) * g.K + (vb ? k : 0)];
+      b[j] = vb ? xv : 0.f;
     }
   }
 }
 
-// One wave: 16x16 tile (r0, c0) over reduction [k0, k1) with nch <= MAXC chunks.
-template <int OP, int NC>
+// One wave: 16x16 tile (r0, c0) over reduction [k0, k0 + 16*nch), nch <= NC.
+// Chunks past nch load clamped addresses and contribute zeros, so the loop is
+// branch-free and every load is issued before the first MFMA.
+template <int OP, int NC, int ACT, int DM>
 __device__ __forceinline__ f32x4v wave_tile(const GemmArgs& g, int r0, int c0, int k0, int nch,
-                                            int lane, float* asum) {
+                                            int lane, uint32_t step, float* asum) {
   const int r = lane & 15, q = lane >> 4;
   float a[NC][4], b[NC][4];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (c < nch) {
-      load_ab<OP>(g, r0, c0, r, k0 + 16 * c + 4 * q, a[c], b[c]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[c][j] = b[c][j] = 0.f;
-    }
-  }
+  for (int c = 0; c < NC; ++c)
+    load_ab<OP, ACT, DM>(g, r0, c0, r, k0 + 16 * c + 4 * q, c < nch, step, a[c], b[c]);
   f32x4v acc = {0.f, 0.f, 0.f, 0.f};
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    if (c < nch) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc = mfma16(a[c][j], b[c][j], acc);
-        s += a[c][j];
-      }
+    for (int j = 0; j < 4; ++j) {
+      acc = mfma16(a[c][j], b[c][j], acc);
+      s += a[c][j];
     }
   }
   *asum = s;
@@ -136,17 +149,18 @@ __device__ __forceinline__ f32x4v wave_tile(const GemmArgs& g, int r0, int c0, i
 
 // Split-reduction job (forward, backward-data): block = one 16x16 tile, wave w
 // takes reduction slice w.  Tiles are numbered row-major over (rows, cols).
-template <int OP>
+template <int OP, int ACT, int DM>
 __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R, int S, int L,
                           float* red) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t step = DM == DM_RNG ? (uint32_t)*g.drop.step : 0u;
   const int ctiles = (cols + 15) / 16;
   const int r0 = (tile / ctiles) * 16, c0 = (tile % ctiles) * 16;
   const int k0 = wave * L;
   int nch = 0;
   if (k0 < R) nch = min(L, R - k0 + 15) / 16;
   float s;
-  f32x4v acc = wave_tile<OP, SPLITC>(g, r0, c0, k0, nch, lane, &s);
+  f32x4v acc = wave_tile<OP, SPLITC, ACT, DM>(g, r0, c0, k0, nch, lane, step, &s);
   const int col = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[wave * 256 + (4 * q + j) * 16 + col] = acc[j];
@@ -158,9 +172,10 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
     const int m = r0 + row, n = c0 + cc;
     if (m < rows && n < cols) {
       if (OP == OP_FWD) {
+        const size_t i = (size_t)m * g.N + n;
         v += g.b[n];
-        if (has_drop(g.drop)) v *= drop_scale(g.drop, m, n, g.N);
-        g.y[(size_t)m * g.N + n] = act_fwd(v, g.act);
+        if (DM != DM_NONE) v *= drop_scale<DM>(g, i, m, n, step);
+        g.y[i] = act_fwd(v, ACT);
       } else {
         g.dx[(size_t)m * g.K + n] = v;
       }
@@ -170,14 +185,16 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
 
 // Weight-gradient job: every wave owns one 16x16 tile of dw (rows n, cols k)
 // and the full reduction over the m_w rows; k-tile 0 also produces db.
+template <int ACT, int DM>
 __device__ void weight_job(const GemmArgs& g, int tile, int ntiles_total) {
   const int lane = threadIdx.x & 63;
   if (tile >= ntiles_total) return;
+  const uint32_t step = DM == DM_RNG ? (uint32_t)*g.drop.step : 0u;
   const int ctiles = (g.K + 15) / 16;
   const int r0 = (tile / ctiles) * 16, c0 = (tile % ctiles) * 16;
   const int nch = (g.m_w + 15) / 16;
   float s;
-  f32x4v acc = wave_tile<OP_BWD_WEIGHT, MAXC>(g, r0, c0, 0, nch, lane, &s);
+  f32x4v acc = wave_tile<OP_BWD_WEIGHT, MAXC, ACT, DM>(g, r0, c0, 0, nch, lane, step, &s);
   const int col = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -192,22 +209,48 @@ __device__ void weight_job(const GemmArgs& g, int tile, int ntiles_total) {
   }
 }
 
+template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
 k_linear_fwd(GemmArgs g, int S, int L) {
   __shared__ float red[16 * 256];
-  split_job<OP_FWD>(g, blockIdx.x, g.M, g.N, g.K, S, L, red);
+  split_job<OP_FWD, ACT, DM>(g, blockIdx.x, g.M, g.N, g.K, S, L, red);
 }
 
 // blocks [0, nbx): dx tiles (split over S waves); the rest: dw tiles, S per block
+template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
 k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt) {
   __shared__ float red[16 * 256];
   if ((int)blockIdx.x < nbx) {
-    split_job<OP_BWD_DATA>(g, blockIdx.x, g.M, g.K, g.N, S, L, red);
+    split_job<OP_BWD_DATA, ACT, DM>(g, blockIdx.x, g.M, g.K, g.N, S, L, red);
   } else {
-    weight_job(g, (blockIdx.x - nbx) * S + (threadIdx.x >> 6), nwt);
+    weight_job<ACT, DM>(g, (blockIdx.x - nbx) * S + (threadIdx.x >> 6), nwt);
   }
 }
+
+// host-side dispatch over the (activation, dropout-source) instantiations
+template <template <int, int> class K, typename... Args>
+static void launch_variant(int act, int dm, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+#define PC_VARIANT(A, D)                                                               \
+  if (act == A && dm == D) {                                                           \
+    auto kfn_ = K<A, D>::fn;                                                           \
+    hipLaunchKernelGGL(kfn_, grid, block, 0, s, args...);                              \
+    return;                                                                            \
+  }
+  PC_VARIANT(ACT_NONE, DM_NONE) PC_VARIANT(ACT_NONE, DM_MASK) PC_VARIANT(ACT_NONE, DM_RNG)
+  PC_VARIANT(ACT_RELU, DM_NONE) PC_VARIANT(ACT_RELU, DM_MASK) PC_VARIANT(ACT_RELU, DM_RNG)
+  PC_VARIANT(ACT_LRELU, DM_NONE) PC_VARIANT(ACT_LRELU, DM_MASK) PC_VARIANT(ACT_LRELU, DM_RNG)
+#undef PC_VARIANT
+}
+
+template <int A, int D>
+struct FwdK {
+  static constexpr auto fn = k_linear_fwd<A, D>;
+};
+template <int A, int D>
+struct BwdK {
+  static constexpr auto fn = k_linear_bwd<A, D>;
+};
 
 static void split_cfg(int R, int* S, int* L) {
   int s = (R + 63) / 64;
@@ -229,8 +272,9 @@ int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, 
   g.M = M; g.N = N; g.K = K;
   int S, L;
   split_cfg(K, &S, &L);
+  PC_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU, "linear_fwd: bad act %d", act);
   const int tiles = ((M + 15) / 16) * ((N + 15) / 16);
-  hipLaunchKernelGGL(k_linear_fwd, dim3(tiles), dim3(64 * S), 0, s, g, S, L);
+  launch_variant<FwdK>(act, drop_mode(g.drop), dim3(tiles), dim3(64 * S), s, g, S, L);
   PC_HIP_CHECK_LAUNCH("k_linear_fwd");
   return PCADV_OK;
 }
@@ -253,7 +297,9 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   const int nwt = dw ? ((N + 15) / 16) * ((K + 15) / 16) : 0;
   const int nbw = (nwt + S - 1) / S;
   if (nbx + nbw == 0) return PCADV_OK;
-  hipLaunchKernelGGL(k_linear_bwd, dim3(nbx + nbw), dim3(64 * S), 0, s, g, S, L, nbx, nwt);
+  PC_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU, "linear_bwd: bad act %d", act);
+  launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx + nbw), dim3(64 * S), s, g, S, L, nbx,
+                       nwt);
   PC_HIP_CHECK_LAUNCH("k_linear_bwd");
   return PCADV_OK;
 }
