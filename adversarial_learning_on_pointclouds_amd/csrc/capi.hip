@@ -26,7 +26,7 @@ size_t feat_bwd_workspace_bytes(int C, int N);
 int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
                     const float*, const float*, const float*, const float*, const float*,
                     const float*, const float*, float*, float*, float*, float*, float*, float*,
-                    float*, float*, void*, size_t, hipStream_t);
+                    float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr);
 size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
@@ -250,6 +250,19 @@ int pcadv_feat_fwd_stamped(const float* pts, int C, int N, const float* w1, cons
 #endif
 
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_workspace_bytes(C, N); }
+
+#ifdef PCADV_STAMPS
+// diagnostic build only: pcadv_feat_bwd with per-workgroup phase timestamps
+int pcadv_feat_bwd_stamped(const float* dgmax, const int32_t* gidx, const float* pts, int C,
+                           int N, const float* w1, const float* b1, const float* w2,
+                           const float* b2, const float* w3, const float* w4, const float* x3,
+                           float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
+                           float* dw4, float* db4, void* workspace, size_t workspace_bytes,
+                           uint64_t* stamps, hipStream_t stream) {
+  return launch_feat_bwd(dgmax, gidx, pts, pts, C, C, N, w1, b1, w2, b2, w3, w4, x3, dw1, db1,
+                         dw2, db2, dw3, db3, dw4, db4, workspace, workspace_bytes, stream, stamps);
+}
+#endif
 
 int pcadv_feat_bwd(const float* dgmax, const int32_t* gidx, const float* pts, int C, int N,
                    const float* w1, const float* b1, const float* w2, const float* b2,

@@ -2,7 +2,7 @@
 //
 // The max-pool has no ReLU before it (pointnet.py:128-129), so channel o of
 // cloud c sends its whole gradient to the single point gidx[c][o]:
-//   dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :]            (k_dw4_gather)
+//   dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :]            (k_feat_bwd_finish)
 //   dX3[c,n,:] = sum_{o: gidx[c,o]=n} g[c,o] W4[o,:]         (k_feat_bwd_chunk)
 // Only points that are the argmax of some channel ("active" points, ~1/4 of a
 // cloud) carry gradient into conv3..conv1, so k_feat_bwd_chunk compacts them
@@ -18,7 +18,7 @@
 //      dX2 = dZ3 W3 and dX1 = dZ2 W2 on v_mfma_f32_16x16x4_f32 (one 16x16 tile
 //      per wave), weight gradients on v_mfma_f32_32x32x2_f32.
 // Each workgroup writes its weight-gradient partials to its own slab;
-// k_reduce_slabs sums the slabs in a fixed order (no atomics).
+// k_feat_bwd_finish sums the slabs in a fixed order (no atomics) and gathers dW4.
 #include "common.h"
 
 namespace pcadv {
@@ -38,14 +38,18 @@ __device__ __forceinline__ f32x4m mfma16(float a, float b, f32x4m c) {
 }
 
 struct BwdLds {
-  int key[BW_MAXO];          // (row << 10) | o of each hit, generation order
-  float hg[BW_MAXO];         // g of each hit, generation order
-  int so[BW_MAXO];           // sorted o
-  float sg[BW_MAXO];         // sorted g
-  int wcnt[8], wact[8];
-  int slot_of_row[BW_PCH];   // active flag, then compact slot (-1 if inactive)
+  int key[BW_MAXO];          // o of each hit, grouped by row (arbitrary order in a row)
+  float hg[BW_MAXO];         // g of each hit, same order
+  int so[BW_MAXO];           // o of each hit, sorted by (row, o)
+  float sg[BW_MAXO];         // g, same order
+  int rcnt[BW_PCH];          // hits per row of the chunk
+  int fill[BW_PCH];          // placement cursor per row
+  int roff[BW_PCH];          // first hit of each row (exclusive scan of rcnt)
+  int wsum[2], wact[2];
   int rows_list[BW_PCH];     // compact slot -> row
-  int hoff[BW_PCH + 4];      // first sorted hit of each compact slot
+  int hoff[BW_PCH + 4];      // first sorted hit of each compact slot; hoff[nact] = nhits
+  int bnd_row[4];            // batch row whose hits group g continued (or -1)
+  alignas(16) float bnd[4][128];  // group g's partial dZ3 sums of that row
   alignas(16) float dz3[BW_RB * SZ3];
   alignas(16) float x2[BW_RB * S64];   // recomputed conv2 output (f32, as the forward)
   alignas(16) float x1[BW_RB * S64];   // recomputed conv1 output
@@ -60,9 +64,17 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
                  int N, const float* __restrict__ w1, const float* __restrict__ b1,
                  const float* __restrict__ w2, const float* __restrict__ b2,
                  const float* __restrict__ w3, const float* __restrict__ w4,
-                 const float* __restrict__ x3, float* __restrict__ slabs) {
+                 const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
+#ifdef PCADV_STAMPS
+  // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+  uint64_t* st_ = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+#define BSTAMP(k) do { if (stamps && threadIdx.x == 0 && (k) < 15) st_[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BSTAMP(k) do { } while (0)
+#endif
+  BSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5, r16 = lane & 15, q = lane >> 4;
   const int c = blockIdx.y, chunk = blockIdx.x, p0 = chunk * BW_PCH;
@@ -78,93 +90,100 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   const __amdgpu_buffer_rsrc_t w2r =
       __builtin_amdgcn_make_buffer_rsrc((void*)w2, (short)0, 64 * 64 * 4, 0x00020000);
   const int boff = (q * 64 + 16 * ct + r16) * 4;
-  if (tid < BW_PCH) L.slot_of_row[tid] = 0;
-  __syncthreads();
-
-  // ---- 1a. hits in increasing o (wave w scans channels [w*O/8, (w+1)*O/8)) ----
-  const int per_wave = O / 8;
-  {
-    int cnt = 0;
-    for (int base = 0; base < per_wave; base += 64) {
-      const int o = wave * per_wave + base + lane;
-      const int a = gidx[(size_t)c * O + o];
-      const bool hit = a >= p0 && a < p0 + BW_PCH;
-      const uint64_t m = __ballot(hit);
-      if (hit) {
-        const int pos = wave * per_wave + cnt + __popcll(m & ((1ull << lane) - 1ull));
-        L.key[pos] = ((a - p0) << 10) | o;
-        L.hg[pos] = dg[(size_t)c * O + o];
-        L.slot_of_row[a - p0] = 1;
-      }
-      cnt += __popcll(m);
-    }
-    if (lane == 0) L.wcnt[wave] = cnt;
+  const __amdgpu_buffer_rsrc_t w4r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w4, (short)0, BW_MAXO * 128 * 4, 0x00020000);
+  // this cloud's x3 rows (C x N x 128 f32 < 4 GB: 32-bit offsets from the cloud base)
+  const __amdgpu_buffer_rsrc_t x3r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x3 + (size_t)c * N * 128), (short)0, N * 128 * 4, 0x00020000);
+  // conv1 weights, fetched up front so they land during the hit sort
+  const int ch1 = tid & 63;
+  const float w1a = w1[ch1 * 3 + 0], w1b = w1[ch1 * 3 + 1], w1c = w1[ch1 * 3 + 2], b1v = b1[ch1];
+  if (tid < BW_PCH) {
+    L.rcnt[tid] = 0;
+    L.fill[tid] = 0;
   }
   __syncthreads();
 
-  // ---- 2. compact the active rows (threads 0..127 own one row each) ----------
-  int nact = 0, nhits = 0;
-  {
-    const bool f = tid < BW_PCH && L.slot_of_row[tid] != 0;
-    const uint64_t m = __ballot(f);
-    if (lane == 0) L.wact[wave] = __popcll(m);
-    __syncthreads();
-    int off = 0;
-    for (int w = 0; w < wave; ++w) off += L.wact[w];
-    for (int w = 0; w < 8; ++w) {
-      nact += L.wact[w];
-      nhits += L.wcnt[w];
-    }
-    const int slot = off + __popcll(m & ((1ull << lane) - 1ull));
-    if (tid < BW_PCH) L.slot_of_row[tid] = f ? slot : -1;
-    if (f) L.rows_list[slot] = tid;
+  // ---- 1. hits: the channels whose argmax falls in this chunk (thread -> 2
+  //      channels, kept in registers); count them per row ----------------------
+  int hrow[2], hpos[2];
+  float hgv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int o = u * BW_T + tid;
+    const int a = o < O ? gidx[(size_t)c * O + o] : -1;
+    const bool hit = a >= p0 && a < p0 + BW_PCH;
+    hrow[u] = hit ? a - p0 : -1;
+    hgv[u] = hit ? dg[(size_t)c * O + o] : 0.f;
+    if (hit) atomicAdd(&L.rcnt[a - p0], 1);
   }
   __syncthreads();
+  BSTAMP(1);
 
-  // ---- 1b. rank-count sort of the hits by key = (row, o) ---------------------
-  auto phys = [&](int j) {
-    int w = 0;
-    while (w < 7 && j >= L.wcnt[w]) { j -= L.wcnt[w]; ++w; }
-    return w * per_wave + j;
-  };
-  for (int j = tid; j < nhits; j += BW_T) {
-    const int pj = phys(j);
-    const int kj = L.key[pj];
-    int rank = 0;
-    for (int w = 0; w < 8; ++w) {
-      const int n = L.wcnt[w];
-      const int* kp = &L.key[w * per_wave];
-      for (int i = 0; i < n; ++i) rank += kp[i] < kj;
-    }
-    L.so[rank] = kj & 1023;
-    L.sg[rank] = L.hg[pj];
-  }
-  {
-    // hits per compact slot (one thread per slot), inclusive scan -> hoff
-    int cnt = 0;
-    if (tid < nact) {
-      const int row = L.rows_list[tid];
-      for (int w = 0; w < 8; ++w) {
-        const int n = L.wcnt[w];
-        const int* kp = &L.key[w * per_wave];
-        for (int i = 0; i < n; ++i) cnt += (kp[i] >> 10) == row;
-      }
-    }
+  // ---- 2. active rows (rcnt > 0) compacted in row order; roff / hoff =
+  //      exclusive scan of the hit counts (waves 0-1 own one row per lane) ----
+  if (wave < 2) {
+    const int row = tid, cnt = L.rcnt[row];
+    const bool f = cnt > 0;
     int v = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const int t = __shfl_up(v, d);
       if (lane >= d) v += t;
     }
-    __syncthreads();  // wact reads of step 2 are done
-    if (lane == 63) L.wact[wave] = v;
-    __syncthreads();
-    int off = 0;
-    for (int w = 0; w < wave; ++w) off += L.wact[w];
-    if (tid < BW_PCH) L.hoff[tid + 1] = off + v;
-    if (tid == 0) L.hoff[0] = 0;
+    const uint64_t m = __ballot(f);
+    if (lane == 63) {
+      L.wsum[wave] = v;
+      L.wact[wave] = __popcll(m);
+    }
+    L.roff[row] = v - cnt;  // wave-local for now
   }
   __syncthreads();
+  const int nact = L.wact[0] + L.wact[1], nhits = L.wsum[0] + L.wsum[1];
+  if (wave < 2) {
+    const int row = tid;
+    const bool f = L.rcnt[row] > 0;
+    const uint64_t m = __ballot(f);
+    const int slot = (wave ? L.wact[0] : 0) + __popcll(m & ((1ull << lane) - 1ull));
+    const int off = L.roff[row] + (wave ? L.wsum[0] : 0);
+    L.roff[row] = off;
+    if (f) {
+      L.rows_list[slot] = row;
+      L.hoff[slot] = off;
+    }
+    if (tid == 0) L.hoff[nact] = nhits;
+  }
+  // first batch's points, issued now (used after the sort)
+  float ptv = 0.f;
+  __syncthreads();
+  if (tid < BW_RB * 3 && tid / 3 < nact)
+    ptv = pts[(size_t)(p0 + L.rows_list[tid / 3]) * 3 + tid % 3];
+  BSTAMP(2);
+
+  // ---- 3. place each hit in its row's segment, then rank it inside the
+  //      segment by o: sorted order (row, o), independent of timing ----------
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    hpos[u] = -1;
+    if (hrow[u] >= 0) {
+      hpos[u] = L.roff[hrow[u]] + atomicAdd(&L.fill[hrow[u]], 1);
+      L.key[hpos[u]] = u * BW_T + tid;
+      L.hg[hpos[u]] = hgv[u];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (hrow[u] >= 0) {
+      const int o = u * BW_T + tid, s0 = L.roff[hrow[u]], s1 = s0 + L.rcnt[hrow[u]];
+      int rank = 0;
+      for (int j = s0; j < s1; ++j) rank += L.key[j] < o;
+      L.so[s0 + rank] = o;
+      L.sg[s0 + rank] = hgv[u];
+    }
+  }
+  __syncthreads();
+  BSTAMP(3);
 
   // register accumulators that live across batches
   f32x16 a_dw3 = {}, a_dw2 = {};
@@ -172,29 +191,32 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 
   for (int b0 = 0; b0 < nact; b0 += BW_RB) {
     const int nb = min(BW_RB, nact - b0);
+    const int sb_ = 4 + 5 * (b0 / BW_RB);
+    (void)sb_;
     // ---- a. recompute x1, x2 of the batch rows from their points, with the
-    //      forward's exact operation order (bit-identical activations) --------
+    //      forward's exact operation order (bit-identical activations); the
+    //      conv2 B fragments (waves 0-1) land during conv1 ----------------------
+    f32x4 bf2[8];
+    if (wave < 2) load_bfrag<64>(w2, 32 * wave, lane, bf2);
     if (tid < BW_RB * 3) {
-      const int r = tid / 3, k = tid % 3;
-      L.pts[r * 4 + k] = r < nb ? pts[(size_t)(p0 + L.rows_list[b0 + r]) * 3 + k] : 0.f;
+      if (b0 > 0 && tid / 3 < nb)
+        ptv = pts[(size_t)(p0 + L.rows_list[b0 + tid / 3]) * 3 + tid % 3];
+      L.pts[(tid / 3) * 4 + tid % 3] = tid / 3 < nb ? ptv : 0.f;
     }
     __syncthreads();
     {
-      const int ch = tid & 63, rg = tid >> 6;  // 8 groups x 4 rows
-      const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
+      const int rg = tid >> 6;  // 8 groups x 4 rows
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int rr = 4 * rg + u;
-        L.x1[rr * S64 + ch] = conv1_point(wa, wb, wc, bb, L.pts[rr * 4 + 0], L.pts[rr * 4 + 1],
-                                          L.pts[rr * 4 + 2]);
+        L.x1[rr * S64 + ch1] = conv1_point(w1a, w1b, w1c, b1v, L.pts[rr * 4 + 0],
+                                           L.pts[rr * 4 + 1], L.pts[rr * 4 + 2]);
       }
     }
     __syncthreads();
     if (wave < 2) {
-      f32x4 bf[8];
-      load_bfrag<64>(w2, 32 * wave, lane, bf);
       f32x16 acc = {};
-      acc = mfma_rows_x_wt<64>(L.x1, S64, bf, acc, lane);
+      acc = mfma_rows_x_wt<64>(L.x1, S64, bf2, acc, lane);
       const int col = 32 * wave + r32;
       const float bias = b2[col];
 #pragma unroll
@@ -203,64 +225,91 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
         L.x2[acc_row(i, lane) * S64 + col] = v > 0.f ? v : 0.f;
       }
     }
+    BSTAMP(sb_);
 
-    // ---- b. dZ3 rows: thread = (column i, 8-row group); the hits of a
-    //      contiguous row range are contiguous in the sorted list -------------
+    // ---- b. dZ3 rows: thread = (column i, group g); the batch's sorted hits
+    //      are split evenly over the 4 groups whatever their spread over rows.
+    //      A row cut by a group boundary gets the later groups' partial sums
+    //      added in group order (fixed order: bitwise reproducible) ----------
     {
-      const int i = tid & 127, rg = tid >> 7;
-      const int s0 = b0 + 8 * rg, s1 = min(s0 + 8, b0 + nb);
-      uint32_t mask = 0;  // conv3 ReLU mask of my rows, prefetched
+      const int i = tid & 127, grp = tid >> 7;
+      uint32_t mask = 0;  // conv3 ReLU mask of rows grp, grp+4, ... (prefetched)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int s = s0 + u;
-        if (s < s1) {
-          const size_t p = (size_t)c * N + p0 + L.rows_list[s];
-          mask |= (x3[p * 128 + i] > 0.f ? 1u : 0u) << u;
+      for (int u = 0; u < BW_RB / 4; ++u) {
+        const int rr = grp + 4 * u;
+        if (rr < nb) {
+          const int p = p0 + L.rows_list[b0 + rr];
+          const float xv =
+              __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(x3r, (p * 128 + i) * 4, 0, 0));
+          mask |= (xv > 0.f ? 1u : 0u) << u;
         }
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) L.dz3[(8 * rg + u) * SZ3 + i] = 0.f;
-      if (s0 < s1) {
-        int s = s0;
-        const int j1 = L.hoff[s1];
+      const int jb0 = L.hoff[b0], nh = L.hoff[b0 + nb] - jb0;
+      const int ja = jb0 + (nh * grp) / 4, je = jb0 + (nh * (grp + 1)) / 4;
+      auto w4_at = [&](int o) {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w4r, (o * 128 + i) * 4, 0, 0));
+      };
+      int brow = -1;
+      if (ja < je) {
+        int s = b0;
+        while (L.hoff[s + 1] <= ja) ++s;
+        bool head = L.hoff[s] >= ja;  // row s starts inside my range
+        if (!head) brow = s - b0;
         int jnext = L.hoff[s + 1];
         float acc = 0.f;
-        int j = L.hoff[s0];
         auto flush = [&]() {
-          L.dz3[(s - b0) * SZ3 + i] = ((mask >> (s - s0)) & 1u) ? acc : 0.f;
+          if (head) L.dz3[(s - b0) * SZ3 + i] = acc;
+          else L.bnd[grp][i] = acc;
           acc = 0.f;
+          head = true;
           ++s;
           jnext = L.hoff[s + 1];
         };
-        for (; j + 8 <= j1; j += 8) {
+        int j = ja;
+        for (; j + 8 <= je; j += 8) {
           float wv[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) wv[u] = w4[(size_t)L.so[j + u] * 128 + i];
+          for (int u = 0; u < 8; ++u) wv[u] = w4_at(L.so[j + u]);
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             while (j + u >= jnext) flush();
             acc = fmaf(L.sg[j + u], wv[u], acc);
           }
         }
-        for (; j + 4 <= j1; j += 4) {
-          float wv[4];
+        if (j < je) {
+          float wv[8];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) wv[u] = w4[(size_t)L.so[j + u] * 128 + i];
+          for (int u = 0; u < 8; ++u)
+            wv[u] = j + u < je ? w4_at(L.so[j + u]) : 0.f;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            while (j + u >= jnext) flush();
-            acc = fmaf(L.sg[j + u], wv[u], acc);
+          for (int u = 0; u < 8; ++u) {
+            if (j + u < je) {
+              while (j + u >= jnext) flush();
+              acc = fmaf(L.sg[j + u], wv[u], acc);
+            }
           }
         }
-        for (; j < j1; ++j) {
-          const float wv = w4[(size_t)L.so[j] * 128 + i];
-          while (j >= jnext) flush();
-          acc = fmaf(L.sg[j], wv, acc);
+        flush();  // the row holding hit je-1
+      }
+      if (i == 0) L.bnd_row[grp] = brow;
+      __syncthreads();
+      // combine the cut rows and apply the conv3 ReLU mask; padding rows -> 0
+#pragma unroll
+      for (int u = 0; u < BW_RB / 4; ++u) {
+        const int rr = grp + 4 * u;
+        float v = 0.f;
+        if (rr < nb) {
+          v = L.dz3[rr * SZ3 + i];
+#pragma unroll
+          for (int g = 1; g < 4; ++g)
+            if (L.bnd_row[g] == rr) v += L.bnd[g][i];
+          v = ((mask >> u) & 1u) ? v : 0.f;
         }
-        flush();  // every active row has at least one hit: s ends at s1
+        L.dz3[rr * SZ3 + i] = v;
       }
     }
     __syncthreads();
+    BSTAMP(sb_ + 1);
 
     // ---- c. dX2 = dZ3 W3 (32 x 128 . 128 x 64), 16x16 tile per wave ---------
     {
@@ -279,6 +328,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       }
     }
     __syncthreads();
+    BSTAMP(sb_ + 2);
 
     // ---- d. dX1 = dZ2 W2 (32 x 64 . 64 x 64), 16x16 tile per wave -----------
     {
@@ -297,6 +347,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       }
     }
     __syncthreads();
+    BSTAMP(sb_ + 3);
 
     // ---- e. weight / bias gradients over the batch rows (32x32x2) ------------
     {
@@ -325,6 +376,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       }
     }
     __syncthreads();
+    BSTAMP(sb_ + 4);
   }
 
   // ---- 4. write this workgroup's slab ----------------------------------------
@@ -356,17 +408,21 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   else if (tid < 320) slab[SL_DB3 + tid - 192] = acc_b;
   else if (tid < 384) slab[SL_DB2 + tid - 320] = acc_b;
   else if (tid < 448) slab[SL_DB1 + tid - 384] = acc_b;
+#ifdef PCADV_STAMPS
+  __syncthreads();
+  if (stamps && threadIdx.x == 0) { st_[14] = __builtin_amdgcn_s_memrealtime(); st_[15] = nact; }
+#endif
+#undef BSTAMP
 }
 
 // out[j] = sum over slabs in fixed order: 128 columns per block (lanes hold
 // float2), 16 waves split the slabs into contiguous ranges, combined in wave
 // order through LDS.
-__global__ void __launch_bounds__(1024)
-k_reduce_slabs(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
-               float* db2, float* dw3, float* db3) {
-  __shared__ float2 part[16][64];
+__device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __restrict__ slabs,
+                                   int nslabs, float* dw1, float* db1, float* dw2, float* db2,
+                                   float* dw3, float* db3) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = blockIdx.x * 128 + 2 * lane;  // SLAB is even: j, j+1 both valid or both not
+  const int j = blk * 128 + 2 * lane;  // SLAB is even: j, j+1 both valid or both not
   const int s0 = wave * nslabs / 16, s1 = (wave + 1) * nslabs / 16;
   float2 acc = make_float2(0.f, 0.f);
   if (j < SLAB) {
@@ -405,11 +461,10 @@ k_reduce_slabs(const float* __restrict__ slabs, int nslabs, float* dw1, float* d
 
 // dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :];  db4[o] = sum_c g[c,o].
 // One wave per channel, lanes hold two of the 128 columns.
-__global__ void __launch_bounds__(256)
-k_dw4_gather(const float* __restrict__ dg, const int32_t* __restrict__ gidx, int C, int N, int O,
-             const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4) {
+__device__ void dw4_wave(int o, const float* __restrict__ dg, const int32_t* __restrict__ gidx,
+                         int C, int N, int O, const float* __restrict__ x3,
+                         float* __restrict__ dw4, float* __restrict__ db4) {
   const int lane = threadIdx.x & 63;
-  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (o >= O) return;
   float ax = 0.f, ay = 0.f, ab = 0.f;
   int c = 0;
@@ -441,19 +496,34 @@ k_dw4_gather(const float* __restrict__ dg, const int32_t* __restrict__ gidx, int
   if (lane == 0) db4[o] = ab;
 }
 
+// One launch after k_feat_bwd_chunk: blocks [0, nred) reduce the slabs
+// (dW1..db3), the rest gather dW4/db4 (16 channels per block; independent of
+// the chunk kernel, they simply share its launch).
+constexpr int FIN_NRED = (SLAB + 127) / 128;
+__global__ void __launch_bounds__(1024)
+k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
+                  float* db2, float* dw3, float* db3, const float* __restrict__ dg,
+                  const int32_t* __restrict__ gidx, int C, int N, int O,
+                  const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4) {
+  __shared__ float2 part[16][64];
+  if ((int)blockIdx.x < FIN_NRED)
+    reduce_slabs_block(blockIdx.x, part, slabs, nslabs, dw1, db1, dw2, db2, dw3, db3);
+  else
+    dw4_wave(((int)blockIdx.x - FIN_NRED) * 16 + (threadIdx.x >> 6), dg, gidx, C, N, O, x3, dw4,
+             db4);
+}
+
 size_t feat_bwd_workspace_bytes(int C, int N) {
   const size_t nchunk = (N + BW_PCH - 1) / BW_PCH;
   return (size_t)C * nchunk * SLAB * sizeof(float);
 }
 
-int launch_dw4_gather(const float* dg, const int32_t* gidx, int C, int N, const float* x3,
-                      float* dw4, float* db4, hipStream_t s);
-
 int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, const float* pts_b,
                     int split, int C, int N, const float* w1, const float* b1, const float* w2,
                     const float* b2, const float* w3, const float* w4, const float* x3,
                     float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
-                    float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s) {
+                    float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s,
+                    uint64_t* stamps) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
@@ -469,23 +539,12 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
     attr_set = true;
   }
   hipLaunchKernelGGL(k_feat_bwd_chunk, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg, gidx, O,
-                     pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs);
+                     pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
-  hipLaunchKernelGGL(k_reduce_slabs, dim3((SLAB + 127) / 128), dim3(1024), 0, s, slabs, C * nchunk,
-                     dw1, db1, dw2, db2, dw3, db3);
-  PC_HIP_CHECK_LAUNCH("k_reduce_slabs");
-  if (dw4) return launch_dw4_gather(dg, gidx, C, N, x3, dw4, db4, s);
-  return PCADV_OK;
-}
-
-// dW4 / db4 alone (independent of k_feat_bwd_chunk: the fused step runs it on
-// a second stream)
-int launch_dw4_gather(const float* dg, const int32_t* gidx, int C, int N, const float* x3,
-                      float* dw4, float* db4, hipStream_t s) {
-  const int O = PCADV_C4;
-  hipLaunchKernelGGL(k_dw4_gather, dim3((O + 3) / 4), dim3(256), 0, s, dg, gidx, C, N, O, x3,
-                     dw4, db4);
-  PC_HIP_CHECK_LAUNCH("k_dw4_gather");
+  PC_REQUIRE(dw4 && db4, "feat_bwd: dw4/db4 required");
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + (O + 15) / 16), dim3(1024), 0, s, slabs,
+                     C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4);
+  PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
   return PCADV_OK;
 }
 

@@ -108,7 +108,7 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
 #ifdef PCADV_STAMPS
   // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
   uint64_t* st = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
-#define STAMP(k) do { if (threadIdx.x == 0) { st[k] = __builtin_amdgcn_s_memrealtime(); if ((k) == 0 || (k) == 14) st[15 - ((k) == 0 ? 0 : 2)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define STAMP(k) do { if (stamps && threadIdx.x == 0) { st[k] = __builtin_amdgcn_s_memrealtime(); if ((k) == 0 || (k) == 14) st[15 - ((k) == 0 ? 0 : 2)] = __builtin_amdgcn_s_memtime(); } } while (0)
 #else
 #define STAMP(k) do { } while (0)
 #endif
