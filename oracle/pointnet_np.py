@@ -434,6 +434,114 @@ def feature_transform_regularizer(trans):
     return float(np.mean(np.sqrt((r.astype(np.float64) ** 2).sum((1, 2)))))
 
 
+def _layer_bwd(dy, x, y, w):
+    """Backward of y = relu(x w^T + b) over rows (point-major): returns
+    (dW, db, dx) given dL/dy."""
+    dz = dy * (y > 0)
+    x2 = x.reshape(-1, x.shape[-1])
+    dz2 = dz.reshape(-1, dz.shape[-1])
+    return (dz2.T @ x2).astype(F32), dz2.sum(0).astype(F32), (dz @ w).astype(F32)
+
+
+def stn_forward_train(p, x, prefix, k):
+    """STNkd forward keeping what its backward needs (models/pointnet.py:59-79)."""
+    h1 = relu(x @ _w(p, prefix + "conv1.weight").T + p[prefix + "conv1.bias"]).astype(F32)
+    h2 = relu(h1 @ _w(p, prefix + "conv2.weight").T + p[prefix + "conv2.bias"]).astype(F32)
+    g, am = conv_max_fwd(h2, _w(p, prefix + "conv3.weight"), p[prefix + "conv3.bias"],
+                         relu_before_max=True)
+    f1 = relu(g @ p[prefix + "fc1.weight"].T + p[prefix + "fc1.bias"]).astype(F32)
+    f2 = relu(f1 @ p[prefix + "fc2.weight"].T + p[prefix + "fc2.bias"]).astype(F32)
+    t = (f2 @ p[prefix + "fc3.weight"].T + p[prefix + "fc3.bias"]).astype(F32)
+    t = t + np.eye(k, dtype=F32).reshape(1, k * k)
+    cache = dict(x=x, h1=h1, h2=h2, g=g, am=am, f1=f1, f2=f2)
+    return t.reshape(-1, k, k).astype(F32), cache
+
+
+def stn_backward(p, cache, dT, prefix):
+    """Autograd of stn_forward_train given dL/dT (B, k, k): parameter grads and
+    dL/dx.  The max-pool follows a ReLU (relu before max, pointnet.py:66-67): the
+    argmax point receives the gradient only when the pooled value is > 0."""
+    x, h1, h2, g, am, f1, f2 = (cache[n] for n in ("x", "h1", "h2", "g", "am", "f1", "f2"))
+    B = x.shape[0]
+    out = OrderedDict()
+    dt = dT.reshape(B, -1).astype(F32)
+    out[prefix + "fc3.weight"] = dt.T @ f2
+    out[prefix + "fc3.bias"] = dt.sum(0)
+    dz = (dt @ p[prefix + "fc3.weight"]) * (f2 > 0)
+    out[prefix + "fc2.weight"] = dz.T @ f1
+    out[prefix + "fc2.bias"] = dz.sum(0)
+    dz = (dz @ p[prefix + "fc2.weight"]) * (f1 > 0)
+    out[prefix + "fc1.weight"] = dz.T @ g
+    out[prefix + "fc1.bias"] = dz.sum(0)
+    dg = ((dz @ p[prefix + "fc1.weight"]) * (g > 0)).astype(F32)
+    W3 = _w(p, prefix + "conv3.weight")
+    dW3, db3, dh2 = conv_max_bwd(dg, am, h2, W3)
+    out[prefix + "conv3.weight"], out[prefix + "conv3.bias"] = dW3[:, :, None], db3
+    dW2, db2, dh1 = _layer_bwd(dh2, h1, h2, _w(p, prefix + "conv2.weight"))
+    out[prefix + "conv2.weight"], out[prefix + "conv2.bias"] = dW2[:, :, None], db2
+    dW1, db1, dx = _layer_bwd(dh1, x, h1, _w(p, prefix + "conv1.weight"))
+    out[prefix + "conv1.weight"], out[prefix + "conv1.bias"] = dW1[:, :, None], db1
+    return OrderedDict((k, v.astype(F32)) for k, v in out.items()), dx
+
+
+def regularizer_bwd(trans):
+    """d/dT of mean_b ||T T^T - I||_F: (2 / (B n_b)) (T T^T - I) T."""
+    B, d, _ = trans.shape
+    a = np.matmul(trans, trans.transpose(0, 2, 1)) - np.eye(d, dtype=F32)[None]
+    n = np.sqrt((a.astype(np.float64) ** 2).sum((1, 2)))
+    return (np.matmul(a, trans) * (2.0 / (B * n))[:, None, None]).astype(F32)
+
+
+def cls_ft_step(p, pts, labels, mask, lambda_cls=1.0, lambda_regu=0.001):
+    """One run_training_pointnet_cls iteration body (utils/trainer.py:254-268) for
+    PointNetCls(feature_transform=True): loss = lambda_cls * CE + lambda_regu *
+    feature_transform_regularizer(trans_feat).  Returns (loss_cls, reg, grads)."""
+    pts = np.ascontiguousarray(pts, F32)
+    x1 = relu(pts @ _w(p, "feat.conv1.weight").T + p["feat.conv1.bias"]).astype(F32)
+    x2 = relu(x1 @ _w(p, "feat.conv2.weight").T + p["feat.conv2.bias"]).astype(F32)
+    trans, sc = stn_forward_train(p, x2, "feat.fstn.", 64)
+    x2t = np.matmul(x2, trans).astype(F32)
+    x3 = relu(x2t @ _w(p, "feat.conv3.weight").T + p["feat.conv3.bias"]).astype(F32)
+    W4 = _w(p, "feat.conv4.weight")
+    gmax, am = conv_max_fwd(x3, W4, p["feat.conv4.bias"])
+    logits, hc = head_fwd(gmax, p, mask)
+    l, dce = cross_entropy(logits, labels)
+    reg = feature_transform_regularizer(trans)
+    # head (reuse cls_backward's head part through a cache without the conv stack)
+    h1, h2, scale = hc
+    g = OrderedDict()
+    dl = (F32(lambda_cls) * dce).astype(F32)
+    g["fc3.weight"] = dl.T @ h2
+    g["fc3.bias"] = dl.sum(0)
+    dz2 = (dl @ p["fc3.weight"]) * (h2 > 0)
+    if scale is not None:
+        dz2 = dz2 * scale
+    g["fc2.weight"] = dz2.T @ h1
+    g["fc2.bias"] = dz2.sum(0)
+    dz1 = (dz2 @ p["fc2.weight"]) * (h1 > 0)
+    g["fc1.weight"] = dz1.T @ gmax
+    g["fc1.bias"] = dz1.sum(0)
+    dgl = (dz1 @ p["fc1.weight"]).astype(F32)
+    dW4, db4, dX3 = conv_max_bwd(dgl, am, x3, W4)
+    g["feat.conv4.weight"], g["feat.conv4.bias"] = dW4[:, :, None], db4
+    dW3, db3, dx2t = _layer_bwd(dX3, x2t, x3, _w(p, "feat.conv3.weight"))
+    g["feat.conv3.weight"], g["feat.conv3.bias"] = dW3[:, :, None], db3
+    # x2t = x2 @ T (models/pointnet.py:120-121)
+    dT = np.matmul(x2.transpose(0, 2, 1), dx2t).astype(F32)
+    dT = dT + F32(lambda_regu) * regularizer_bwd(trans)
+    dx2 = np.matmul(dx2t, trans.transpose(0, 2, 1)).astype(F32)
+    gs, dx2s = stn_backward(p, sc, dT, "feat.fstn.")
+    g.update(gs)
+    dx2 = dx2 + dx2s
+    dW2, db2, dx1 = _layer_bwd(dx2, x1, x2, _w(p, "feat.conv2.weight"))
+    g["feat.conv2.weight"], g["feat.conv2.bias"] = dW2[:, :, None], db2
+    dW1, db1, _ = _layer_bwd(dx1, pts, x1, _w(p, "feat.conv1.weight"))
+    g["feat.conv1.weight"], g["feat.conv1.bias"] = dW1[:, :, None], db1
+    grads = OrderedDict((k, g[k].astype(F32).reshape(p[k].shape)) for k in p)
+    aux = dict(logits=logits, gmax=gmax, am=am, trans=trans, am_stn=sc["am"], x2t=x2t, x3=x3)
+    return l, reg, grads, aux
+
+
 # --------------------------------------------------------------------------
 # segmentation net (models/pointnet.py:261-317) - forward only
 # --------------------------------------------------------------------------

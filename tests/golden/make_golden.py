@@ -62,7 +62,7 @@ def make_mask(rng, B, width=256, p=0.3):
     return (rng.random((B, width)) >= p).astype(np.float32)
 
 
-def main(ref_root):
+def main(ref_root, only=None):
     sys.dont_write_bytecode = True
     sys.path.insert(0, ref_root)
     import torch
@@ -92,6 +92,64 @@ def main(ref_root):
                 return x
             m = torch.from_numpy(self.masks.pop(0))
             return x * (m / (1.0 - self.p))
+
+    # ---------------- G7: feature-transform cls step (run_training_pointnet_cls) ----
+    # utils/trainer.py:222-268 with PointNetCls(feature_transform=True): loss =
+    # lambda_cls * CE + lambda_regu * feature_transform_regularizer(trans_feat).
+    # The reference regularizer moves its identity to CUDA (models/pointnet.py:
+    # 345-353); the harness swaps in the same formula with a CPU identity.
+    def g7():
+        Gf7 = onp.make_params(onp.cls_ft_spec(40), seed=7)
+        rng = np.random.default_rng(71)
+        pts7 = rng.uniform(-1, 1, (B_SMALL, N_PTS, 3)).astype(np.float32)
+        lab7 = rng.integers(0, 40, B_SMALL).astype(np.int64)
+        mask7 = make_mask(rng, B_SMALL)
+        model = load(PointNetCls(k=40, feature_transform=True), Gf7)
+        model.dropout = MaskDropout([mask7.copy()])
+        rec = {"cls": [], "reg": []}
+
+        def reg_cpu(trans):
+            d = trans.size(1)
+            r = torch.mean(torch.norm(torch.bmm(trans, trans.transpose(2, 1)) -
+                                      torch.eye(d)[None], dim=(1, 2)))
+            rec["reg"].append(float(r.item()))
+            return r
+
+        class RecCE(nn.Module):
+            def forward(self, a, b):
+                r = nn.functional.cross_entropy(a, b)
+                rec["cls"].append(float(r.item()))
+                return r
+
+        optimizer = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        args = argparse.Namespace(device=torch.device("cpu"), total_iterations=1, lambda_cls=1.0,
+                                  lambda_regu=0.001, iter_save_epoch=10 ** 9,
+                                  iter_test_epoch=10 ** 9, exp_dir=tempfile.mkdtemp(prefix="g7_"),
+                                  tensorboard=False, batch_size=B_SMALL)
+        logger = logging.getLogger("golden7")
+        logger.addHandler(logging.NullHandler())
+        logger.propagate = False
+        batch = (torch.from_numpy(pts7), torch.from_numpy(lab7))
+        orig = rtrainer.feature_transform_regularizer
+        rtrainer.feature_transform_regularizer = reg_cpu
+        try:
+            rtrainer.run_training_pointnet_cls(
+                trainloader_gt=[batch], trainloader_gt_iter=enumerate([batch]),
+                testloader=[batch], model=model, cls_loss=RecCE(), optimizer=optimizer,
+                train_logger=logger, test_logger=logger, writer=None, args=args)
+        finally:
+            rtrainer.feature_transform_regularizer = orig
+        out = dict(g_seed=7, data_seed=71, B=B_SMALL, N=N_PTS, pts=pts7, labels=lab7,
+                   mask=mask7, lambda_cls=1.0, lambda_regu=0.001,
+                   loss_cls=np.float64(rec["cls"][0]), reg=np.float64(rec["reg"][0]))
+        for name, p in model.named_parameters():
+            summarize("grad." + name, p.grad.numpy(), out)
+            summarize("param." + name, p.detach().numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g7_cls_ft_step.npz"), **out)
+
+    if only == "g7":
+        g7()
+        return
 
     # ---------------- G1: cls forward (eval) ----------------
     G = onp.make_params(onp.cls_spec(40), seed=1)
@@ -241,6 +299,9 @@ def main(ref_root):
                         logits=lg.numpy(), gmax=gl.numpy()[:, :, 0], trans=trans.numpy(),
                         reg=np.float64(reg.item()))
 
+    g7()
+
+
     # ---------------- G6: segmentation forward ----------------
     Sp = onp.make_params(onp.seg_spec(50), seed=6)
     ms = load(PointNetSeg(50), Sp).eval()
@@ -260,4 +321,8 @@ def main(ref_root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("ref_root", nargs="?", default="/root/reference")
+    ap.add_argument("--only", default=None, help="g7: regenerate only that fixture")
+    a = ap.parse_args()
+    main(a.ref_root, a.only)

@@ -105,3 +105,21 @@ def test_g6_seg():
     out, g = onp.seg_forward(S, pts, fx["cls"])
     assert rel_err(g[:, :, 0], fx["gmax"]) < 1e-4
     check_tensor(fx, "out", out, tol=1e-4)
+
+
+def test_g7_cls_ft_step():
+    """run_training_pointnet_cls with feature_transform=True (T-Net path, SURVEY
+    row a7): CE + 0.001 * regularizer, gradients of every parameter and the
+    parameters after the Adam step."""
+    fx = load("g7_cls_ft_step.npz")
+    G = onp.make_params(onp.cls_ft_spec(40), seed=int(fx["g_seed"]))
+    l, reg, grads, _ = onp.cls_ft_step(G, fx["pts"], fx["labels"], fx["mask"],
+                                       float(fx["lambda_cls"]), float(fx["lambda_regu"]))
+    assert abs(l - float(fx["loss_cls"])) < 1e-4
+    assert abs(reg - float(fx["reg"])) < 1e-3
+    for name, g in grads.items():
+        check_tensor(fx, "grad." + name, g, tol=1e-4)
+    opt = onp.Adam(G)
+    opt.step(grads)
+    for name, v in G.items():
+        check_tensor(fx, "param." + name, v, tol=1e-5)
