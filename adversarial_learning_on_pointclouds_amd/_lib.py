@@ -78,10 +78,18 @@ SIGNATURES = {
     "pcadv_feat_bwd_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_feat_bwd": (_i, [_vp, _vp, _vp, _i, _i] + [_vp] * 7 + [_vp] * 8 + [_vp, _sz, _vp]),
     "pcadv_conv_max_fwd": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp]),
-    "pcadv_linear_fwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _u64, _f, _vp]),
+    "pcadv_linear_fwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _u64, _f, _i, _vp]),
     "pcadv_linear_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _u64, _f, _vp, _vp, _vp, _vp, _vp,
                               _i, _i, _i, _i, _vp]),
     "pcadv_adam": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _vp]),
+    "pcadv_pw_fwd": (_i, [_vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "pcadv_pw_bwd_data": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp]),
+    "pcadv_pw_bwd_weight_workspace_bytes": (_sz, [_i, _i, _i]),
+    "pcadv_pw_bwd_weight": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _sz,
+                                 _vp]),
+    "pcadv_conv_max_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "pcadv_tnet_reg_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "pcadv_tnet_reg_bwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_adv_step_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_adv_step": (_i, [ctypes.POINTER(AdvArgs), _vp]),
     "pcadv_adv_step_adam": (_i, [ctypes.POINTER(AdvArgs), _vp]),

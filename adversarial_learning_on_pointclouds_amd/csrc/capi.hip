@@ -33,7 +33,18 @@ int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float
                           const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
                           hipStream_t, uint64_t* stamps = nullptr, int stagger = 20);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
-                      const float*, const int32_t*, uint64_t, float, hipStream_t);
+                      const float*, const int32_t*, uint64_t, float, hipStream_t,
+                      int add_identity_k = 0);
+int launch_pw_fwd(const float*, int, int, const float*, const float*, int, int, int, int, float*,
+                  hipStream_t);
+int launch_pw_bwd_data(const float*, const float*, int, int, int, const float*, int, int, int,
+                       float*, int, hipStream_t);
+size_t pw_bwd_weight_workspace_bytes(int M, int O, int K);
+int launch_pw_bwd_weight(const float*, const float*, int, const float*, int, int, int, int, int,
+                         float*, float*, void*, size_t, hipStream_t);
+int launch_convmax_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
+                       const float*, int, float*, float*, float*, hipStream_t);
+int launch_tnet_reg(const float*, int, int, float*, float*, const float*, float*, hipStream_t);
 int launch_linear_bwd(const float*, const float*, int, const float*, const int32_t*, uint64_t,
                       float, const float*, const float*, float*, float*, float*, int, int, int,
                       int, hipStream_t);
@@ -225,7 +236,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 1; }
+int pcadv_abi_version(void) { return 2; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -284,9 +295,49 @@ int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, cons
 
 int pcadv_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int Nout,
                      int K, int act, const float* drop_mask, const int32_t* rng_step,
-                     uint64_t rng_seed, float drop_p, hipStream_t stream) {
+                     uint64_t rng_seed, float drop_p, int add_identity_k, hipStream_t stream) {
   return launch_linear_fwd(x, w, b, y, M, Nout, K, act, drop_mask, rng_step, rng_seed, drop_p,
-                           stream);
+                           stream, add_identity_k);
+}
+
+int pcadv_pw_fwd(const float* x, int M, int K, const float* w, const float* b, int O, int act,
+                 int w_kmajor, int rows_per_w, float* y, hipStream_t stream) {
+  return launch_pw_fwd(x, M, K, w, b, O, act, w_kmajor, rows_per_w, y, stream);
+}
+
+int pcadv_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,
+                      int K, int w_kmajor, int rows_per_w, float* dx, int accumulate,
+                      hipStream_t stream) {
+  return launch_pw_bwd_data(dy, y, act, M, O, w, K, w_kmajor, rows_per_w, dx, accumulate, stream);
+}
+
+size_t pcadv_pw_bwd_weight_workspace_bytes(int M, int O, int K) {
+  return pw_bwd_weight_workspace_bytes(M, O, K);
+}
+
+int pcadv_pw_bwd_weight(const float* dy, const float* y, int act, const float* x, int M, int O,
+                        int K, int rows_per_group, int dw_kmajor, float* dw, float* db,
+                        void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  return launch_pw_bwd_weight(dy, y, act, x, M, O, K, rows_per_group, dw_kmajor, dw, db,
+                              workspace, workspace_bytes, stream);
+}
+
+int pcadv_conv_max_bwd(const float* dgmax, const int32_t* gidx, const float* gmax_relu,
+                       const float* x, int C, int N, int K, const float* w, int O, float* dw,
+                       float* db, float* dx, hipStream_t stream) {
+  return launch_convmax_bwd(dgmax, gidx, gmax_relu, x, C, N, K, w, O, dw, db, dx, stream);
+}
+
+int pcadv_tnet_reg_fwd(const float* T, int B, int k, float* norms, float* reg,
+                       hipStream_t stream) {
+  PC_REQUIRE(norms && reg, "tnet_reg_fwd: norms and reg are required");
+  return launch_tnet_reg(T, B, k, norms, reg, nullptr, nullptr, stream);
+}
+
+int pcadv_tnet_reg_bwd(const float* T, int B, int k, const float* grad_reg, float* dT,
+                       hipStream_t stream) {
+  PC_REQUIRE(grad_reg && dT, "tnet_reg_bwd: grad_reg and dT are required");
+  return launch_tnet_reg(T, B, k, nullptr, nullptr, grad_reg, dT, stream);
 }
 
 int pcadv_linear_bwd(const float* dy, const float* y, int act, const float* drop_mask,

@@ -50,6 +50,7 @@ struct GemmArgs {
   float* dw;
   float* db;
   int M, N, K, m_w;
+  int diag;  // forward: add the k x k identity to the flattened output (0: off)
 };
 
 // dropout scale s at (m, n) of an [M][N] output
@@ -127,13 +128,13 @@ __device__ __forceinline__ void load_ab(const GemmArgs& g, int r0, int c0, int r
 // branch-free and every load is issued before the first MFMA.
 template <int OP, int NC, int ACT, int DM>
 __device__ __forceinline__ f32x4v wave_tile(const GemmArgs& g, int r0, int c0, int k0, int nch,
-                                            int lane, uint32_t step, float* asum) {
+                                            int lane, uint32_t step, float* asum,
+                                            f32x4v acc = {0.f, 0.f, 0.f, 0.f}) {
   const int r = lane & 15, q = lane >> 4;
   float a[NC][4], b[NC][4];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
     load_ab<OP, ACT, DM>(g, r0, c0, r, k0 + 16 * c + 4 * q, c < nch, step, a[c], b[c]);
-  f32x4v acc = {0.f, 0.f, 0.f, 0.f};
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -157,10 +158,15 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
   const int ctiles = (cols + 15) / 16;
   const int r0 = (tile / ctiles) * 16, c0 = (tile % ctiles) * 16;
   const int k0 = wave * L;
-  int nch = 0;
-  if (k0 < R) nch = min(L, R - k0 + 15) / 16;
-  float s;
-  f32x4v acc = wave_tile<OP, SPLITC, ACT, DM>(g, r0, c0, k0, nch, lane, step, &s);
+  // a slice longer than 16 * SPLITC (reductions > 1024) runs in rounds
+  f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+  for (int base = 0; base < L; base += 16 * SPLITC) {
+    const int kb = k0 + base;
+    int nch = 0;
+    if (kb < R) nch = min(min(L - base, 16 * SPLITC), R - kb + 15) / 16;
+    float s;
+    acc = wave_tile<OP, SPLITC, ACT, DM>(g, r0, c0, kb, nch, lane, step, &s, acc);
+  }
   const int col = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[wave * 256 + (4 * q + j) * 16 + col] = acc[j];
@@ -175,7 +181,10 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
         const size_t i = (size_t)m * g.N + n;
         v += g.b[n];
         if (DM != DM_NONE) v *= drop_scale<DM>(g, i, m, n, step);
-        g.y[i] = act_fwd(v, ACT);
+        float o = act_fwd(v, ACT);
+        // STNkd / STN3d add the flattened identity (models/pointnet.py:38-41,74-77)
+        if (g.diag && n % (g.diag + 1) == 0) o += 1.f;
+        g.y[i] = o;
       } else {
         g.dx[(size_t)m * g.K + n] = v;
       }
@@ -263,11 +272,13 @@ static void split_cfg(int R, int* S, int* L) {
 
 int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N,
                       int K, int act, const float* mask, const int32_t* step, uint64_t seed,
-                      float p, hipStream_t s) {
-  PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0 && K <= 16 * 16 * SPLITC,
-             "linear_fwd: bad shape M=%d N=%d K=%d", M, N, K);
+                      float p, hipStream_t s, int add_identity_k) {
+  PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0, "linear_fwd: bad shape M=%d N=%d K=%d", M, N,
+             K);
+  PC_REQUIRE(add_identity_k == 0 || add_identity_k * add_identity_k == N,
+             "linear_fwd: identity of size %d does not match %d outputs", add_identity_k, N);
   GemmArgs g{};
-  g.x = x; g.w = w; g.b = b; g.y = y; g.act = act;
+  g.x = x; g.w = w; g.b = b; g.y = y; g.act = act; g.diag = add_identity_k;
   g.drop = DropSpec{mask, step, seed, p};
   g.M = M; g.N = N; g.K = K;
   int S, L;
@@ -284,7 +295,7 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
                       float* dx, float* dw, float* db, int M, int m_w, int N, int K,
                       hipStream_t s) {
   PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0 && m_w >= 0 && m_w <= M &&
-                 m_w <= 16 * MAXC && N <= 16 * 16 * SPLITC,
+                 m_w <= 16 * MAXC,
              "linear_bwd: bad shape M=%d m_w=%d N=%d K=%d", M, m_w, N, K);
   GemmArgs g{};
   g.x = x; g.w = w; g.dy = dy; g.yact = y; g.act = act;

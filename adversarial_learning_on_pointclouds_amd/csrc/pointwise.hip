@@ -1,0 +1,561 @@
+// Point-wise layers of the feature-transform path on gfx950
+// (PointNetCls(feature_transform=True): STNkd models/pointnet.py:46-79, the
+// feature transform bmm :118-122, feature_transform_regularizer :345-353).
+//
+//   k_pw_fwd        y = act(x w^T + b) over rows = points (1x1 Conv1d), K = 64/128
+//                   on v_mfma_f32_32x32x2_f32; K = 3 on the VALU.  The weight may
+//                   be one matrix per cloud in either layout, so the same kernel
+//                   runs the per-cloud transform x2 . T (bmm).
+//   k_pw_bwd_data   dx = (dy * act'(y)) w, optionally accumulated into dx
+//   k_pw_bwd_weight per-256-row partial dW / db slabs (one group = all rows, or
+//                   one cloud for dT), then k_pw_reduce sums the slabs in order
+//   k_convmax_bwd   sparse backward of conv + max over points (optionally with
+//                   the ReLU before the max): dW/db by gathering the argmax rows,
+//                   dX rows from the hits sorted by channel (deterministic)
+//   k_tnet_reg      ||T T^T - I||_F per cloud, and its gradient
+// All reductions run in a fixed order: results are bitwise reproducible.
+#include "common.h"
+
+namespace pcadv {
+
+constexpr int PW_ROWS = 64;   // points per workgroup tile
+constexpr int PW_T = 256;     // 4 waves
+constexpr int PWW_ROWS = 256; // rows per weight-gradient slab
+constexpr int PWW_SUB = 32;   // rows staged in LDS at a time by the weight kernel
+
+// A weight operand: conv layout W[o][k], or "kmajor" T[k][o] (the bmm's
+// transform); one matrix per `rows_per_w` rows when rows_per_w > 0.
+struct WView {
+  const float* w;
+  int O, K;
+  int kmajor;
+  int rows_per_w;
+  long long stride;
+  __device__ const float* base(int row0) const {
+    return rows_per_w ? w + (size_t)(row0 / rows_per_w) * stride : w;
+  }
+  __device__ float get(const float* b, int o, int k) const {
+    return kmajor ? b[(size_t)k * O + o] : b[(size_t)o * K + k];
+  }
+};
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int K, int ACT>
+__global__ void __launch_bounds__(PW_T)
+k_pw_fwd(const float* __restrict__ x, int M, WView wv, const float* __restrict__ b,
+         float* __restrict__ y) {
+  constexpr int SK = K + 4;
+  __shared__ __attribute__((aligned(16))) float xs[PW_ROWS * SK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * PW_ROWS, o0 = blockIdx.y * 128;
+  const int O = wv.O;
+  const float* w = wv.base(r0);
+  for (int e = tid; e < PW_ROWS * K / 4; e += PW_T) {
+    const int row = e / (K / 4), c4 = e % (K / 4);
+    const f32x4 v = r0 + row < M ? *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + row) * K + 4 * c4)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(xs + row * SK + 4 * c4) = v;
+  }
+  __syncthreads();
+  const int oc = o0 + 32 * wave;
+  if (oc >= O) return;  // O % 32 == 0: whole waves leave
+  const int r = lane & 31, h = lane >> 5;
+  f32x4 bf[K / 8];
+#pragma unroll
+  for (int g = 0; g < K / 8; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, oc + r, 8 * g + 4 * h + j);
+  f32x16 acc0 = {}, acc1 = {};
+  acc0 = mfma_rows_x_wt<K>(xs, SK, bf, acc0, lane);
+  acc1 = mfma_rows_x_wt<K>(xs + 32 * SK, SK, bf, acc1, lane);
+  const int col = oc + r;
+  const float bias = b ? b[col] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ra = r0 + acc_row(i, lane), rb = ra + 32;
+    if (ra < M) y[(size_t)ra * O + col] = act_fwd(acc0[i] + bias, ACT);
+    if (rb < M) y[(size_t)rb * O + col] = act_fwd(acc1[i] + bias, ACT);
+  }
+}
+
+// K = 3 (conv1 on the points): thread = (column, 32-row group), VALU, the fma
+// order of conv1_point (shared with the fused classifier kernels)
+template <int ACT>
+__global__ void __launch_bounds__(PW_T)
+k_pw_fwd3(const float* __restrict__ x, int M, WView wv, const float* __restrict__ b,
+          float* __restrict__ y) {
+  __shared__ float xs[PW_ROWS * 4];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * PW_ROWS, o0 = blockIdx.y * 128;
+  const int O = wv.O;
+  const float* w = wv.base(r0);
+  if (tid < PW_ROWS * 3) {
+    const int row = tid / 3, k = tid % 3;
+    xs[row * 4 + k] = r0 + row < M ? x[(size_t)(r0 + row) * 3 + k] : 0.f;
+  }
+  __syncthreads();
+  const int o = o0 + (tid & 127), rg = tid >> 7;
+  if (o >= O) return;
+  const float wa = wv.get(w, o, 0), wb = wv.get(w, o, 1), wc = wv.get(w, o, 2);
+  const float bb = b ? b[o] : 0.f;
+  for (int i = 0; i < 32; ++i) {
+    const int row = 32 * rg + i;
+    if (r0 + row >= M) break;
+    const float v = fmaf(wc, xs[row * 4 + 2], fmaf(wb, xs[row * 4 + 1], fmaf(wa, xs[row * 4], bb)));
+    y[(size_t)(r0 + row) * O + o] = act_fwd(v, ACT);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward, input gradient: dx[m][k] (+)= sum_o dz[m][o] w[o][k], dz = dy act'(y)
+// ---------------------------------------------------------------------------
+template <int R, int ACT>
+__global__ void __launch_bounds__(PW_T)
+k_pw_bwd_data(const float* __restrict__ dy, const float* __restrict__ yv, int M, WView wv,
+              float* __restrict__ dx, int accumulate) {
+  constexpr int SR = R + 4;
+  __shared__ __attribute__((aligned(16))) float zs[PW_ROWS * SR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * PW_ROWS, k0 = blockIdx.y * 128;
+  const int K = wv.K;
+  const float* w = wv.base(r0);
+  for (int e = tid; e < PW_ROWS * R / 4; e += PW_T) {
+    const int row = e / (R / 4), c4 = e % (R / 4);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r0 + row < M) {
+      v = *reinterpret_cast<const f32x4*>(dy + (size_t)(r0 + row) * R + 4 * c4);
+      if (ACT != ACT_NONE) {
+        const f32x4 yy = *reinterpret_cast<const f32x4*>(yv + (size_t)(r0 + row) * R + 4 * c4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= act_bwd(yy[j], ACT);
+      }
+    }
+    *reinterpret_cast<f32x4*>(zs + row * SR + 4 * c4) = v;
+  }
+  __syncthreads();
+  const int kc = k0 + 32 * wave;
+  if (kc >= K) return;  // K % 32 == 0
+  const int r = lane & 31, h = lane >> 5;
+  // B[o][k] = w[o][k]: lane (r, h) holds column kc + r at o = 8g + 4h + j
+  f32x4 bf[R / 8];
+#pragma unroll
+  for (int g = 0; g < R / 8; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, 8 * g + 4 * h + j, kc + r);
+  f32x16 acc0 = {}, acc1 = {};
+  acc0 = mfma_rows_x_wt<R>(zs, SR, bf, acc0, lane);
+  acc1 = mfma_rows_x_wt<R>(zs + 32 * SR, SR, bf, acc1, lane);
+  const int col = kc + r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ra = r0 + acc_row(i, lane), rb = ra + 32;
+    if (ra < M) {
+      float* p = dx + (size_t)ra * K + col;
+      *p = accumulate ? *p + acc0[i] : acc0[i];
+    }
+    if (rb < M) {
+      float* p = dx + (size_t)rb * K + col;
+      *p = accumulate ? *p + acc1[i] : acc1[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward, weight gradient: per PWW_ROWS rows a slab of dW (O x K, layout
+// [o][k] or [k][o]) and db (O)
+// ---------------------------------------------------------------------------
+template <int O, int K, int ACT>
+__global__ void __launch_bounds__(PW_T)
+k_pw_bwd_weight(const float* __restrict__ dy, const float* __restrict__ yv,
+                const float* __restrict__ x, int M, int kmajor, float* __restrict__ slabs) {
+  constexpr int SO = O + 32, SX = K + 32;  // row strides = 32 banks mod 64: conflict-free
+  constexpr int NTILE = (O / 32) * (K / 32), NT = (NTILE + 3) / 4;
+  __shared__ __attribute__((aligned(16))) float zs[PWW_SUB * SO];
+  __shared__ __attribute__((aligned(16))) float xs[PWW_SUB * SX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int rbase = blockIdx.x * PWW_ROWS;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+  float dbacc = 0.f;
+  for (int sub = 0; sub < PWW_ROWS / PWW_SUB; ++sub) {
+    const int r0 = rbase + sub * PWW_SUB;
+    for (int e = tid; e < PWW_SUB * O / 4; e += PW_T) {
+      const int row = e / (O / 4), c4 = e % (O / 4);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r0 + row < M) {
+        v = *reinterpret_cast<const f32x4*>(dy + (size_t)(r0 + row) * O + 4 * c4);
+        if (ACT != ACT_NONE) {
+          const f32x4 yy = *reinterpret_cast<const f32x4*>(yv + (size_t)(r0 + row) * O + 4 * c4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] *= act_bwd(yy[j], ACT);
+        }
+      }
+      *reinterpret_cast<f32x4*>(zs + row * SO + 4 * c4) = v;
+    }
+    for (int e = tid; e < PWW_SUB * K / 4; e += PW_T) {
+      const int row = e / (K / 4), c4 = e % (K / 4);
+      const f32x4 v = r0 + row < M ? *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + row) * K + 4 * c4)
+                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(xs + row * SX + 4 * c4) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int tile = wave + 4 * t;
+      if (tile < NTILE) {
+        const int ot = tile / (K / 32), kt = tile % (K / 32);
+        const float* ap = zs + h * SO + 32 * ot + r;
+        const float* bp = xs + h * SX + 32 * kt + r;
+#pragma unroll
+        for (int s = 0; s < PWW_SUB / 2; ++s)
+          acc[t] = mfma32(ap[2 * s * SO], bp[2 * s * SX], acc[t]);
+      }
+    }
+    if (tid < O)
+      for (int row = 0; row < PWW_SUB; ++row) dbacc += zs[row * SO + tid];
+    __syncthreads();
+  }
+  float* slab = slabs + (size_t)blockIdx.x * (O * K + O);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tile = wave + 4 * t;
+    if (tile < NTILE) {
+      const int ot = tile / (K / 32), kt = tile % (K / 32);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int o = 32 * ot + acc_row(i, lane), k = 32 * kt + r;
+        slab[kmajor ? k * O + o : o * K + k] = acc[t][i];
+      }
+    }
+  }
+  if (tid < O) slab[O * K + tid] = dbacc;
+}
+
+// K = 3 (conv1 weights over the points): thread = (o, k) with k = 3 -> bias
+__global__ void __launch_bounds__(PW_T)
+k_pw_bwd_weight3(const float* __restrict__ dy, const float* __restrict__ yv, int act,
+                 const float* __restrict__ x, int M, int O, float* __restrict__ slabs) {
+  const int tid = threadIdx.x;
+  const int o = tid % O, k = tid / O;  // O <= 64: 4 * O <= 256 threads
+  const int rbase = blockIdx.x * PWW_ROWS;
+  float acc = 0.f;
+  if (k < 4) {
+    for (int i = 0; i < PWW_ROWS; ++i) {
+      const int m = rbase + i;
+      if (m >= M) break;
+      float z = dy[(size_t)m * O + o];
+      if (act != ACT_NONE) z *= act_bwd(yv[(size_t)m * O + o], act);
+      acc = fmaf(z, k < 3 ? x[(size_t)m * 3 + k] : 1.f, acc);
+    }
+    float* slab = slabs + (size_t)blockIdx.x * (O * 3 + O);
+    if (k < 3) slab[o * 3 + k] = acc;
+    else slab[O * 3 + o] = acc;
+  }
+}
+
+// out[g][j] = sum_{s < per} slabs[g*per + s][j] in slab order; j < W: dW,
+// j = W.. : db
+__global__ void __launch_bounds__(256)
+k_pw_reduce(const float* __restrict__ slabs, int per, int width, int wsize,
+            float* __restrict__ dw, float* __restrict__ db) {
+  const int j = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+  if (j >= width) return;
+  const float* s = slabs + (size_t)g * per * width + j;
+  float acc = 0.f;
+  for (int i = 0; i < per; ++i) acc += s[(size_t)i * width];
+  if (j < wsize) dw[(size_t)g * wsize + j] = acc;
+  else if (db) db[(size_t)g * (width - wsize) + j - wsize] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// conv + max over points, backward (sparse; optional ReLU before the max)
+// ---------------------------------------------------------------------------
+constexpr int CMB_PCH = 128;  // points per workgroup
+constexpr int CMB_T = 512;
+constexpr int CMB_MAXO = 1024;
+
+struct CmbLds {
+  int so[CMB_MAXO];
+  float sg[CMB_MAXO];
+  int okey[CMB_MAXO];
+  float ogv[CMB_MAXO];
+  int rcnt[CMB_PCH], fill[CMB_PCH], roff[CMB_PCH];
+  int wsum[2];
+};
+
+__device__ __forceinline__ float cm_g(const float* dg, const float* gmax, size_t i) {
+  const float g = dg[i];
+  return gmax ? (gmax[i] > 0.f ? g : 0.f) : g;
+}
+
+// blocks [0, C * nchunk): dX rows of one (cloud, 128-point chunk); the rest:
+// dW/db, one wave per output channel
+__global__ void __launch_bounds__(CMB_T)
+k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
+              const float* __restrict__ gmax, const float* __restrict__ x, int C, int N, int K,
+              const float* __restrict__ w, int O, float* __restrict__ dw, float* __restrict__ db,
+              float* __restrict__ dx, int nchunk) {
+  __shared__ CmbLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nxb = dx ? C * nchunk : 0;
+  if ((int)blockIdx.x >= nxb) {
+    // ---- dW[o,:] = sum_c g'[c,o] x[c, gidx[c,o], :], db[o] = sum_c g'[c,o]
+    const int o = ((int)blockIdx.x - nxb) * 8 + wave;
+    if (o >= O) return;
+    float a0 = 0.f, a1 = 0.f, ab = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const size_t i = (size_t)c * O + o;
+      const float g = cm_g(dg, gmax, i);
+      const float* row = x + ((size_t)c * N + gidx[i]) * K;
+      if (lane < K) a0 = fmaf(g, row[lane], a0);
+      if (lane + 64 < K) a1 = fmaf(g, row[lane + 64], a1);
+      ab += g;
+    }
+    if (lane < K) dw[(size_t)o * K + lane] = a0;
+    if (lane + 64 < K) dw[(size_t)o * K + lane + 64] = a1;
+    if (lane == 0 && db) db[o] = ab;
+    return;
+  }
+  // ---- dX rows: hits (channels whose argmax is in the chunk) sorted by (row, o)
+  const int c = blockIdx.x / nchunk, p0 = (blockIdx.x % nchunk) * CMB_PCH;
+  if (tid < CMB_PCH) {
+    L.rcnt[tid] = 0;
+    L.fill[tid] = 0;
+  }
+  __syncthreads();
+  constexpr int PER = CMB_MAXO / CMB_T;
+  int hrow[PER];
+  float hg[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int o = u * CMB_T + tid;
+    const int a = o < O ? gidx[(size_t)c * O + o] : -1;
+    const bool hit = a >= p0 && a < p0 + CMB_PCH;
+    hrow[u] = hit ? a - p0 : -1;
+    hg[u] = hit ? cm_g(dg, gmax, (size_t)c * O + o) : 0.f;
+    if (hit) atomicAdd(&L.rcnt[a - p0], 1);
+  }
+  __syncthreads();
+  if (wave < 2) {
+    const int cnt = L.rcnt[tid];
+    int v = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(v, d);
+      if (lane >= d) v += t;
+    }
+    if (lane == 63) L.wsum[wave] = v;
+    L.roff[tid] = v - cnt;
+  }
+  __syncthreads();
+  if (wave == 1) L.roff[tid] += L.wsum[0];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < PER; ++u)
+    if (hrow[u] >= 0) {
+      const int p = L.roff[hrow[u]] + atomicAdd(&L.fill[hrow[u]], 1);
+      L.okey[p] = u * CMB_T + tid;
+      L.ogv[p] = hg[u];
+    }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < PER; ++u)
+    if (hrow[u] >= 0) {
+      const int o = u * CMB_T + tid, s0 = L.roff[hrow[u]], s1 = s0 + L.rcnt[hrow[u]];
+      int rank = 0;
+      for (int j = s0; j < s1; ++j) rank += L.okey[j] < o;
+      L.so[s0 + rank] = o;
+      L.sg[s0 + rank] = hg[u];
+    }
+  __syncthreads();
+  // thread = (column k, row group): rows grp, grp + 4, ...; inactive rows -> 0
+  const int k = tid & 127, grp = tid >> 7;
+  if (k >= K) return;
+  for (int row = grp; row < CMB_PCH; row += 4) {
+    if (p0 + row >= N) break;
+    const int s0 = L.roff[row], s1 = s0 + L.rcnt[row];
+    float acc = 0.f;
+    for (int j = s0; j < s1; ++j) acc = fmaf(L.sg[j], w[(size_t)L.so[j] * K + k], acc);
+    dx[((size_t)c * N + p0 + row) * K + k] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// feature_transform_regularizer: ||T T^T - I||_F per cloud and its gradient
+// (2 * gscale / (B n_b)) (T T^T - I) T
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_tnet_reg(const float* __restrict__ T, int B, int k, float* __restrict__ norms,
+           const float* __restrict__ gscale, float* __restrict__ dT) {
+  extern __shared__ float sm[];
+  float* t = sm;              // k x k
+  float* a = sm + k * k;      // k x k
+  __shared__ double part[256];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const float* tb = T + (size_t)b * k * k;
+  for (int e = tid; e < k * k; e += 256) t[e] = tb[e];
+  __syncthreads();
+  double ss = 0.0;
+  for (int e = tid; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    float v = 0.f;
+    for (int l = 0; l < k; ++l) v = fmaf(t[i * k + l], t[j * k + l], v);
+    v -= (i == j) ? 1.f : 0.f;
+    a[e] = v;
+    ss += (double)v * v;
+  }
+  part[tid] = ss;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) part[tid] += part[tid + s];
+    __syncthreads();
+  }
+  const float n = (float)sqrt(part[0]);
+  if (!dT) {
+    if (tid == 0) norms[b] = n;
+    return;
+  }
+  const float scale = 2.f * (*gscale) / ((float)B * n);
+  for (int e = tid; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    float v = 0.f;
+    for (int l = 0; l < k; ++l) v = fmaf(a[i * k + l], t[l * k + j], v);
+    dT[(size_t)b * k * k + e] = scale * v;
+  }
+}
+
+__global__ void k_mean(const float* __restrict__ v, int n, float* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += v[i];
+    *out = (float)(s / n);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static WView make_view(const float* w, int O, int K, int kmajor, int rows_per_w) {
+  return WView{w, O, K, kmajor, rows_per_w, (long long)O * K};
+}
+
+int launch_pw_fwd(const float* x, int M, int K, const float* w, const float* b, int O, int act,
+                  int w_kmajor, int rows_per_w, float* y, hipStream_t s) {
+  PC_REQUIRE(M > 0 && (K == 3 || K == 64 || K == 128) && O > 0 && O % 32 == 0,
+             "pw_fwd: unsupported shape M=%d K=%d O=%d", M, K, O);
+  PC_REQUIRE(act == ACT_NONE || act == ACT_RELU, "pw_fwd: act %d", act);
+  PC_REQUIRE(rows_per_w == 0 || rows_per_w % PW_ROWS == 0,
+             "pw_fwd: rows per weight matrix (%d) must be a multiple of %d", rows_per_w, PW_ROWS);
+  const WView wv = make_view(w, O, K, w_kmajor, rows_per_w);
+  const dim3 grid((M + PW_ROWS - 1) / PW_ROWS, (O + 127) / 128);
+  if (K == 3) {
+    if (act == ACT_RELU) hipLaunchKernelGGL(k_pw_fwd3<ACT_RELU>, grid, dim3(PW_T), 0, s, x, M, wv, b, y);
+    else hipLaunchKernelGGL(k_pw_fwd3<ACT_NONE>, grid, dim3(PW_T), 0, s, x, M, wv, b, y);
+  }
+#define PW_CASE(KK, A)                                                                      \
+  if (K == KK && act == A)                                                                 \
+    hipLaunchKernelGGL((k_pw_fwd<KK, A>), grid, dim3(PW_T), 0, s, x, M, wv, b, y);
+  PW_CASE(64, ACT_NONE) PW_CASE(64, ACT_RELU) PW_CASE(128, ACT_NONE) PW_CASE(128, ACT_RELU)
+#undef PW_CASE
+  PC_HIP_CHECK_LAUNCH("k_pw_fwd");
+  return PCADV_OK;
+}
+
+int launch_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,
+                       int K, int w_kmajor, int rows_per_w, float* dx, int accumulate,
+                       hipStream_t s) {
+  PC_REQUIRE(M > 0 && (O == 64 || O == 128) && K > 0 && K % 32 == 0,
+             "pw_bwd_data: unsupported shape M=%d O=%d K=%d", M, O, K);
+  PC_REQUIRE(act == ACT_NONE || act == ACT_RELU, "pw_bwd_data: act %d", act);
+  PC_REQUIRE(rows_per_w == 0 || rows_per_w % PW_ROWS == 0, "pw_bwd_data: rows per weight %d",
+             rows_per_w);
+  PC_REQUIRE(act == ACT_NONE || y, "pw_bwd_data: the layer output is needed for act'");
+  const WView wv = make_view(w, O, K, w_kmajor, rows_per_w);
+  const dim3 grid((M + PW_ROWS - 1) / PW_ROWS, (K + 127) / 128);
+#define PW_CASE(R, A)                                                                      \
+  if (O == R && act == A)                                                                  \
+    hipLaunchKernelGGL((k_pw_bwd_data<R, A>), grid, dim3(PW_T), 0, s, dy, y, M, wv, dx, accumulate);
+  PW_CASE(64, ACT_NONE) PW_CASE(64, ACT_RELU) PW_CASE(128, ACT_NONE) PW_CASE(128, ACT_RELU)
+#undef PW_CASE
+  PC_HIP_CHECK_LAUNCH("k_pw_bwd_data");
+  return PCADV_OK;
+}
+
+size_t pw_bwd_weight_workspace_bytes(int M, int O, int K) {
+  const size_t nslab = (M + PWW_ROWS - 1) / PWW_ROWS;
+  return nslab * (size_t)(O * K + O) * sizeof(float);
+}
+
+int launch_pw_bwd_weight(const float* dy, const float* y, int act, const float* x, int M, int O,
+                         int K, int rows_per_group, int dw_kmajor, float* dw, float* db, void* ws,
+                         size_t ws_bytes, hipStream_t s) {
+  PC_REQUIRE(M > 0 && (O == 64 || O == 128) && (K == 3 || K == 64 || K == 128),
+             "pw_bwd_weight: unsupported shape M=%d O=%d K=%d", M, O, K);
+  PC_REQUIRE(act == ACT_NONE || act == ACT_RELU, "pw_bwd_weight: act %d", act);
+  PC_REQUIRE(rows_per_group == 0 || (M % rows_per_group == 0 && rows_per_group % PWW_ROWS == 0),
+             "pw_bwd_weight: rows per group %d must divide M=%d and be a multiple of %d",
+             rows_per_group, M, PWW_ROWS);
+  PC_REQUIRE(K != 3 || (!dw_kmajor && O <= 64), "pw_bwd_weight: K=3 needs O <= 64, [o][k]");
+  PC_REQUIRE(ws && ws_bytes >= pw_bwd_weight_workspace_bytes(M, O, K),
+             "pw_bwd_weight: workspace too small");
+  float* slabs = static_cast<float*>(ws);
+  const int nslab = (M + PWW_ROWS - 1) / PWW_ROWS;
+  if (K == 3) {
+    hipLaunchKernelGGL(k_pw_bwd_weight3, dim3(nslab), dim3(PW_T), 0, s, dy, y, act, x, M, O, slabs);
+  } else {
+#define PW_CASE(OO, KK, A)                                                                 \
+  if (O == OO && K == KK && act == A)                                                      \
+    hipLaunchKernelGGL((k_pw_bwd_weight<OO, KK, A>), dim3(nslab), dim3(PW_T), 0, s, dy, y, x, M, \
+                       dw_kmajor, slabs);
+    PW_CASE(64, 64, ACT_NONE) PW_CASE(64, 64, ACT_RELU) PW_CASE(64, 128, ACT_NONE)
+    PW_CASE(64, 128, ACT_RELU) PW_CASE(128, 64, ACT_NONE) PW_CASE(128, 64, ACT_RELU)
+    PW_CASE(128, 128, ACT_NONE) PW_CASE(128, 128, ACT_RELU)
+#undef PW_CASE
+  }
+  PC_HIP_CHECK_LAUNCH("k_pw_bwd_weight");
+  const int width = O * K + O;
+  const int groups = rows_per_group ? M / rows_per_group : 1;
+  const int per = rows_per_group ? rows_per_group / PWW_ROWS : nslab;
+  hipLaunchKernelGGL(k_pw_reduce, dim3((width + 255) / 256, groups), dim3(256), 0, s, slabs, per,
+                     width, O * K, dw, db);
+  PC_HIP_CHECK_LAUNCH("k_pw_reduce");
+  return PCADV_OK;
+}
+
+int launch_convmax_bwd(const float* dg, const int32_t* gidx, const float* gmax, const float* x,
+                       int C, int N, int K, const float* w, int O, float* dw, float* db,
+                       float* dx, hipStream_t s) {
+  PC_REQUIRE(C > 0 && N > 0 && K > 0 && K <= 128 && O > 0 && O <= CMB_MAXO && dw,
+             "convmax_bwd: unsupported shape C=%d N=%d K=%d O=%d", C, N, K, O);
+  const int nchunk = (N + CMB_PCH - 1) / CMB_PCH;
+  const int nxb = dx ? C * nchunk : 0;
+  hipLaunchKernelGGL(k_convmax_bwd, dim3(nxb + (O + 7) / 8), dim3(CMB_T), 0, s, dg, gidx, gmax, x,
+                     C, N, K, w, O, dw, db, dx, nchunk);
+  PC_HIP_CHECK_LAUNCH("k_convmax_bwd");
+  return PCADV_OK;
+}
+
+int launch_tnet_reg(const float* T, int B, int k, float* norms, float* reg,
+                    const float* gscale, float* dT, hipStream_t s) {
+  PC_REQUIRE(B > 0 && k > 0 && k <= 64, "tnet_reg: unsupported B=%d k=%d", B, k);
+  const size_t lds = 2 * (size_t)k * k * sizeof(float);
+  if (!dT) {
+    hipLaunchKernelGGL(k_tnet_reg, dim3(B), dim3(256), lds, s, T, B, k, norms, nullptr, nullptr);
+    PC_HIP_CHECK_LAUNCH("k_tnet_reg");
+    if (reg) {
+      hipLaunchKernelGGL(k_mean, dim3(1), dim3(64), 0, s, norms, B, reg);
+      PC_HIP_CHECK_LAUNCH("k_mean");
+    }
+    return PCADV_OK;
+  }
+  PC_REQUIRE(gscale, "tnet_reg: backward needs the upstream gradient");
+  hipLaunchKernelGGL(k_tnet_reg, dim3(B), dim3(256), lds, s, T, B, k, norms, gscale, dT);
+  PC_HIP_CHECK_LAUNCH("k_tnet_reg");
+  return PCADV_OK;
+}
+
+}  // namespace pcadv

@@ -12,7 +12,10 @@ from . import _lib
 from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, check, ptr, stream_ptr
 
 __all__ = ["ACT_NONE", "ACT_RELU", "ACT_LRELU", "feat_fwd", "feat_bwd", "conv_max_fwd",
-           "linear_fwd", "linear_bwd", "adam_", "PointFeatFunction", "LinearFunction"]
+           "conv_max_bwd", "linear_fwd", "linear_bwd", "adam_", "pw_fwd", "pw_bwd_data",
+           "pw_bwd_weight", "tnet_reg_fwd", "tnet_reg_bwd", "PointFeatFunction",
+           "LinearFunction", "PointwiseFunction", "TransformFunction", "ConvMaxFunction",
+           "RegularizerFunction"]
 
 
 def _req(t, name, shape=None, dtype=torch.float32):
@@ -101,11 +104,119 @@ def conv_max_fwd(x, w, b, relu_before_max=False):
     return gmax, gidx
 
 
+def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True):
+    """Backward of conv_max_fwd: (dx (C, N, K) or None, dw like w, db (O,))."""
+    lib = _lib.load()
+    _req(x, "x")
+    C, N, K = x.shape
+    wm = _req(_mat(w), "w")
+    O = wm.shape[0]
+    _req(dgmax, "dgmax", (C, O))
+    _req(gidx, "gidx", (C, O), torch.int32)
+    if gmax_relu is not None:
+        _req(gmax_relu, "gmax", (C, O))
+    dx = torch.empty(C, N, K, device=x.device) if need_dx else None
+    dw = torch.empty_like(w)
+    db = torch.empty(O, device=x.device)
+    check(lib.pcadv_conv_max_bwd(ptr(dgmax), ptr(gidx), ptr(gmax_relu), ptr(x), C, N, K, ptr(wm),
+                                 O, ptr(dw), ptr(db), ptr(dx), stream_ptr()), "pcadv_conv_max_bwd")
+    return dx, dw, db
+
+
+# ---------------------------------------------------------------------------
+# point-wise layers (rows = points): the feature-transform path
+# ---------------------------------------------------------------------------
+
+def _rows(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+def pw_fwd(x, w, b, act, kmajor=False, rows_per_w=0):
+    """act(x W^T + b) over the last dim of x (..., K) -> (..., O).  W: Conv1d
+    weight [O, K(, 1)], or with kmajor a [K, O] matrix (per rows_per_w rows:
+    a (G, K, O) stack, e.g. one transform per cloud)."""
+    lib = _lib.load()
+    _req(x, "x")
+    K = x.shape[-1]
+    M = x.numel() // K
+    if kmajor:
+        _req(w, "w")
+        O = w.shape[-1]
+    else:
+        wm = _req(_mat(w), "w")
+        O = wm.shape[0]
+    if b is not None:
+        _req(b, "b", (O,))
+    y = torch.empty(*x.shape[:-1], O, device=x.device)
+    check(lib.pcadv_pw_fwd(ptr(x), M, K, ptr(w), ptr(b), O, act, int(bool(kmajor)), rows_per_w,
+                           ptr(y), stream_ptr()), "pcadv_pw_fwd")
+    return y
+
+
+def pw_bwd_data(dy, y, act, w, K, kmajor=False, rows_per_w=0, out=None):
+    """dx = (dy * act'(y)) W; accumulated into `out` when given."""
+    lib = _lib.load()
+    _req(dy, "dy")
+    O = dy.shape[-1]
+    M = dy.numel() // O
+    if y is not None:
+        _req(y, "y", tuple(dy.shape))
+    dx = out if out is not None else torch.empty(*dy.shape[:-1], K, device=dy.device)
+    _req(dx, "dx", tuple(dy.shape[:-1]) + (K,))
+    check(lib.pcadv_pw_bwd_data(ptr(dy), ptr(y), act, M, O, ptr(w), K, int(bool(kmajor)),
+                                rows_per_w, ptr(dx), int(out is not None), stream_ptr()),
+          "pcadv_pw_bwd_data")
+    return dx
+
+
+def pw_bwd_weight(dy, y, act, x, rows_per_group=0, kmajor=False, need_db=True):
+    """(dW, db) of y = act(x W^T + b): dW (groups, O, K) or kmajor (groups, K, O)."""
+    lib = _lib.load()
+    _req(dy, "dy")
+    _req(x, "x")
+    O, K = dy.shape[-1], x.shape[-1]
+    M = dy.numel() // O
+    if y is not None:
+        _req(y, "y", tuple(dy.shape))
+    G = rows_per_group if rows_per_group else M
+    groups = M // G
+    dw = torch.empty(groups, *((K, O) if kmajor else (O, K)), device=dy.device)
+    db = torch.empty(groups, O, device=dy.device) if need_db else None
+    nb = lib.pcadv_pw_bwd_weight_workspace_bytes(M, O, K)
+    ws = torch.empty(nb, device=dy.device, dtype=torch.uint8)
+    check(lib.pcadv_pw_bwd_weight(ptr(dy), ptr(y), act, ptr(x), M, O, K, rows_per_group,
+                                  int(bool(kmajor)), ptr(dw), ptr(db), ptr(ws), nb, stream_ptr()),
+          "pcadv_pw_bwd_weight")
+    return dw, db
+
+
+def tnet_reg_fwd(T):
+    """feature_transform_regularizer: (reg (), norms (B,))."""
+    lib = _lib.load()
+    _req(T, "trans")
+    B, k, _ = T.shape
+    norms = torch.empty(B, device=T.device)
+    reg = torch.empty((), device=T.device)
+    check(lib.pcadv_tnet_reg_fwd(ptr(T), B, k, ptr(norms), ptr(reg), stream_ptr()),
+          "pcadv_tnet_reg_fwd")
+    return reg, norms
+
+
+def tnet_reg_bwd(T, grad_reg):
+    lib = _lib.load()
+    _req(T, "trans")
+    g = _req(grad_reg.reshape(1).contiguous(), "grad")
+    B, k, _ = T.shape
+    dT = torch.empty_like(T)
+    check(lib.pcadv_tnet_reg_bwd(ptr(T), B, k, ptr(g), ptr(dT), stream_ptr()), "pcadv_tnet_reg_bwd")
+    return dT
+
+
 # ---------------------------------------------------------------------------
 # linear / 1x1 conv on B x C x 1
 # ---------------------------------------------------------------------------
 
-def linear_fwd(x, w, b, act=ACT_NONE, mask=None, p=0.0):
+def linear_fwd(x, w, b, act=ACT_NONE, mask=None, p=0.0, add_identity_k=0):
     lib = _lib.load()
     _req(x, "x")
     M, K = x.shape
@@ -118,7 +229,7 @@ def linear_fwd(x, w, b, act=ACT_NONE, mask=None, p=0.0):
         _req(mask, "dropout mask", (M, Nout))
     y = torch.empty(M, Nout, device=x.device)
     check(lib.pcadv_linear_fwd(ptr(x), ptr(wm), ptr(b), ptr(y), M, Nout, K, act, ptr(mask), None,
-                               0, float(p), stream_ptr()), "pcadv_linear_fwd")
+                               0, float(p), int(add_identity_k), stream_ptr()), "pcadv_linear_fwd")
     return y
 
 
@@ -180,11 +291,11 @@ class PointFeatFunction(torch.autograd.Function):
 
 
 class LinearFunction(torch.autograd.Function):
-    """act(mask/(1-p) * (x w^T + b)) for nn.Linear / 1x1 Conv1d layers."""
+    """act(mask/(1-p) * (x w^T + b)) [+ I] for nn.Linear / 1x1 Conv1d layers."""
 
     @staticmethod
-    def forward(ctx, x, w, b, act, mask, p):
-        y = linear_fwd(x, w, b, act, mask, p)
+    def forward(ctx, x, w, b, act, mask, p, add_identity_k=0):
+        y = linear_fwd(x, w, b, act, mask, p, add_identity_k)
         ctx.save_for_backward(x, w, y, mask if mask is not None else torch.empty(0))
         ctx.act, ctx.p, ctx.has_mask = act, p, mask is not None
         return y
@@ -195,4 +306,92 @@ class LinearFunction(torch.autograd.Function):
         dx, dw, db = linear_bwd(dy.contiguous(), y, ctx.act, mask if ctx.has_mask else None, ctx.p,
                                 x, w, need_dx=ctx.needs_input_grad[0],
                                 need_dw=ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
+
+
+class PointwiseFunction(torch.autograd.Function):
+    """1x1 Conv1d + activation over the points of point-major x (B, N, K)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x = x.contiguous()
+        y = pw_fwd(x, w, b, act)
+        ctx.save_for_backward(x, w, y)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        act = ctx.act
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = pw_bwd_data(dy, y if act != ACT_NONE else None, act, _mat(w), x.shape[-1])
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dwg, dbg = pw_bwd_weight(dy, y if act != ACT_NONE else None, act, x)
+            dw, db = dwg.reshape(w.shape), dbg.reshape(-1)
+        return dx, dw, db, None
+
+
+class TransformFunction(torch.autograd.Function):
+    """x (B, N, k) @ T (B, k, k): the feature transform (models/pointnet.py:120-121)."""
+
+    @staticmethod
+    def forward(ctx, x, T):
+        x, T = x.contiguous(), T.contiguous()
+        B, N, k = x.shape
+        if T.shape != (B, k, k):
+            raise ValueError(f"transform: expected T of shape {(B, k, k)}, got {tuple(T.shape)}")
+        y = pw_fwd(x, T, None, ACT_NONE, kmajor=True, rows_per_w=N)
+        ctx.save_for_backward(x, T)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, T = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, k = x.shape[1], x.shape[2]
+        dx = dT = None
+        if ctx.needs_input_grad[0]:
+            dx = pw_bwd_data(dy, None, ACT_NONE, T, k, kmajor=True, rows_per_w=N)
+        if ctx.needs_input_grad[1]:
+            dT, _ = pw_bwd_weight(dy, None, ACT_NONE, x, rows_per_group=N, kmajor=True,
+                                  need_db=False)
+        return dx, dT
+
+
+class ConvMaxFunction(torch.autograd.Function):
+    """1x1 Conv1d (128 -> O) then max over points, optionally with the ReLU before
+    the max (T-Nets).  Returns the pooled (B, O); the backward is sparse."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, relu_before_max):
+        x = x.contiguous()
+        gmax, gidx = conv_max_fwd(x, w, b, relu_before_max)
+        ctx.save_for_backward(x, w, gmax, gidx)
+        ctx.relu = bool(relu_before_max)
+        return gmax
+
+    @staticmethod
+    def backward(ctx, dg):
+        x, w, gmax, gidx = ctx.saved_tensors
+        dx, dw, db = conv_max_bwd(dg.contiguous(), gidx, x, w, gmax if ctx.relu else None,
+                                  need_dx=ctx.needs_input_grad[0])
+        return dx, dw, db, None
+
+
+class RegularizerFunction(torch.autograd.Function):
+    """feature_transform_regularizer (models/pointnet.py:345-353)."""
+
+    @staticmethod
+    def forward(ctx, T):
+        T = T.contiguous()
+        reg, _ = tnet_reg_fwd(T)
+        ctx.save_for_backward(T)
+        return reg
+
+    @staticmethod
+    def backward(ctx, g):
+        (T,) = ctx.saved_tensors
+        return tnet_reg_bwd(T, g.to(torch.float32))

@@ -10,14 +10,15 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .ops import ACT_NONE, ACT_RELU, LinearFunction, PointFeatFunction
+from .ops import (ACT_NONE, ACT_RELU, ConvMaxFunction, LinearFunction, PointFeatFunction,
+                  PointwiseFunction, RegularizerFunction, TransformFunction)
 
 __all__ = ["PointNetfeat", "PointNetCls", "STN3d", "STNkd", "feature_transform_regularizer"]
 
 
 class STNkd(nn.Module):
-    """k x k transform regressor (models/pointnet.py:46-79).  Parameters only in
-    this round; its HIP forward is a later §8 row (a7)."""
+    """k x k transform regressor (models/pointnet.py:46-79): relu(conv1..conv3),
+    ReLU then max over points, relu(fc1), relu(fc2), fc3 + identity."""
 
     def __init__(self, k=64):
         super().__init__()
@@ -30,8 +31,19 @@ class STNkd(nn.Module):
         self.relu = nn.ReLU()
         self.k = k
 
+    def forward_points(self, xp):
+        """xp: B x N x k point-major -> B x k x k."""
+        h = PointwiseFunction.apply(xp, self.conv1.weight, self.conv1.bias, ACT_RELU)
+        h = PointwiseFunction.apply(h, self.conv2.weight, self.conv2.bias, ACT_RELU)
+        g = ConvMaxFunction.apply(h, self.conv3.weight, self.conv3.bias, True)
+        f = LinearFunction.apply(g, self.fc1.weight, self.fc1.bias, ACT_RELU, None, 0.0)
+        f = LinearFunction.apply(f, self.fc2.weight, self.fc2.bias, ACT_RELU, None, 0.0)
+        t = LinearFunction.apply(f, self.fc3.weight, self.fc3.bias, ACT_NONE, None, 0.0, self.k)
+        return t.view(-1, self.k, self.k)
+
     def forward(self, x):
-        raise NotImplementedError("STNkd HIP forward is not built yet (feature_transform=True)")
+        """x: B x k x N (the reference layout)."""
+        return self.forward_points(x.transpose(1, 2).contiguous())
 
 
 class STN3d(STNkd):
@@ -56,22 +68,31 @@ class PointNetfeat(nn.Module):
             self.fstn = STNkd(k=64)
 
     def forward_points(self, pts):
-        """pts: C x N x 3 (point-major, as PointNetCls receives it)."""
+        """pts: C x N x 3 (point-major, as PointNetCls receives it) ->
+        (global C x 1024, trans_feat or None)."""
         if self.feature_transform:
-            raise NotImplementedError("feature_transform=True: STNkd HIP path not built yet")
+            # models/pointnet.py:115-130 with the STNkd(64) feature transform;
+            # point-wise kernels + the sparse max-pool backward
+            x = PointwiseFunction.apply(pts.contiguous(), self.conv1.weight, self.conv1.bias,
+                                        ACT_RELU)
+            x = PointwiseFunction.apply(x, self.conv2.weight, self.conv2.bias, ACT_RELU)
+            trans_feat = self.fstn.forward_points(x)
+            x = TransformFunction.apply(x, trans_feat)
+            x = PointwiseFunction.apply(x, self.conv3.weight, self.conv3.bias, ACT_RELU)
+            return ConvMaxFunction.apply(x, self.conv4.weight, self.conv4.bias, False), trans_feat
         gmax, gidx = PointFeatFunction.apply(
             pts.contiguous(), self.conv1.weight, self.conv1.bias, self.conv2.weight,
             self.conv2.bias, self.conv3.weight, self.conv3.bias, self.conv4.weight,
             self.conv4.bias)
         self.last_argmax = gidx
-        return gmax
+        return gmax, None
 
     def forward(self, x):
         # the reference receives B x C x N; the kernels read the point-major
         # B x N x 3 layout, which is a free view when x came from a transpose.
-        g = self.forward_points(x.transpose(1, 2))
+        g, trans_feat = self.forward_points(x.transpose(1, 2))
         if self.global_feat:
-            return g, None
+            return g, trans_feat
         n_pts = x.size(2)
         raise NotImplementedError("global_feat=False (per-point concat) is not on the hot path")
 
@@ -100,17 +121,15 @@ class PointNetCls(nn.Module):
         return (torch.rand(B, 256, device=device) >= self.dropout.p).float()
 
     def forward(self, x):
-        x_global = self.feat.forward_points(x)
+        x_global, trans_feat = self.feat.forward_points(x)
         h = LinearFunction.apply(x_global, self.fc1.weight, self.fc1.bias, ACT_RELU, None, 0.0)
         mask = self._dropout_mask(x.shape[0], x.device)
         h = LinearFunction.apply(h, self.fc2.weight, self.fc2.bias, ACT_RELU, mask,
                                  float(self.dropout.p))
         out = LinearFunction.apply(h, self.fc3.weight, self.fc3.bias, ACT_NONE, None, 0.0)
-        return out, x_global.unsqueeze(2), None
+        return out, x_global.unsqueeze(2), trans_feat
 
 
 def feature_transform_regularizer(trans):
-    """mean_b ||T T^T - I||_F (models/pointnet.py:345-353), on trans's device."""
-    d = trans.size(1)
-    eye = torch.eye(d, device=trans.device, dtype=trans.dtype)[None]
-    return torch.mean(torch.norm(torch.bmm(trans, trans.transpose(2, 1)) - eye, dim=(1, 2)))
+    """mean_b ||T T^T - I||_F (models/pointnet.py:345-353) on the HIP device."""
+    return RegularizerFunction.apply(trans)

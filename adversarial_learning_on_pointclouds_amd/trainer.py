@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .discriminator import DeepConvDiscNet
-from .pointnet import PointNetCls
+from .pointnet import PointNetCls, feature_transform_regularizer
 from .step import AdvTrainStep
 from .utils import make_D_label
 
@@ -189,10 +189,15 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
         pts, cls = pts.float().to(args.device), cls.long().to(args.device)
         pred, global_gt, high_feat = model(pts)
         l = cls_loss(pred, cls)
-        (args.lambda_cls * l).backward()
+        loss = args.lambda_cls * l
+        l_regu = None
+        if high_feat is not None:  # feature_transform=True (:256-268)
+            l_regu = feature_transform_regularizer(high_feat)
+            loss = loss + args.lambda_regu * l_regu
+        loss.backward()
         optimizer.step()
         train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
-            i_iter, args.total_iterations, l.item(), 0.0))
+            i_iter, args.total_iterations, l.item(), 0.0 if l_regu is None else l_regu.item()))
         if i_iter % args.iter_save_epoch == 0:
             torch.save(model.state_dict(), os.path.join(
                 args.exp_dir, "model_train_epoch_{}.pth".format(i_iter // len(trainloader_gt))))

@@ -119,15 +119,62 @@ int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, cons
                        int O, int relu_before_max, float* gmax, int32_t* gidx,
                        hipStream_t stream);
 
+/* ---- point-wise layers: the feature-transform path --------------------------
+ * (PointNetCls(feature_transform=True): PointNetfeat conv1/conv2/conv3 with the
+ * STNkd(64) transform, models/pointnet.py:46-79,109-122.)  Rows are points,
+ * point-major [M][C].
+ *
+ * pcadv_pw_fwd: y[M][O] = act(x[M][K] W^T + b) (b may be NULL), K in {3, 64,
+ * 128}, O % 32 == 0, act NONE/RELU.  W is the Conv1d weight [O][K], or with
+ * w_kmajor=1 a [K][O] matrix (y = x T: the feature-transform bmm,
+ * pointnet.py:120-121); rows_per_w > 0 (a multiple of 64) uses one matrix per
+ * rows_per_w rows (one per cloud, W + cloud * O * K). */
+int pcadv_pw_fwd(const float* x, int M, int K, const float* w, const float* b, int O, int act,
+                 int w_kmajor, int rows_per_w, float* y, hipStream_t stream);
+
+/* dx[M][K] (+)= (dy * act'(y)) W  (y = that layer's output; O in {64, 128},
+ * K % 32 == 0); accumulate=1 adds into dx. */
+int pcadv_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,
+                      int K, int w_kmajor, int rows_per_w, float* dx, int accumulate,
+                      hipStream_t stream);
+
+/* dW = sum over rows of (dy * act'(y))^T x and db (NULL: skipped), per group
+ * of rows_per_group rows (0: all rows; a multiple of 256 dividing M): dw holds
+ * M / rows_per_group matrices, [O][K] or with dw_kmajor=1 [K][O] (dT of the
+ * bmm).  O in {64, 128}, K in {3, 64, 128}.  Deterministic (fixed-order
+ * reduction over 256-row slabs in the workspace). */
+size_t pcadv_pw_bwd_weight_workspace_bytes(int M, int O, int K);
+int pcadv_pw_bwd_weight(const float* dy, const float* y, int act, const float* x, int M, int O,
+                        int K, int rows_per_group, int dw_kmajor, float* dw, float* db,
+                        void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* Backward of pcadv_conv_max_fwd: each channel's gradient goes to its argmax
+ * point (times [gmax > 0] when gmax_relu is given: the ReLU before the max of
+ * the T-Nets, pointnet.py:30-31,63-64).  dw [O][K], db [O] (may be NULL), dx
+ * [C][N][K] (NULL: skipped; rows of points without hits are written as 0). */
+int pcadv_conv_max_bwd(const float* dgmax, const int32_t* gidx, const float* gmax_relu,
+                       const float* x, int C, int N, int K, const float* w, int O, float* dw,
+                       float* db, float* dx, hipStream_t stream);
+
+/* feature_transform_regularizer (pointnet.py:345-353): norms[b] =
+ * ||T_b T_b^T - I||_F and *reg = mean_b norms[b]; backward dT = *grad_reg *
+ * (2 / (B norms[b])) (T T^T - I) T.  k <= 64. */
+int pcadv_tnet_reg_fwd(const float* T, int B, int k, float* norms, float* reg,
+                       hipStream_t stream);
+int pcadv_tnet_reg_bwd(const float* T, int B, int k, const float* grad_reg, float* dT,
+                       hipStream_t stream);
+
 /* ---- linear / 1x1 conv on B x C x 1 ----------------------------------------
  * y[M][Nout] = act(s * (x[M][K] w[Nout][K]^T + b)), where s is the dropout
  * scale: drop_mask[M][Nout] in {0,1} times 1/(1-drop_p) when drop_mask is
  * non-NULL, else a device Philox draw keyed by (rng_seed, *rng_step) when
- * rng_step is non-NULL, else 1.  K % 4 == 0. */
+ * rng_step is non-NULL, else 1.  K % 4 == 0.  add_identity_k > 0 (with
+ * Nout == k*k) adds the flattened k x k identity after the activation: the
+ * T-Net output transform (STNkd fc3 + iden, models/pointnet.py:70-77). */
 int pcadv_linear_fwd(const float* x, const float* w, const float* b, float* y,
                      int M, int Nout, int K, int act,
                      const float* drop_mask, const int32_t* rng_step, uint64_t rng_seed,
-                     float drop_p, hipStream_t stream);
+                     float drop_p, int add_identity_k, hipStream_t stream);
 
 /* Backward of pcadv_linear_fwd.  dz = dy * act'(y) * s (y = the forward output).
  * dx[M][K] = dz w (skipped when dx is NULL); dw[Nout][K] = sum over the first

@@ -24,7 +24,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
-    assert lib.pcadv_abi_version() == 1
+    assert lib.pcadv_abi_version() == 2
 
 
 def test_layout_matches_header_enums():
@@ -80,6 +80,6 @@ def test_make_D_label_and_pool():
 def test_error_message_roundtrip():
     from adversarial_learning_on_pointclouds_amd import _lib
     lib = _lib.load()
-    rc = lib.pcadv_linear_fwd(None, None, None, None, 0, 0, 0, 0, None, None, 0, 0.0, None)
+    rc = lib.pcadv_linear_fwd(None, None, None, None, 0, 0, 0, 0, None, None, 0, 0.0, 0, None)
     assert rc == -1
     assert b"bad shape" in lib.pcadv_last_error()

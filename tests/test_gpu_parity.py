@@ -302,7 +302,7 @@ def test_device_rng_dropout_and_labels_statistics():
     y = torch.empty_like(x)
     cnt = torch.tensor([5], device=DEV, dtype=torch.int32)
     L.check(L.load().pcadv_linear_fwd(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), 2 * B, 256, 256, 0,
-                                      None, L.ptr(cnt), 99, 0.3, L.stream_ptr()), "linear")
+                                      None, L.ptr(cnt), 99, 0.3, 0, L.stream_ptr()), "linear")
     keep = (y > 0).float().mean().item()
     assert abs(keep - 0.7) < 0.03
     assert torch.allclose(y[y > 0], torch.full_like(y[y > 0], 1 / 0.7))
