@@ -34,7 +34,7 @@ int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float
                           hipStream_t, uint64_t* stamps = nullptr, int stagger = 20);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t,
-                      int add_identity_k = 0);
+                      int add_identity_k = 0, float* mask_out = nullptr);
 int launch_pw_fwd(const float*, int, int, const float*, const float*, int, int, int, int, float*,
                   hipStream_t);
 int launch_pw_bwd_data(const float*, const float*, int, int, int, const float*, int, int, int,
@@ -45,25 +45,29 @@ int launch_pw_bwd_weight(const float*, const float*, int, const float*, int, int
 int launch_convmax_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
                        const float*, int, float*, float*, float*, hipStream_t);
 int launch_tnet_reg(const float*, int, int, float*, float*, const float*, float*, hipStream_t);
-int launch_linear_bwd(const float*, const float*, int, const float*, const int32_t*, uint64_t,
-                      float, const float*, const float*, float*, float*, float*, int, int, int,
-                      int, hipStream_t);
-int launch_cls_loss(const float*, const int64_t*, int, int, float, float*, float*, float*,
-                    hipStream_t);
-int launch_disc_loss(const float*, int, const float*, const float*, const int32_t*, uint64_t,
-                     float, float*, float*, hipStream_t);
-int launch_lsm_bwd(const float*, const float*, int, int, float*, hipStream_t);
 int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, const float*,
                  float*, float*, int64_t, float, const int32_t*, int, float, float, float,
                  hipStream_t);
 int launch_inc(int32_t*, hipStream_t);
+size_t disc_tail_slab_floats();
+int head_rowblocks(int B);
+int disc_rowblocks(int B);
+int launch_head_fwd(const float*, const float*, const float*, const int64_t*, int, float, float*,
+                    float*, float*, const float*, const float*, float*, float*, hipStream_t);
+int launch_disc_tail(const float*, int, const float*, const float*, const float*, const float*,
+                     const float*, const float*, const float*, const float*, const int32_t*,
+                     uint64_t, float, float*, float*, float*, hipStream_t);
+int launch_head_bwd(const float*, const float*, const float*, int, const float*, const float*,
+                    float*, float*, float*, float*, const float*, const float*, float*,
+                    hipStream_t);
 
 // ---- workspace carve for the fused step ------------------------------------
 struct StepWs {
   float *x3, *gmax, *h1, *h2, *logits, *dlogits, *dh2, *dh1, *dgmax;
-  float *din, *d1, *d2, *d3, *d4, *d5, *dout;
-  float *ddout, *dd5, *dd4, *dd3, *dd2, *dd1, *ddin;
+  float *din, *d1, *d2, *d3;
+  float *dd3, *dd2, *dd1;
   float *mask;
+  float *lpart, *lpart3, *dslabs;
   int32_t* gidx;
   void* feat_ws;
   size_t feat_ws_bytes;
@@ -95,17 +99,13 @@ static StepWs carve(int B, int N, char* base) {
   w.d1 = take(R * 512);
   w.d2 = take(R * 256);
   w.d3 = take(R * 256);
-  w.d4 = take(R * 64);
-  w.d5 = take(R * 64);
-  w.dout = take(R);
-  w.ddout = take(R);
-  w.dd5 = take(R * 64);
-  w.dd4 = take(R * 64);
   w.dd3 = take(R * 256);
   w.dd2 = take(R * 256);
   w.dd1 = take(R * 512);
-  w.ddin = take(R * 40);
   w.mask = take(C * 256);
+  w.lpart = take(head_rowblocks(B));
+  w.lpart3 = take(3 * (size_t)disc_rowblocks(B));
+  w.dslabs = take((size_t)disc_rowblocks(B) * disc_tail_slab_floats());
   w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
   if (feat_fwd_workspace_bytes((int)C, N) > w.feat_ws_bytes)
     w.feat_ws_bytes = feat_fwd_workspace_bytes((int)C, N);
@@ -163,56 +163,63 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
                                w.feat_ws, w.feat_ws_bytes, s));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
+  // fc2 + dropout: a device-drawn mask is stored for the backward
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
-                           PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s));
-  PC_TRY(launch_linear_fwd(w.h2, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, logits, C, 40, 256,
-                           PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, s));
-  // ---- losses on the logits; D input rows [lsm_gt; lsm_nogt; lsm_nogt] -----
-  PC_TRY(launch_cls_loss(logits, a->labels, B, 40, a->lambda_cls, w.din, w.dlogits, a->losses, s));
-  // ---- discriminator forward (:499, :530, :546 share parameters) -----------
-  PC_TRY(launch_linear_fwd(w.din, D + PCADV_D_CONV1_W, D + PCADV_D_CONV1_B, w.d1, R, 512, 40,
-                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
+                           PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s, 0,
+                           mask ? nullptr : w.mask));
+  const float* bmask = w.mask;  // explicit masks were staged there too
+  // ---- fc3 -> log_softmax / CE (GT rows) -> D conv1 for the GT and noGT rows;
+  //      D input rows are [lsm_gt; lsm_nogt; lsm_nogt] (:472, :492, :499) -----
+  PC_TRY(launch_head_fwd(w.h2, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, a->labels, B, a->lambda_cls,
+                         logits, w.dlogits, w.din, D + PCADV_D_CONV1_W, D + PCADV_D_CONV1_B, w.d1,
+                         w.lpart, s));
+  // ---- discriminator conv2, conv3 over the R = 3B rows (:499, :530, :546) ---
   PC_TRY(launch_linear_fwd(w.d1, D + PCADV_D_CONV2_W, D + PCADV_D_CONV2_B, w.d2, R, 256, 512,
                            PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.d2, D + PCADV_D_CONV3_W, D + PCADV_D_CONV3_B, w.d3, R, 256, 256,
                            PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
-  PC_TRY(launch_linear_fwd(w.d3, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, w.d4, R, 64, 256,
-                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
-  PC_TRY(launch_linear_fwd(w.d4, D + PCADV_D_CONV5_W, D + PCADV_D_CONV5_B, w.d5, R, 64, 64,
-                           PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, s));
-  PC_TRY(launch_linear_fwd(w.d5, D + PCADV_D_FC_W, D + PCADV_D_FC_B, w.dout, R, 1, 64,
-                           PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, s));
-  PC_TRY(launch_disc_loss(w.dout, B, a->soft_gt, a->soft_nogt, st, a->rng_seed, a->lambda_adv,
-                          w.ddout, a->losses, s));
-  // ---- discriminator backward: param grads from rows [0,2B) (D loss), input
-  //      grad of rows [2B,3B) (generator's adversarial loss, D frozen) --------
+  // ---- conv4 -> conv5 -> fc, the three BCE terms, and back to dL/d(conv3) ---
+  PC_TRY(launch_disc_tail(w.d3, B, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, D + PCADV_D_CONV5_W,
+                          D + PCADV_D_CONV5_B, D + PCADV_D_FC_W, D + PCADV_D_FC_B, a->soft_gt,
+                          a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
+                          s));
+  // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
+  //      input grads of all rows (rows [2B,3B) feed the generator, D frozen) ---
   const int MW = 2 * B;
-  PC_TRY(launch_linear_bwd(w.ddout, w.dout, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.d5,
-                           D + PCADV_D_FC_W, w.dd5, gD + PCADV_D_FC_W, gD + PCADV_D_FC_B, R, MW,
-                           1, 64, s));
-  PC_TRY(launch_linear_bwd(w.dd5, w.d5, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d4,
-                           D + PCADV_D_CONV5_W, w.dd4, gD + PCADV_D_CONV5_W, gD + PCADV_D_CONV5_B,
-                           R, MW, 64, 64, s));
-  PC_TRY(launch_linear_bwd(w.dd4, w.d4, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d3,
-                           D + PCADV_D_CONV4_W, w.dd3, gD + PCADV_D_CONV4_W, gD + PCADV_D_CONV4_B,
-                           R, MW, 64, 256, s));
-  PC_TRY(launch_linear_bwd(w.dd3, w.d3, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d2,
-                           D + PCADV_D_CONV3_W, w.dd2, gD + PCADV_D_CONV3_W, gD + PCADV_D_CONV3_B,
-                           R, MW, 256, 256, s));
+  {
+    LinBwdExtra ex{};  // + sum of the conv4/conv5/fc partial-gradient slabs
+    ex.red_src = w.dslabs;
+    ex.red_dst = gD + PCADV_D_CONV4_W;
+    ex.red_n = (int)disc_tail_slab_floats();
+    ex.red_cnt = disc_rowblocks(B);
+    PC_TRY(launch_linear_bwd(w.dd3, w.d3, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d2,
+                             D + PCADV_D_CONV3_W, w.dd2, gD + PCADV_D_CONV3_W,
+                             gD + PCADV_D_CONV3_B, R, MW, 256, 256, s, &ex));
+  }
   PC_TRY(launch_linear_bwd(w.dd2, w.d2, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d1,
                            D + PCADV_D_CONV2_W, w.dd1, gD + PCADV_D_CONV2_W, gD + PCADV_D_CONV2_B,
                            R, MW, 256, 512, s));
-  PC_TRY(launch_linear_bwd(w.dd1, w.d1, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.din,
-                           D + PCADV_D_CONV1_W, w.ddin, gD + PCADV_D_CONV1_W, gD + PCADV_D_CONV1_B,
-                           R, MW, 512, 40, s));
-  PC_TRY(launch_lsm_bwd(w.din, w.ddin, B, 40, w.dlogits, s));
-  // ---- generator head backward (:520) --------------------------------------
-  PC_TRY(launch_linear_bwd(w.dlogits, logits, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h2,
-                           G + PCADV_G_FC3_W, w.dh2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, C,
-                           40, 256, s));
-  PC_TRY(launch_linear_bwd(w.dh2, w.h2, PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, w.h1,
-                           G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C, C,
-                           256, 512, s));
+  // ---- D conv1 input grad of the adversarial rows -> log_softmax backward ->
+  //      fc3 input grad; D conv1 weight grad; the four losses -----------------
+  PC_TRY(launch_head_bwd(w.dd1, w.d1, w.din, B, D + PCADV_D_CONV1_W, G + PCADV_G_FC3_W, w.dlogits,
+                         w.dh2, gD + PCADV_D_CONV1_W, gD + PCADV_D_CONV1_B, w.lpart, w.lpart3,
+                         a->losses, s));
+  // ---- generator head backward (:520); fc3's weight grad rides along -------
+  {
+    LinBwdExtra ex{};
+    ex.dy = w.dlogits;
+    ex.act = PCADV_ACT_NONE;
+    ex.x = w.h2;
+    ex.dw = gG + PCADV_G_FC3_W;
+    ex.db = gG + PCADV_G_FC3_B;
+    ex.M = C;
+    ex.m_w = C;
+    ex.N = 40;
+    ex.K = 256;
+    PC_TRY(launch_linear_bwd(w.dh2, w.h2, PCADV_ACT_RELU, bmask, nullptr, 0, a->drop_p,
+                             w.h1, G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W,
+                             gG + PCADV_G_FC2_B, C, C, 256, 512, s, &ex));
+  }
   PC_TRY(launch_linear_bwd(w.dh1, w.h1, PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, w.gmax,
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));

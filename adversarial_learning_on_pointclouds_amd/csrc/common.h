@@ -124,6 +124,28 @@ __device__ __forceinline__ float conv1_point(float wa, float wb, float wc, float
   return v > 0.f ? v : 0.f;
 }
 
+// Work added to a linear-backward launch (linear.hip): an extra weight-gradient
+// job dw[N][K] (+ db) = sum over the first m_w rows of dy^T x (no activation,
+// no dropout), and a fixed-order sum of red_cnt slabs of red_n floats.
+struct LinBwdExtra {
+  const float* dy;
+  const float* y;
+  int act;
+  const float* mask;
+  const int32_t* step;
+  const float* x;
+  float* dw;
+  float* db;
+  int M, m_w, N, K;
+  const float* red_src;
+  float* red_dst;
+  int red_n, red_cnt;
+};
+int launch_linear_bwd(const float* dy, const float* y, int act, const float* mask,
+                      const int32_t* step, uint64_t seed, float p, const float* x, const float* w,
+                      float* dx, float* dw, float* db, int M, int m_w, int N, int K,
+                      hipStream_t s, const LinBwdExtra* extra = nullptr);
+
 }  // namespace pcadv
 
 #define PC_HIP_CHECK_LAUNCH(what)                                              \

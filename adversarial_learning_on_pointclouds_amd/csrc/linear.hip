@@ -51,6 +51,7 @@ struct GemmArgs {
   float* db;
   int M, N, K, m_w;
   int diag;  // forward: add the k x k identity to the flattened output (0: off)
+  float* mask_out;  // forward, device-drawn dropout: store the {0,1} mask here
 };
 
 // dropout scale s at (m, n) of an [M][N] output
@@ -180,7 +181,12 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
       if (OP == OP_FWD) {
         const size_t i = (size_t)m * g.N + n;
         v += g.b[n];
-        if (DM != DM_NONE) v *= drop_scale<DM>(g, i, m, n, step);
+        if (DM != DM_NONE) {
+          const float sc = drop_scale<DM>(g, i, m, n, step);
+          v *= sc;
+          // the drawn mask, for a backward that should not redraw it
+          if (DM == DM_RNG && g.mask_out) g.mask_out[i] = sc != 0.f ? 1.f : 0.f;
+        }
         float o = act_fwd(v, ACT);
         // STNkd / STN3d add the flattened identity (models/pointnet.py:38-41,74-77)
         if (g.diag && n % (g.diag + 1) == 0) o += 1.f;
@@ -225,15 +231,37 @@ k_linear_fwd(GemmArgs g, int S, int L) {
   split_job<OP_FWD, ACT, DM>(g, blockIdx.x, g.M, g.N, g.K, S, L, red);
 }
 
-// blocks [0, nbx): dx tiles (split over S waves); the rest: dw tiles, S per block
+// Independent work that rides along a backward launch (saves a dependent
+// launch): a second weight-gradient job (no activation / dropout), and a
+// fixed-order sum of partial slabs: red_dst[j] = sum_s red_src[s * red_n + j].
+struct BwdExtra {
+  GemmArgs g2;
+  int nwt2;
+  const float* red_src;
+  float* red_dst;
+  int red_n, red_cnt;
+};
+
+// blocks [0, nbx): dx tiles (split over S waves); then dw tiles (S per block);
+// then the extra weight tiles; then the slab reduction
 template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
-k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt) {
+k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex) {
   __shared__ float red[16 * 256];
-  if ((int)blockIdx.x < nbx) {
-    split_job<OP_BWD_DATA, ACT, DM>(g, blockIdx.x, g.M, g.K, g.N, S, L, red);
+  const int b = blockIdx.x, nbw = (nwt + S - 1) / S, nbw2 = (ex.nwt2 + S - 1) / S;
+  if (b < nbx) {
+    split_job<OP_BWD_DATA, ACT, DM>(g, b, g.M, g.K, g.N, S, L, red);
+  } else if (b < nbx + nbw) {
+    weight_job<ACT, DM>(g, (b - nbx) * S + (threadIdx.x >> 6), nwt);
+  } else if (b < nbx + nbw + nbw2) {
+    weight_job<ACT_NONE, DM_NONE>(ex.g2, (b - nbx - nbw) * S + (threadIdx.x >> 6), ex.nwt2);
   } else {
-    weight_job<ACT, DM>(g, (blockIdx.x - nbx) * S + (threadIdx.x >> 6), nwt);
+    const int j = (b - nbx - nbw - nbw2) * blockDim.x + threadIdx.x;
+    if (j < ex.red_n) {
+      float acc = 0.f;
+      for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_n + j];
+      ex.red_dst[j] = acc;
+    }
   }
 }
 
@@ -272,13 +300,14 @@ static void split_cfg(int R, int* S, int* L) {
 
 int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N,
                       int K, int act, const float* mask, const int32_t* step, uint64_t seed,
-                      float p, hipStream_t s, int add_identity_k) {
+                      float p, hipStream_t s, int add_identity_k, float* mask_out) {
   PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0, "linear_fwd: bad shape M=%d N=%d K=%d", M, N,
              K);
   PC_REQUIRE(add_identity_k == 0 || add_identity_k * add_identity_k == N,
              "linear_fwd: identity of size %d does not match %d outputs", add_identity_k, N);
   GemmArgs g{};
   g.x = x; g.w = w; g.b = b; g.y = y; g.act = act; g.diag = add_identity_k;
+  g.mask_out = mask_out;
   g.drop = DropSpec{mask, step, seed, p};
   g.M = M; g.N = N; g.K = K;
   int S, L;
@@ -293,7 +322,7 @@ int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, 
 int launch_linear_bwd(const float* dy, const float* y, int act, const float* mask,
                       const int32_t* step, uint64_t seed, float p, const float* x, const float* w,
                       float* dx, float* dw, float* db, int M, int m_w, int N, int K,
-                      hipStream_t s) {
+                      hipStream_t s, const LinBwdExtra* extra) {
   PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0 && m_w >= 0 && m_w <= M &&
                  m_w <= 16 * MAXC,
              "linear_bwd: bad shape M=%d m_w=%d N=%d K=%d", M, m_w, N, K);
@@ -307,10 +336,35 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   const int nbx = dx ? ((M + 15) / 16) * ((K + 15) / 16) : 0;
   const int nwt = dw ? ((N + 15) / 16) * ((K + 15) / 16) : 0;
   const int nbw = (nwt + S - 1) / S;
-  if (nbx + nbw == 0) return PCADV_OK;
+  BwdExtra ex{};
+  int nbe = 0;
+  if (extra) {
+    if (extra->dw) {
+      const LinBwdExtra& e = *extra;
+      PC_REQUIRE(e.M > 0 && e.N > 0 && e.K > 0 && e.m_w > 0 && e.m_w <= e.M &&
+                     e.m_w <= 16 * MAXC && e.act == ACT_NONE && !e.mask && !e.step,
+                 "linear_bwd: bad extra weight job (M=%d m_w=%d N=%d K=%d)", e.M, e.m_w, e.N, e.K);
+      GemmArgs& g2 = ex.g2;
+      g2.x = e.x; g2.dy = e.dy; g2.yact = e.y; g2.act = ACT_NONE;
+      g2.dw = e.dw; g2.db = e.db;
+      g2.M = e.M; g2.N = e.N; g2.K = e.K; g2.m_w = e.m_w;
+      ex.nwt2 = ((e.N + 15) / 16) * ((e.K + 15) / 16);
+      nbe += (ex.nwt2 + S - 1) / S;
+    }
+    if (extra->red_src) {
+      PC_REQUIRE(extra->red_dst && extra->red_n > 0 && extra->red_cnt > 0,
+                 "linear_bwd: bad extra reduction");
+      ex.red_src = extra->red_src;
+      ex.red_dst = extra->red_dst;
+      ex.red_n = extra->red_n;
+      ex.red_cnt = extra->red_cnt;
+      nbe += (ex.red_n + 64 * S - 1) / (64 * S);
+    }
+  }
+  if (nbx + nbw + nbe == 0) return PCADV_OK;
   PC_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU, "linear_bwd: bad act %d", act);
-  launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx + nbw), dim3(64 * S), s, g, S, L, nbx,
-                       nwt);
+  launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx + nbw + nbe), dim3(64 * S), s, g, S, L,
+                       nbx, nwt, ex);
   PC_HIP_CHECK_LAUNCH("k_linear_bwd");
   return PCADV_OK;
 }

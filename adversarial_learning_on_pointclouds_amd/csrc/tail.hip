@@ -1,0 +1,549 @@
+// Row-block fused kernels for the small end of the adversarial step (gfx950).
+//
+// At B = 32 every layer of the classifier head and of the discriminator is a
+// few hundred kFLOP, so a launch per layer costs more than the layer.  Where a
+// chain of layers has small weights, one workgroup takes 16 rows through the
+// whole chain with the activations in LDS:
+//
+//   k_head_fwd  fc3 (models/pointnet.py:202) -> log_softmax / CrossEntropy
+//               (utils/trainer.py:469-472,492) -> discriminator conv1 + LeakyReLU
+//               (models/discriminator.py:43) for the GT and noGT rows
+//   k_disc_tail discriminator conv4 -> conv5 -> fc (discriminator.py:46-51), the
+//               BCE terms of trainer.py:507,537,553 with make_D_label's soft
+//               labels (utils/utils.py:22-31), then back through fc, conv5 and
+//               conv4 to dL/d(conv3 output); per-workgroup partial weight
+//               gradients of conv4/conv5/fc (summed by a later launch)
+//   k_head_bwd  discriminator conv1 input gradient of the adversarial rows ->
+//               log_softmax backward -> fc3 input gradient; extra workgroups
+//               compute conv1's weight gradient; finalises the four losses
+//
+// Each layer is a set of 16x16 output tiles on v_mfma_f32_16x16x4_f32 (exact
+// f32), one reduction chunk of <= 128 per work item; items are spread over the
+// 16 waves and their partial tiles summed in a fixed order.
+#include "common.h"
+
+namespace pcadv {
+
+constexpr int TR = 16;     // rows per workgroup
+constexpr int TT = 1024;   // 16 waves
+constexpr int TW = TT / 64;
+
+typedef float f32x4t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4t mfma16t(float a, float b, f32x4t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+enum BMode { B_OK = 0, B_KO = 1 };  // B[k][j] = W[j * ldw + k]  |  W[k * ldw + j]
+
+// out[r][j] = act(sum_k A[r][k] B[k][j] + bias[j]) for the 16 rows, j < NC.
+// A: LDS [16][as]; W: weights in LDS (staged by lds_fill) or global; out: LDS
+// or global [16][os].  One work item = one 16x16 output tile over a reduction
+// chunk of <= 128; with a single chunk the tile goes straight to `out`,
+// otherwise the chunk partials meet in scratch (>= items * 256 floats, LDS).
+// Rows >= dup_row are also written at out + dup_off (the duplicated noGT rows
+// of the discriminator input).
+template <int K, int NC, int MODE, int ACT>
+__device__ __forceinline__ void rows_layer(const float* A, int as, const float* W, int ldw,
+                                           const float* __restrict__ bias, float* out, int os,
+                                           float* scratch, int nrows = TR, int dup_row = TR,
+                                           long dup_off = 0) {
+  constexpr int KC = K < 128 ? K : 128;
+  constexpr int C = (K + KC - 1) / KC, T = (NC + 15) / 16, ITEMS = T * C;
+  constexpr int NS = (KC + 3) / 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, q = lane >> 4;
+  for (int it = wave; it < ITEMS; it += TW) {
+    const int t = it / C, c = it % C, j = 16 * t + r, k0 = c * KC;
+    // every operand read is issued before the first MFMA of the tile
+    float av[NS], bv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int k = k0 + 4 * s + q;
+      const bool vk = k < K && 4 * s + q < KC, v = vk && j < NC;
+      const int jj = v ? j : 0, kk = v ? k : 0;
+      const float w = MODE == B_OK ? W[jj * ldw + kk] : W[kk * ldw + jj];
+      const float a = A[r * as + (vk ? k : 0)];
+      bv[s] = v ? w : 0.f;
+      av[s] = vk ? a : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMA chain
+    f32x4t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc = mfma16t(av[s], bv[s], acc);
+    if (C == 1) {
+      if (j < NC) {
+        const float bj = bias ? bias[j] : 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int row = 4 * q + v;
+          if (row < nrows) {
+            const float o = act_fwd(acc[v] + bj, ACT);
+            out[row * os + j] = o;
+            if (row >= dup_row) out[row * os + j + dup_off] = o;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) scratch[it * 256 + (4 * q + v) * 16 + r] = acc[v];
+    }
+  }
+  __syncthreads();
+  if (C > 1) {
+    for (int e = tid; e < nrows * NC; e += TT) {
+      const int row = e / NC, col = e % NC, t = col >> 4;
+      float v = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) v += scratch[(t * C + c) * 256 + row * 16 + (col & 15)];
+      if (bias) v += bias[col];
+      const float o = act_fwd(v, ACT);
+      out[row * os + col] = o;
+      if (row >= dup_row) out[row * os + col + dup_off] = o;
+    }
+    __syncthreads();
+  }
+}
+
+// Staging of global row-major matrices into LDS (padded row stride `ld`,
+// cols % 4 == 0; rows past `valid` are zero-filled).  All the float4 loads of
+// a thread (<= 8) are issued before any LDS store: one memory round trip for
+// every matrix of the kernel.  No barrier (the caller syncs).
+struct Fill {
+  float* dst;
+  int ld;
+  const float* src;
+  int rows, cols, valid;
+};
+
+template <int NF>
+__device__ __forceinline__ void lds_fill(const Fill (&f)[NF]) {
+  int base[NF + 1];
+  base[0] = 0;
+#pragma unroll
+  for (int d = 0; d < NF; ++d) base[d + 1] = base[d] + f[d].rows * (f[d].cols / 4);
+  f32x4 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = threadIdx.x + u * TT;
+    v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < NF; ++d)
+      if (e >= base[d] && e < base[d + 1]) {
+        const int c4 = f[d].cols / 4, row = (e - base[d]) / c4, col = (e - base[d]) % c4;
+        if (row < f[d].valid)
+          v[u] = *reinterpret_cast<const f32x4*>(f[d].src + (size_t)row * f[d].cols + 4 * col);
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = threadIdx.x + u * TT;
+#pragma unroll
+    for (int d = 0; d < NF; ++d)
+      if (e >= base[d] && e < base[d + 1]) {
+        const int c4 = f[d].cols / 4, row = (e - base[d]) / c4, col = (e - base[d]) % c4;
+        float* p = f[d].dst + row * f[d].ld + 4 * col;
+        p[0] = v[u][0];
+        p[1] = v[u][1];
+        p[2] = v[u][2];
+        p[3] = v[u][3];
+      }
+  }
+}
+
+// dst[o][k] = sum_r Z[r][o] X[r][k] over the 16 rows (Z rows that must not
+// contribute are zero), db[o] = sum_r Z[r][o]; O, K multiples of 16.
+template <int O, int K>
+__device__ void rows_wgrad(const float* Z, int zs, const float* X, int xs, float* __restrict__ dst,
+                           float* __restrict__ db) {
+  constexpr int TO = O / 16, TK = K / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, q = lane >> 4;
+  for (int t = wave; t < TO * TK; t += TW) {
+    const int o0 = 16 * (t / TK), k0 = 16 * (t % TK);
+    f32x4t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = 4 * s + q;
+      acc = mfma16t(Z[row * zs + o0 + r], X[row * xs + k0 + r], acc);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dst[(size_t)(o0 + 4 * q + v) * K + k0 + r] = acc[v];
+  }
+  for (int o = tid; o < O; o += TT) {
+    float s = 0.f;
+    for (int row = 0; row < TR; ++row) s += Z[row * zs + o];
+    db[o] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_head_fwd: rows m of the 2B generator outputs
+// ---------------------------------------------------------------------------
+struct HeadFwdLds {
+  float w1[512 * 44];          // discriminator conv1 weight [512][40], padded rows
+  alignas(16) float h2[TR * 260];
+  float lg[TR * 44];
+  float lsm[TR * 44];
+  float rl[TR];
+  alignas(16) float scratch[6 * 256];
+};
+
+__global__ void __launch_bounds__(TT)
+k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const float* __restrict__ b3,
+           const int64_t* __restrict__ labels, int B, float lambda_cls, float* __restrict__ logits,
+           float* __restrict__ dlogits, float* __restrict__ din, const float* __restrict__ dw1,
+           const float* __restrict__ db1, float* __restrict__ d1, float* __restrict__ lpart) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  HeadFwdLds& L = *reinterpret_cast<HeadFwdLds*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = 2 * B, r0 = blockIdx.x * TR, nrows = min(TR, C - r0);
+  {
+    const Fill f[2] = {{L.w1, 44, dw1, 512, 40, 512}, {L.h2, 260, h2 + (size_t)r0 * 256, TR, 256, nrows}};
+    lds_fill(f);  // 6144 float4: 6 per thread
+  }
+  __syncthreads();
+  rows_layer<256, 40, B_OK, ACT_NONE>(L.h2, 260, w3, 256, b3, L.lg, 44, L.scratch);
+  // log_softmax, CrossEntropy (GT rows), discriminator input rows: one wave per row
+  {
+    const int row = wave, m = r0 + row;
+    const float v = lane < 40 ? L.lg[row * 44 + lane] : -INFINITY;
+    float mx = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float e = lane < 40 ? expf(v - mx) : 0.f;
+    float se = e;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+    const float lsm = (v - mx) - logf(se);
+    if (lane < 40) L.lsm[row * 44 + lane] = lsm;
+    float rloss = 0.f;
+    if (m < C && lane < 40) {
+      logits[(size_t)m * 40 + lane] = v;
+      din[(size_t)m * 40 + lane] = lsm;
+      if (m >= B) din[(size_t)(m + B) * 40 + lane] = lsm;
+    }
+    if (m < B) {
+      const int y = (int)labels[m];
+      const float sm = expf(lsm);
+      if (lane < 40)
+        dlogits[(size_t)m * 40 + lane] = lambda_cls * ((lane == y ? sm - 1.f : sm) / (float)B);
+      rloss = -__shfl(lsm, y);
+    }
+    if (lane == 0) L.rl[row] = rloss;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int row = 0; row < TR; ++row) s += L.rl[row];
+    lpart[blockIdx.x] = s;
+  }
+  // D conv1 on the GT rows (D rows [0,B)) and noGT rows (D rows [B,2B) and,
+  // identical, [2B,3B)): rows r0.. of d1, copied to r0+B.. for noGT blocks
+  rows_layer<40, 512, B_OK, ACT_LRELU>(L.lsm, 44, L.w1, 44, db1, d1 + (size_t)r0 * 512, 512,
+                                       nullptr, nrows, max(0, B - r0), (long)B * 512);
+}
+
+// ---------------------------------------------------------------------------
+// k_disc_tail: rows m of the 3B discriminator rows
+// ---------------------------------------------------------------------------
+constexpr int DT_SLAB = 64 * 256 + 64 + 64 * 64 + 64 + 64 + 1;  // = gD[conv4.w .. fc.b]
+
+struct DiscTailLds {
+  float w4[64 * 260];          // conv4 weight [64][256], padded rows
+  float w5[64 * 68];           // conv5 weight [64][64]
+  float wf[64];                // fc weight [1][64]
+  alignas(16) float x3[TR * 260];   // conv3 output rows (conv4 input)
+  float a4[TR * 68];
+  float a5[TR * 68];
+  float out[TR * 4];
+  float z5[TR * 68];
+  float z4[TR * 68];
+  float lt[3][TR];
+  alignas(16) float scratch[8 * 256];
+};
+
+__global__ void __launch_bounds__(TT)
+k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
+            const float* __restrict__ b4, const float* __restrict__ w5,
+            const float* __restrict__ b5, const float* __restrict__ wf,
+            const float* __restrict__ bf, const float* __restrict__ soft_gt,
+            const float* __restrict__ soft_nogt, const int32_t* __restrict__ step, uint64_t seed,
+            float lambda_adv, float* __restrict__ dd3, float* __restrict__ slabs,
+            float* __restrict__ lpart3) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  DiscTailLds& L = *reinterpret_cast<DiscTailLds*>(smem);
+  const int tid = threadIdx.x;
+  const int R = 3 * B, r0 = blockIdx.x * TR, nrows = min(TR, R - r0);
+  {
+    const Fill f[4] = {{L.w4, 260, w4, 64, 256, 64}, {L.w5, 68, w5, 64, 64, 64},
+                       {L.wf, 64, wf, 1, 64, 1}, {L.x3, 260, d3 + (size_t)r0 * 256, TR, 256, nrows}};
+    lds_fill(f);  // 6160 float4: <= 7 per thread
+  }
+  __syncthreads();
+  rows_layer<256, 64, B_OK, ACT_LRELU>(L.x3, 260, L.w4, 260, b4, L.a4, 68, L.scratch);
+  rows_layer<64, 64, B_OK, ACT_LRELU>(L.a4, 68, L.w5, 68, b5, L.a5, 68, L.scratch);
+  rows_layer<64, 1, B_OK, ACT_NONE>(L.a5, 68, L.wf, 64, bf, L.out, 4, L.scratch);
+  // BCEWithLogits terms (train_classification.py:200): rows [0,B) D(lsm_gt) vs U(0.7,1.05),
+  // [B,2B) D(lsm_nogt) vs U(0,0.305), [2B,3B) adversarial vs 1
+  if (tid < TR) {
+    const int m = r0 + tid;
+    float g = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
+    if (m < R) {
+      const float x = L.out[tid * 4];
+      float y, f;
+      if (m < B) {
+        y = soft_gt ? soft_gt[m]
+                    : 0.7f + 0.35f * rng_uniform(seed, (uint32_t)*step, RNG_LABEL_GT, (uint32_t)m);
+        f = 0.5f;
+      } else if (m < 2 * B) {
+        y = soft_nogt ? soft_nogt[m - B]
+                      : 0.305f * rng_uniform(seed, (uint32_t)*step, RNG_LABEL_NOGT,
+                                             (uint32_t)(m - B));
+        f = 0.5f;
+      } else {
+        y = 1.f;
+        f = lambda_adv;
+      }
+      g = f * (1.f / (1.f + expf(-x)) - y) / (float)B;
+      const float bce = fmaxf(x, 0.f) - x * y + log1pf(expf(-fabsf(x)));
+      if (m < B) l1 = bce;
+      else if (m < 2 * B) l2 = bce;
+      else l0 = bce;
+    }
+    L.out[tid * 4 + 1] = g;
+    L.lt[0][tid] = l0;
+    L.lt[1][tid] = l1;
+    L.lt[2][tid] = l2;
+  }
+  __syncthreads();
+  if (tid < 3) {
+    float s = 0.f;
+    for (int row = 0; row < TR; ++row) s += L.lt[tid][row];
+    lpart3[blockIdx.x * 3 + tid] = s;
+  }
+  // backward: fc (dz = dL/dout, no activation), conv5, conv4
+  rows_layer<1, 64, B_KO, ACT_NONE>(L.out + 1, 4, L.wf, 64, nullptr, L.z5, 68, L.scratch);
+  for (int e = tid; e < TR * 64; e += TT) {
+    const int row = e >> 6, col = e & 63;
+    L.z5[row * 68 + col] *= act_bwd(L.a5[row * 68 + col], ACT_LRELU);
+  }
+  __syncthreads();
+  rows_layer<64, 64, B_KO, ACT_NONE>(L.z5, 68, L.w5, 68, nullptr, L.z4, 68, L.scratch);
+  for (int e = tid; e < TR * 64; e += TT) {
+    const int row = e >> 6, col = e & 63;
+    L.z4[row * 68 + col] *= act_bwd(L.a4[row * 68 + col], ACT_LRELU);
+  }
+  __syncthreads();
+  rows_layer<64, 256, B_KO, ACT_NONE>(L.z4, 68, L.w4, 260, nullptr, dd3 + (size_t)r0 * 256, 256,
+                                      L.scratch, nrows);
+  // partial weight gradients over this block's D-loss rows (m < 2B; the
+  // adversarial rows train only the generator)
+  for (int e = tid; e < TR * 64; e += TT) {
+    const int row = e >> 6, col = e & 63;
+    if (r0 + row >= 2 * B) {
+      L.z4[row * 68 + col] = 0.f;
+      L.z5[row * 68 + col] = 0.f;
+    }
+  }
+  if (tid < TR && r0 + tid >= 2 * B) L.out[tid * 4 + 1] = 0.f;
+  __syncthreads();
+  float* slab = slabs + (size_t)blockIdx.x * DT_SLAB;
+  rows_wgrad<64, 256>(L.z4, 68, L.x3, 260, slab, slab + 64 * 256);
+  rows_wgrad<64, 64>(L.z5, 68, L.a4, 68, slab + 64 * 256 + 64, slab + 64 * 256 + 64 + 4096);
+  if (tid < 64) {
+    float s = 0.f;
+    for (int row = 0; row < TR; ++row) s = fmaf(L.out[row * 4 + 1], L.a5[row * 68 + tid], s);
+    slab[64 * 256 + 64 + 4096 + 64 + tid] = s;
+  } else if (tid == 64) {
+    float s = 0.f;
+    for (int row = 0; row < TR; ++row) s += L.out[row * 4 + 1];
+    slab[DT_SLAB - 1] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_head_bwd: rows m of the 2B generator outputs (+ conv1 weight-grad blocks)
+// ---------------------------------------------------------------------------
+struct HeadBwdLds {
+  float w1[512 * 48];          // discriminator conv1 weight [512][40], rows padded to 48
+  alignas(16) float z1[TR * 516];
+  float ddin[TR * 44];
+  float dl[TR * 44];
+  alignas(16) float scratch[12 * 256];
+};
+
+__global__ void __launch_bounds__(TT)
+k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
+           const float* __restrict__ din, int B, const float* __restrict__ dw1,
+           const float* __restrict__ w3, float* __restrict__ dlogits, float* __restrict__ dh2,
+           float* __restrict__ gw1, float* __restrict__ gb1, const float* __restrict__ lpart,
+           int nlp, const float* __restrict__ lpart3, int nlp3, float* __restrict__ losses) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  HeadBwdLds& L = *reinterpret_cast<HeadBwdLds*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = 2 * B, nrb = (C + TR - 1) / TR;
+  if ((int)blockIdx.x >= nrb) {
+    // discriminator conv1 weight gradient over the D-loss rows [0, 2B):
+    // dW[o][k] = sum_m dz[m][o] din[m][k], dz = dd1 * lrelu'(d1); wave = 16x16 tile
+    const int t = ((int)blockIdx.x - nrb) * TW + wave;
+    constexpr int TK = 3;  // 40 columns in 3 tiles
+    if (t >= 32 * TK) return;
+    const int o0 = 16 * (t / TK), k0 = 16 * (t % TK), r = lane & 15, q = lane >> 4;
+    f32x4t acc = {0.f, 0.f, 0.f, 0.f};
+    float s = 0.f;
+    for (int m0 = 0; m0 < C; m0 += 16) {
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = m0 + 4 * u + q;
+        const bool vm = m < C;
+        const size_t ia = (size_t)(vm ? m : 0) * 512 + o0 + r;
+        const float z = dd1[ia] * act_bwd(d1[ia], ACT_LRELU);
+        a[u] = vm ? z : 0.f;
+        const bool vb = vm && k0 + r < 40;
+        const float xv = din[(size_t)(vm ? m : 0) * 40 + (vb ? k0 + r : 0)];
+        b[u] = vb ? xv : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc = mfma16t(a[u], b[u], acc);
+        s += a[u];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      if (k0 + r < 40) gw1[(size_t)(o0 + 4 * q + v) * 40 + k0 + r] = acc[v];
+    if (k0 == 0) {
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      if (q == 0) gb1[o0 + r] = s;
+    }
+    return;
+  }
+  const int r0 = blockIdx.x * TR, nrows = min(TR, C - r0);
+  // dz of the adversarial D rows m + B (m in [B, 2B)); zero for GT rows.  The
+  // row loads are issued together with the conv1 weight staging.
+  f32x4 zd[2], zy[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
+    const bool v = m >= B && m < C;
+    const size_t i = v ? (size_t)(m + B) * 512 + 4 * c4 : 0;
+    zd[u] = *reinterpret_cast<const f32x4*>(dd1 + i);
+    zy[u] = *reinterpret_cast<const f32x4*>(d1 + i);
+  }
+  {
+    const Fill f[1] = {{L.w1, 48, dw1, 512, 40, 512}};
+    lds_fill(f);  // 5120 float4: 5 per thread
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
+    const bool v = m >= B && m < C;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      L.z1[row * 516 + 4 * c4 + i] = v ? zd[u][i] * act_bwd(zy[u][i], ACT_LRELU) : 0.f;
+  }
+  __syncthreads();
+  rows_layer<512, 40, B_KO, ACT_NONE>(L.z1, 516, L.w1, 48, nullptr, L.ddin, 44, L.scratch);
+  // log_softmax backward (noGT rows) / the CE gradient of the GT rows
+  {
+    const int row = wave, m = r0 + row;
+    float dl = 0.f;
+    if (m >= B && m < C) {
+      const float g = lane < 40 ? L.ddin[row * 44 + lane] : 0.f;
+      float s = g;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      if (lane < 40) {
+        dl = g - expf(din[(size_t)m * 40 + lane]) * s;
+        dlogits[(size_t)m * 40 + lane] = dl;
+      }
+    } else if (m < B && lane < 40) {
+      dl = dlogits[(size_t)m * 40 + lane];
+    }
+    if (lane < 40) L.dl[row * 44 + lane] = dl;
+  }
+  __syncthreads();
+  rows_layer<40, 256, B_KO, ACT_NONE>(L.dl, 44, w3, 256, nullptr, dh2 + (size_t)r0 * 256, 256,
+                                      nullptr, nrows);
+  if (blockIdx.x == 0 && tid == 0) {
+    // losses: CE mean, adversarial BCE mean, 0.5 x D-loss means (row-block order)
+    float s = 0.f;
+    for (int i = 0; i < nlp; ++i) s += lpart[i];
+    losses[0] = s / (float)B;
+    float a = 0.f, g = 0.f, n = 0.f;
+    for (int i = 0; i < nlp3; ++i) {
+      a += lpart3[3 * i];
+      g += lpart3[3 * i + 1];
+      n += lpart3[3 * i + 2];
+    }
+    losses[1] = a / (float)B;
+    losses[2] = 0.5f * g / (float)B;
+    losses[3] = 0.5f * n / (float)B;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <typename K>
+static int set_lds(K kern, size_t bytes, const char* what) {
+  static_assert(sizeof(K) > 0, "");
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
+    set_error("%s: cannot reserve %zu bytes of LDS", what, bytes);
+    return PCADV_EHIP;
+  }
+  return PCADV_OK;
+}
+
+size_t disc_tail_slab_floats() { return DT_SLAB; }
+int head_rowblocks(int B) { return (2 * B + TR - 1) / TR; }
+int disc_rowblocks(int B) { return (3 * B + TR - 1) / TR; }
+
+int launch_head_fwd(const float* h2, const float* w3, const float* b3, const int64_t* labels, int B,
+                    float lambda_cls, float* logits, float* dlogits, float* din, const float* dw1,
+                    const float* db1, float* d1, float* lpart, hipStream_t s) {
+  static bool once = false;
+  if (!once) {
+    if (set_lds(k_head_fwd, sizeof(HeadFwdLds), "head_fwd") != PCADV_OK) return PCADV_EHIP;
+    once = true;
+  }
+  hipLaunchKernelGGL(k_head_fwd, dim3(head_rowblocks(B)), dim3(TT), sizeof(HeadFwdLds), s, h2, w3,
+                     b3, labels, B, lambda_cls, logits, dlogits, din, dw1, db1, d1, lpart);
+  PC_HIP_CHECK_LAUNCH("k_head_fwd");
+  return PCADV_OK;
+}
+
+int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, const float* w5,
+                     const float* b5, const float* wf, const float* bf, const float* soft_gt,
+                     const float* soft_nogt, const int32_t* step, uint64_t seed, float lambda_adv,
+                     float* dd3, float* slabs, float* lpart3, hipStream_t s) {
+  static bool once = false;
+  if (!once) {
+    if (set_lds(k_disc_tail, sizeof(DiscTailLds), "disc_tail") != PCADV_OK) return PCADV_EHIP;
+    once = true;
+  }
+  hipLaunchKernelGGL(k_disc_tail, dim3(disc_rowblocks(B)), dim3(TT), sizeof(DiscTailLds), s, d3, B,
+                     w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3, slabs,
+                     lpart3);
+  PC_HIP_CHECK_LAUNCH("k_disc_tail");
+  return PCADV_OK;
+}
+
+int launch_head_bwd(const float* dd1, const float* d1, const float* din, int B, const float* dw1,
+                    const float* w3, float* dlogits, float* dh2, float* gw1, float* gb1,
+                    const float* lpart, const float* lpart3, float* losses, hipStream_t s) {
+  static bool once = false;
+  if (!once) {
+    if (set_lds(k_head_bwd, sizeof(HeadBwdLds), "head_bwd") != PCADV_OK) return PCADV_EHIP;
+    once = true;
+  }
+  const int nrb = head_rowblocks(B), nwb = (32 * 3 + TW - 1) / TW;
+  hipLaunchKernelGGL(k_head_bwd, dim3(nrb + nwb), dim3(TT), sizeof(HeadBwdLds), s, dd1, d1, din, B,
+                     dw1, w3, dlogits, dh2, gw1, gb1, lpart, nrb, lpart3, disc_rowblocks(B),
+                     losses);
+  PC_HIP_CHECK_LAUNCH("k_head_bwd");
+  return PCADV_OK;
+}
+
+}  // namespace pcadv
