@@ -57,6 +57,9 @@ int launch_head_fwd(const float*, const float*, const float*, const int64_t*, in
 int launch_disc_tail(const float*, int, const float*, const float*, const float*, const float*,
                      const float*, const float*, const float*, const float*, const int32_t*,
                      uint64_t, float, float*, float*, float*, hipStream_t);
+#ifdef PCADV_STAMPS
+int tail_stamps_read(uint64_t* host);
+#endif
 int launch_head_bwd(const float*, const float*, const float*, int, const float*, const float*,
                     float*, float*, float*, float*, const float*, const float*, float*,
                     hipStream_t);
@@ -270,6 +273,8 @@ int pcadv_feat_fwd_stamped(const float* pts, int C, int N, const float* w1, cons
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_workspace_bytes(C, N); }
 
 #ifdef PCADV_STAMPS
+int pcadv_tail_stamps(uint64_t* host) { return tail_stamps_read(host); }
+
 // diagnostic build only: pcadv_feat_bwd with per-workgroup phase timestamps
 int pcadv_feat_bwd_stamped(const float* dgmax, const int32_t* gidx, const float* pts, int C,
                            int N, const float* w1, const float* b1, const float* w2,

@@ -29,6 +29,14 @@ constexpr int TT = 1024;   // 16 waves
 constexpr int TW = TT / 64;
 
 typedef float f32x4t __attribute__((ext_vector_type(4)));
+
+#ifdef PCADV_STAMPS
+// diagnostic build only: phase timestamps (s_memrealtime) [kernel][block][16]
+__device__ uint64_t g_tail_stamps[3][16][16];
+#define TSTAMP(kern, k) do { if (threadIdx.x == 0 && blockIdx.x < 16) g_tail_stamps[kern][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TSTAMP(kern, k) do { } while (0)
+#endif
 __device__ __forceinline__ f32x4t mfma16t(float a, float b, f32x4t c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -42,12 +50,14 @@ enum BMode { B_OK = 0, B_KO = 1 };  // B[k][j] = W[j * ldw + k]  |  W[k * ldw + 
 // otherwise the chunk partials meet in scratch (>= items * 256 floats, LDS).
 // Rows >= dup_row are also written at out + dup_off (the duplicated noGT rows
 // of the discriminator input).
-template <int K, int NC, int MODE, int ACT>
+// KC0: reduction chunk per work item (default min(K, 128)); smaller chunks
+// spread a narrow layer over more waves at the cost of a partial-sum pass.
+template <int K, int NC, int MODE, int ACT, int KC0 = 128>
 __device__ __forceinline__ void rows_layer(const float* A, int as, const float* W, int ldw,
                                            const float* __restrict__ bias, float* out, int os,
                                            float* scratch, int nrows = TR, int dup_row = TR,
                                            long dup_off = 0) {
-  constexpr int KC = K < 128 ? K : 128;
+  constexpr int KC = K < KC0 ? K : KC0;
   constexpr int C = (K + KC - 1) / KC, T = (NC + 15) / 16, ITEMS = T * C;
   constexpr int NS = (KC + 3) / 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, q = lane >> 4;
@@ -114,15 +124,15 @@ struct Fill {
   int rows, cols, valid;
 };
 
-template <int NF>
+template <int NF, int NPT = 8>
 __device__ __forceinline__ void lds_fill(const Fill (&f)[NF]) {
   int base[NF + 1];
   base[0] = 0;
 #pragma unroll
   for (int d = 0; d < NF; ++d) base[d + 1] = base[d] + f[d].rows * (f[d].cols / 4);
-  f32x4 v[8];
+  f32x4 v[NPT];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < NPT; ++u) {
     const int e = threadIdx.x + u * TT;
     v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -134,7 +144,7 @@ __device__ __forceinline__ void lds_fill(const Fill (&f)[NF]) {
       }
   }
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < NPT; ++u) {
     const int e = threadIdx.x + u * TT;
 #pragma unroll
     for (int d = 0; d < NF; ++d)
@@ -179,6 +189,9 @@ __device__ void rows_wgrad(const float* Z, int zs, const float* X, int xs, float
 // ---------------------------------------------------------------------------
 struct HeadFwdLds {
   float w1[512 * 44];          // discriminator conv1 weight [512][40], padded rows
+  float w3[40 * 260];          // fc3 weight [40][256], padded rows
+  float b1[512];
+  float b3[40];
   alignas(16) float h2[TR * 260];
   float lg[TR * 44];
   float lsm[TR * 44];
@@ -194,13 +207,19 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
   extern __shared__ __attribute__((aligned(16))) char smem[];
   HeadFwdLds& L = *reinterpret_cast<HeadFwdLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  TSTAMP(0, 0);
   const int C = 2 * B, r0 = blockIdx.x * TR, nrows = min(TR, C - r0);
+  const int label = wave < nrows && r0 + wave < B ? (int)labels[r0 + wave] : 0;
   {
-    const Fill f[2] = {{L.w1, 44, dw1, 512, 40, 512}, {L.h2, 260, h2 + (size_t)r0 * 256, TR, 256, nrows}};
-    lds_fill(f);  // 6144 float4: 6 per thread
+    const Fill f[5] = {{L.w1, 44, dw1, 512, 40, 512}, {L.h2, 260, h2 + (size_t)r0 * 256, TR, 256, nrows},
+                       {L.b1, 512, db1, 1, 512, 1}, {L.b3, 40, b3, 1, 40, 1},
+                       {L.w3, 260, w3, 40, 256, 40}};
+    lds_fill<5, 9>(f);  // 8842 float4: <= 9 per thread
   }
   __syncthreads();
-  rows_layer<256, 40, B_OK, ACT_NONE>(L.h2, 260, w3, 256, b3, L.lg, 44, L.scratch);
+  TSTAMP(0, 1);
+  rows_layer<256, 40, B_OK, ACT_NONE>(L.h2, 260, L.w3, 260, L.b3, L.lg, 44, L.scratch);
+  TSTAMP(0, 2);
   // log_softmax, CrossEntropy (GT rows), discriminator input rows: one wave per row
   {
     const int row = wave, m = r0 + row;
@@ -221,7 +240,7 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
       if (m >= B) din[(size_t)(m + B) * 40 + lane] = lsm;
     }
     if (m < B) {
-      const int y = (int)labels[m];
+      const int y = label;
       const float sm = expf(lsm);
       if (lane < 40)
         dlogits[(size_t)m * 40 + lane] = lambda_cls * ((lane == y ? sm - 1.f : sm) / (float)B);
@@ -237,8 +256,10 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
   }
   // D conv1 on the GT rows (D rows [0,B)) and noGT rows (D rows [B,2B) and,
   // identical, [2B,3B)): rows r0.. of d1, copied to r0+B.. for noGT blocks
-  rows_layer<40, 512, B_OK, ACT_LRELU>(L.lsm, 44, L.w1, 44, db1, d1 + (size_t)r0 * 512, 512,
+  TSTAMP(0, 3);
+  rows_layer<40, 512, B_OK, ACT_LRELU>(L.lsm, 44, L.w1, 44, L.b1, d1 + (size_t)r0 * 512, 512,
                                        nullptr, nrows, max(0, B - r0), (long)B * 512);
+  TSTAMP(0, 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -250,6 +271,7 @@ struct DiscTailLds {
   float w4[64 * 260];          // conv4 weight [64][256], padded rows
   float w5[64 * 68];           // conv5 weight [64][64]
   float wf[64];                // fc weight [1][64]
+  float b4[64], b5[64], bf[4];
   alignas(16) float x3[TR * 260];   // conv3 output rows (conv4 input)
   float a4[TR * 68];
   float a5[TR * 68];
@@ -257,7 +279,7 @@ struct DiscTailLds {
   float z5[TR * 68];
   float z4[TR * 68];
   float lt[3][TR];
-  alignas(16) float scratch[8 * 256];
+  alignas(16) float scratch[16 * 256];
 };
 
 __global__ void __launch_bounds__(TT)
@@ -271,16 +293,32 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DiscTailLds& L = *reinterpret_cast<DiscTailLds*>(smem);
   const int tid = threadIdx.x;
+  TSTAMP(1, 0);
   const int R = 3 * B, r0 = blockIdx.x * TR, nrows = min(TR, R - r0);
+  // per-row label inputs, fetched with the weights (thread t < 16: row r0 + t)
+  float ysoft = 0.f;
+  uint32_t stepv = 0;
+  if (tid < TR) {
+    const int m = r0 + tid;
+    if (m < B && soft_gt) ysoft = soft_gt[m];
+    else if (m >= B && m < 2 * B && soft_nogt) ysoft = soft_nogt[m - B];
+    if (m < 2 * B && ((m < B && !soft_gt) || (m >= B && !soft_nogt))) stepv = (uint32_t)*step;
+  }
+  if (tid == 0) L.bf[0] = bf[0];
   {
-    const Fill f[4] = {{L.w4, 260, w4, 64, 256, 64}, {L.w5, 68, w5, 64, 64, 64},
-                       {L.wf, 64, wf, 1, 64, 1}, {L.x3, 260, d3 + (size_t)r0 * 256, TR, 256, nrows}};
-    lds_fill(f);  // 6160 float4: <= 7 per thread
+    const Fill f[6] = {{L.w4, 260, w4, 64, 256, 64}, {L.w5, 68, w5, 64, 64, 64},
+                       {L.wf, 64, wf, 1, 64, 1}, {L.x3, 260, d3 + (size_t)r0 * 256, TR, 256, nrows},
+                       {L.b4, 64, b4, 1, 64, 1}, {L.b5, 64, b5, 1, 64, 1}};
+    lds_fill(f);  // 6192 float4: <= 7 per thread
   }
   __syncthreads();
-  rows_layer<256, 64, B_OK, ACT_LRELU>(L.x3, 260, L.w4, 260, b4, L.a4, 68, L.scratch);
-  rows_layer<64, 64, B_OK, ACT_LRELU>(L.a4, 68, L.w5, 68, b5, L.a5, 68, L.scratch);
-  rows_layer<64, 1, B_OK, ACT_NONE>(L.a5, 68, L.wf, 64, bf, L.out, 4, L.scratch);
+  TSTAMP(1, 1);
+  rows_layer<256, 64, B_OK, ACT_LRELU, 64>(L.x3, 260, L.w4, 260, L.b4, L.a4, 68, L.scratch);
+  TSTAMP(1, 2);
+  rows_layer<64, 64, B_OK, ACT_LRELU, 16>(L.a4, 68, L.w5, 68, L.b5, L.a5, 68, L.scratch);
+  TSTAMP(1, 3);
+  rows_layer<64, 1, B_OK, ACT_NONE, 4>(L.a5, 68, L.wf, 64, L.bf, L.out, 4, L.scratch);
+  TSTAMP(1, 4);
   // BCEWithLogits terms (train_classification.py:200): rows [0,B) D(lsm_gt) vs U(0.7,1.05),
   // [B,2B) D(lsm_nogt) vs U(0,0.305), [2B,3B) adversarial vs 1
   if (tid < TR) {
@@ -290,13 +328,11 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
       const float x = L.out[tid * 4];
       float y, f;
       if (m < B) {
-        y = soft_gt ? soft_gt[m]
-                    : 0.7f + 0.35f * rng_uniform(seed, (uint32_t)*step, RNG_LABEL_GT, (uint32_t)m);
+        y = soft_gt ? ysoft : 0.7f + 0.35f * rng_uniform(seed, stepv, RNG_LABEL_GT, (uint32_t)m);
         f = 0.5f;
       } else if (m < 2 * B) {
-        y = soft_nogt ? soft_nogt[m - B]
-                      : 0.305f * rng_uniform(seed, (uint32_t)*step, RNG_LABEL_NOGT,
-                                             (uint32_t)(m - B));
+        y = soft_nogt ? ysoft
+                      : 0.305f * rng_uniform(seed, stepv, RNG_LABEL_NOGT, (uint32_t)(m - B));
         f = 0.5f;
       } else {
         y = 1.f;
@@ -320,13 +356,16 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
     lpart3[blockIdx.x * 3 + tid] = s;
   }
   // backward: fc (dz = dL/dout, no activation), conv5, conv4
+  TSTAMP(1, 5);
   rows_layer<1, 64, B_KO, ACT_NONE>(L.out + 1, 4, L.wf, 64, nullptr, L.z5, 68, L.scratch);
+  TSTAMP(1, 6);
   for (int e = tid; e < TR * 64; e += TT) {
     const int row = e >> 6, col = e & 63;
     L.z5[row * 68 + col] *= act_bwd(L.a5[row * 68 + col], ACT_LRELU);
   }
   __syncthreads();
-  rows_layer<64, 64, B_KO, ACT_NONE>(L.z5, 68, L.w5, 68, nullptr, L.z4, 68, L.scratch);
+  rows_layer<64, 64, B_KO, ACT_NONE, 16>(L.z5, 68, L.w5, 68, nullptr, L.z4, 68, L.scratch);
+  TSTAMP(1, 7);
   for (int e = tid; e < TR * 64; e += TT) {
     const int row = e >> 6, col = e & 63;
     L.z4[row * 68 + col] *= act_bwd(L.a4[row * 68 + col], ACT_LRELU);
@@ -334,6 +373,7 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
   __syncthreads();
   rows_layer<64, 256, B_KO, ACT_NONE>(L.z4, 68, L.w4, 260, nullptr, dd3 + (size_t)r0 * 256, 256,
                                       L.scratch, nrows);
+  TSTAMP(1, 8);
   // partial weight gradients over this block's D-loss rows (m < 2B; the
   // adversarial rows train only the generator)
   for (int e = tid; e < TR * 64; e += TT) {
@@ -346,8 +386,10 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
   if (tid < TR && r0 + tid >= 2 * B) L.out[tid * 4 + 1] = 0.f;
   __syncthreads();
   float* slab = slabs + (size_t)blockIdx.x * DT_SLAB;
+  TSTAMP(1, 9);
   rows_wgrad<64, 256>(L.z4, 68, L.x3, 260, slab, slab + 64 * 256);
   rows_wgrad<64, 64>(L.z5, 68, L.a4, 68, slab + 64 * 256 + 64, slab + 64 * 256 + 64 + 4096);
+  TSTAMP(1, 10);
   if (tid < 64) {
     float s = 0.f;
     for (int row = 0; row < TR; ++row) s = fmaf(L.out[row * 4 + 1], L.a5[row * 68 + tid], s);
@@ -418,7 +460,14 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
     }
     return;
   }
+  TSTAMP(2, 0);
   const int r0 = blockIdx.x * TR, nrows = min(TR, C - r0);
+  // this wave's row of log_softmax outputs (noGT) or CE gradient (GT)
+  float lsm_or_dl = 0.f;
+  {
+    const int m = r0 + wave;
+    if (m < C && lane < 40) lsm_or_dl = m >= B ? din[(size_t)m * 40 + lane] : dlogits[(size_t)m * 40 + lane];
+  }
   // dz of the adversarial D rows m + B (m in [B, 2B)); zero for GT rows.  The
   // row loads are issued together with the conv1 weight staging.
   f32x4 zd[2], zy[2];
@@ -443,7 +492,9 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
       L.z1[row * 516 + 4 * c4 + i] = v ? zd[u][i] * act_bwd(zy[u][i], ACT_LRELU) : 0.f;
   }
   __syncthreads();
+  TSTAMP(2, 1);
   rows_layer<512, 40, B_KO, ACT_NONE>(L.z1, 516, L.w1, 48, nullptr, L.ddin, 44, L.scratch);
+  TSTAMP(2, 2);
   // log_softmax backward (noGT rows) / the CE gradient of the GT rows
   {
     const int row = wave, m = r0 + row;
@@ -454,17 +505,19 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
       if (lane < 40) {
-        dl = g - expf(din[(size_t)m * 40 + lane]) * s;
+        dl = g - expf(lsm_or_dl) * s;
         dlogits[(size_t)m * 40 + lane] = dl;
       }
     } else if (m < B && lane < 40) {
-      dl = dlogits[(size_t)m * 40 + lane];
+      dl = lsm_or_dl;
     }
     if (lane < 40) L.dl[row * 44 + lane] = dl;
   }
   __syncthreads();
+  TSTAMP(2, 3);
   rows_layer<40, 256, B_KO, ACT_NONE>(L.dl, 44, w3, 256, nullptr, dh2 + (size_t)r0 * 256, 256,
                                       nullptr, nrows);
+  TSTAMP(2, 4);
   if (blockIdx.x == 0 && tid == 0) {
     // losses: CE mean, adversarial BCE mean, 0.5 x D-loss means (row-block order)
     float s = 0.f;
@@ -545,5 +598,13 @@ int launch_head_bwd(const float* dd1, const float* d1, const float* din, int B, 
   PC_HIP_CHECK_LAUNCH("k_head_bwd");
   return PCADV_OK;
 }
+
+#ifdef PCADV_STAMPS
+int tail_stamps_read(uint64_t* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tail_stamps), sizeof(g_tail_stamps)) == hipSuccess
+             ? PCADV_OK
+             : PCADV_EHIP;
+}
+#endif
 
 }  // namespace pcadv
