@@ -31,7 +31,7 @@ size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
                           const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
-                          hipStream_t, uint64_t* stamps = nullptr, int stagger = 20);
+                          hipStream_t, uint64_t* stamps = nullptr);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t,
                       int add_identity_k = 0, float* mask_out = nullptr);
@@ -264,9 +264,9 @@ int pcadv_feat_fwd_stamped(const float* pts, int C, int N, const float* w1, cons
                            const float* w2, const float* b2, const float* w3, const float* b3,
                            const float* w4, const float* b4, float* x3, float* gmax,
                            int32_t* gidx, void* workspace, size_t workspace_bytes,
-                           uint64_t* stamps, int stagger, hipStream_t stream) {
+                           uint64_t* stamps, hipStream_t stream) {
   return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
-                               nullptr, workspace, workspace_bytes, stream, stamps, stagger);
+                               nullptr, workspace, workspace_bytes, stream, stamps);
 }
 #endif
 

@@ -29,14 +29,21 @@ constexpr int FF_O = 1024;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// Two 128-point tiles per workgroup.  X holds tile A's conv3 output split to
+// bf16 hi/lo; Y holds tile A's, then tile B's conv1/conv2 outputs (f32), and
+// finally tile B's split conv3 output.
 struct FwdLds {
-  alignas(16) float pts[FF_P * 4];
-  alignas(16) float x2[FF_P * S64];
+  alignas(16) float pts[2][FF_P * 4];
+  alignas(16) __bf16 x[2][FF_P * FF_SB];  // tile A x3: hi, lo
   union U {
-    float x1[FF_P * S64];          // dies after conv2
-    __bf16 x3[2][FF_P * FF_SB];    // hi, lo: born in conv3's epilogue
+    struct {
+      float x1[FF_P * S64];
+      float x2[FF_P * S64];
+    } f;
+    __bf16 x3[2][FF_P * FF_SB];            // tile B x3: hi, lo
   };
-  alignas(16) U u;
+  alignas(16) U y;
+  int sync[2];                             // producer-wave arrival counters
 };
 
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -95,6 +102,34 @@ __device__ __forceinline__ void top2_merge(float v, int p, float& v1, int& i1, f
   i2 = ni2;
 }
 
+// wave-group barrier among the 4 producer waves (4..7) through an LDS counter:
+// every wave publishes its LDS writes, then waits for the others
+// (every spin is bounded: a lost arrival cannot hang the device)
+__device__ __forceinline__ void group_wait(int* cnt, int target) {
+  for (int spin = 0; spin < (1 << 22); ++spin) {
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void group_sync(int* cnt, int target) {
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS (and memory) writes are done
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  group_wait(cnt, target);
+}
+
+constexpr int FF_NB = 6;  // tile-A channel units a consumer wave runs while tile B's conv1-3 run
+
+// Pipelined over two point tiles A, B of one cloud:
+//   phase A  all 8 waves: conv1..conv3 of tile A (x1, x2 in Y; x3 -> HBM + X)
+//   phase B  waves 0-3: conv4 + screening of tile A, 6 of their 8 channel
+//            units; waves 4-7: conv1..conv3 of tile B (x3 kept in registers)
+//   phase C  waves 4-7 split tile B's x3 into Y; then waves 0-3 finish their
+//            2 tile-A units and take 3 tile-B units, waves 4-7 take 5 tile-B
+//            units (32 tile-B units in all)
+// so the matrix pipe is fed by conv4 while tile B's narrow layers run.
 __global__ void __launch_bounds__(FF_T)
 k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
                  int N, const float* __restrict__ w1, const float* __restrict__ b1,
@@ -102,66 +137,63 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
                  const float* __restrict__ w3, const float* __restrict__ b3,
                  const float* __restrict__ w4, const float* __restrict__ b4,
                  float* __restrict__ x3g, int2* __restrict__ part, int32_t* inc_counter,
-                 uint64_t* __restrict__ stamps, int stagger) {
+                 uint64_t* __restrict__ stamps, int T) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FwdLds& L = *reinterpret_cast<FwdLds*>(smem);
 #ifdef PCADV_STAMPS
   // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
   uint64_t* st = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
-#define STAMP(k) do { if (stamps && threadIdx.x == 0) { st[k] = __builtin_amdgcn_s_memrealtime(); if ((k) == 0 || (k) == 14) st[15 - ((k) == 0 ? 0 : 2)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define STAMP(k) do { if (stamps && (threadIdx.x & 63) == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
 #endif
-  STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int c = blockIdx.y, tile = blockIdx.x, p0 = tile * FF_P, T = gridDim.x;
-  if (inc_counter && tid == 0 && c == 0 && tile == 0) *inc_counter += 1;
+  const int c = blockIdx.y, tA = 2 * blockIdx.x, tB = tA + 1;
+  const bool hasB = tB < T;
+  if (wave == 0) STAMP(0);
+  if (inc_counter && tid == 0 && c == 0 && blockIdx.x == 0) *inc_counter += 1;
   const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
 
-  // conv2 / conv3 B fragments are fetched up front: they land during conv1
+  // conv2 / conv3 B fragments of phase A are fetched up front: they land during conv1
   f32x4 bf2[8], bf3[8];
   load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
   load_bfrag<64>(w3, 32 * (wave & 3), lane, bf3);
-  if (tid < FF_P * 3) {
-    const int p = tid / 3, k = tid % 3;
-    L.pts[p * 4 + k] = (p0 + p < N) ? pts[(size_t)(p0 + p) * 3 + k] : 0.f;
+  for (int e = tid; e < 2 * FF_P * 3; e += FF_T) {
+    const int t = e / (FF_P * 3), p = (e % (FF_P * 3)) / 3, k = e % 3;
+    const int gp = (tA + t) * FF_P + p;
+    L.pts[t][p * 4 + k] = gp < N ? pts[(size_t)gp * 3 + k] : 0.f;
   }
+  if (tid < 2) L.sync[tid] = 0;
   __syncthreads();
 
-  STAMP(1);
-  // ---- conv1 (3 -> 64) + ReLU: thread = (channel, 16-point group) ------------
-  {
-    const int ch = tid & 63, pg = tid >> 6;
+  // ---- conv1 (3 -> 64) + ReLU of one tile: NT threads = (channel, point group)
+  auto conv1 = [&](const float* ps, int t0, int NT) {
+    const int ch = t0 & 63, pg = t0 >> 6, per = FF_P / (NT / 64);
     const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int p = pg * 16 + i;
-      L.u.x1[p * S64 + ch] =
-          conv1_point(wa, wb, wc, bb, L.pts[p * 4 + 0], L.pts[p * 4 + 1], L.pts[p * 4 + 2]);
+    for (int i = 0; i < per; ++i) {
+      const int p = pg * per + i;
+      L.y.f.x1[p * S64 + ch] = conv1_point(wa, wb, wc, bb, ps[p * 4 + 0], ps[p * 4 + 1], ps[p * 4 + 2]);
     }
-  }
-  __syncthreads();
-
-  STAMP(2);
-  // ---- conv2 (64 -> 64) + ReLU: wave -> (point tile, channel tile) ----------
-  {
-    const int pt = wave >> 1, ct = wave & 1;
+  };
+  // ---- conv2 (64 -> 64) + ReLU, one 32x32 tile (point tile pt, channel tile ct)
+  auto conv2 = [&](int pt, int ct, const f32x4* bf) {
     f32x16 acc = {};
-    acc = mfma_rows_x_wt<64>(L.u.x1 + 32 * pt * S64, S64, bf2, acc, lane);
+    acc = mfma_rows_x_wt<64>(L.y.f.x1 + 32 * pt * S64, S64, bf, acc, lane);
     const int col = 32 * ct + r;
     const float bias = b2[col];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float v = acc[i] + bias;
-      L.x2[(32 * pt + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
+      L.y.f.x2[(32 * pt + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
     }
-  }
+  };
+  // ================= phase A: conv1..conv3 of tile A, all waves ===============
+  conv1(L.pts[0], tid, FF_T);
   __syncthreads();
-
-  STAMP(3);
-  // W4 fragments (f32) of this wave's first conv4 channel tile, issued before
-  // conv3's epilogue so they land during it
+  conv2(wave >> 1, wave & 1, bf2);
+  __syncthreads();
+  // W4 fragments (f32) of a channel unit; one unit is prefetched at a time
   f32x4 wf[16];
   auto wload = [&](int o0) {
     const float* row = w4 + (size_t)(o0 + r) * 128 + 8 * h;
@@ -171,97 +203,159 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
       wf[2 * kb + 1] = *reinterpret_cast<const f32x4*>(row + 16 * kb + 4);
     }
   };
-  // ---- conv3 (64 -> 128) + ReLU: wave -> (channel tile, 2 point tiles) ------
   {
     const int ct = wave & 3, pp = 2 * (wave >> 2);
     f32x16 acc0 = {}, acc1 = {};
-    acc0 = mfma_rows_x_wt<64>(L.x2 + 32 * pp * S64, S64, bf3, acc0, lane);
-    acc1 = mfma_rows_x_wt<64>(L.x2 + 32 * (pp + 1) * S64, S64, bf3, acc1, lane);
-    wload(128 * wave);
+    acc0 = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * pp * S64, S64, bf3, acc0, lane);
+    acc1 = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * (pp + 1) * S64, S64, bf3, acc1, lane);
+    // first conv4 unit of the consumer waves (channel tile 8 * wave)
+    if (wave < 4) wload(256 * wave);
     const int col = 32 * ct + r;
     const float bias = b3[col];
+    const int p0 = tA * FF_P;
     float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int row = 32 * (pp + s) + acc_row(i, lane);
-        float v = (s == 0 ? acc0[i] : acc1[i]) + bias;
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = 32 * (pp + s2) + acc_row(i, lane);
+        float v = (s2 == 0 ? acc0[i] : acc1[i]) + bias;
         v = v > 0.f ? v : 0.f;
         if (p0 + row < N) xg[(size_t)row * 128] = v;
         const __bf16 hb = (__bf16)v;
-        L.u.x3[0][row * FF_SB + col] = hb;
-        L.u.x3[1][row * FF_SB + col] = (__bf16)(v - (float)hb);
+        L.x[0][row * FF_SB + col] = hb;
+        L.x[1][row * FF_SB + col] = (__bf16)(v - (float)hb);
       }
     }
   }
   __syncthreads();
+  if (wave == 0 || wave == 4) STAMP(1 + (wave >> 2));
 
-  STAMP(4);
-  // ---- conv4 (128 -> 1024) split-bf16 MFMA + top-2 over the tile's points ---
-  // wave -> channels [128*wave, 128*wave + 128) as 4 tiles of 32
-  {
-    const __bf16* xh = L.u.x3[0] + r * FF_SB + 8 * h;
-    const __bf16* xl = L.u.x3[1] + r * FF_SB + 8 * h;
+  // ---- conv4 (128 -> 1024) split-bf16 MFMA + top-2 screening of one channel
+  //      unit (32 channels x the tile's 128 points); wf holds the unit's W4
+  //      fragments and is refilled with those of `next` (-1: none) -----------
+  auto conv4_unit = [&](const __bf16* xhi, const __bf16* xlo, int tile, int ct, int next) {
+    const __bf16* xh = xhi + r * FF_SB + 8 * h;
+    const __bf16* xl = xlo + r * FF_SB + 8 * h;
+    const int p0 = tile * FF_P;
     const bool full = p0 + FF_P <= N;
-    // waves w and w+4 share a SIMD and run the same program: delay the upper
-    // half by about half a tile so one wave's epilogue (VALU) overlaps the
-    // other's MFMAs instead of both idling the matrix pipe together
-    if (__builtin_amdgcn_readfirstlane(wave) >= 4)
-      for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(1);
-    for (int ct = 0; ct < 4; ++ct) {
-      const int o0 = 128 * wave + 32 * ct;
-      bf16x8 bh[8], bl[8];
+    const int o0 = 32 * ct;
+    bf16x8 bh[8], bl[8];
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) split8(wf[2 * kb], wf[2 * kb + 1], bh[kb], bl[kb]);
-      f32x16 acc[4] = {{}, {}, {}, {}};
+    for (int kb = 0; kb < 8; ++kb) split8(wf[2 * kb], wf[2 * kb + 1], bh[kb], bl[kb]);
+    f32x16 acc[4] = {{}, {}, {}, {}};
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
+    for (int kb = 0; kb < 8; ++kb) {
 #pragma unroll
-        for (int pt = 0; pt < 4; ++pt) {
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(xh + 32 * pt * FF_SB + 16 * kb);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(xl + 32 * pt * FF_SB + 16 * kb);
-          acc[pt] = mfma_bf16(al, bh[kb], acc[pt]);
-          acc[pt] = mfma_bf16(ah, bl[kb], acc[pt]);
-          acc[pt] = mfma_bf16(ah, bh[kb], acc[pt]);
+      for (int pt = 0; pt < 4; ++pt) {
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(xh + 32 * pt * FF_SB + 16 * kb);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(xl + 32 * pt * FF_SB + 16 * kb);
+        acc[pt] = mfma_bf16(al, bh[kb], acc[pt]);
+        acc[pt] = mfma_bf16(ah, bl[kb], acc[pt]);
+        acc[pt] = mfma_bf16(ah, bh[kb], acc[pt]);
+      }
+    }
+    // the next unit's weights are fetched only now, when bh/bl are dead, so the
+    // prefetch buffer and the split fragments never live at the same time
+    __builtin_amdgcn_sched_barrier(0);
+    if (next >= 0) wload(32 * next);
+    __builtin_amdgcn_sched_barrier(0);
+    // screening top-2 over the tile's 128 points (bias is added by the exact
+    // re-evaluation in k_gmax_combine; it does not change the order)
+    int k1 = KEY_NONE, k2 = KEY_NONE;
+    if (full) {
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          key_push(screen_key(acc[pt][i], 32 * pt + acc_row(i, lane)), k1, k2);
+    } else {
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int idx = 32 * pt + acc_row(i, lane);
+          if (p0 + idx < N) key_push(screen_key(acc[pt][i], idx), k1, k2);
         }
+    }
+    // lanes l and l+32 hold the same channel over interleaved rows
+    const int o1 = __shfl_xor(k1, 32), o2 = __shfl_xor(k2, 32);
+    k2 = max(min(k1, o1), max(k2, o2));
+    k1 = max(k1, o1);
+    if (lane < 32) part[((size_t)c * T + tile) * FF_O + o0 + r] = make_int2(k1, k2);
+  };
+
+  // per-wave unit lists: consumer wave w owns tile-A channel tiles 8w..8w+7;
+  // tile-B channel tiles: waves 4-7 -> 5 each from 0, waves 0-3 -> 3 each from 20
+  const int nBu = hasB ? (wave < 4 ? 3 : 5) : 0;
+  const int bBase = wave < 4 ? 20 + 3 * wave : 5 * (wave - 4);
+
+  if (wave < 4) {
+    // ================= phase B, consumers: tile-A units 0..5 ==================
+    for (int j = 0; j < FF_NB; ++j) conv4_unit(L.x[0], L.x[1], tA, 8 * wave + j, 8 * wave + j + 1);
+    STAMP(3);
+  } else if (hasB) {
+    // ================= phase B, producers: conv1..conv3 of tile B =============
+    const int pw = wave - 4, t0 = tid - 256;
+    conv1(L.pts[1], t0, 256);
+    group_sync(&L.sync[0], 4);
+    f32x4 bfa[8], bfb[8];
+    load_bfrag<64>(w2, 0, lane, bfa);
+    load_bfrag<64>(w2, 32, lane, bfb);
+    conv2(pw, 0, bfa);
+    conv2(pw, 1, bfb);
+    group_sync(&L.sync[0], 8);
+    // conv3: producer wave pw -> channel tile pw, all 4 point tiles
+    load_bfrag<64>(w3, 32 * pw, lane, bf3);
+    f32x16 acc3[4];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      acc3[pt] = f32x16{};
+      acc3[pt] = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * pt * S64, S64, bf3, acc3[pt], lane);
+    }
+    const int col = 32 * pw + r;
+    const float bias = b3[col];
+    const int p0 = tB * FF_P;
+    float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 32 * pt + acc_row(i, lane);
+        float v = acc3[pt][i] + bias;
+        v = v > 0.f ? v : 0.f;
+        acc3[pt][i] = v;
+        if (p0 + row < N) xg[(size_t)row * 128] = v;
       }
-      if (wave == 0) STAMP(5 + 2 * ct);
-      // next tile's weights are fetched only now, when bh/bl are dead, so the
-      // prefetch buffer and the split fragments never live at the same time
-      __builtin_amdgcn_sched_barrier(0);
-      if (ct < 3) wload(o0 + 32);
-      __builtin_amdgcn_sched_barrier(0);
-      // screening top-2 over the tile's 128 points (bias is added by the exact
-      // re-evaluation in k_gmax_combine; it does not change the order)
-      int k1 = KEY_NONE, k2 = KEY_NONE;
-      if (full) {
+    STAMP(4);
+    // ================= phase C, producers: split tile B's x3 into Y ===========
+    group_sync(&L.sync[1], 4);  // every producer's conv3 MFMAs have read x2
 #pragma unroll
-        for (int pt = 0; pt < 4; ++pt)
+    for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            key_push(screen_key(acc[pt][i], 32 * pt + acc_row(i, lane)), k1, k2);
-      } else {
-#pragma unroll
-        for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int idx = 32 * pt + acc_row(i, lane);
-            if (p0 + idx < N) key_push(screen_key(acc[pt][i], idx), k1, k2);
-          }
+      for (int i = 0; i < 16; ++i) {
+        const int row = 32 * pt + acc_row(i, lane);
+        const float v = acc3[pt][i];
+        const __bf16 hb = (__bf16)v;
+        L.y.x3[0][row * FF_SB + col] = hb;
+        L.y.x3[1][row * FF_SB + col] = (__bf16)(v - (float)hb);
       }
-      // lanes l and l+32 hold the same channel over interleaved rows
-      const int o1 = __shfl_xor(k1, 32), o2 = __shfl_xor(k2, 32);
-      k2 = max(min(k1, o1), max(k2, o2));
-      k1 = max(k1, o1);
-      if (lane < 32) part[((size_t)c * T + tile) * FF_O + o0 + r] = make_int2(k1, k2);
-      if (wave == 0) STAMP(6 + 2 * ct);
+    wload(32 * bBase);
+    group_sync(&L.sync[1], 8);
+  }
+
+  if (wave < 4) {
+    // ================= phase C, consumers: tile-A units 6, 7; tile-B units ====
+    conv4_unit(L.x[0], L.x[1], tA, 8 * wave + 6, 8 * wave + 7);
+    conv4_unit(L.x[0], L.x[1], tA, 8 * wave + 7, nBu > 0 ? bBase : -1);
+    if (nBu > 0) {
+      // tile B's split x3 is complete once all 4 producers have arrived
+      group_wait(&L.sync[1], 8);
     }
   }
-#ifdef PCADV_STAMPS
-  __syncthreads();
-#endif
-  STAMP(14);
+  for (int j = 0; j < nBu; ++j)
+    conv4_unit(L.y.x3[0], L.y.x3[1], tB, bBase + j, j + 1 < nBu ? bBase + j + 1 : -1);
+  if (wave == 0 || wave == 4) STAMP(5 + (wave >> 2));
 #undef STAMP
 }
 
@@ -276,7 +370,14 @@ k_gmax_combine(const int2* __restrict__ part, int T, int C, int N,
   const int q = threadIdx.x & 3;
   const int g = blockIdx.x * 64 + (threadIdx.x >> 2);  // (cloud, channel) pair
   const int c = g / FF_O, o = g % FF_O;
-  if (c >= C) return;  // C * FF_O is a multiple of 64: whole waves leave together
+  if (c >= C) return;  // C * FF_O is a multiple of 64: whole waves leave
+  // this lane's quarter of W4[o] and the bias do not depend on the merge:
+  // fetched together with the partials
+  const float* wrow = w4 + (size_t)o * 128 + 32 * q;
+  f32x4 wv[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) wv[u] = *reinterpret_cast<const f32x4*>(wrow + 4 * u);
+  const float bias = b4[o];
   float v1 = -INFINITY, v2 = -INFINITY;
   int i1 = 0x7fffffff, i2 = 0x7fffffff;
   for (int t = q; t < T; t += 4) {
@@ -293,17 +394,19 @@ k_gmax_combine(const int2* __restrict__ part, int T, int C, int N,
   }
   if (i1 == 0x7fffffff) i1 = 0;
   // screening error <= ~1.2e-5 sum|x w| (+2^-16 key truncation): re-check
-  // anything within a far wider window of the winner in exact f32
+  // anything within a far wider window of the winner in exact f32; both rows
+  // are fetched in one round trip
   const bool near = i2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
-  const float* wrow = w4 + (size_t)o * 128 + 32 * q;
-  auto dot = [&](int n) {
-    const float* xrow = x3g + ((size_t)c * N + n) * 128 + 32 * q;
-    f32x4 xv[8], wv[8];
+  const float* x1r = x3g + ((size_t)c * N + i1) * 128 + 32 * q;
+  const float* x2r = x3g + ((size_t)c * N + (near ? i2 : i1)) * 128 + 32 * q;
+  f32x4 xa[8], xb[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      xv[u] = *reinterpret_cast<const f32x4*>(xrow + 4 * u);
-      wv[u] = *reinterpret_cast<const f32x4*>(wrow + 4 * u);
-    }
+  for (int u = 0; u < 8; ++u) xa[u] = *reinterpret_cast<const f32x4*>(x1r + 4 * u);
+  if (near) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xb[u] = *reinterpret_cast<const f32x4*>(x2r + 4 * u);
+  }
+  auto dot = [&](const f32x4* xv) {
     float d = 0.f;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -316,10 +419,9 @@ k_gmax_combine(const int2* __restrict__ part, int T, int C, int N,
     d += __shfl_xor(d, 2);
     return d;
   };
-  const float bias = b4[o];
-  const float e1 = dot(i1) + bias;
+  const float e1 = dot(xa) + bias;
   float e2 = 0.f;
-  if (near) e2 = dot(i2) + bias;
+  if (near) e2 = dot(xb) + bias;
   const bool second = near && ranks_before(e2, i2, e1, i1);
   if (q == 0) {
     gmax[(size_t)c * FF_O + o] = second ? e2 : e1;
@@ -336,7 +438,7 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
                           const float* w1, const float* b1, const float* w2, const float* b2,
                           const float* w3, const float* b3, const float* w4, const float* b4,
                           float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
-                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int stagger) {
+                          size_t ws_bytes, hipStream_t s, uint64_t* stamps) {
   PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
   PC_REQUIRE(ws && ws_bytes >= feat_fwd_workspace_bytes(C, N), "feat_fwd: workspace too small");
   const int T = (N + FF_P - 1) / FF_P;
@@ -351,9 +453,9 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
     attr_set = true;
   }
   int2* part = static_cast<int2*>(ws);
-  hipLaunchKernelGGL(k_feat_fwd_fused, dim3(T, C), dim3(FF_T), sizeof(FwdLds), s, pts_a, pts_b,
-                     split, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, part, inc_counter, stamps,
-                     stagger);
+  hipLaunchKernelGGL(k_feat_fwd_fused, dim3((T + 1) / 2, C), dim3(FF_T), sizeof(FwdLds), s, pts_a,
+                     pts_b, split, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, part, inc_counter, stamps,
+                     T);
   PC_HIP_CHECK_LAUNCH("k_feat_fwd_fused");
   hipLaunchKernelGGL(k_gmax_combine, dim3(C * FF_O / 64), dim3(256), 0, s, part, T, C, N, x3, w4,
                      b4, gmax, gidx);
