@@ -23,7 +23,7 @@
 namespace pcadv {
 
 constexpr int FF_P = 128;   // points per workgroup
-constexpr int FF_T = 512;   // threads (8 waves, 1 workgroup per CU)
+constexpr int FF_T = 1024;  // threads (16 waves = 4 per SIMD, 1 workgroup per CU)
 constexpr int FF_SB = 136;  // bf16 row stride of the x3 hi/lo tiles (272 B)
 constexpr int FF_O = 1024;
 
@@ -48,17 +48,6 @@ struct FwdLds {
 
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// split 8 floats into bf16 hi / lo parts (x ~= hi + lo to ~2^-17 relative)
-__device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, bf16x8& hi, bf16x8& lo) {
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 hb = (__bf16)v[j];
-    hi[j] = hb;
-    lo[j] = (__bf16)(v[j] - (float)hb);
-  }
 }
 
 // Screening keys: the f32 value mapped to an order-preserving int32 with the
@@ -120,22 +109,40 @@ __device__ __forceinline__ void group_sync(int* cnt, int target) {
   group_wait(cnt, target);
 }
 
-constexpr int FF_NB = 6;  // tile-A channel units a consumer wave runs while tile B's conv1-3 run
+// conv4 weights split once per launch into bf16 hi / lo ([1024][128] each), so
+// the screening loop loads its B operands directly
+__global__ void __launch_bounds__(256)
+k_w4_split(const float* __restrict__ w4, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= FF_O * 128) return;
+  const f32x4 v = *reinterpret_cast<const f32x4*>(w4 + i);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 hb = (__bf16)v[j];
+    hi[i + j] = hb;
+    lo[i + j] = (__bf16)(v[j] - (float)hb);
+  }
+}
 
-// Pipelined over two point tiles A, B of one cloud:
-//   phase A  all 8 waves: conv1..conv3 of tile A (x1, x2 in Y; x3 -> HBM + X)
-//   phase B  waves 0-3: conv4 + screening of tile A, 6 of their 8 channel
-//            units; waves 4-7: conv1..conv3 of tile B (x3 kept in registers)
-//   phase C  waves 4-7 split tile B's x3 into Y; then waves 0-3 finish their
-//            2 tile-A units and take 3 tile-B units, waves 4-7 take 5 tile-B
-//            units (32 tile-B units in all)
-// so the matrix pipe is fed by conv4 while tile B's narrow layers run.
+constexpr int FF_NB = 2;   // tile-A units a consumer wave runs while tile B's conv1-3 run
+constexpr int FF_NCW = 8;  // consumer waves (0-7); producer waves 8-15
+
+// Pipelined over two point tiles A, B of one cloud (16 waves, 4 per SIMD):
+//   phase A  all waves: conv1..conv3 of tile A (x1, x2 in Y; x3 -> HBM + X)
+//   phase B  waves 0-7: conv4 + screening of tile A, 2 of their 4 channel
+//            units; waves 8-15: conv1..conv3 of tile B (x3 kept in registers)
+//   phase C  waves 8-15 split tile B's x3 into Y; waves 0-7 finish their 2
+//            tile-A units and take 1 tile-B unit each, waves 8-15 take 3
+//            tile-B units each (32 tile-B units in all)
+// A unit is 32 channels x 128 points, run in two 64-point halves so that a
+// wave stays within 128 VGPRs: four waves per SIMD keep the matrix pipe fed
+// while any one of them waits on LDS or runs its screening epilogue.
 __global__ void __launch_bounds__(FF_T)
 k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
                  int N, const float* __restrict__ w1, const float* __restrict__ b1,
                  const float* __restrict__ w2, const float* __restrict__ b2,
                  const float* __restrict__ w3, const float* __restrict__ b3,
-                 const float* __restrict__ w4, const float* __restrict__ b4,
+                 const __bf16* __restrict__ w4hi, const __bf16* __restrict__ w4lo,
                  float* __restrict__ x3g, int2* __restrict__ part, int32_t* inc_counter,
                  uint64_t* __restrict__ stamps, int T) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -155,10 +162,6 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
   if (inc_counter && tid == 0 && c == 0 && blockIdx.x == 0) *inc_counter += 1;
   const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
 
-  // conv2 / conv3 B fragments of phase A are fetched up front: they land during conv1
-  f32x4 bf2[8], bf3[8];
-  load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
-  load_bfrag<64>(w3, 32 * (wave & 3), lane, bf3);
   for (int e = tid; e < 2 * FF_P * 3; e += FF_T) {
     const int t = e / (FF_P * 3), p = (e % (FF_P * 3)) / 3, k = e % 3;
     const int gp = (tA + t) * FF_P + p;
@@ -177,7 +180,9 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
     }
   };
   // ---- conv2 (64 -> 64) + ReLU, one 32x32 tile (point tile pt, channel tile ct)
-  auto conv2 = [&](int pt, int ct, const f32x4* bf) {
+  auto conv2 = [&](int pt, int ct) {
+    f32x4 bf[8];
+    load_bfrag<64>(w2, 32 * ct, lane, bf);
     f32x16 acc = {};
     acc = mfma_rows_x_wt<64>(L.y.f.x1 + 32 * pt * S64, S64, bf, acc, lane);
     const int col = 32 * ct + r;
@@ -188,94 +193,95 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
       L.y.f.x2[(32 * pt + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
     }
   };
-  // ================= phase A: conv1..conv3 of tile A, all waves ===============
-  conv1(L.pts[0], tid, FF_T);
-  __syncthreads();
-  conv2(wave >> 1, wave & 1, bf2);
-  __syncthreads();
-  // W4 fragments (f32) of a channel unit; one unit is prefetched at a time
-  f32x4 wf[16];
-  auto wload = [&](int o0) {
-    const float* row = w4 + (size_t)(o0 + r) * 128 + 8 * h;
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      wf[2 * kb] = *reinterpret_cast<const f32x4*>(row + 16 * kb);
-      wf[2 * kb + 1] = *reinterpret_cast<const f32x4*>(row + 16 * kb + 4);
-    }
-  };
-  {
-    const int ct = wave & 3, pp = 2 * (wave >> 2);
-    f32x16 acc0 = {}, acc1 = {};
-    acc0 = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * pp * S64, S64, bf3, acc0, lane);
-    acc1 = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * (pp + 1) * S64, S64, bf3, acc1, lane);
-    // first conv4 unit of the consumer waves (channel tile 8 * wave)
-    if (wave < 4) wload(256 * wave);
+  // ---- conv3 (64 -> 128) + ReLU, one 32x32 tile; the value also goes to HBM
+  auto conv3 = [&](int tile, int pt, int ct, f32x16& acc) {
+    f32x4 bf[8];
+    load_bfrag<64>(w3, 32 * ct, lane, bf);
+    acc = f32x16{};
+    acc = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * pt * S64, S64, bf, acc, lane);
     const int col = 32 * ct + r;
     const float bias = b3[col];
-    const int p0 = tA * FF_P;
+    const int p0 = tile * FF_P;
     float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int row = 32 * (pp + s2) + acc_row(i, lane);
-        float v = (s2 == 0 ? acc0[i] : acc1[i]) + bias;
-        v = v > 0.f ? v : 0.f;
-        if (p0 + row < N) xg[(size_t)row * 128] = v;
-        const __bf16 hb = (__bf16)v;
-        L.x[0][row * FF_SB + col] = hb;
-        L.x[1][row * FF_SB + col] = (__bf16)(v - (float)hb);
-      }
+      const int row = 32 * pt + acc_row(i, lane);
+      float v = acc[i] + bias;
+      v = v > 0.f ? v : 0.f;
+      acc[i] = v;
+      if (p0 + row < N) xg[(size_t)row * 128] = v;
     }
+  };
+  auto x3_split = [&](__bf16* hi, __bf16* lo, int pt, int ct, const f32x16& acc) {
+    const int col = 32 * ct + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = 32 * pt + acc_row(i, lane);
+      const __bf16 hb = (__bf16)acc[i];
+      hi[row * FF_SB + col] = hb;
+      lo[row * FF_SB + col] = (__bf16)(acc[i] - (float)hb);
+    }
+  };
+
+  // ================= phase A: conv1..conv3 of tile A, all waves ===============
+  conv1(L.pts[0], tid, FF_T);
+  __syncthreads();
+  if (wave < 8) conv2(wave >> 1, wave & 1);
+  __syncthreads();
+  {
+    f32x16 acc;
+    conv3(tA, wave >> 2, wave & 3, acc);
+    x3_split(L.x[0], L.x[1], wave >> 2, wave & 3, acc);
   }
   __syncthreads();
-  if (wave == 0 || wave == 4) STAMP(1 + (wave >> 2));
+  if (wave == 0 || wave == 8) STAMP(1 + (wave >> 3));
 
   // ---- conv4 (128 -> 1024) split-bf16 MFMA + top-2 screening of one channel
-  //      unit (32 channels x the tile's 128 points); wf holds the unit's W4
-  //      fragments and is refilled with those of `next` (-1: none) -----------
-  auto conv4_unit = [&](const __bf16* xhi, const __bf16* xlo, int tile, int ct, int next) {
-    const __bf16* xh = xhi + r * FF_SB + 8 * h;
-    const __bf16* xl = xlo + r * FF_SB + 8 * h;
+  //      unit (32 channels x the tile's 128 points) --------------------------
+  auto conv4_unit = [&](const __bf16* xhi, const __bf16* xlo, int tile, int ct) {
     const int p0 = tile * FF_P;
     const bool full = p0 + FF_P <= N;
     const int o0 = 32 * ct;
+    // B operands: lane (r, h) holds W4[o0 + r][16 kb + 8 h .. + 8) hi and lo
     bf16x8 bh[8], bl[8];
+    {
+      const __bf16* ph = w4hi + (size_t)(o0 + r) * 128 + 8 * h;
+      const __bf16* pl = w4lo + (size_t)(o0 + r) * 128 + 8 * h;
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) split8(wf[2 * kb], wf[2 * kb + 1], bh[kb], bl[kb]);
-    f32x16 acc[4] = {{}, {}, {}, {}};
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(xh + 32 * pt * FF_SB + 16 * kb);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(xl + 32 * pt * FF_SB + 16 * kb);
-        acc[pt] = mfma_bf16(al, bh[kb], acc[pt]);
-        acc[pt] = mfma_bf16(ah, bl[kb], acc[pt]);
-        acc[pt] = mfma_bf16(ah, bh[kb], acc[pt]);
+      for (int kb = 0; kb < 8; ++kb) {
+        bh[kb] = *reinterpret_cast<const bf16x8*>(ph + 16 * kb);
+        bl[kb] = *reinterpret_cast<const bf16x8*>(pl + 16 * kb);
       }
     }
-    // the next unit's weights are fetched only now, when bh/bl are dead, so the
-    // prefetch buffer and the split fragments never live at the same time
-    __builtin_amdgcn_sched_barrier(0);
-    if (next >= 0) wload(32 * next);
-    __builtin_amdgcn_sched_barrier(0);
-    // screening top-2 over the tile's 128 points (bias is added by the exact
-    // re-evaluation in k_gmax_combine; it does not change the order)
     int k1 = KEY_NONE, k2 = KEY_NONE;
-    if (full) {
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt)
+    for (int half = 0; half < 2; ++half) {
+      const __bf16* xh = xhi + (64 * half + r) * FF_SB + 8 * h;
+      const __bf16* xl = xlo + (64 * half + r) * FF_SB + 8 * h;
+      f32x16 acc[2] = {{}, {}};
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          key_push(screen_key(acc[pt][i], 32 * pt + acc_row(i, lane)), k1, k2);
-    } else {
+      for (int kb = 0; kb < 8; ++kb) {
+        // bound the scheduler's look-ahead to one k-block: within 128 VGPRs the
+        // other three waves of the SIMD, not deep prefetch, hide LDS latency
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt)
+        for (int pt = 0; pt < 2; ++pt) {
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(xh + 32 * pt * FF_SB + 16 * kb);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(xl + 32 * pt * FF_SB + 16 * kb);
+          acc[pt] = mfma_bf16(al, bh[kb], acc[pt]);
+          acc[pt] = mfma_bf16(ah, bl[kb], acc[pt]);
+          acc[pt] = mfma_bf16(ah, bh[kb], acc[pt]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // screening top-2 over these 64 points (bias is added by the exact
+      // re-evaluation in k_gmax_combine; it does not change the order)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int idx = 32 * pt + acc_row(i, lane);
-          if (p0 + idx < N) key_push(screen_key(acc[pt][i], idx), k1, k2);
+          const int idx = 64 * half + 32 * pt + acc_row(i, lane);
+          if (full || p0 + idx < N) key_push(screen_key(acc[pt][i], idx), k1, k2);
         }
     }
     // lanes l and l+32 hold the same channel over interleaved rows
@@ -285,77 +291,41 @@ k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_
     if (lane < 32) part[((size_t)c * T + tile) * FF_O + o0 + r] = make_int2(k1, k2);
   };
 
-  // per-wave unit lists: consumer wave w owns tile-A channel tiles 8w..8w+7;
-  // tile-B channel tiles: waves 4-7 -> 5 each from 0, waves 0-3 -> 3 each from 20
-  const int nBu = hasB ? (wave < 4 ? 3 : 5) : 0;
-  const int bBase = wave < 4 ? 20 + 3 * wave : 5 * (wave - 4);
+  // unit lists: consumer wave w (0-7) owns tile-A channel tiles 4w..4w+3;
+  // tile-B channel tiles: producers (8-15) -> 3 each from 0, consumers -> 1 each from 24
+  const bool consumer = wave < FF_NCW;
+  const int nBu = hasB ? (consumer ? 1 : 3) : 0;
+  const int bBase = consumer ? 24 + wave : 3 * (wave - FF_NCW);
 
-  if (wave < 4) {
-    // ================= phase B, consumers: tile-A units 0..5 ==================
-    for (int j = 0; j < FF_NB; ++j) conv4_unit(L.x[0], L.x[1], tA, 8 * wave + j, 8 * wave + j + 1);
+  if (consumer) {
+    // ================= phase B, consumers: tile-A units 0..FF_NB-1 ===========
+    for (int j = 0; j < FF_NB; ++j) conv4_unit(L.x[0], L.x[1], tA, 4 * wave + j);
     STAMP(3);
   } else if (hasB) {
     // ================= phase B, producers: conv1..conv3 of tile B =============
-    const int pw = wave - 4, t0 = tid - 256;
-    conv1(L.pts[1], t0, 256);
-    group_sync(&L.sync[0], 4);
-    f32x4 bfa[8], bfb[8];
-    load_bfrag<64>(w2, 0, lane, bfa);
-    load_bfrag<64>(w2, 32, lane, bfb);
-    conv2(pw, 0, bfa);
-    conv2(pw, 1, bfb);
+    const int pw = wave - FF_NCW;
+    conv1(L.pts[1], tid - 64 * FF_NCW, FF_T - 64 * FF_NCW);
     group_sync(&L.sync[0], 8);
-    // conv3: producer wave pw -> channel tile pw, all 4 point tiles
-    load_bfrag<64>(w3, 32 * pw, lane, bf3);
-    f32x16 acc3[4];
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt) {
-      acc3[pt] = f32x16{};
-      acc3[pt] = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * pt * S64, S64, bf3, acc3[pt], lane);
-    }
-    const int col = 32 * pw + r;
-    const float bias = b3[col];
-    const int p0 = tB * FF_P;
-    float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 32 * pt + acc_row(i, lane);
-        float v = acc3[pt][i] + bias;
-        v = v > 0.f ? v : 0.f;
-        acc3[pt][i] = v;
-        if (p0 + row < N) xg[(size_t)row * 128] = v;
-      }
+    conv2(pw >> 1, pw & 1);
+    group_sync(&L.sync[0], 16);
+    f32x16 acc3[2];
+    conv3(tB, pw >> 2, pw & 3, acc3[0]);
+    conv3(tB, (pw >> 2) + 2, pw & 3, acc3[1]);
     STAMP(4);
     // ================= phase C, producers: split tile B's x3 into Y ===========
-    group_sync(&L.sync[1], 4);  // every producer's conv3 MFMAs have read x2
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 32 * pt + acc_row(i, lane);
-        const float v = acc3[pt][i];
-        const __bf16 hb = (__bf16)v;
-        L.y.x3[0][row * FF_SB + col] = hb;
-        L.y.x3[1][row * FF_SB + col] = (__bf16)(v - (float)hb);
-      }
-    wload(32 * bBase);
-    group_sync(&L.sync[1], 8);
+    group_sync(&L.sync[1], 8);  // every producer's conv3 MFMAs have read x2
+    x3_split(L.y.x3[0], L.y.x3[1], pw >> 2, pw & 3, acc3[0]);
+    x3_split(L.y.x3[0], L.y.x3[1], (pw >> 2) + 2, pw & 3, acc3[1]);
+    group_sync(&L.sync[1], 16);
   }
 
-  if (wave < 4) {
-    // ================= phase C, consumers: tile-A units 6, 7; tile-B units ====
-    conv4_unit(L.x[0], L.x[1], tA, 8 * wave + 6, 8 * wave + 7);
-    conv4_unit(L.x[0], L.x[1], tA, 8 * wave + 7, nBu > 0 ? bBase : -1);
-    if (nBu > 0) {
-      // tile B's split x3 is complete once all 4 producers have arrived
-      group_wait(&L.sync[1], 8);
-    }
+  if (consumer) {
+    // ================= phase C, consumers: remaining tile-A units =============
+    for (int j = FF_NB; j < 4; ++j) conv4_unit(L.x[0], L.x[1], tA, 4 * wave + j);
+    if (nBu > 0) group_wait(&L.sync[1], 16);  // tile B's split x3 is complete
   }
-  for (int j = 0; j < nBu; ++j)
-    conv4_unit(L.y.x3[0], L.y.x3[1], tB, bBase + j, j + 1 < nBu ? bBase + j + 1 : -1);
-  if (wave == 0 || wave == 4) STAMP(5 + (wave >> 2));
+  for (int j = 0; j < nBu; ++j) conv4_unit(L.y.x3[0], L.y.x3[1], tB, bBase + j);
+  if (wave == 0 || wave == 8) STAMP(5 + (wave >> 3));
 #undef STAMP
 }
 
@@ -429,9 +399,14 @@ k_gmax_combine(const int2* __restrict__ part, int T, int C, int N,
   }
 }
 
-size_t feat_fwd_workspace_bytes(int C, int N) {
+// workspace: per-tile top-2 partials, then W4 split into bf16 hi / lo
+static size_t part_bytes(int C, int N) {
   const size_t T = (N + FF_P - 1) / FF_P;
-  return (size_t)C * T * FF_O * sizeof(int2);
+  return ((size_t)C * T * FF_O * sizeof(int2) + 255) & ~(size_t)255;
+}
+
+size_t feat_fwd_workspace_bytes(int C, int N) {
+  return part_bytes(C, N) + 2 * (size_t)FF_O * 128 * sizeof(__bf16);
 }
 
 int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int C, int N,
@@ -453,9 +428,13 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
     attr_set = true;
   }
   int2* part = static_cast<int2*>(ws);
+  __bf16* w4hi = reinterpret_cast<__bf16*>(static_cast<char*>(ws) + part_bytes(C, N));
+  __bf16* w4lo = w4hi + FF_O * 128;
+  hipLaunchKernelGGL(k_w4_split, dim3(FF_O * 128 / 4 / 256), dim3(256), 0, s, w4, w4hi, w4lo);
+  PC_HIP_CHECK_LAUNCH("k_w4_split");
   hipLaunchKernelGGL(k_feat_fwd_fused, dim3((T + 1) / 2, C), dim3(FF_T), sizeof(FwdLds), s, pts_a,
-                     pts_b, split, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, part, inc_counter, stamps,
-                     T);
+                     pts_b, split, N, w1, b1, w2, b2, w3, b3, w4hi, w4lo, x3, part, inc_counter,
+                     stamps, T);
   PC_HIP_CHECK_LAUNCH("k_feat_fwd_fused");
   hipLaunchKernelGGL(k_gmax_combine, dim3(C * FF_O / 64), dim3(256), 0, s, part, T, C, N, x3, w4,
                      b4, gmax, gidx);

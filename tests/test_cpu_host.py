@@ -56,7 +56,8 @@ def test_workspace_sizes():
     lib = _lib.load()
     # x3 (C*N*128 f32) is the only per-point activation the step keeps
     assert lib.pcadv_adv_step_workspace_bytes(32, 1024) > 64 * 1024 * 128 * 4
-    assert lib.pcadv_feat_fwd_workspace_bytes(64, 1024) == 64 * 8 * 1024 * 8
+    # per-tile top-2 partials + conv4 weights split into bf16 hi / lo
+    assert lib.pcadv_feat_fwd_workspace_bytes(64, 1024) == 64 * 8 * 1024 * 8 + 2 * 1024 * 128 * 2
     assert lib.pcadv_feat_bwd_workspace_bytes(64, 1024) == 64 * 8 * 12736 * 4
 
 
