@@ -183,7 +183,7 @@ def main():
                                          "profiles", "r*_pmc_traffic.json")))
     if prof:
         kern = json.load(open(prof[-1]))["kernels"]
-        names = ("pcadv::k_feat_fwd_fused", "pcadv::k_gmax_combine")
+        names = ("pcadv::k_w4_split", "pcadv::k_feat_fwd_fused", "pcadv::k_gmax_combine")
         if all(n in kern for n in names):
             traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
             traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))
@@ -208,7 +208,7 @@ def main():
                    "global_batch": 2 * B * world, "points": N,
                    "parallelism": f"dp{world}", "hip_graph": use_graph},
         "roofline": {"bound": "mfma",
-                     "kernel": "k_feat_fwd_fused + k_gmax_combine (PointNetfeat conv1..4 + max)",
+                     "kernel": "k_w4_split + k_feat_fwd_fused + k_gmax_combine (PointNetfeat conv1..4 + max)",
                      "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",

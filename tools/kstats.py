@@ -2,13 +2,17 @@
 plus per-step accounting over the timed graph replays."""
 import collections
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_traffic import kname  # noqa: E402
 
 path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
 d = collections.defaultdict(list)
 for x in rows:
-    name = x["Kernel_Name"].split("(")[0].replace("void ", "")[:40]
+    name = kname(x["Kernel_Name"])[:40]
     key = (name, x["Grid_Size_X"], x["Grid_Size_Y"], x["Workgroup_Size_X"])
     d[key].append((int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3)
 tot = 0

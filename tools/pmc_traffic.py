@@ -15,7 +15,21 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
+
+
+def kname(raw):
+    """Kernel name without arguments; mangled names rocprofv3 could not demangle
+    (e.g. __bf16 parameters) are reduced to ns::name."""
+    m = re.match(r"_ZN(\d+)(\w+)", raw)
+    if m:
+        n = int(m.group(1))
+        ns, rest = m.group(2)[:n], m.group(2)[n:]
+        m2 = re.match(r"(\d+)(\w+)", rest)
+        if m2:
+            return ns + "::" + m2.group(2)[:int(m2.group(1))]
+    return raw.split("(")[0].replace("void ", "")
 
 
 def load(d, counter):
@@ -24,7 +38,7 @@ def load(d, counter):
     for row in csv.DictReader(open(f)):
         if row["Counter_Name"] != counter:
             continue
-        name = row["Kernel_Name"].split("(")[0].replace("void ", "")
+        name = kname(row["Kernel_Name"])
         per[name].append(float(row["Counter_Value"]) * 1024.0)
     return per
 
