@@ -1,77 +1,212 @@
-// Fused PointNetfeat forward (models/pointnet.py:109-132, feature_transform=False)
-// on gfx950: conv1 -> conv2 -> conv3 -> conv4 -> max over points, one
-// workgroup per (cloud, 128-point tile), nothing but conv3's output leaves the
-// chip.
+// PointNetfeat forward (models/pointnet.py:109-132, feature_transform=False) on
+// gfx950 in two launches:
 //
-//   conv1 (3 -> 64)    VALU, exact f32
-//   conv2 (64 -> 64)   v_mfma_f32_32x32x2_f32 (exact f32)
-//   conv3 (64 -> 128)  v_mfma_f32_32x32x2_f32; x3 is written to HBM in f32 (the
-//                      backward and the exact re-evaluation below read it) and
-//                      kept in LDS split as bf16 hi + lo
-//   conv4 (128 -> 1024) + max: three bf16 MFMAs per product
-//                      (x_hi w_hi + x_hi w_lo + x_lo w_hi, f32 accumulate,
-//                      v_mfma_f32_32x32x16_bf16): relative error <= ~1.2e-5 of
-//                      sum|x w|, at 16x the per-cycle rate of the f32 MFMA.  The
-//                      epilogue keeps the top-2 (value, point) per channel.
+//   k_point_mlp   one workgroup per (cloud, 128-point tile): conv1 -> conv2 ->
+//                 conv3 (+ ReLU), exact f32.  Only x3 (post-ReLU conv3, the
+//                 operand of conv4, the exact re-evaluation and the backward)
+//                 leaves the chip.
+//     conv1 (3 -> 64)    VALU, in the fma order the backward's recompute uses
+//     conv2 (64 -> 64)   v_mfma_f32_32x32x2_f32 (exact f32, k-ordered)
+//     conv3 (64 -> 128)  v_mfma_f32_32x32x2_f32
 //
-// k_gmax_combine then merges the per-tile top-2 keys of each channel and
-// re-evaluates the winner in exact f32 (and the runner-up whenever the two are
-// within the split-product error bound), so gmax is an f32 dot product and the
-// argmax follows the f32 values, first index on ties (torch.max on CPU).
+//   k_conv4_max   one workgroup per (cloud, 256-channel block), weight-
+//                 stationary: each of the 8 waves holds its 32 channels of W4 as
+//                 bf16 hi + lo in registers and the cloud's points stream
+//                 through LDS in 64-point steps (x3 f32 from L2/MALL, split to
+//                 bf16 hi + lo once per workgroup).  conv4 runs as three
+//                 v_mfma_f32_32x32x16_bf16 per product (x_hi w_hi + x_hi w_lo +
+//                 x_lo w_hi, f32 accumulate; relative error <= ~1.2e-5 of
+//                 sum|x w|) and the screening epilogue keeps each lane's top-2
+//                 (value, point) over the whole cloud in registers.  The tail
+//                 re-evaluates the winner (and the runner-up on near-ties) as an
+//                 exact f32 dot product, so gmax is f32 and the argmax follows
+//                 the f32 values with the first index on ties (torch.max on
+//                 CPU).  The 128 MB conv4 output never exists.
 #include "common.h"
+
+#include <type_traits>
+#include <utility>
 
 namespace pcadv {
 
-constexpr int FF_P = 128;   // points per workgroup
-constexpr int FF_T = 1024;  // threads (16 waves = 4 per SIMD, 1 workgroup per CU)
-constexpr int FF_SB = 136;  // bf16 row stride of the x3 hi/lo tiles (272 B)
-constexpr int FF_O = 1024;
+// ============================================================================
+// k_point_mlp: conv1..conv3
+// ============================================================================
+constexpr int PM_P = 128;  // points per workgroup
+
+// NT 32x32 f32 MFMA tiles (point tiles 0..NT-1 of a_lds) against one 32-column
+// block of W: the NT accumulation chains are interleaved so the matrix pipe
+// always has an independent MFMA to issue.  Each chain runs in the k order of
+// mfma_rows_x_wt (common.h), so results are bitwise those of the single-tile
+// form the backward's recompute uses.
+template <int K, int NT>
+__device__ __forceinline__ void mfma_tiles(const float* __restrict__ a_lds, int a_stride,
+                                           const f32x4* bfrag, f32x16 (&acc)[NT], int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < K / 8; ++g) {
+    f32x4 a[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      a[t] = *reinterpret_cast<const f32x4*>(a_lds + (32 * t + r) * a_stride + 8 * g + 4 * h);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma32(a[t][j], bfrag[g][j], acc[t]);
+  }
+}
+constexpr int PM_T = 256;  // 4 waves; 2 workgroups per CU (72 KB of LDS each)
+
+struct MlpLds {
+  alignas(16) float pts[PM_P * 4];
+  alignas(16) float x1[PM_P * S64];
+  alignas(16) float x2[PM_P * S64];
+};
+
+__global__ void __launch_bounds__(PM_T)
+k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split, int N,
+            const float* __restrict__ w1, const float* __restrict__ b1,
+            const float* __restrict__ w2, const float* __restrict__ b2,
+            const float* __restrict__ w3, const float* __restrict__ b3,
+            float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  MlpLds& L = *reinterpret_cast<MlpLds*>(smem);
+#ifdef PCADV_STAMPS
+  uint64_t* st = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+#define STAMP(k) do { if (stamps && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+  STAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31;
+  const int c = blockIdx.y, p0 = blockIdx.x * PM_P;
+  if (inc_counter && tid == 0 && c == 0 && blockIdx.x == 0) *inc_counter += 1;
+  const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
+
+  // B fragments of this wave's conv2 / conv3 channel tiles, issued before the
+  // point loads so both latencies overlap
+  f32x4 bf2[8], bf3[8];
+  load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
+  load_bfrag<64>(w3, 32 * wave, lane, bf3);
+  for (int e = tid; e < PM_P * 3; e += PM_T) {
+    const int p = e / 3, k = e % 3;
+    L.pts[p * 4 + k] = p0 + p < N ? pts[(size_t)(p0 + p) * 3 + k] : 0.f;
+  }
+  __syncthreads();
+  STAMP(1);
+  {  // conv1 (3 -> 64) + ReLU: thread = (channel, 32-point group)
+    const int ch = tid & 63, pg = tid >> 6;
+    const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
+#pragma unroll 4
+    for (int i = 0; i < 32; ++i) {
+      const int p = pg * 32 + i;
+      L.x1[p * S64 + ch] =
+          conv1_point(wa, wb, wc, bb, L.pts[p * 4 + 0], L.pts[p * 4 + 1], L.pts[p * 4 + 2]);
+    }
+  }
+  __syncthreads();
+  STAMP(2);
+  {  // conv2 (64 -> 64) + ReLU: wave = (channel tile wave & 1, point tiles 2 (wave >> 1) + j)
+    const int col = 32 * (wave & 1) + r;
+    const float bias = b2[col];
+    const int pt0 = 2 * (wave >> 1);
+    f32x16 acc[2] = {{}, {}};
+    mfma_tiles<64, 2>(L.x1 + 32 * pt0 * S64, S64, bf2, acc, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float v = acc[j][i] + bias;
+        L.x2[(32 * (pt0 + j) + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
+      }
+  }
+  __syncthreads();
+  STAMP(3);
+  {  // conv3 (64 -> 128) + ReLU -> x3 (HBM): wave = channel tile, all 4 point tiles
+    const int col = 32 * wave + r;
+    const float bias = b3[col];
+    float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
+    f32x16 acc[4] = {{}, {}, {}, {}};
+    mfma_tiles<64, 4>(L.x2, S64, bf3, acc, lane);
+    STAMP(4);
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 32 * pt + acc_row(i, lane);
+        const float v = acc[pt][i] + bias;
+        if (p0 + row < N) xg[(size_t)row * 128] = v > 0.f ? v : 0.f;
+      }
+  }
+  STAMP(5);
+#undef STAMP
+}
+
+// ============================================================================
+// k_conv4_max: conv4 (128 -> 1024) + max over points
+// ============================================================================
+constexpr int C4_O = 1024;  // conv4 output channels
+constexpr int C4_CB = 256;  // channels per workgroup (8 waves x 32)
+constexpr int C4_T = 512;
+constexpr int C4_P = 64;    // points per step
+constexpr int C4_SB = 136;  // bf16 row stride of the x3 hi / lo tiles (272 B: conflict-free b128 reads)
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// Two 128-point tiles per workgroup.  X holds tile A's conv3 output split to
-// bf16 hi/lo; Y holds tile A's, then tile B's conv1/conv2 outputs (f32), and
-// finally tile B's split conv3 output.
-struct FwdLds {
-  alignas(16) float pts[2][FF_P * 4];
-  alignas(16) __bf16 x[2][FF_P * FF_SB];  // tile A x3: hi, lo
-  union U {
-    struct {
-      float x1[FF_P * S64];
-      float x2[FF_P * S64];
-    } f;
-    __bf16 x3[2][FF_P * FF_SB];            // tile B x3: hi, lo
-  };
-  alignas(16) U y;
-  int sync[2];                             // producer-wave arrival counters
+struct C4Lds {
+  alignas(16) __bf16 x[2][2][C4_P * C4_SB];  // [buffer][hi, lo]
 };
 
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// Screening keys: the f32 value mapped to an order-preserving int32 with the
-// point's index inside the 128-point tile packed into the low 7 bits (stored
-// as 127 - idx, so equal screening values rank the lower index first).  One
-// v_max_i32 + one v_med3_i32 then keep the top-2 (value, point) pairs; the 7
-// dropped mantissa bits (2^-16 relative) sit far inside the near-tie window
-// that k_gmax_combine re-checks in exact f32.
-__device__ __forceinline__ int screen_key(float v, int idx) {
+// Screening keys: the f32 value mapped to an order-preserving int32 whose low
+// 6 bits are replaced by 63 - (the point's row inside its 64-point step, less
+// the lane-half offset 4 h), so v_max_i32 / v_med3_i32 keep the top-2 (value,
+// row) of a lane with the lower row first on equal truncated values.  The 6 dropped bits (2^-17 relative) sit far
+// inside the near-tie window the exact re-evaluation re-checks; NaN maps above
+// +inf as torch.max ranks it.
+__device__ __forceinline__ int screen_key(float v, int lowc) {
   const int b = __float_as_int(v);
-  const int ord = b ^ ((b >> 31) & 0x7fffffff);   // int order == float order
-  return (ord & ~0x7f) | (127 - idx);
+  const int ord = b ^ ((b >> 31) & 0x7fffffff);  // int order == float order
+  return (ord & ~63) | lowc;
 }
+// The same key in three instructions (hipcc spends four): t = sign smear;
+// x = b ^ (t & 0x7fffffc0) (order-preserving except in the low bits, which
+// are replaced); key = (x & ~63) | LOWC.  v_bitop3 table index = 4 S0 + 2 S1 + S2.
+// Only for accumulators whose MFMAs retired several instructions earlier
+// (inline asm is outside the compiler's MFMA hazard tracking).
+template <int LOWC>
+__device__ __forceinline__ int screen_key_asm(float v, int m_ord, int m_hi) {
+  int t;
+  asm("v_ashrrev_i32 %0, 31, %1\n\t"
+      "v_bitop3_b32 %0, %1, %0, %2 bitop3:0x78\n\t"
+      "v_bitop3_b32 %0, %0, %3, %4 bitop3:0xea"
+      : "=&v"(t)
+      : "v"(v), "s"(m_ord), "s"(m_hi), "n"(LOWC));
+  return t;
+}
+// push acc element I (row acc_row(I, 0) of the unit, plus 4 h) into a lane's top-2
+template <int I>
+__device__ __forceinline__ void screen_one(const f32x16& acc, int m_ord, int m_hi, int& k1,
+                                           int& k2) {
+  const int key = screen_key_asm<31 - ((I & 3) + 8 * (I >> 2))>(acc[I], m_ord, m_hi);
+  k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1: v_med3_i32
+  k1 = max(k1, key);
+}
+template <int I0, int... J>
+__device__ __forceinline__ void screen_seq(const f32x16& acc, int m_ord, int m_hi, int& k1,
+                                           int& k2, std::integer_sequence<int, J...>) {
+  (screen_one<I0 + J>(acc, m_ord, m_hi, k1, k2), ...);
+}
+__device__ __forceinline__ int key_row(int k) { return 31 - (k & 63); }
 __device__ __forceinline__ float key_value(int k) {
-  const int ord = k & ~0x7f;
+  const int ord = k & ~63;
   return __int_as_float(ord ^ ((ord >> 31) & 0x7fffffff));
 }
-__device__ __forceinline__ int key_index(int k) { return 127 - (k & 0x7f); }
 constexpr int KEY_NONE = (int)0x80000000;  // below every real key
-
-__device__ __forceinline__ void key_push(int k, int& k1, int& k2) {
-  k2 = max(min(k, k1), k2);  // median(k, k1, k2) for k2 <= k1: v_med3_i32
-  k1 = max(k1, k);
-}
 
 // (va, ia) ranks before (vb, ib): larger value, NaN above all, lower index on ties
 __device__ __forceinline__ bool ranks_before(float va, int ia, float vb, int ib) {
@@ -80,333 +215,298 @@ __device__ __forceinline__ bool ranks_before(float va, int ia, float vb, int ib)
   return va > vb || (va == vb && ia < ib);
 }
 
-__device__ __forceinline__ void top2_merge(float v, int p, float& v1, int& i1, float& v2, int& i2) {
-  const bool a = ranks_before(v, p, v1, i1);
-  const bool b = !a && ranks_before(v, p, v2, i2);
-  const float nv2 = a ? v1 : (b ? v : v2);
-  const int ni2 = a ? i1 : (b ? p : i2);
-  v1 = a ? v : v1;
-  i1 = a ? p : i1;
-  v2 = nv2;
-  i2 = ni2;
+// Merge one step's top-2 keys (n1 >= n2, both tagged with step u) into the
+// running top-2 (r1 >= r2, tags t1, t2) of earlier steps.  Keys of different
+// steps compare by their truncated value only (the low bits are rows within a
+// step): on equal values the earlier step, i.e. the lower point index, stays.
+__device__ __forceinline__ void pair_merge(int n1, int u1, int n2, int u2, int& r1, int& t1,
+                                           int& r2, int& t2) {
+  const int m1 = n1 & ~63, m2 = n2 & ~63, q1 = r1 & ~63, q2 = r2 & ~63;
+  const bool a = m1 > q1;
+  const int sa = q1 >= m2 ? r1 : n2;
+  const int ta = q1 >= m2 ? t1 : u2;
+  const int sb = q2 >= m1 ? r2 : n1;
+  const int tb = q2 >= m1 ? t2 : u1;
+  r2 = a ? sa : sb;
+  t2 = a ? ta : tb;
+  r1 = a ? n1 : r1;
+  t1 = a ? u1 : t1;
 }
 
-// wave-group barrier among the 4 producer waves (4..7) through an LDS counter:
-// every wave publishes its LDS writes, then waits for the others
-// (every spin is bounded: a lost arrival cannot hang the device)
-__device__ __forceinline__ void group_wait(int* cnt, int target) {
-  for (int spin = 0; spin < (1 << 22); ++spin) {
-    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__device__ __forceinline__ void group_sync(int* cnt, int target) {
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS (and memory) writes are done
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  group_wait(cnt, target);
-}
-
-// conv4 weights split once per launch into bf16 hi / lo ([1024][128] each), so
-// the screening loop loads its B operands directly
-__global__ void __launch_bounds__(256)
-k_w4_split(const float* __restrict__ w4, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
-  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= FF_O * 128) return;
-  const f32x4 v = *reinterpret_cast<const f32x4*>(w4 + i);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const __bf16 hb = (__bf16)v[j];
-    hi[i + j] = hb;
-    lo[i + j] = (__bf16)(v[j] - (float)hb);
-  }
-}
-
-constexpr int FF_NB = 2;   // tile-A units a consumer wave runs while tile B's conv1-3 run
-constexpr int FF_NCW = 8;  // consumer waves (0-7); producer waves 8-15
-
-// Pipelined over two point tiles A, B of one cloud (16 waves, 4 per SIMD):
-//   phase A  all waves: conv1..conv3 of tile A (x1, x2 in Y; x3 -> HBM + X)
-//   phase B  waves 0-7: conv4 + screening of tile A, 2 of their 4 channel
-//            units; waves 8-15: conv1..conv3 of tile B (x3 kept in registers)
-//   phase C  waves 8-15 split tile B's x3 into Y; waves 0-7 finish their 2
-//            tile-A units and take 1 tile-B unit each, waves 8-15 take 3
-//            tile-B units each (32 tile-B units in all)
-// A unit is 32 channels x 128 points, run in two 64-point halves so that a
-// wave stays within 128 VGPRs: four waves per SIMD keep the matrix pipe fed
-// while any one of them waits on LDS or runs its screening epilogue.
-__global__ void __launch_bounds__(FF_T)
-k_feat_fwd_fused(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
-                 int N, const float* __restrict__ w1, const float* __restrict__ b1,
-                 const float* __restrict__ w2, const float* __restrict__ b2,
-                 const float* __restrict__ w3, const float* __restrict__ b3,
-                 const __bf16* __restrict__ w4hi, const __bf16* __restrict__ w4lo,
-                 float* __restrict__ x3g, int2* __restrict__ part, int32_t* inc_counter,
-                 uint64_t* __restrict__ stamps, int T) {
+__global__ void __launch_bounds__(C4_T)
+k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
+            const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
+            uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  FwdLds& L = *reinterpret_cast<FwdLds*>(smem);
+  C4Lds& L = *reinterpret_cast<C4Lds*>(smem);
+  // XCD-aware order: consecutive workgroup ids run on different XCDs, so the
+  // ids are remapped to keep the 4 channel blocks of a cloud on one XCD (they
+  // stream the same x3 through that XCD's L2)
+  int bid = blockIdx.x;
+  const int nwg = gridDim.x;
+  if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);
+  const int c = bid >> 2, cb = bid & 3;
 #ifdef PCADV_STAMPS
-  // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
-  uint64_t* st = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
-#define STAMP(k) do { if (stamps && (threadIdx.x & 63) == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  uint64_t* st = stamps + (size_t)blockIdx.x * 16;
+#define STAMP(k) do { if (stamps && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
 #endif
+  STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int c = blockIdx.y, tA = 2 * blockIdx.x, tB = tA + 1;
-  const bool hasB = tB < T;
-  if (wave == 0) STAMP(0);
-  if (inc_counter && tid == 0 && c == 0 && blockIdx.x == 0) *inc_counter += 1;
-  const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
+  const int o = cb * C4_CB + 32 * wave + r;  // this lane's output channel
+  const float* xc = x3g + (size_t)c * N * 128;
+  const int S = (N + C4_P - 1) / C4_P;
 
-  for (int e = tid; e < 2 * FF_P * 3; e += FF_T) {
-    const int t = e / (FF_P * 3), p = (e % (FF_P * 3)) / 3, k = e % 3;
-    const int gp = (tA + t) * FF_P + p;
-    L.pts[t][p * 4 + k] = gp < N ? pts[(size_t)gp * 3 + k] : 0.f;
-  }
-  if (tid < 2) L.sync[tid] = 0;
-  __syncthreads();
-
-  // ---- conv1 (3 -> 64) + ReLU of one tile: NT threads = (channel, point group)
-  auto conv1 = [&](const float* ps, int t0, int NT) {
-    const int ch = t0 & 63, pg = t0 >> 6, per = FF_P / (NT / 64);
-    const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
-    for (int i = 0; i < per; ++i) {
-      const int p = pg * per + i;
-      L.y.f.x1[p * S64 + ch] = conv1_point(wa, wb, wc, bb, ps[p * 4 + 0], ps[p * 4 + 1], ps[p * 4 + 2]);
-    }
-  };
-  // ---- conv2 (64 -> 64) + ReLU, one 32x32 tile (point tile pt, channel tile ct)
-  auto conv2 = [&](int pt, int ct) {
-    f32x4 bf[8];
-    load_bfrag<64>(w2, 32 * ct, lane, bf);
-    f32x16 acc = {};
-    acc = mfma_rows_x_wt<64>(L.y.f.x1 + 32 * pt * S64, S64, bf, acc, lane);
-    const int col = 32 * ct + r;
-    const float bias = b2[col];
+  // staging map: thread = (row tid >> 3, 16 consecutive k at 16 (tid & 7));
+  // rows past the cloud re-read its last row (screening masks them)
+  const int srow = tid >> 3, sk = 16 * (tid & 7);
+  f32x4 stg[4];
+  auto stage_load = [&](int s) {
+    const int p = min(s * C4_P + srow, N - 1);
+    const f32x4* src = reinterpret_cast<const f32x4*>(xc + (size_t)p * 128 + sk);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float v = acc[i] + bias;
-      L.y.f.x2[(32 * pt + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
-    }
+    for (int j = 0; j < 4; ++j) stg[j] = src[j];
   };
-  // ---- conv3 (64 -> 128) + ReLU, one 32x32 tile; the value also goes to HBM
-  auto conv3 = [&](int tile, int pt, int ct, f32x16& acc) {
-    f32x4 bf[8];
-    load_bfrag<64>(w3, 32 * ct, lane, bf);
-    acc = f32x16{};
-    acc = mfma_rows_x_wt<64>(L.y.f.x2 + 32 * pt * S64, S64, bf, acc, lane);
-    const int col = 32 * ct + r;
-    const float bias = b3[col];
-    const int p0 = tile * FF_P;
-    float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
+  auto stage_write = [&](int buf) {  // split the staged f32 rows into bf16 hi / lo
+    bf16x8 hi[2], lo[2];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = 32 * pt + acc_row(i, lane);
-      float v = acc[i] + bias;
-      v = v > 0.f ? v : 0.f;
-      acc[i] = v;
-      if (p0 + row < N) xg[(size_t)row * 128] = v;
+    for (int j = 0; j < 16; ++j) {
+      const float v = stg[j >> 2][j & 3];
+      const __bf16 hb = (__bf16)v;
+      hi[j >> 3][j & 7] = hb;
+      lo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
     }
+    bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf][0][srow * C4_SB + sk]);
+    bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf][1][srow * C4_SB + sk]);
+    dh[0] = hi[0];
+    dh[1] = hi[1];
+    dl[0] = lo[0];
+    dl[1] = lo[1];
   };
-  auto x3_split = [&](__bf16* hi, __bf16* lo, int pt, int ct, const f32x16& acc) {
-    const int col = 32 * ct + r;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = 32 * pt + acc_row(i, lane);
-      const __bf16 hb = (__bf16)acc[i];
-      hi[row * FF_SB + col] = hb;
-      lo[row * FF_SB + col] = (__bf16)(acc[i] - (float)hb);
-    }
-  };
-
-  // ================= phase A: conv1..conv3 of tile A, all waves ===============
-  conv1(L.pts[0], tid, FF_T);
-  __syncthreads();
-  if (wave < 8) conv2(wave >> 1, wave & 1);
-  __syncthreads();
+  stage_load(0);
+  // W4 rows of this lane's channel, k = 16 kb + 8 h .. + 8, split to bf16 hi / lo
+  bf16x8 bh[8], bl[8];
   {
-    f32x16 acc;
-    conv3(tA, wave >> 2, wave & 3, acc);
-    x3_split(L.x[0], L.x[1], wave >> 2, wave & 3, acc);
+    const float* wrow = w4 + (size_t)o * 128 + 8 * h;
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = j < 4 ? u0[j] : u1[j - 4];
+        const __bf16 hb = (__bf16)v;
+        bh[kb][j] = hb;
+        bl[kb][j] = (__bf16)(v - (float)hb);
+      }
+    }
   }
+  stage_write(0);
+  stage_load(1);
   __syncthreads();
-  if (wave == 0 || wave == 8) STAMP(1 + (wave >> 3));
+  STAMP(1);
 
-  // ---- conv4 (128 -> 1024) split-bf16 MFMA + top-2 screening of one channel
-  //      unit (32 channels x the tile's 128 points) --------------------------
-  auto conv4_unit = [&](const __bf16* xhi, const __bf16* xlo, int tile, int ct) {
-    const int p0 = tile * FF_P;
-    const bool full = p0 + FF_P <= N;
-    const int o0 = 32 * ct;
-    // B operands: lane (r, h) holds W4[o0 + r][16 kb + 8 h .. + 8) hi and lo
-    bf16x8 bh[8], bl[8];
-    {
-      const __bf16* ph = w4hi + (size_t)(o0 + r) * 128 + 8 * h;
-      const __bf16* pl = w4lo + (size_t)(o0 + r) * 128 + 8 * h;
+  // Running top-2 keys of this lane (r1 >= r2) and the 32-point units they came
+  // from.  Low key bits of acc element i: 31 - acc_row(i, 0), a compile-time
+  // constant; the lane's rows are acc_row(i, 0) + 4 h and are decoded with the
+  // lane's own h (keys are only compared within a lane).
+  int r1 = KEY_NONE, r2 = KEY_NONE;
+  int t1 = -1, t2 = -1;
+  auto screen_unit = [&](const f32x16& acc, int u, auto MASKED, int kb_lo, int kb_hi, int& k1,
+                         int& k2) {
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
-        bh[kb] = *reinterpret_cast<const bf16x8*>(ph + 16 * kb);
-        bl[kb] = *reinterpret_cast<const bf16x8*>(pl + 16 * kb);
-      }
+    for (int i = 2 * kb_lo; i < 2 * kb_hi; ++i) {
+      if constexpr (decltype(MASKED)::value)
+        if (u * 32 + acc_row(i, lane) >= N) continue;
+      const int key = screen_key(acc[i], 31 - acc_row(i, 0));
+      k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1: v_med3_i32
+      k1 = max(k1, key);
     }
-    int k1 = KEY_NONE, k2 = KEY_NONE;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const __bf16* xh = xhi + (64 * half + r) * FF_SB + 8 * h;
-      const __bf16* xl = xlo + (64 * half + r) * FF_SB + 8 * h;
-      f32x16 acc[2] = {{}, {}};
-#pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
-        // bound the scheduler's look-ahead to one k-block: within 128 VGPRs the
-        // other three waves of the SIMD, not deep prefetch, hide LDS latency
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(xh + 32 * pt * FF_SB + 16 * kb);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(xl + 32 * pt * FF_SB + 16 * kb);
-          acc[pt] = mfma_bf16(al, bh[kb], acc[pt]);
-          acc[pt] = mfma_bf16(ah, bl[kb], acc[pt]);
-          acc[pt] = mfma_bf16(ah, bh[kb], acc[pt]);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // screening top-2 over these 64 points (bias is added by the exact
-      // re-evaluation in k_gmax_combine; it does not change the order)
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int idx = 64 * half + 32 * pt + acc_row(i, lane);
-          if (full || p0 + idx < N) key_push(screen_key(acc[pt][i], idx), k1, k2);
-        }
-    }
-    // lanes l and l+32 hold the same channel over interleaved rows
-    const int o1 = __shfl_xor(k1, 32), o2 = __shfl_xor(k2, 32);
-    k2 = max(min(k1, o1), max(k2, o2));
-    k1 = max(k1, o1);
-    if (lane < 32) part[((size_t)c * T + tile) * FF_O + o0 + r] = make_int2(k1, k2);
+  };
+  // unmasked screening of acc elements [I, I + CNT) with the asm keys
+  const int m_ord = 0x7fffffc0, m_hi = ~63;
+  auto screen_fast = [&](const f32x16& acc, auto I, auto CNT, int& k1, int& k2) {
+    screen_seq<decltype(I)::value>(acc, m_ord, m_hi, k1, k2,
+                                   std::make_integer_sequence<int, decltype(CNT)::value>{});
   };
 
-  // unit lists: consumer wave w (0-7) owns tile-A channel tiles 4w..4w+3;
-  // tile-B channel tiles: producers (8-15) -> 3 each from 0, consumers -> 1 each from 24
-  const bool consumer = wave < FF_NCW;
-  const int nBu = hasB ? (consumer ? 1 : 3) : 0;
-  const int bBase = consumer ? 24 + wave : 3 * (wave - FF_NCW);
-
-  if (consumer) {
-    // ================= phase B, consumers: tile-A units 0..FF_NB-1 ===========
-    for (int j = 0; j < FF_NB; ++j) conv4_unit(L.x[0], L.x[1], tA, 4 * wave + j);
-    STAMP(3);
-  } else if (hasB) {
-    // ================= phase B, producers: conv1..conv3 of tile B =============
-    const int pw = wave - FF_NCW;
-    conv1(L.pts[1], tid - 64 * FF_NCW, FF_T - 64 * FF_NCW);
-    group_sync(&L.sync[0], 8);
-    conv2(pw >> 1, pw & 1);
-    group_sync(&L.sync[0], 16);
-    f32x16 acc3[2];
-    conv3(tB, pw >> 2, pw & 3, acc3[0]);
-    conv3(tB, (pw >> 2) + 2, pw & 3, acc3[1]);
-    STAMP(4);
-    // ================= phase C, producers: split tile B's x3 into Y ===========
-    group_sync(&L.sync[1], 8);  // every producer's conv3 MFMAs have read x2
-    x3_split(L.y.x3[0], L.y.x3[1], pw >> 2, pw & 3, acc3[0]);
-    x3_split(L.y.x3[0], L.y.x3[1], (pw >> 2) + 2, pw & 3, acc3[1]);
-    group_sync(&L.sync[1], 16);
+  // Software pipeline over 32-point units (step s, half pt): the 24 MFMAs of a
+  // unit are issued in the same scheduling regions as the screening of the
+  // previous unit (the other accumulator) and a share of the staging work, so
+  // one wave's matrix and vector work overlap.
+  f32x16 accA, accB;  // units of half 0 / half 1 of a step
+  auto unit = [&](int s, int pt, f32x16& cur, const f32x16& prev, auto SCREEN, auto MASKED) {
+    const int buf = s & 1;
+    const __bf16* xh = &L.x[buf][0][(32 * pt + r) * C4_SB + 8 * h];
+    const __bf16* xl = &L.x[buf][1][(32 * pt + r) * C4_SB + 8 * h];
+    const int uprev = 2 * s + pt - 1;
+    int k1 = KEY_NONE, k2 = KEY_NONE;
+    bf16x8 fa[3][2];  // A fragments, a 3-deep register ring: [k-block % 3][hi, lo]
+    auto frag = [&](int kb) {
+      fa[kb % 3][0] = *reinterpret_cast<const bf16x8*>(xh + 16 * kb);
+      fa[kb % 3][1] = *reinterpret_cast<const bf16x8*>(xl + 16 * kb);
+    };
+    frag(0);
+    frag(1);
+    cur = f32x16{};
+    bf16x8 shi[2], slo[2];
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (kb + 2 < 8) frag(kb + 2);  // two k-blocks (six MFMAs) ahead of its use
+      const bf16x8 ah = fa[kb % 3][0], al = fa[kb % 3][1];
+      cur = mfma_bf16(al, bh[kb], cur);
+      cur = mfma_bf16(ah, bl[kb], cur);
+      cur = mfma_bf16(ah, bh[kb], cur);
+      if constexpr (decltype(SCREEN)::value && decltype(MASKED)::value) {
+        screen_unit(prev, uprev, MASKED, kb, kb + 1, k1, k2);
+        asm volatile("" ::"v"(k1), "v"(k2));
+      } else if constexpr (decltype(SCREEN)::value) {
+        // 16 values over k-blocks 1..7 (2,2,2,2,2,3,3); none in k-block 0, so the
+        // previous unit's MFMAs have retired before the asm reads them
+        using IC = std::integral_constant<int, 0>;
+        if (kb == 1) screen_fast(prev, IC{}, std::integral_constant<int, 2>{}, k1, k2);
+        if (kb == 2) screen_fast(prev, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, k1, k2);
+        if (kb == 3) screen_fast(prev, std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{}, k1, k2);
+        if (kb == 4) screen_fast(prev, std::integral_constant<int, 6>{}, std::integral_constant<int, 2>{}, k1, k2);
+        if (kb == 5) screen_fast(prev, std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{}, k1, k2);
+        if (kb == 6) screen_fast(prev, std::integral_constant<int, 10>{}, std::integral_constant<int, 3>{}, k1, k2);
+        if (kb == 7) screen_fast(prev, std::integral_constant<int, 13>{}, std::integral_constant<int, 3>{}, k1, k2);
+        // pin the keys to this region (otherwise the IR passes sink the whole
+        // screening below the MFMAs, next to its only use)
+        asm volatile("" ::"v"(k1), "v"(k2));
+      }
+      if (pt == 0 && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
+#pragma unroll
+        for (int j = 4 * kb; j < 4 * kb + 4; ++j) {
+          const float v = stg[j >> 2][j & 3];
+          const __bf16 hb = (__bf16)v;
+          shi[j >> 3][j & 7] = hb;
+          slo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
+        }
+        asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
+      }
+      if (pt == 0 && kb == 4) {  // the next step's tile (buffer free since the barrier)
+        bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][srow * C4_SB + sk]);
+        bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][srow * C4_SB + sk]);
+        dh[0] = shi[0];
+        dh[1] = shi[1];
+        dl[0] = slo[0];
+        dl[1] = slo[1];
+      }
+      if (pt == 1 && kb == 1) stage_load(s + 2);  // (clamped: past the end it re-reads)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (decltype(SCREEN)::value) pair_merge(k1, uprev, k2, uprev, r1, t1, r2, t2);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  unit(0, 0, accA, accB, F_{}, F_{});
+  if (S > 1) unit(0, 1, accB, accA, T_{}, F_{});
+  else unit(0, 1, accB, accA, T_{}, T_{});
+  __syncthreads();
+  for (int s = 1; s < S; ++s) {
+    unit(s, 0, accA, accB, T_{}, F_{});
+    if (s + 1 < S) unit(s, 1, accB, accA, T_{}, F_{});
+    else unit(s, 1, accB, accA, T_{}, T_{});
+    __syncthreads();
   }
-
-  if (consumer) {
-    // ================= phase C, consumers: remaining tile-A units =============
-    for (int j = FF_NB; j < 4; ++j) conv4_unit(L.x[0], L.x[1], tA, 4 * wave + j);
-    if (nBu > 0) group_wait(&L.sync[1], 16);  // tile B's split x3 is complete
+  {  // the last unit
+    int k1 = KEY_NONE, k2 = KEY_NONE;
+    screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2);
+    pair_merge(k1, 2 * S - 1, k2, 2 * S - 1, r1, t1, r2, t2);
   }
-  for (int j = 0; j < nBu; ++j) conv4_unit(L.y.x3[0], L.y.x3[1], tB, bBase + j);
-  if (wave == 0 || wave == 8) STAMP(5 + (wave >> 3));
+  STAMP(2);
+
+  // lanes l and l + 32 hold the same channel over interleaved rows
+  {
+    const int o1 = __shfl_xor(r1, 32), o2 = __shfl_xor(r2, 32);
+    const int u1 = __shfl_xor(t1, 32), u2 = __shfl_xor(t2, 32);
+    // order by (value, global index): decode both pairs first
+    const int hm = 4 * h, ho = 4 - hm;  // row offsets of this lane half and the other
+    const int i1 = t1 < 0 ? 0x7fffffff : t1 * 32 + key_row(r1) + hm;
+    const int i2 = t2 < 0 ? 0x7fffffff : t2 * 32 + key_row(r2) + hm;
+    const int j1 = u1 < 0 ? 0x7fffffff : u1 * 32 + key_row(o1) + ho;
+    const int j2 = u2 < 0 ? 0x7fffffff : u2 * 32 + key_row(o2) + ho;
+    float v1 = t1 < 0 ? -INFINITY : key_value(r1), v2 = t2 < 0 ? -INFINITY : key_value(r2);
+    int a1 = i1, a2 = i2;
+    if (ranks_before(v2, a2, v1, a1)) {  // equal truncated values: order by index
+      const float tv = v1;
+      v1 = v2;
+      v2 = tv;
+      a1 = i2;
+      a2 = i1;
+    }
+    const float w1v = u1 < 0 ? -INFINITY : key_value(o1), w2v = u2 < 0 ? -INFINITY : key_value(o2);
+    // insert (w1v, j1) and (w2v, j2)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float v = q == 0 ? w1v : w2v;
+      const int p = q == 0 ? j1 : j2;
+      const bool a = ranks_before(v, p, v1, a1);
+      const bool b = !a && ranks_before(v, p, v2, a2);
+      const float nv2 = a ? v1 : (b ? v : v2);
+      const int na2 = a ? a1 : (b ? p : a2);
+      v1 = a ? v : v1;
+      a1 = a ? p : a1;
+      v2 = nv2;
+      a2 = na2;
+    }
+    if (a1 == 0x7fffffff) a1 = 0;
+    // screening error <= ~1.2e-5 sum|x w| (+2^-17 key truncation): anything
+    // within a far wider window of the winner is re-checked in exact f32.  Each
+    // half-wave lane computes 64 of the 128 terms of both dot products.
+    const bool near = a2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
+    const float* wr = w4 + (size_t)o * 128 + 64 * h;
+    const float* xa = xc + (size_t)a1 * 128 + 64 * h;
+    const float* xb = xc + (size_t)(near ? a2 : a1) * 128 + 64 * h;
+    float e1 = 0.f, e2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f32x4 wv[8], av[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        wv[u] = *reinterpret_cast<const f32x4*>(wr + 32 * q + 4 * u);
+        av[u] = *reinterpret_cast<const f32x4*>(xa + 32 * q + 4 * u);
+      }
+      if (near) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bv[u] = *reinterpret_cast<const f32x4*>(xb + 32 * q + 4 * u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e1 = fmaf(av[u][j], wv[u][j], e1);
+      }
+      if (near) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e2 = fmaf(bv[u][j], wv[u][j], e2);
+        }
+      }
+    }
+    e1 += __shfl_xor(e1, 32);
+    e2 += __shfl_xor(e2, 32);
+    const float bias = b4[o];
+    e1 += bias;
+    e2 += bias;
+    const bool second = near && ranks_before(e2, a2, e1, a1);
+    if (h == 0) {
+      gmax[(size_t)c * C4_O + o] = second ? e2 : e1;
+      gidx[(size_t)c * C4_O + o] = second ? a2 : a1;
+    }
+  }
+  STAMP(3);
 #undef STAMP
 }
 
-// Four lanes per (cloud, channel): merge the T tile partials (top-2 screening
-// keys), then exact f32 dot products over x3 rows (each lane 32 of the 128
-// terms) for the winner and, on near-ties, the runner-up.
-__global__ void __launch_bounds__(256)
-k_gmax_combine(const int2* __restrict__ part, int T, int C, int N,
-               const float* __restrict__ x3g, const float* __restrict__ w4,
-               const float* __restrict__ b4, float* __restrict__ gmax,
-               int32_t* __restrict__ gidx) {
-  const int q = threadIdx.x & 3;
-  const int g = blockIdx.x * 64 + (threadIdx.x >> 2);  // (cloud, channel) pair
-  const int c = g / FF_O, o = g % FF_O;
-  if (c >= C) return;  // C * FF_O is a multiple of 64: whole waves leave
-  // this lane's quarter of W4[o] and the bias do not depend on the merge:
-  // fetched together with the partials
-  const float* wrow = w4 + (size_t)o * 128 + 32 * q;
-  f32x4 wv[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) wv[u] = *reinterpret_cast<const f32x4*>(wrow + 4 * u);
-  const float bias = b4[o];
-  float v1 = -INFINITY, v2 = -INFINITY;
-  int i1 = 0x7fffffff, i2 = 0x7fffffff;
-  for (int t = q; t < T; t += 4) {
-    const int2 kk = part[((size_t)c * T + t) * FF_O + o];
-    if (kk.x != KEY_NONE) top2_merge(key_value(kk.x), t * FF_P + key_index(kk.x), v1, i1, v2, i2);
-    if (kk.y != KEY_NONE) top2_merge(key_value(kk.y), t * FF_P + key_index(kk.y), v1, i1, v2, i2);
-  }
-#pragma unroll
-  for (int m = 1; m < 4; m <<= 1) {
-    const float a1 = __shfl_xor(v1, m), a2 = __shfl_xor(v2, m);
-    const int j1 = __shfl_xor(i1, m), j2 = __shfl_xor(i2, m);
-    top2_merge(a1, j1, v1, i1, v2, i2);
-    top2_merge(a2, j2, v1, i1, v2, i2);
-  }
-  if (i1 == 0x7fffffff) i1 = 0;
-  // screening error <= ~1.2e-5 sum|x w| (+2^-16 key truncation): re-check
-  // anything within a far wider window of the winner in exact f32; both rows
-  // are fetched in one round trip
-  const bool near = i2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
-  const float* x1r = x3g + ((size_t)c * N + i1) * 128 + 32 * q;
-  const float* x2r = x3g + ((size_t)c * N + (near ? i2 : i1)) * 128 + 32 * q;
-  f32x4 xa[8], xb[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) xa[u] = *reinterpret_cast<const f32x4*>(x1r + 4 * u);
-  if (near) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) xb[u] = *reinterpret_cast<const f32x4*>(x2r + 4 * u);
-  }
-  auto dot = [&](const f32x4* xv) {
-    float d = 0.f;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      d = fmaf(xv[u].x, wv[u].x, d);
-      d = fmaf(xv[u].y, wv[u].y, d);
-      d = fmaf(xv[u].z, wv[u].z, d);
-      d = fmaf(xv[u].w, wv[u].w, d);
-    }
-    d += __shfl_xor(d, 1);
-    d += __shfl_xor(d, 2);
-    return d;
-  };
-  const float e1 = dot(xa) + bias;
-  float e2 = 0.f;
-  if (near) e2 = dot(xb) + bias;
-  const bool second = near && ranks_before(e2, i2, e1, i1);
-  if (q == 0) {
-    gmax[(size_t)c * FF_O + o] = second ? e2 : e1;
-    gidx[(size_t)c * FF_O + o] = second ? i2 : i1;
-  }
-}
-
-// workspace: per-tile top-2 partials, then W4 split into bf16 hi / lo
-static size_t part_bytes(int C, int N) {
-  const size_t T = (N + FF_P - 1) / FF_P;
-  return ((size_t)C * T * FF_O * sizeof(int2) + 255) & ~(size_t)255;
-}
-
 size_t feat_fwd_workspace_bytes(int C, int N) {
-  return part_bytes(C, N) + 2 * (size_t)FF_O * 128 * sizeof(__bf16);
+  (void)C;
+  (void)N;
+  return 256;  // no scratch: kept so callers can size a shared workspace
 }
 
 int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int C, int N,
@@ -414,31 +514,31 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
                           const float* w3, const float* b3, const float* w4, const float* b4,
                           float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
                           size_t ws_bytes, hipStream_t s, uint64_t* stamps) {
+  (void)ws;
+  (void)ws_bytes;
   PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
-  PC_REQUIRE(ws && ws_bytes >= feat_fwd_workspace_bytes(C, N), "feat_fwd: workspace too small");
-  const int T = (N + FF_P - 1) / FF_P;
+  PC_REQUIRE((size_t)C * 4 <= 0x7fffffff / 1, "feat_fwd: too many clouds (%d)", C);
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_fwd_fused),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(FwdLds)) != hipSuccess) {
-      set_error("feat_fwd: cannot reserve %zu bytes of LDS", sizeof(FwdLds));
+                            (int)sizeof(C4Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(MlpLds)) != hipSuccess) {
+      set_error("feat_fwd: cannot reserve LDS (%zu / %zu bytes)", sizeof(C4Lds), sizeof(MlpLds));
       return PCADV_EHIP;
     }
     attr_set = true;
   }
-  int2* part = static_cast<int2*>(ws);
-  __bf16* w4hi = reinterpret_cast<__bf16*>(static_cast<char*>(ws) + part_bytes(C, N));
-  __bf16* w4lo = w4hi + FF_O * 128;
-  hipLaunchKernelGGL(k_w4_split, dim3(FF_O * 128 / 4 / 256), dim3(256), 0, s, w4, w4hi, w4lo);
-  PC_HIP_CHECK_LAUNCH("k_w4_split");
-  hipLaunchKernelGGL(k_feat_fwd_fused, dim3((T + 1) / 2, C), dim3(FF_T), sizeof(FwdLds), s, pts_a,
-                     pts_b, split, N, w1, b1, w2, b2, w3, b3, w4hi, w4lo, x3, part, inc_counter,
-                     stamps, T);
-  PC_HIP_CHECK_LAUNCH("k_feat_fwd_fused");
-  hipLaunchKernelGGL(k_gmax_combine, dim3(C * FF_O / 64), dim3(256), 0, s, part, T, C, N, x3, w4,
-                     b4, gmax, gidx);
-  PC_HIP_CHECK_LAUNCH("k_gmax_combine");
+  const int T = (N + PM_P - 1) / PM_P;
+  hipLaunchKernelGGL(k_point_mlp, dim3(T, C), dim3(PM_T), sizeof(MlpLds), s, pts_a, pts_b, split,
+                     N, w1, b1, w2, b2, w3, b3, x3, inc_counter,
+                     stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr);
+  PC_HIP_CHECK_LAUNCH("k_point_mlp");
+  hipLaunchKernelGGL(k_conv4_max, dim3(C * (C4_O / C4_CB)), dim3(C4_T), sizeof(C4Lds), s, x3, C,
+                     N, w4, b4, gmax, gidx, stamps);
+  PC_HIP_CHECK_LAUNCH("k_conv4_max");
   return PCADV_OK;
 }
 

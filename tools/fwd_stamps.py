@@ -1,0 +1,97 @@
+"""Per-phase timestamps of the fused feature forward / backward (diagnostic
+build: `make stamps` -> build/stamps/libpcadv_stamps.so, never the product
+library).  s_memrealtime ticks at 100 MHz (10 ns).
+
+    python tools/fwd_stamps.py [C] [N]
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["PCADV_LIB"] = os.path.join(REPO, "build", "stamps", "libpcadv_stamps.so")
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+from adversarial_learning_on_pointclouds_amd import _lib  # noqa: E402
+from adversarial_learning_on_pointclouds_amd._lib import stream_ptr  # noqa: E402
+
+
+def summarize(tag, st, cols):
+    st = st.astype(np.int64)
+    t0 = st[:, 0].min()
+    rel = (st - t0) * 10 / 1e3  # us
+    print(f"== {tag}: {st.shape[0]} workgroups; first start 0, last start "
+          f"{rel[:, 0].max():.2f} us, last end {max(rel[:, c].max() for c in cols[-1:]):.2f} us")
+    prev = 0
+    for c in cols:
+        d = (st[:, c] - st[:, prev]) * 10 / 1e3
+        print(f"  stamp {prev:2d}->{c:2d}: median {np.median(d):7.2f} us  p10 {np.percentile(d, 10):7.2f}"
+              f"  p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f}")
+        prev = c
+
+
+def main():
+    C = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(0)
+    pts = (torch.rand(C, N, 3, generator=g) * 2 - 1).to(dev)
+    def u(*s, fan):
+        return ((torch.rand(*s, generator=g) * 2 - 1) / fan ** 0.5).to(dev)
+    w1, b1 = u(64, 3, fan=3), u(64, fan=3)
+    w2, b2 = u(64, 64, fan=64), u(64, fan=64)
+    w3, b3 = u(128, 64, fan=64), u(128, fan=64)
+    w4, b4 = u(1024, 128, fan=128), u(1024, fan=128)
+    x3 = torch.empty(C, N, 128, device=dev)
+    gmax = torch.empty(C, 1024, device=dev)
+    gidx = torch.empty(C, 1024, device=dev, dtype=torch.int32)
+    nb = lib.pcadv_feat_fwd_workspace_bytes(C, N)
+    ws = torch.empty(nb, device=dev, dtype=torch.uint8)
+    T = (N + 127) // 128
+    stamps = torch.zeros(C * ((T + 1) // 2) * 16 + C * T * 16, device=dev, dtype=torch.int64)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    f = lib.pcadv_feat_fwd_stamped
+    f.restype = ctypes.c_int
+    args = [P(pts), C, N, P(w1), P(b1), P(w2), P(b2), P(w3), P(b3), P(w4), P(b4), P(x3), P(gmax),
+            P(gidx), P(ws), ctypes.c_size_t(nb), P(stamps), stream_ptr()]
+    for _ in range(5):
+        assert f(*args) == 0
+    torch.cuda.synchronize()
+    nwg = C * 4
+    st = stamps[:nwg * 16].view(nwg, 16).cpu().numpy()
+    # k_conv4_max thread 0: 0 start, 1 W4 + first tile staged, 2 point loop done, 3 end
+    summarize("k_conv4_max", st, [1, 2, 3])
+    st1 = stamps[nwg * 16:nwg * 16 + C * T * 16].view(C * T, 16).cpu().numpy()
+    # k_point_mlp thread 0: 1 pts/W loaded, 2 conv1, 3 conv2, 4 conv3 MFMAs, 5 x3 stored
+    summarize("k_point_mlp", st1, [1, 2, 3, 4, 5])
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(20):
+        f(*args)
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"  feat_fwd (k_point_mlp + k_conv4_max) event time: {ev0.elapsed_time(ev1) / 20 * 1e3:.2f} us")
+
+    dg = torch.randn(C, 1024, device=dev) * 1e-3
+    grads = [torch.empty_like(t) for t in (w1, b1, w2, b2, w3, b3, w4, b4)]
+    nbb = lib.pcadv_feat_bwd_workspace_bytes(C, N)
+    wsb = torch.empty(nbb, device=dev, dtype=torch.uint8)
+    sb = torch.zeros(C * T * 16, device=dev, dtype=torch.int64)
+    fb = lib.pcadv_feat_bwd_stamped
+    fb.restype = ctypes.c_int
+    bargs = [P(dg), P(gidx), P(pts), C, N, P(w1), P(b1), P(w2), P(b2), P(w3), P(w4), P(x3)] + \
+            [P(t) for t in grads] + [P(wsb), ctypes.c_size_t(nbb), P(sb), stream_ptr()]
+    for _ in range(5):
+        assert fb(*bargs) == 0
+    torch.cuda.synchronize()
+    sbn = sb.view(C * T, 16).cpu().numpy()
+    cols = [c for c in range(1, 15) if (sbn[:, c] > 0).all()]
+    summarize("k_feat_bwd_chunk thread 0", sbn, cols)
+    print("  active rows per chunk: median", np.median(sbn[:, 15]))
+
+
+if __name__ == "__main__":
+    main()
