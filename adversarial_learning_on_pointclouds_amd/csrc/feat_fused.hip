@@ -127,17 +127,22 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     const int col = 32 * wave + r;
     const float bias = b3[col];
     float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
-    f32x16 acc[4] = {{}, {}, {}, {}};
-    mfma_tiles<64, 4>(L.x2, S64, bf3, acc, lane);
-    STAMP(4);
+    // two point tiles at a time: the stores of one pair are in flight while
+    // the next pair's MFMAs run
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
+    for (int half = 0; half < 2; ++half) {
+      f32x16 acc[2] = {{}, {}};
+      mfma_tiles<64, 2>(L.x2 + 64 * half * S64, S64, bf3, acc, lane);
+      if (half == 1) STAMP(4);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 32 * pt + acc_row(i, lane);
-        const float v = acc[pt][i] + bias;
-        if (p0 + row < N) xg[(size_t)row * 128] = v > 0.f ? v : 0.f;
-      }
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = 64 * half + 32 * t + acc_row(i, lane);
+          const float v = acc[t][i] + bias;
+          if (p0 + row < N) xg[(size_t)row * 128] = v > 0.f ? v : 0.f;
+        }
+    }
   }
   STAMP(5);
 #undef STAMP
@@ -146,6 +151,9 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
 // ============================================================================
 // k_conv4_max: conv4 (128 -> 1024) + max over points
 // ============================================================================
+#ifndef PCADV_C4_DIAG
+#define PCADV_C4_DIAG 0  // diagnostic builds only: 1 = no screening, 2 = no staging
+#endif
 constexpr int C4_O = 1024;  // conv4 output channels
 constexpr int C4_CB = 256;  // channels per workgroup (8 waves x 32)
 constexpr int C4_T = 512;
@@ -154,8 +162,10 @@ constexpr int C4_SB = 136;  // bf16 row stride of the x3 hi / lo tiles (272 B: c
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-struct C4Lds {
-  alignas(16) __bf16 x[2][2][C4_P * C4_SB];  // [buffer][hi, lo]
+constexpr int C4_WS = 132;  // f32 row stride of the prologue's W4 staging (conflict-free b128 reads)
+union C4Lds {
+  alignas(16) __bf16 x[2][2][C4_P * C4_SB];  // x3 tiles [buffer][hi, lo]
+  alignas(16) float w[8][32 * C4_WS];        // prologue only: each wave's 32 rows of W4
 };
 
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -207,6 +217,29 @@ __device__ __forceinline__ float key_value(int k) {
   return __int_as_float(ord ^ ((ord >> 31) & 0x7fffffff));
 }
 constexpr int KEY_NONE = (int)0x80000000;  // below every real key
+
+// Sum over the 32 lanes of each half-wave, the total in every lane of the half
+// (DPP quad / half-row / row mirrors, then one swizzle across the two rows);
+// every lane adds the same operands, so all get bitwise the same total.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// Sum over each octet of lanes (8 k .. 8 k + 7), the total in all eight
+__device__ __forceinline__ float octet_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += dpp<0x141>(v);  // row_half_mirror: lane i <- 7 - i within 8 (the other quad)
+  return v;
+}
+__device__ __forceinline__ float half_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += dpp<0x141>(v);  // row_half_mirror: lane i <- 7 - i within 8 (the other quad)
+  v += dpp<0x140>(v);  // row_mirror: lane i <- 15 - i within 16 (the other 8)
+  v += __shfl_xor(v, 16);
+  return v;
+}
 
 // (va, ia) ranks before (vb, ib): larger value, NaN above all, lower index on ties
 __device__ __forceinline__ bool ranks_before(float va, int ia, float vb, int ib) {
@@ -286,10 +319,23 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     dl[1] = lo[1];
   };
   stage_load(0);
-  // W4 rows of this lane's channel, k = 16 kb + 8 h .. + 8, split to bf16 hi / lo
+  // W4 rows of this wave's 32 channels: coalesced 1 KB loads into the wave's
+  // own LDS rows (no workgroup barrier: only this wave reads them back), then
+  // each lane takes k = 16 kb + 8 h .. + 8 of its channel, split to bf16 hi / lo
   bf16x8 bh[8], bl[8];
   {
-    const float* wrow = w4 + (size_t)o * 128 + 8 * h;
+    const float* wsrc = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128;
+    float* wl = L.w[wave];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = 4 * (lane + 64 * i);  // float index in the 32 x 128 block
+      *reinterpret_cast<f32x4*>(wl + (e >> 7) * C4_WS + (e & 127)) =
+          *reinterpret_cast<const f32x4*>(wsrc + e);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float* wrow = wl + r * C4_WS + 8 * h;
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const f32x4 u0 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb);
@@ -303,6 +349,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       }
     }
   }
+  __syncthreads();  // every wave holds its fragments before tile 0 overwrites the staging rows
   stage_write(0);
   stage_load(1);
   __syncthreads();
@@ -363,7 +410,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       if constexpr (decltype(SCREEN)::value && decltype(MASKED)::value) {
         screen_unit(prev, uprev, MASKED, kb, kb + 1, k1, k2);
         asm volatile("" ::"v"(k1), "v"(k2));
-      } else if constexpr (decltype(SCREEN)::value) {
+      } else if constexpr (decltype(SCREEN)::value && !(PCADV_C4_DIAG & 1)) {
         // 16 values over k-blocks 1..7 (2,2,2,2,2,3,3); none in k-block 0, so the
         // previous unit's MFMAs have retired before the asm reads them
         using IC = std::integral_constant<int, 0>;
@@ -378,7 +425,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         // screening below the MFMAs, next to its only use)
         asm volatile("" ::"v"(k1), "v"(k2));
       }
-      if (pt == 0 && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
+      if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
 #pragma unroll
         for (int j = 4 * kb; j < 4 * kb + 4; ++j) {
           const float v = stg[j >> 2][j & 3];
@@ -388,7 +435,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         }
         asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
       }
-      if (pt == 0 && kb == 4) {  // the next step's tile (buffer free since the barrier)
+      if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb == 4) {  // the next step's tile (buffer free since the barrier)
         bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][srow * C4_SB + sk]);
         bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][srow * C4_SB + sk]);
         dh[0] = shi[0];
@@ -396,7 +443,9 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         dl[0] = slo[0];
         dl[1] = slo[1];
       }
-      if (pt == 1 && kb == 1) stage_load(s + 2);  // (clamped: past the end it re-reads)
+      // tile s + 2 into the staging registers just freed (clamped: past the
+      // end it re-reads the last row): 1.5 units ahead of its conversion
+      if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb == 4) stage_load(s + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (decltype(SCREEN)::value) pair_merge(k1, uprev, k2, uprev, r1, t1, r2, t2);
@@ -456,43 +505,57 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     }
     if (a1 == 0x7fffffff) a1 = 0;
     // screening error <= ~1.2e-5 sum|x w| (+2^-17 key truncation): anything
-    // within a far wider window of the winner is re-checked in exact f32.  Each
-    // half-wave lane computes 64 of the 128 terms of both dot products.
+    // within a far wider window of the winner is re-checked in exact f32 (the
+    // second row is the first again when there is no near-tie)
     const bool near = a2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
-    const float* wr = w4 + (size_t)o * 128 + 64 * h;
-    const float* xa = xc + (size_t)a1 * 128 + 64 * h;
-    const float* xb = xc + (size_t)(near ? a2 : a1) * 128 + 64 * h;
-    float e1 = 0.f, e2 = 0.f;
+    const int b2 = near ? a2 : a1;
+    STAMP(4);
+    // Exact dot products, eight lanes per row: in pass G lane l takes channel
+    // 8 G + (l >> 3) and terms 16 (l & 7) .. + 16, so a load instruction reads
+    // eight 128-B lines whole (a lane-per-row layout would touch 64 lines) and
+    // the partial sums meet in three DPP steps within the lane octet.
+    const int oc = lane >> 3, part = lane & 7;
+    const float* wbase = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128 + 16 * part;
+    f32x4 wv[4][4], av[4][4], bv[4][4];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      f32x4 wv[8], av[8], bv[8];
+    for (int G = 0; G < 4; ++G) {
+      const int ch = 8 * G + oc;
+      const int p1 = __shfl(a1, ch), p2 = __shfl(b2, ch);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        wv[u] = *reinterpret_cast<const f32x4*>(wr + 32 * q + 4 * u);
-        av[u] = *reinterpret_cast<const f32x4*>(xa + 32 * q + 4 * u);
-      }
-      if (near) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) bv[u] = *reinterpret_cast<const f32x4*>(xb + 32 * q + 4 * u);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e1 = fmaf(av[u][j], wv[u][j], e1);
-      }
-      if (near) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) e2 = fmaf(bv[u][j], wv[u][j], e2);
-        }
+      for (int u = 0; u < 4; ++u) {
+        wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)ch * 128 + 4 * u);
+        av[G][u] = *reinterpret_cast<const f32x4*>(xc + (size_t)p1 * 128 + 16 * part + 4 * u);
+        bv[G][u] = *reinterpret_cast<const f32x4*>(xc + (size_t)p2 * 128 + 16 * part + 4 * u);
       }
     }
-    e1 += __shfl_xor(e1, 32);
-    e2 += __shfl_xor(e2, 32);
+#ifdef PCADV_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    STAMP(5);
+    float res1 = 0.f, res2 = 0.f;
+#pragma unroll
+    for (int G = 0; G < 4; ++G) {
+      float e1 = 0.f, e2 = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          e1 = fmaf(av[G][u][t], wv[G][u][t], e1);
+          e2 = fmaf(bv[G][u][t], wv[G][u][t], e2);
+        }
+      e1 = octet_sum(e1);
+      e2 = octet_sum(e2);
+      // channel ch = 8 G + k was summed in lanes 8 k .. 8 k + 7: owner lanes
+      // r in [8 G, 8 G + 8) (both halves) fetch it
+      const int src = 8 * ((r - 8 * G) & 7);
+      const float f1 = __shfl(e1, src), f2 = __shfl(e2, src);
+      if ((r >> 3) == G) {
+        res1 = f1;
+        res2 = f2;
+      }
+    }
     const float bias = b4[o];
-    e1 += bias;
-    e2 += bias;
+    const float e1 = res1 + bias, e2 = res2 + bias;
     const bool second = near && ranks_before(e2, a2, e1, a1);
     if (h == 0) {
       gmax[(size_t)c * C4_O + o] = second ? e2 : e1;

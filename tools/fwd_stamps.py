@@ -11,7 +11,7 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["PCADV_LIB"] = os.path.join(REPO, "build", "stamps", "libpcadv_stamps.so")
+os.environ["PCADV_LIB"] = os.environ.get("PCADV_STAMPS_LIB", os.path.join(REPO, "build", "stamps", "libpcadv_stamps.so"))
 sys.path.insert(0, REPO)
 import torch  # noqa: E402
 from adversarial_learning_on_pointclouds_amd import _lib  # noqa: E402
@@ -63,7 +63,7 @@ def main():
     nwg = C * 4
     st = stamps[:nwg * 16].view(nwg, 16).cpu().numpy()
     # k_conv4_max thread 0: 0 start, 1 W4 + first tile staged, 2 point loop done, 3 end
-    summarize("k_conv4_max", st, [1, 2, 3])
+    summarize("k_conv4_max", st, [1, 2, 4, 5, 3])
     st1 = stamps[nwg * 16:nwg * 16 + C * T * 16].view(C * T, 16).cpu().numpy()
     # k_point_mlp thread 0: 1 pts/W loaded, 2 conv1, 3 conv2, 4 conv3 MFMAs, 5 x3 stored
     summarize("k_point_mlp", st1, [1, 2, 3, 4, 5])
