@@ -1,13 +1,13 @@
 // PointNetfeat forward (models/pointnet.py:109-132, feature_transform=False) on
 // gfx950 in two launches:
 //
-//   k_point_mlp   one workgroup per (cloud, 128-point tile): conv1 -> conv2 ->
-//                 conv3 (+ ReLU), exact f32.  Only x3 (post-ReLU conv3, the
-//                 operand of conv4, the exact re-evaluation and the backward)
-//                 leaves the chip.
+//   k_point_mlp   64-point tiles, two per workgroup: conv1 -> conv2 -> conv3
+//                 (+ ReLU).  Only x3 (post-ReLU conv3, the operand of conv4,
+//                 the exact re-evaluation and the backward) leaves the chip.
 //     conv1 (3 -> 64)    VALU, in the fma order the backward's recompute uses
 //     conv2 (64 -> 64)   v_mfma_f32_32x32x2_f32 (exact f32, k-ordered)
-//     conv3 (64 -> 128)  v_mfma_f32_32x32x2_f32
+//     conv3 (64 -> 128)  six v_mfma_f32_32x32x16_bf16 products of three-way
+//                        bf16 splits (f32-level accuracy)
 //
 //   k_conv4_max   one workgroup per (cloud, 256-channel block), weight-
 //                 stationary: each of the 8 waves holds its 32 channels of W4 as
@@ -29,122 +29,153 @@
 
 namespace pcadv {
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// f32 -> three bf16 whose sum is the f32 value (round-to-nearest splits: each
+// residual is exact in f32 and the last one fits 8 significant bits)
+__device__ __forceinline__ void split3(float v, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)v;
+  const float r1 = v - (float)hi;
+  mid = (__bf16)r1;
+  lo = (__bf16)(r1 - (float)mid);
+}
+
 // ============================================================================
 // k_point_mlp: conv1..conv3
 // ============================================================================
-constexpr int PM_P = 128;  // points per workgroup
-
-// NT 32x32 f32 MFMA tiles (point tiles 0..NT-1 of a_lds) against one 32-column
-// block of W: the NT accumulation chains are interleaved so the matrix pipe
-// always has an independent MFMA to issue.  Each chain runs in the k order of
-// mfma_rows_x_wt (common.h), so results are bitwise those of the single-tile
-// form the backward's recompute uses.
-template <int K, int NT>
-__device__ __forceinline__ void mfma_tiles(const float* __restrict__ a_lds, int a_stride,
-                                           const f32x4* bfrag, f32x16 (&acc)[NT], int lane) {
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int g = 0; g < K / 8; ++g) {
-    f32x4 a[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      a[t] = *reinterpret_cast<const f32x4*>(a_lds + (32 * t + r) * a_stride + 8 * g + 4 * h);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma32(a[t][j], bfrag[g][j], acc[t]);
-  }
-}
-constexpr int PM_T = 256;  // 4 waves; 2 workgroups per CU (72 KB of LDS each)
+constexpr int PM_P = 64;    // points per tile
+constexpr int PM_T = 256;   // 4 waves; 2 workgroups per CU (register-bound)
+constexpr int PM_TPW = 2;   // tiles per workgroup (the next tile's points are prefetched)
+constexpr int X2S = 72;     // bf16 row stride of the x2 planes (144 B: conflict-free b128 reads)
 
 struct MlpLds {
   alignas(16) float pts[PM_P * 4];
   alignas(16) float x1[PM_P * S64];
-  alignas(16) float x2[PM_P * S64];
+  alignas(16) __bf16 x2[3][PM_P * X2S];  // conv2 output split in bf16 hi / mid / lo
 };
 
-__global__ void __launch_bounds__(PM_T)
+// conv1 and conv2 run in exact f32 (VALU, then v_mfma_f32_32x32x2_f32 in the k
+// order of mfma_rows_x_wt), bitwise what the backward recomputes.  conv3 runs
+// on the bf16 matrix pipe as six products of the three-way splits of x2 and W3
+// (h h, h m, m h, h l, m m, l h; the dropped m l, l m, l l terms are < 2^-23 of
+// |x w|), f32 accumulate: f32-level accuracy at 6/16 of the f32 MFMA cycles.
+__global__ void __launch_bounds__(PM_T) __attribute__((amdgpu_waves_per_eu(2)))
 k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split, int N,
-            const float* __restrict__ w1, const float* __restrict__ b1,
+            int T, int ntiles, const float* __restrict__ w1, const float* __restrict__ b1,
             const float* __restrict__ w2, const float* __restrict__ b2,
             const float* __restrict__ w3, const float* __restrict__ b3,
             float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MlpLds& L = *reinterpret_cast<MlpLds*>(smem);
 #ifdef PCADV_STAMPS
-  uint64_t* st = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+  uint64_t* st = stamps + (size_t)blockIdx.x * 16;
 #define STAMP(k) do { if (stamps && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
 #endif
   STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31;
-  const int c = blockIdx.y, p0 = blockIdx.x * PM_P;
-  if (inc_counter && tid == 0 && c == 0 && blockIdx.x == 0) *inc_counter += 1;
-  const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
+  const int r = lane & 31, h = lane >> 5;
+  if (inc_counter && tid == 0 && blockIdx.x == 0) *inc_counter += 1;
 
-  // B fragments of this wave's conv2 / conv3 channel tiles, issued before the
-  // point loads so both latencies overlap
-  f32x4 bf2[8], bf3[8];
+  // points of a tile: thread e < 192 holds one coordinate
+  auto pts_load = [&](int tile) {
+    const int c = tile / T, p0 = (tile % T) * PM_P;
+    const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
+    const int p = tid / 3;
+    return (tid < PM_P * 3 && p0 + p < N) ? pts[(size_t)p0 * 3 + tid] : 0.f;
+  };
+  int tile = blockIdx.x * PM_TPW;
+  float pv = tile < ntiles ? pts_load(tile) : 0.f;
+
+  // conv2: wave = (point tile wave >> 1, channel tile wave & 1), f32 B fragments
+  f32x4 bf2[8];
   load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
-  load_bfrag<64>(w3, 32 * wave, lane, bf3);
-  for (int e = tid; e < PM_P * 3; e += PM_T) {
-    const int p = e / 3, k = e % 3;
-    L.pts[p * 4 + k] = p0 + p < N ? pts[(size_t)(p0 + p) * 3 + k] : 0.f;
-  }
-  __syncthreads();
-  STAMP(1);
-  {  // conv1 (3 -> 64) + ReLU: thread = (channel, 32-point group)
-    const int ch = tid & 63, pg = tid >> 6;
-    const float wa = w1[ch * 3 + 0], wb = w1[ch * 3 + 1], wc = w1[ch * 3 + 2], bb = b1[ch];
-#pragma unroll 4
-    for (int i = 0; i < 32; ++i) {
-      const int p = pg * 32 + i;
-      L.x1[p * S64 + ch] =
-          conv1_point(wa, wb, wc, bb, L.pts[p * 4 + 0], L.pts[p * 4 + 1], L.pts[p * 4 + 2]);
+  const float bias2 = b2[32 * (wave & 1) + r];
+  // conv3: wave = channel tile (32 channels), W3 rows split three ways:
+  // lane (r, h) holds k = 16 kb + 8 h .. + 8 of channel 32 wave + r
+  bf16x8 w3h[4], w3m[4], w3l[4];
+  {
+    const float* wrow = w3 + (size_t)(32 * wave + r) * 64 + 8 * h;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 a, m, l;
+        split3(j < 4 ? u0[j] : u1[j - 4], a, m, l);
+        w3h[kb][j] = a;
+        w3m[kb][j] = m;
+        w3l[kb][j] = l;
+      }
     }
   }
-  __syncthreads();
-  STAMP(2);
-  {  // conv2 (64 -> 64) + ReLU: wave = (channel tile wave & 1, point tiles 2 (wave >> 1) + j)
-    const int col = 32 * (wave & 1) + r;
-    const float bias = b2[col];
-    const int pt0 = 2 * (wave >> 1);
-    f32x16 acc[2] = {{}, {}};
-    mfma_tiles<64, 2>(L.x1 + 32 * pt0 * S64, S64, bf2, acc, lane);
+  const float bias3 = b3[32 * wave + r];
+  // conv1: thread = (channel tid & 63, 16-point group tid >> 6)
+  const int c1 = tid & 63, pg = tid >> 6;
+  const float wa = w1[c1 * 3 + 0], wb = w1[c1 * 3 + 1], wc = w1[c1 * 3 + 2], bb1 = b1[c1];
+  STAMP(1);
+
+  for (int it = 0; it < PM_TPW && tile < ntiles; ++it, ++tile) {
+    const int c = tile / T, p0 = (tile % T) * PM_P;
+    if (tid < PM_P * 3) L.pts[(tid / 3) * 4 + tid % 3] = pv;
+    __syncthreads();  // (also: every wave is past the previous tile's conv3 reads)
+    if (it + 1 < PM_TPW && tile + 1 < ntiles) pv = pts_load(tile + 1);  // in flight during this tile
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < 16; ++i) {
+      const int p = pg * 16 + i;
+      const f32x4 q = *reinterpret_cast<const f32x4*>(&L.pts[p * 4]);
+      L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
+    }
+    __syncthreads();
+    {  // conv2 + ReLU, written to LDS split three ways for conv3
+      const int pt = wave >> 1, col = 32 * (wave & 1) + r;
+      f32x16 acc = {};
+      acc = mfma_rows_x_wt<64>(L.x1 + 32 * pt * S64, S64, bf2, acc, lane);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float v = acc[j][i] + bias;
-        L.x2[(32 * (pt0 + j) + acc_row(i, lane)) * S64 + col] = v > 0.f ? v : 0.f;
+        float v = acc[i] + bias2;
+        v = v > 0.f ? v : 0.f;
+        const int row = 32 * pt + acc_row(i, lane);
+        split3(v, L.x2[0][row * X2S + col], L.x2[1][row * X2S + col], L.x2[2][row * X2S + col]);
       }
-  }
-  __syncthreads();
-  STAMP(3);
-  {  // conv3 (64 -> 128) + ReLU -> x3 (HBM): wave = channel tile, all 4 point tiles
-    const int col = 32 * wave + r;
-    const float bias = b3[col];
-    float* xg = x3g + ((size_t)c * N + p0) * 128 + col;
-    // two point tiles at a time: the stores of one pair are in flight while
-    // the next pair's MFMAs run
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    }
+    __syncthreads();
+    {  // conv3 (64 -> 128) + ReLU -> x3 (HBM): wave = channel tile, both point tiles
       f32x16 acc[2] = {{}, {}};
-      mfma_tiles<64, 2>(L.x2 + 64 * half * S64, S64, bf3, acc, lane);
-      if (half == 1) STAMP(4);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const int off = (32 * pt + r) * X2S + 16 * kb + 8 * h;
+          const bf16x8 xh = *reinterpret_cast<const bf16x8*>(&L.x2[0][off]);
+          const bf16x8 xm = *reinterpret_cast<const bf16x8*>(&L.x2[1][off]);
+          const bf16x8 xl = *reinterpret_cast<const bf16x8*>(&L.x2[2][off]);
+          acc[pt] = mfma_bf16(xl, w3h[kb], acc[pt]);
+          acc[pt] = mfma_bf16(xm, w3m[kb], acc[pt]);
+          acc[pt] = mfma_bf16(xh, w3l[kb], acc[pt]);
+          acc[pt] = mfma_bf16(xm, w3h[kb], acc[pt]);
+          acc[pt] = mfma_bf16(xh, w3m[kb], acc[pt]);
+          acc[pt] = mfma_bf16(xh, w3h[kb], acc[pt]);
+        }
+      }
+      float* xg = x3g + ((size_t)c * N + p0) * 128 + 32 * wave + r;
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int row = 64 * half + 32 * t + acc_row(i, lane);
-          const float v = acc[t][i] + bias;
+          const int row = 32 * pt + acc_row(i, lane);
+          const float v = acc[pt][i] + bias3;
           if (p0 + row < N) xg[(size_t)row * 128] = v > 0.f ? v : 0.f;
         }
     }
   }
-  STAMP(5);
+  STAMP(2);
 #undef STAMP
 }
 
@@ -168,9 +199,6 @@ union C4Lds {
   alignas(16) float w[8][32 * C4_WS];        // prologue only: each wave's 32 rows of W4
 };
 
-__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
 
 // Screening keys: the f32 value mapped to an order-preserving int32 whose low
 // 6 bits are replaced by 63 - (the point's row inside its 64-point step, less
@@ -595,8 +623,9 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
     attr_set = true;
   }
   const int T = (N + PM_P - 1) / PM_P;
-  hipLaunchKernelGGL(k_point_mlp, dim3(T, C), dim3(PM_T), sizeof(MlpLds), s, pts_a, pts_b, split,
-                     N, w1, b1, w2, b2, w3, b3, x3, inc_counter,
+  const int ntiles = C * T;
+  hipLaunchKernelGGL(k_point_mlp, dim3((ntiles + PM_TPW - 1) / PM_TPW), dim3(PM_T), sizeof(MlpLds),
+                     s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3, inc_counter,
                      stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
   hipLaunchKernelGGL(k_conv4_max, dim3(C * (C4_O / C4_CB)), dim3(C4_T), sizeof(C4Lds), s, x3, C,
