@@ -1,11 +1,11 @@
 """Print one step's kernel timeline from a rocprofv3 kernel trace (the last
-complete graph replay: a k_feat_fwd_fused followed by the step's kernels)."""
+complete graph replay: a k_point_mlp followed by the step's kernels)."""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "k_feat_fwd_fused" in r["Kernel_Name"]
+starts = [i for i, r in enumerate(rows) if "k_point_mlp" in r["Kernel_Name"]
           and i + 2 < len(rows) and "k_linear_fwd" in rows[i + 2]["Kernel_Name"]]
 which = int(sys.argv[2]) if len(sys.argv) > 2 else -2
 i0 = starts[which]
