@@ -148,9 +148,9 @@ def main():
     losses = step.losses.cpu().numpy().tolist()
     finite = all(np.isfinite(losses))
 
-    # dominant kernel: the fused PointNetfeat forward (k_feat_fwd_fused, conv1..conv4
-    # + per-tile top-2) and its k_gmax_combine, timed with HIP events on the stream
-    # they are launched on, same inputs as the step (the last resident batch)
+    # dominant kernels: the PointNetfeat forward (k_point_mlp: conv1..conv3;
+    # k_conv4_max: conv4 + max with the exact re-evaluation), timed with HIP events on
+    # the stream they are launched on, same inputs as the step (the last resident batch)
     pg, lab, pn = pool[(args.steps - 1) % POOL]
     pts_all = torch.cat([pg, pn], 0).contiguous()
     fw = [model.feat.conv1.weight, model.feat.conv1.bias, model.feat.conv2.weight,
@@ -170,20 +170,22 @@ def main():
     # 2 * N * (3*64 + 64*64 + 64*128 + 128*1024) per cloud
     flops = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64 + 64 * 128 + 128 * 1024)
     achieved = flops / kern_s / 1e12
-    # Ceiling of this kernel pair on MI355X: conv1..conv3 (1.64 GFLOP) at the dense
-    # f32 MFMA / VALU peak (157.3 TF) plus conv4 (17.18 GFLOP), run as 3 bf16 MFMAs
-    # per f32 product, at the dense bf16 peak / 3 (2500/3 TF).  The composite peak is
-    # the total FLOPs over that minimum time (MI355X_MICROARCH.md peaks).
-    f13 = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64 + 64 * 128)
-    f4 = flops - f13
-    t_min = f13 / 157.3e12 + f4 / (2500e12 / 3.0)
+    # Ceiling of this pair on MI355X, by the pipe each layer runs on: conv1 (VALU)
+    # and conv2 (f32 MFMA) at the dense f32 peak (157.3 TF); conv3 as six bf16
+    # products per f32 product at the dense bf16 peak / 6; conv4 as three at the
+    # bf16 peak / 3 (2500 TF dense).  The composite peak is the total FLOPs over
+    # that minimum time (MI355X_MICROARCH.md peaks).
+    f12 = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64)
+    f3 = 2.0 * (2 * B) * N * (64 * 128)
+    f4 = flops - f12 - f3
+    t_min = f12 / 157.3e12 + f3 / (2500e12 / 6.0) + f4 / (2500e12 / 3.0)
     peak = flops / t_min / 1e12
     traffic, traffic_src = None, None
     prof = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                          "profiles", "r*_pmc_traffic.json")))
     if prof:
         kern = json.load(open(prof[-1]))["kernels"]
-        names = ("pcadv::k_w4_split", "pcadv::k_feat_fwd_fused", "pcadv::k_gmax_combine")
+        names = ("pcadv::k_point_mlp", "pcadv::k_conv4_max")
         if all(n in kern for n in names):
             traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
             traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))
@@ -208,7 +210,7 @@ def main():
                    "global_batch": 2 * B * world, "points": N,
                    "parallelism": f"dp{world}", "hip_graph": use_graph},
         "roofline": {"bound": "mfma",
-                     "kernel": "k_w4_split + k_feat_fwd_fused + k_gmax_combine (PointNetfeat conv1..4 + max)",
+                     "kernel": "k_point_mlp + k_conv4_max (PointNetfeat conv1..4 + max, 2 launches)",
                      "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
@@ -216,7 +218,7 @@ def main():
                      "algorithmic_bytes_per_launch": 2 * B * N * (3 + 128) * 4 + 2 * B * 1024 * 8,
                      "avg_launch_us": round(kern_s * 1e6, 2),
                      "algorithmic_flops_per_launch": flops,
-                     "peak_basis": "f32 MFMA 157.3 TF for conv1-3 + bf16 2500/3 TF for conv4"},
+                     "peak_basis": "f32 157.3 TF for conv1-2, bf16 2500/6 TF for conv3 (6 split products), bf16 2500/3 TF for conv4 (3 split products)"},
         "step_mfma": {"gflop_per_step": step_gflop, "achieved_tflops": round(step_tf, 2),
                       "frac_of_f32_peak": round(step_tf / 157.3, 4)},
         "losses_last_step": [round(v, 5) for v in losses],
