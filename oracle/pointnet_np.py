@@ -564,3 +564,117 @@ def seg_forward(p, pts, cls):
     h = relu(h @ p["fc3.weight"].T + p["fc3.bias"])
     out = h @ p["fc4.weight"].T + p["fc4.bias"]
     return out.transpose(0, 2, 1).astype(F32), g[:, :, None].astype(F32)
+
+
+# --------------------------------------------------------------------------
+# segmentation training step (models/pointnet.py:282-317 forward + autograd;
+# utils/trainer.py:310-400 run_training_pointnet_seg: CrossEntropyLoss over
+# every point, pointnet/train_pointnet_seg.py:152; backward; Adam)
+# --------------------------------------------------------------------------
+
+def seg_forward_train(p, pts, cls):
+    """PointNetSeg.forward keeping what the backward needs.  Returns logits
+    (B, N, C) point-major, gmax (B, 2048), and the cache."""
+    pts = np.ascontiguousarray(pts, F32)
+    B, N, _ = pts.shape
+    xs = []
+    h = pts
+    for i in range(1, 7):
+        h = relu(h @ _w(p, f"conv{i}.weight").T + p[f"conv{i}.bias"]).astype(F32)
+        xs.append(h)
+    x6 = xs[5]
+    am = x6.argmax(1)                                        # first index on ties (torch.max)
+    g = np.take_along_axis(x6, am[:, None, :], 1)[:, 0, :]   # (B, 2048)
+    loc = np.concatenate(xs[:5], axis=2)                     # (B, N, 960) = x1..x5
+    W1 = p["fc1.weight"]
+    # fc1 over [x1..x5 | tile(gmax) | tile(cls)] (pointnet.py:304-310): the tiled
+    # parts are the same for every point of a cloud
+    cvec = cls.reshape(B, -1).astype(F32)
+    cb = (g @ W1[:, 960:3008].T + cvec @ W1[:, 3008:].T + p["fc1.bias"]).astype(F32)
+    h1 = relu(loc @ W1[:, :960].T + cb[:, None, :]).astype(F32)
+    h2 = relu(h1 @ p["fc2.weight"].T + p["fc2.bias"]).astype(F32)
+    h3 = relu(h2 @ p["fc3.weight"].T + p["fc3.bias"]).astype(F32)
+    out = (h3 @ p["fc4.weight"].T + p["fc4.bias"]).astype(F32)
+    cache = dict(pts=pts, xs=xs, am=am, g=g, loc=loc, cvec=cvec, h1=h1, h2=h2, h3=h3)
+    return out, g, cache
+
+
+def seg_cross_entropy(logits, seg):
+    """CrossEntropyLoss()(pred (B, C, N), seg (B, N)): mean over all B*N points.
+    logits point-major (B, N, C).  Returns (loss, dloss/dlogits)."""
+    B, N, C = logits.shape
+    lsm = log_softmax(logits.reshape(B * N, C))
+    lab = seg.reshape(-1)
+    loss = -float(np.mean(lsm[np.arange(B * N), lab].astype(np.float64)))
+    grad = np.exp(lsm)
+    grad[np.arange(B * N), lab] -= 1.0
+    return loss, (grad / F32(B * N)).astype(F32).reshape(B, N, C)
+
+
+def seg_backward(p, cache, dout):
+    """Gradients of every PointNetSeg parameter given dL/dlogits (B, N, C)."""
+    B, N, _ = dout.shape
+    g_ = OrderedDict()
+
+    def lin_bwd(dy, x, name):
+        x2 = x.reshape(-1, x.shape[-1])
+        d2 = dy.reshape(-1, dy.shape[-1])
+        g_[name + ".weight"] = (d2.T @ x2).astype(F32)
+        g_[name + ".bias"] = d2.sum(0).astype(F32)
+
+    h1, h2, h3 = cache["h1"], cache["h2"], cache["h3"]
+    lin_bwd(dout, h3, "fc4")
+    dz = (dout @ p["fc4.weight"]) * (h3 > 0)
+    lin_bwd(dz, h2, "fc3")
+    dz = (dz @ p["fc3.weight"]) * (h2 > 0)
+    lin_bwd(dz, h1, "fc2")
+    dz1 = ((dz @ p["fc2.weight"]) * (h1 > 0)).astype(F32)   # (B, N, 256)
+    W1 = p["fc1.weight"]
+    loc = cache["loc"]
+    dW1 = np.zeros_like(W1)
+    dW1[:, :960] = dz1.reshape(-1, 256).T @ loc.reshape(-1, 960)
+    s1 = dz1.sum(1)                                          # (B, 256): the tiled parts
+    dW1[:, 960:3008] = s1.T @ cache["g"]
+    dW1[:, 3008:] = s1.T @ cache["cvec"]
+    g_["fc1.weight"] = dW1.astype(F32)
+    g_["fc1.bias"] = dz1.reshape(-1, 256).sum(0).astype(F32)
+    dloc = (dz1 @ W1[:, :960]).astype(F32)                    # (B, N, 960)
+    dg = (s1 @ W1[:, 960:3008]).astype(F32)                   # (B, 2048)
+    xs = cache["xs"]
+    # max over points with the ReLU before it: dg reaches the argmax point
+    # when the max is positive (relu'(z) = [x6 > 0] there)
+    am = cache["am"]
+    w6 = _w(p, "conv6.weight")
+    x5 = xs[4]
+    act = (cache["g"] > 0).astype(F32)
+    dgz = dg * act                                             # (B, 2048)
+    dW6 = np.zeros_like(w6)
+    dx5_max = np.zeros_like(x5)
+    for b in range(B):
+        rows = x5[b, am[b]]                                    # (2048, 512)
+        dW6 += dgz[b][:, None] * rows
+        np.add.at(dx5_max[b], am[b], dgz[b][:, None] * w6)
+    g_["conv6.weight"] = dW6.astype(F32)[:, :, None]
+    g_["conv6.bias"] = dgz.sum(0).astype(F32)
+    offs = [0, 64, 192, 320, 448, 960]
+    dy = dx5_max + dloc[:, :, offs[4]:offs[5]]
+    for i in range(5, 0, -1):
+        x = xs[i - 1]
+        xin = xs[i - 2] if i > 1 else cache["pts"]
+        dz = (dy * (x > 0)).astype(F32)
+        w = _w(p, f"conv{i}.weight")
+        g_[f"conv{i}.weight"] = (dz.reshape(-1, dz.shape[-1]).T @ xin.reshape(-1, xin.shape[-1])
+                                 ).astype(F32)[:, :, None]
+        g_[f"conv{i}.bias"] = dz.reshape(-1, dz.shape[-1]).sum(0).astype(F32)
+        if i > 1:
+            dy = (dz @ w).astype(F32) + dloc[:, :, offs[i - 2]:offs[i - 1]]
+    return OrderedDict((k, g_[k].reshape(p[k].shape).astype(F32)) for k in p)
+
+
+def seg_step(p, pts, cls, seg, lambda_seg=1.0):
+    """One run_training_pointnet_seg iteration's loss and gradients (before
+    optimizer.step()).  Returns (loss, grads, logits (B, N, C), gmax, am)."""
+    out, g, cache = seg_forward_train(p, pts, cls)
+    loss, dout = seg_cross_entropy(out, seg)
+    grads = seg_backward(p, cache, (dout * F32(lambda_seg)).astype(F32))
+    return loss, grads, out, g, cache["am"]

@@ -147,8 +147,39 @@ def main(ref_root, only=None):
             summarize("param." + name, p.detach().numpy(), out)
         np.savez_compressed(os.path.join(HERE, "g7_cls_ft_step.npz"), **out)
 
+    # ---------------- G8: segmentation training step (run_training_pointnet_seg) ----
+    # utils/trainer.py:334-349: pred, _ = model(pts, cls); l = seg_loss(pred, seg)
+    # with seg_loss = CrossEntropyLoss() (pointnet/train_pointnet_seg.py:152);
+    # (lambda_seg * l).backward(); optimizer.step() with Adam(lr=1e-4).
+    def g8():
+        Sp = onp.make_params(onp.seg_spec(50), seed=8)
+        model = load(PointNetSeg(50), Sp).train()
+        B8, N8 = 2, 512
+        pts8 = make_pts(81, B8, N8)
+        rng8 = np.random.default_rng(82)
+        cls8 = np.zeros((B8, 1, 16), np.float32)
+        cls8[np.arange(B8), 0, rng8.integers(0, 16, B8)] = 1
+        seg8 = rng8.integers(0, 50, (B8, N8)).astype(np.int64)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        opt.zero_grad()
+        pred, glob = model(torch.from_numpy(pts8), torch.from_numpy(cls8))
+        l = torch.nn.CrossEntropyLoss()(pred, torch.from_numpy(seg8))
+        (1.0 * l).backward()
+        out = dict(s_seed=8, pts_seed=81, cls=cls8, seg=seg8, loss=np.float64(l.item()),
+                   gmax=glob.detach().numpy()[:, :, 0])
+        summarize("logits", pred.detach().numpy(), out)
+        for name, p in model.named_parameters():
+            summarize("grad." + name, p.grad.numpy(), out)
+        opt.step()
+        for name, p in model.named_parameters():
+            summarize("param." + name, p.detach().numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g8_seg_step.npz"), **out)
+
     if only == "g7":
         g7()
+        return
+    if only == "g8":
+        g8()
         return
 
     # ---------------- G1: cls forward (eval) ----------------
@@ -314,6 +345,7 @@ def main(ref_root, only=None):
     out = dict(s_seed=6, pts_seed=61, cls=cls, gmax=sg.numpy()[:, :, 0])
     summarize("out", so.numpy(), out)
     np.savez_compressed(os.path.join(HERE, "g6_seg_fwd.npz"), **out)
+    g8()
 
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
@@ -323,6 +355,6 @@ def main(ref_root, only=None):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("ref_root", nargs="?", default="/root/reference")
-    ap.add_argument("--only", default=None, help="g7: regenerate only that fixture")
+    ap.add_argument("--only", default=None, help="g7 or g8: regenerate only that fixture")
     a = ap.parse_args()
     main(a.ref_root, a.only)

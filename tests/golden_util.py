@@ -36,3 +36,24 @@ def check_tensor(fx, prefix, arr, tol=1e-3):
     assert e <= tol, f"{prefix}: sample/l2/absmax err {e:.3e} > {tol}"
     assert e_sum <= max(tol, 1e-3), f"{prefix}: sum err {e_sum:.3e}"
     return e
+
+
+def check_tensor_rel(fx, prefix, arr, tol=1e-3):
+    """As check_tensor, but scaled by the tensor's own max|ref| (not max(1, .)):
+    the strict form for gradients, which are far below 1."""
+    arr = np.asarray(arr, np.float32)
+    if prefix in fx:
+        ref = np.asarray(fx[prefix], np.float64)
+        assert arr.shape == ref.shape, (prefix, arr.shape, ref.shape)
+        scale = max(float(np.max(np.abs(ref))), 1e-30)
+        e = float(np.max(np.abs(arr.astype(np.float64) - ref))) / scale
+        assert e <= tol, f"{prefix}: rel err {e:.3e} > {tol}"
+        return e
+    flat = arr.reshape(-1).astype(np.float64)
+    scale = max(float(fx[prefix + ".absmax"]), 1e-30)
+    e_val = float(np.max(np.abs(flat[fx[prefix + ".idx"]] - fx[prefix + ".val"]))) / scale
+    e_l2 = abs(np.sqrt((flat ** 2).sum()) - float(fx[prefix + ".l2"])) / max(float(fx[prefix + ".l2"]), 1e-30)
+    e_max = abs(np.abs(flat).max() - float(fx[prefix + ".absmax"])) / scale
+    e = max(e_val, e_l2, e_max)
+    assert e <= tol, f"{prefix}: sample/l2/absmax rel err {e:.3e} > {tol}"
+    return e

@@ -123,3 +123,24 @@ def test_g7_cls_ft_step():
     opt.step(grads)
     for name, v in G.items():
         check_tensor(fx, "param." + name, v, tol=1e-5)
+
+
+def test_g8_seg_step():
+    """run_training_pointnet_seg (BASELINE configs[3]):
+    PointNetSeg forward, per-point CrossEntropyLoss, gradients of every
+    parameter (strict relative form) and the parameters after one Adam step."""
+    from golden_util import check_tensor_rel
+    fx = load("g8_seg_step.npz")
+    S = onp.make_params(onp.seg_spec(50), seed=int(fx["s_seed"]))
+    B, N = fx["seg"].shape
+    pts = np.random.default_rng(int(fx["pts_seed"])).uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    loss, grads, logits, gmax, _ = onp.seg_step(S, pts, fx["cls"], fx["seg"])
+    assert abs(loss - float(fx["loss"])) < 1e-5 * max(1.0, abs(float(fx["loss"])))
+    check_tensor_rel(fx, "gmax", gmax, tol=1e-5)
+    check_tensor_rel(fx, "logits", logits.transpose(0, 2, 1), tol=1e-5)
+    for name, g in grads.items():
+        check_tensor_rel(fx, "grad." + name, g, tol=1e-4)
+    opt = onp.Adam(S)
+    opt.step(grads)
+    for name, v in S.items():
+        check_tensor(fx, "param." + name, v, tol=1e-5)
