@@ -63,6 +63,25 @@ int tail_stamps_read(uint64_t* host);
 int launch_head_bwd(const float*, const float*, const float*, int, const float*, const float*,
                     float*, float*, float*, float*, const float*, const float*, float*,
                     hipStream_t);
+int launch_gemm(const float*, long long, int, const float*, long long, const float*, long long,
+                int, float*, long long, int, int, int, const float*, const float*, int, int, int,
+                int, hipStream_t);
+size_t gemm_wgrad_workspace_bytes(int, int, int);
+int launch_gemm_wgrad(const float*, long long, const float*, long long, const float*, long long,
+                      int, int, int, float*, long long, int, void*, size_t, hipStream_t);
+size_t colsum_workspace_bytes(int, int);
+int launch_colsum(const float*, const float*, long long, long long, int, int, float*, int, void*,
+                  size_t, hipStream_t);
+int launch_group_colsum(const float*, const float*, long long, long long, int, int, int, float*,
+                        hipStream_t);
+size_t conv_max_x3_workspace_bytes(int, int, int);
+int launch_conv_max_x3(const float*, long long, int, int, int, const float*, const float*, int,
+                       int, float*, int32_t*, void*, size_t, hipStream_t);
+int launch_cmx_bwd(const float*, const float*, const int32_t*, const float*, long long, int, int,
+                   int, int, const float*, float*, float*, float*, long long, hipStream_t);
+size_t row_ce_workspace_bytes(int);
+int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
+                  size_t, hipStream_t);
 
 // ---- workspace carve for the fused step ------------------------------------
 struct StepWs {
@@ -367,6 +386,67 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
   PC_TRY(launch_adam2(param, grad, exp_avg, exp_avg_sq, n, lr, nullptr, nullptr, nullptr, nullptr,
                       0, 0.f, step_count, 1, beta1, beta2, eps, stream));
   return launch_inc(step_count, stream);
+}
+
+// ---- dense point-wise GEMM engine (segmentation net) -----------------------
+int pcadv_gemm(const float* a, int64_t lda, int ta, const float* amask, int64_t ldm,
+               const float* b, int64_t ldb, int tb, float* c, int64_t ldc, int M, int N, int K,
+               const float* bias, const float* bias_rows, int rows_per_group, int relu,
+               int accumulate, int precise, hipStream_t stream) {
+  return launch_gemm(a, lda, ta, amask, ldm, b, ldb, tb, c, ldc, M, N, K, bias, bias_rows,
+                     rows_per_group, relu, accumulate, precise, stream);
+}
+
+size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin) {
+  return gemm_wgrad_workspace_bytes(rows, O, Kin);
+}
+
+int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* ymask, int64_t ldm,
+                     const float* x, int64_t ldx, int rows, int O, int Kin, float* dw, int64_t ldo,
+                     int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  return launch_gemm_wgrad(dz, ldz, ymask, ldm, x, ldx, rows, O, Kin, dw, ldo, accumulate,
+                           workspace, workspace_bytes, stream);
+}
+
+size_t pcadv_colsum_workspace_bytes(int M, int N) { return colsum_workspace_bytes(M, N); }
+
+int pcadv_colsum(const float* x, const float* ymask, int64_t ld, int64_t ldm, int M, int N,
+                 float* out, int accumulate, void* workspace, size_t workspace_bytes,
+                 hipStream_t stream) {
+  return launch_colsum(x, ymask, ld, ldm, M, N, out, accumulate, workspace, workspace_bytes,
+                       stream);
+}
+
+int pcadv_group_colsum(const float* x, const float* ymask, int64_t ld, int64_t ldm, int M, int N,
+                       int rows_per_group, float* out, hipStream_t stream) {
+  return launch_group_colsum(x, ymask, ld, ldm, M, N, rows_per_group, out, stream);
+}
+
+size_t pcadv_conv_max_x3_workspace_bytes(int C, int Npts, int O) {
+  return conv_max_x3_workspace_bytes(C, Npts, O);
+}
+
+int pcadv_conv_max_x3(const float* x, int64_t ldx, int C, int Npts, int K, const float* w,
+                      const float* b, int O, int relu, float* gmax, int32_t* gidx,
+                      void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  return launch_conv_max_x3(x, ldx, C, Npts, K, w, b, O, relu, gmax, gidx, workspace,
+                            workspace_bytes, stream);
+}
+
+int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* gidx,
+                          const float* x, int64_t ldx, int C, int Npts, int O, int K,
+                          const float* w, float* dw, float* db, float* dx, int64_t lddx,
+                          hipStream_t stream) {
+  return launch_cmx_bwd(dgmax, gmax, gidx, x, ldx, C, Npts, O, K, w, dw, db, dx, lddx, stream);
+}
+
+size_t pcadv_row_ce_workspace_bytes(int M) { return row_ce_workspace_bytes(M); }
+
+int pcadv_row_ce(const float* logits, int64_t ld, const int64_t* labels, int M, int ncls,
+                 float scale, float* loss, float* dlogits, void* workspace,
+                 size_t workspace_bytes, hipStream_t stream) {
+  return launch_row_ce(logits, ld, labels, M, ncls, scale, loss, dlogits, workspace,
+                       workspace_bytes, stream);
 }
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N) { return carve(B, N, nullptr).total; }

@@ -1,0 +1,334 @@
+"""PointNetSeg on the pcadv dense point-wise GEMM engine (csrc/gemm.hip).
+
+Mirrors models/pointnet.py:261-317 of the reference: same class name,
+constructor argument, forward signature (x: B x N x 3, cls: B x 1 x 16) and
+return tuple (logits B x C x N, x_global B x 2048 x 1), same state_dict keys
+and shapes, so reference checkpoints load unchanged.  The training loop
+run_training_pointnet_seg (utils/trainer.py:310-400) is mirrored in
+trainer.py.
+
+Layout: activations are point-major rows (B*N rows).  conv1..conv5 write
+their outputs straight into the column blocks of one [B*N][960] buffer, which
+is both the next layer's input and the per-point part of fc1's 3024-wide
+input (pointnet.py:304-306: [x1..x5 | tile(x_global) | tile(cls)]).  The
+tiled parts are the same for every point of a cloud, so they are folded into
+a per-cloud bias of fc1 (a B-row GEMM) instead of being materialised.
+conv6 + ReLU + max over points never materialises the [B*N][2048] output: a
+screened GEMM keeps per-tile candidates and the winner is re-evaluated in f32.
+
+Numerics: the GEMMs multiply bf16 hi/lo splits of the f32 operands (three
+MFMA products, f32 accumulate; relative error <= ~1.2e-5 of sum|a b| per
+layer); tests/test_gpu_seg.py holds the tolerances.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import check, stream_ptr
+
+__all__ = ["PointNetSeg", "seg_cross_entropy"]
+
+_LOC = 960                       # x1..x5 widths 64 + 128 + 128 + 128 + 512
+_FWD_PRECISE = os.environ.get("PCADV_SEG_PRECISE", "0") == "1"  # diagnostics: six-product forward
+_OFF = [0, 64, 192, 320, 448, 960]
+_CONV = [(3, 64), (64, 128), (128, 128), (128, 128), (128, 512), (512, 2048)]
+
+
+def _p(t, off=0):
+    return ctypes.c_void_p(t.data_ptr() + 4 * off)
+
+
+def _ws(nbytes, dev):
+    return torch.empty(max(int(nbytes), 256), device=dev, dtype=torch.uint8)
+
+
+class _Engine:
+    """Thin, validated calls into the C ABI (every launch on the current stream)."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+
+    def gemm(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, amask=None, ldm=0, bias=None,
+             bias_rows=None, rows_per_group=0, relu=False, accumulate=False, precise=False,
+             a_off=0, b_off=0, c_off=0, m_off=0):
+        check(self.lib.pcadv_gemm(_p(a, a_off), lda, ta, None if amask is None else _p(amask, m_off),
+                                  ldm, _p(b, b_off), ldb, tb, _p(c, c_off), ldc, M, N, K,
+                                  None if bias is None else _p(bias),
+                                  None if bias_rows is None else _p(bias_rows), rows_per_group,
+                                  int(relu), int(accumulate), int(precise), stream_ptr()),
+              "pcadv_gemm")
+
+    def wgrad(self, dz, ldz, x, ldx, rows, O, K, dw, ldo, *, ymask=None, ldm=0, dz_off=0,
+              x_off=0, m_off=0, dw_off=0):
+        nb = self.lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K)
+        ws = _ws(nb, dz.device)
+        check(self.lib.pcadv_gemm_wgrad(_p(dz, dz_off), ldz,
+                                        None if ymask is None else _p(ymask, m_off), ldm,
+                                        _p(x, x_off), ldx, rows, O, K, _p(dw, dw_off), ldo, 0,
+                                        _p(ws), ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
+
+    def colsum(self, x, ld, M, N, out, *, ymask=None, ldm=0, x_off=0, m_off=0):
+        nb = self.lib.pcadv_colsum_workspace_bytes(M, N)
+        ws = _ws(nb, x.device)
+        check(self.lib.pcadv_colsum(_p(x, x_off), None if ymask is None else _p(ymask, m_off), ld,
+                                    ldm, M, N, _p(out), 0, _p(ws), ws.numel(), stream_ptr()),
+              "pcadv_colsum")
+
+    def group_colsum(self, x, ld, M, N, rows_per_group, out, *, ymask=None, ldm=0):
+        check(self.lib.pcadv_group_colsum(_p(x), None if ymask is None else _p(ymask), ld, ldm, M,
+                                          N, rows_per_group, _p(out), stream_ptr()),
+              "pcadv_group_colsum")
+
+
+_ENGINE = None
+
+
+def _engine():
+    global _ENGINE
+    if _ENGINE is None:
+        _ENGINE = _Engine()
+    return _ENGINE
+
+
+def _wmat(w):
+    return w.reshape(w.shape[0], -1)
+
+
+def _check_dev(t, name, shape=None, dtype=torch.float32):
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: pcadv ops run on the HIP device only (got {t.device})")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+
+
+def seg_forward(pts, cls, params):
+    """PointNetSeg forward (pointnet.py:282-317) on the engine.  Returns a dict
+    with logits (B*N, C) point-major, gmax (B, 2048), gidx (B, 2048) and every
+    activation the backward needs."""
+    E = _engine()
+    B, N, _ = pts.shape
+    M = B * N
+    dev = pts.device
+    pts = pts.contiguous()
+    cvec = cls.reshape(B, -1).contiguous()
+    W = [_wmat(params[2 * i]).contiguous() for i in range(6)]
+    bc = [params[2 * i + 1].contiguous() for i in range(6)]
+    Wf = [params[12 + 2 * i].contiguous() for i in range(4)]
+    bf = [params[13 + 2 * i].contiguous() for i in range(4)]
+    ncls = Wf[3].shape[0]
+    xloc = torch.empty(M, _LOC, device=dev)
+    # conv1..conv5 + ReLU into the column blocks of xloc
+    src, ld, off = pts, 3, 0
+    for i in range(5):
+        K, O = _CONV[i]
+        E.gemm(src, ld, W[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True, a_off=off,
+               c_off=_OFF[i], precise=_FWD_PRECISE)
+        src, ld, off = xloc, _LOC, _OFF[i]
+    # conv6 + ReLU + max over the points of each cloud
+    gmax = torch.empty(B, 2048, device=dev)
+    gidx = torch.empty(B, 2048, device=dev, dtype=torch.int32)
+    nb = E.lib.pcadv_conv_max_x3_workspace_bytes(B, N, 2048)
+    ws = _ws(nb, dev)
+    check(E.lib.pcadv_conv_max_x3(_p(xloc, _OFF[4]), _LOC, B, N, 512, _p(W[5]), _p(bc[5]),
+                                  2048, 1, _p(gmax), _p(gidx), _p(ws), ws.numel(),
+                                  stream_ptr()), "pcadv_conv_max_x3")
+    # fc1: per-cloud bias from the tiled global feature and class vector
+    W1 = Wf[0]
+    cb = torch.empty(B, 256, device=dev)
+    E.gemm(gmax, 2048, W1, 3024, cb, 256, B, 256, 2048, bias=bf[0], b_off=960,
+           precise=_FWD_PRECISE)
+    E.gemm(cvec, cvec.shape[1], W1, 3024, cb, 256, B, 256, cvec.shape[1], b_off=3008,
+           accumulate=True)
+    h1 = torch.empty(M, 256, device=dev)
+    E.gemm(xloc, _LOC, W1, 3024, h1, 256, M, 256, _LOC, bias_rows=cb, rows_per_group=N,
+           relu=True, precise=_FWD_PRECISE)
+    h2 = torch.empty(M, 256, device=dev)
+    E.gemm(h1, 256, Wf[1], 256, h2, 256, M, 256, 256, bias=bf[1], relu=True,
+           precise=_FWD_PRECISE)
+    h3 = torch.empty(M, 128, device=dev)
+    E.gemm(h2, 256, Wf[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True,
+           precise=_FWD_PRECISE)
+    logits = torch.empty(M, ncls, device=dev)
+    E.gemm(h3, 128, Wf[3], 128, logits, ncls, M, ncls, 128, bias=bf[3], precise=_FWD_PRECISE)
+    return dict(pts=pts, cvec=cvec, xloc=xloc, gmax=gmax, gidx=gidx, h1=h1, h2=h2, h3=h3, W=W,
+                Wf=Wf, logits=logits, dims=(B, N, ncls))
+
+
+def seg_backward(fw, dlogits, dgmax_out=None):
+    """Gradients of the 20 parameters (state_dict order) given dL/dlogits
+    (B*N, C) (and optionally dL/dgmax), from the activations of seg_forward."""
+    E = _engine()
+    pts, cvec, xloc, gmax, gidx = fw["pts"], fw["cvec"], fw["xloc"], fw["gmax"], fw["gidx"]
+    h1, h2, h3, W, Wf = fw["h1"], fw["h2"], fw["h3"], fw["W"], fw["Wf"]
+    B, N, ncls = fw["dims"]
+    M = B * N
+    dev = xloc.device
+    dl = torch.zeros(M, ncls, device=dev) if dlogits is None else dlogits.reshape(M, ncls).contiguous()
+    g = {}
+    # ---- fc4 .. fc2 (dz = dy relu'(y) is applied as A is staged) ---------
+    dW4 = torch.empty_like(Wf[3]); db4 = torch.empty(ncls, device=dev)
+    E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128)
+    E.colsum(dl, ncls, M, ncls, db4)
+    dh3 = torch.empty(M, 128, device=dev)
+    E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, precise=True)
+    dW3 = torch.empty_like(Wf[2]); db3 = torch.empty(128, device=dev)
+    E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, ymask=h3, ldm=128)
+    E.colsum(dh3, 128, M, 128, db3, ymask=h3, ldm=128)
+    dh2 = torch.empty(M, 256, device=dev)
+    E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, amask=h3, ldm=128, precise=True)
+    dW2 = torch.empty_like(Wf[1]); db2 = torch.empty(256, device=dev)
+    E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, ymask=h2, ldm=256)
+    E.colsum(dh2, 256, M, 256, db2, ymask=h2, ldm=256)
+    dh1 = torch.empty(M, 256, device=dev)
+    E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, amask=h2, ldm=256, precise=True)
+    # ---- fc1: local columns, then the per-cloud (tiled) columns ----------
+    W1 = Wf[0]
+    dW1 = torch.empty_like(W1)
+    E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, ymask=h1, ldm=256)
+    s1 = torch.empty(B, 256, device=dev)  # per-cloud sums of dz1
+    E.group_colsum(dh1, 256, M, 256, N, s1, ymask=h1, ldm=256)
+    E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960)
+    E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008)
+    db1 = torch.empty(256, device=dev)
+    E.colsum(s1, 256, B, 256, db1)
+    dloc = torch.empty(M, _LOC, device=dev)
+    E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, amask=h1, ldm=256, precise=True)
+    dg = torch.empty(B, 2048, device=dev)
+    E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=True)
+    if dgmax_out is not None:
+        dg += dgmax_out.reshape(B, 2048)
+    # ---- conv6 + ReLU + max: the gradient reaches the argmax points -------
+    dW6 = torch.empty_like(W[5]); db6 = torch.empty(2048, device=dev)
+    check(E.lib.pcadv_conv_max_x3_bwd(_p(dg), _p(gmax), _p(gidx), _p(xloc, _OFF[4]), _LOC, B,
+                                      N, 2048, 512, _p(W[5]), _p(dW6), _p(db6),
+                                      _p(dloc, _OFF[4]), _LOC, stream_ptr()),
+          "pcadv_conv_max_x3_bwd")
+    # ---- conv5 .. conv1 (each layer's output gradient also carries fc1's) --
+    dWc = [None] * 6
+    dbc = [None] * 6
+    dWc[5], dbc[5] = dW6, db6
+    for i in range(4, -1, -1):
+        K, O = _CONV[i]
+        dWc[i] = torch.empty_like(W[i])
+        dbc[i] = torch.empty(O, device=dev)
+        if i > 0:
+            E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, ymask=xloc, ldm=_LOC,
+                    dz_off=_OFF[i], m_off=_OFF[i], x_off=_OFF[i - 1])
+        else:
+            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, ymask=xloc, ldm=_LOC,
+                    dz_off=_OFF[i], m_off=_OFF[i])
+        E.colsum(dloc, _LOC, M, O, dbc[i], ymask=xloc, ldm=_LOC, x_off=_OFF[i], m_off=_OFF[i])
+        if i > 0:
+            E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, amask=xloc, ldm=_LOC,
+                   accumulate=True, precise=True, a_off=_OFF[i], m_off=_OFF[i],
+                   c_off=_OFF[i - 1])
+    grads = []
+    for i in range(6):
+        grads += [dWc[i].view(O_shape(i)), dbc[i]]
+    grads += [dW1, db1, dW2, db2, dW3, db3, dW4, db4]
+    return grads
+
+
+class SegNetFunction(torch.autograd.Function):
+    """PointNetSeg forward and its whole backward as one autograd node.
+
+    Inputs: pts (B, N, 3), cls (B, 1, 16), then the 20 parameters in state_dict
+    order.  Outputs: logits point-major (B, N, C), gmax (B, 2048), gidx (B, 2048)
+    int32 (argmax over points, non-differentiable)."""
+
+    @staticmethod
+    def forward(ctx, pts, cls, *params):
+        fw = seg_forward(pts, cls, params)
+        ctx.save_for_backward(fw["pts"], fw["cvec"], fw["xloc"], fw["gmax"], fw["gidx"], fw["h1"],
+                              fw["h2"], fw["h3"], *fw["W"], *fw["Wf"])
+        ctx.dims = fw["dims"]
+        ctx.mark_non_differentiable(fw["gidx"])
+        B, N, ncls = fw["dims"]
+        return fw["logits"].view(B, N, ncls), fw["gmax"], fw["gidx"]
+
+    @staticmethod
+    def backward(ctx, dlogits, dgmax_out, _dgidx):
+        t = ctx.saved_tensors
+        fw = dict(pts=t[0], cvec=t[1], xloc=t[2], gmax=t[3], gidx=t[4], h1=t[5], h2=t[6], h3=t[7],
+                  W=list(t[8:14]), Wf=list(t[14:18]), dims=ctx.dims)
+        B, N, ncls = ctx.dims
+        dl = None if dlogits is None else dlogits.reshape(B * N, ncls)
+        return (None, None, *seg_backward(fw, dl, dgmax_out))
+
+
+def O_shape(i):
+    K, O = _CONV[i]
+    return (O, K, 1)
+
+
+def seg_cross_entropy(logits_pm, seg, scale=1.0):
+    """CrossEntropyLoss()(pred (B, C, N), seg (B, N)) for point-major logits
+    (B, N, C): the mean over all points (pointnet/train_pointnet_seg.py:152,
+    utils/trainer.py:344), on the device."""
+    return _RowCE.apply(logits_pm, seg, float(scale))
+
+
+class _RowCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits_pm, seg, scale):
+        lib = _lib.load()
+        B, N, C = logits_pm.shape
+        M = B * N
+        lg = logits_pm.reshape(M, C).contiguous()
+        _check_dev(lg, "logits")
+        lab = seg.reshape(M).to(torch.int64).contiguous()
+        _check_dev(lab, "seg", dtype=torch.int64)
+        loss = torch.empty((), device=lg.device)
+        d = torch.empty_like(lg)
+        ws = _ws(lib.pcadv_row_ce_workspace_bytes(M), lg.device)
+        check(lib.pcadv_row_ce(_p(lg), C, _p(lab), M, C, 1.0, _p(loss), _p(d), _p(ws), ws.numel(),
+                               stream_ptr()), "pcadv_row_ce")
+        ctx.save_for_backward(d)
+        ctx.shape = (B, N, C)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        (d,) = ctx.saved_tensors
+        return (d * gl).view(ctx.shape), None, None
+
+
+class PointNetSeg(nn.Module):
+    """models/pointnet.py:261-317.  forward(x: B x N x 3, cls: B x 1 x 16) ->
+    (logits B x NUM_SEG_CLASSES x N, x_global B x 2048 x 1)."""
+
+    def __init__(self, NUM_SEG_CLASSES):
+        super().__init__()
+        self.output_dim = NUM_SEG_CLASSES
+        self.conv1 = nn.Conv1d(3, 64, 1)
+        self.conv2 = nn.Conv1d(64, 128, 1)
+        self.conv3 = nn.Conv1d(128, 128, 1)
+        self.conv4 = nn.Conv1d(128, 128, 1)
+        self.conv5 = nn.Conv1d(128, 512, 1)
+        self.conv6 = nn.Conv1d(512, 2048, 1)
+        self.fc1 = nn.Linear(3024, 256)
+        self.fc2 = nn.Linear(256, 256)
+        self.fc3 = nn.Linear(256, 128)
+        self.fc4 = nn.Linear(128, self.output_dim)
+
+    def forward_points(self, x, cls):
+        """Point-major logits (B, N, C), x_global (B, 2048), argmax (B, 2048)."""
+        B, N, c3 = x.shape
+        if c3 != 3:
+            raise ValueError(f"x: expected B x N x 3, got {tuple(x.shape)}")
+        if cls.numel() != B * 16:
+            raise ValueError(f"cls: expected B x 1 x 16, got {tuple(cls.shape)}")
+        _check_dev(x, "x")
+        params = [p for _, p in self.named_parameters()]
+        return SegNetFunction.apply(x.float().contiguous(), cls.float().reshape(B, 1, 16), *params)
+
+    def forward(self, x, cls):
+        logits, g, _ = self.forward_points(x, cls)
+        return logits.permute(0, 2, 1), g.unsqueeze(2)

@@ -23,6 +23,11 @@
  *   pcadv_adam                       <- torch.optim.Adam step
  *                                       (train_classification.py:110-122,
  *                                        utils/trainer.py:558-559)
+ *   pcadv_gemm / _gemm_wgrad / _colsum / _conv_max_x3 / _row_ce
+ *                                    <- PointNetSeg.forward + autograd + the
+ *                                       per-point CrossEntropyLoss
+ *                                       (models/pointnet.py:261-317,
+ *                                        utils/trainer.py:310-400)
  *   pcadv_adv_step                   <- one iteration of utils/trainer.py:run_training
  *                                       (:426-559) incl. the losses of
  *                                       train_classification.py:199-200 and
@@ -184,6 +189,64 @@ int pcadv_linear_bwd(const float* dy, const float* y, int act,
                      float drop_p, const float* x, const float* w,
                      float* dx, float* dw, float* db, int M, int m_w, int Nout, int K,
                      hipStream_t stream);
+
+/* ---- dense point-wise GEMM engine: the segmentation net ---------------------
+ * (PointNetSeg, models/pointnet.py:261-317; run_training_pointnet_seg,
+ * utils/trainer.py:310-400.)  Rows are points (point-major [B*N][C]); f32
+ * operands are split to bf16 hi + lo and multiplied as three bf16 MFMA products
+ * with f32 accumulation (relative error <= ~1.2e-5 of sum|a b|).
+ *
+ * pcadv_gemm: C[m][n] (+)= sum_k A[m][k] B[n][k] (+ bias[n] + bias_rows[m /
+ * rows_per_group][n]), ReLU optional.  A[m][k] = a[m*lda + k] (ta = 0) or
+ * a[k*lda + m] (ta = 1, only with tb = 1); B[n][k] = b[n*ldb + k] (tb = 0: a
+ * weight [out][in], the forward) or b[k*ldb + n] (tb = 1: dX = dZ W).  amask
+ * (nullable, stored like A with stride ldm) zeroes A where amask <= 0 (relu'
+ * of a layer output).  accumulate = 1 adds into C.  precise = 1 multiplies six
+ * products of hi/mid/lo splits instead (f32-level accuracy; the gradients). */
+int pcadv_gemm(const float* a, int64_t lda, int ta, const float* amask, int64_t ldm,
+               const float* b, int64_t ldb, int tb, float* c, int64_t ldc, int M, int N, int K,
+               const float* bias, const float* bias_rows, int rows_per_group, int relu,
+               int accumulate, int precise, hipStream_t stream);
+
+/* Weight gradient dw[o][k] (row stride ldo) (+)= sum over `rows` points of
+ * dz[p][o] [ymask[p][o] > 0] x[p][k]: six-product (f32-level) GEMM over
+ * fixed-order slabs of the point axis. */
+size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin);
+int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* ymask, int64_t ldm,
+                     const float* x, int64_t ldx, int rows, int O, int Kin, float* dw, int64_t ldo,
+                     int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* Column sums (bias gradients): out[n] (+)= sum_m x[m][n] [ymask[m][n] > 0];
+ * pcadv_group_colsum writes one row of sums per rows_per_group rows. */
+size_t pcadv_colsum_workspace_bytes(int M, int N);
+int pcadv_colsum(const float* x, const float* ymask, int64_t ld, int64_t ldm, int M, int N,
+                 float* out, int accumulate, void* workspace, size_t workspace_bytes,
+                 hipStream_t stream);
+int pcadv_group_colsum(const float* x, const float* ymask, int64_t ld, int64_t ldm, int M, int N,
+                       int rows_per_group, float* out, hipStream_t stream);
+
+/* conv + (ReLU) + max over the Npts points of each of C clouds (conv6 + the
+ * global max, pointnet.py:301-303): gmax [C][O], gidx [C][O] (first index on
+ * ties of the f32 values; with relu the pooled value is relu(max)).  A screened
+ * GEMM keeps per-128-point-tile top-2 candidates; the winner (and the
+ * runner-up on near-ties) is re-evaluated as an f32 dot product of x and w. */
+size_t pcadv_conv_max_x3_workspace_bytes(int C, int Npts, int O);
+int pcadv_conv_max_x3(const float* x, int64_t ldx, int C, int Npts, int K, const float* w,
+                      const float* b, int O, int relu, float* gmax, int32_t* gidx,
+                      void* workspace, size_t workspace_bytes, hipStream_t stream);
+/* Its backward: g' = dgmax [gmax > 0]; dw [O][K] and db [O] overwritten
+ * (nullable), dx rows (stride lddx, nullable) accumulated: deterministic. */
+int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* gidx,
+                          const float* x, int64_t ldx, int C, int Npts, int O, int K,
+                          const float* w, float* dw, float* db, float* dx, int64_t lddx,
+                          hipStream_t stream);
+
+/* CrossEntropyLoss over rows (the per-point segmentation loss, mean over M
+ * points): *loss, and dlogits = scale * dL/dlogits (same stride ld). */
+size_t pcadv_row_ce_workspace_bytes(int M);
+int pcadv_row_ce(const float* logits, int64_t ld, const int64_t* labels, int M, int ncls,
+                 float scale, float* loss, float* dlogits, void* workspace,
+                 size_t workspace_bytes, hipStream_t stream);
 
 /* ---- Adam (torch.optim.Adam semantics, amsgrad=False, weight_decay=0) ------
  * step_count: device int32, incremented by this call (t = *step_count + 1). */

@@ -56,8 +56,13 @@ def test_workspace_sizes():
     lib = _lib.load()
     # x3 (C*N*128 f32) is the only per-point activation the step keeps
     assert lib.pcadv_adv_step_workspace_bytes(32, 1024) > 64 * 1024 * 128 * 4
-    # per-tile top-2 partials + conv4 weights split into bf16 hi / lo
-    assert lib.pcadv_feat_fwd_workspace_bytes(64, 1024) == 64 * 8 * 1024 * 8 + 2 * 1024 * 128 * 2
+    # the two-kernel forward keeps its screening state in registers: no scratch
+    assert lib.pcadv_feat_fwd_workspace_bytes(64, 1024) == 256
+    # segmentation engine: point-axis slabs of the weight gradient (32 x O x K),
+    # per-128-point-tile top-2 keys of conv6 + max, CE partials
+    assert lib.pcadv_gemm_wgrad_workspace_bytes(32768, 2048, 512) == 32 * 2048 * 512 * 4 + 256
+    assert lib.pcadv_conv_max_x3_workspace_bytes(16, 2048, 2048) == 16 * 16 * 2048 * 8 + 256
+    assert lib.pcadv_row_ce_workspace_bytes(32768) == 128 * 4 + 256
     assert lib.pcadv_feat_bwd_workspace_bytes(64, 1024) == 64 * 8 * 12736 * 4
 
 

@@ -1,0 +1,314 @@
+"""Segmentation path (BASELINE configs[3]): the dense point-wise
+GEMM engine (csrc/gemm.hip) through its C ABI, and PointNetSeg on top of it,
+against float64 torch references, the numpy oracle and the reference goldens
+g6 (forward) / g8 (training step).  Runs on an MI355X only.
+
+Tolerances: the forward GEMMs multiply bf16 hi/lo splits (three MFMA
+products, f32 accumulate), bounded by 2e-5 * (|A| |B|^T) elementwise; the
+gradient GEMMs six products of hi/mid/lo splits (f32-level).  The forward
+outputs (logits, x_global) are held to the north_star's 1e-3 (they agree to
+~5e-6).  The backward is held to 1e-4 elementwise against the oracle's
+backward evaluated on this forward's own activations and ReLU masks.  End to
+end, gradients are compared in relative L2 (1e-2): any two f32 implementations
+of a ReLU net route a whole gradient element differently where a
+pre-activation lies within rounding of 0 (the oracle and the fp64 reference
+agree to 1e-6 only because numpy's f32 rounding flips almost none of them)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pointnet_np as onp
+from golden_util import check_tensor_l2, check_tensor_rel, load
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from adversarial_learning_on_pointclouds_amd import _lib
+    from adversarial_learning_on_pointclouds_amd._lib import check, stream_ptr
+    from adversarial_learning_on_pointclouds_amd.seg import (PointNetSeg, seg_backward,
+                                                             seg_cross_entropy, seg_forward)
+
+DEV = "cuda"
+
+
+def _p(t, off=0):
+    return ctypes.c_void_p(t.data_ptr() + 4 * off)
+
+
+def _t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def _bound(A, B):
+    return 2e-5 * (np.abs(A) @ np.abs(B).T) + 1e-30
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 50, 70), (128, 128, 32), (1000, 256, 960), (7, 2048, 3)])
+def test_gemm_forward_vs_fp64(M, N, K):
+    lib = _lib.load()
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((N, K)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    br = rng.standard_normal((2, N)).astype(np.float32)
+    C = torch.empty(M, N, device=DEV)
+    rpg = (M + 1) // 2
+    tA, tW, tb, tbr = _t(A), _t(W), _t(b), _t(br)  # alive across the launch
+    check(lib.pcadv_gemm(_p(tA), K, 0, None, 0, _p(tW), K, 0, _p(C), N, M, N, K, _p(tb), _p(tbr),
+                         rpg, 1, 0, 0, stream_ptr()), "gemm")
+    ref = A.astype(np.float64) @ W.astype(np.float64).T + b + br[np.arange(M) // rpg]
+    ref = np.maximum(ref, 0)
+    assert (np.abs(C.cpu().numpy() - ref) <= _bound(A, W) + 1e-6).all()
+
+
+def test_gemm_data_grad_masked_accumulate():
+    """dX (+)= (dY * [Y > 0]) W with a strided, offset output (the seg backward's form)."""
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    M, O, K = 517, 128, 64
+    dY = rng.standard_normal((M, O)).astype(np.float32)
+    Y = rng.standard_normal((M, O)).astype(np.float32)
+    W = rng.standard_normal((O, K)).astype(np.float32)
+    base = rng.standard_normal((M, 200)).astype(np.float32)
+    out = _t(base)
+    tdY, tY, tW = _t(dY), _t(Y), _t(W)
+    check(lib.pcadv_gemm(_p(tdY), O, 0, _p(tY), O, _p(tW), K, 1, _p(out, 64), 200, M, K, O,
+                         None, None, 0, 0, 1, 1, stream_ptr()), "gemm")
+    dz = dY * (Y > 0)
+    ref = base.astype(np.float64).copy()
+    ref[:, 64:128] += dz.astype(np.float64) @ W.astype(np.float64)
+    got = out.cpu().numpy()
+    # six-product (precise) form: f32-level, 1e-6 of sum|a b|
+    assert (np.abs(got[:, 64:128] - ref[:, 64:128]) <= _bound(dz, W.T) / 20 + 1e-5).all()
+    assert np.array_equal(got[:, :64], base[:, :64]) and np.array_equal(got[:, 128:], base[:, 128:])
+
+
+@pytest.mark.parametrize("rows", [300, 32768])
+def test_gemm_weight_grad(rows):
+    lib = _lib.load()
+    rng = np.random.default_rng(rows)
+    O, K = 96, 40
+    dZ = rng.standard_normal((rows, O)).astype(np.float32)
+    Y = rng.standard_normal((rows, O)).astype(np.float32)
+    X = rng.standard_normal((rows, K)).astype(np.float32)
+    dW = torch.empty(O, K, device=DEV)
+    nb = lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K)
+    ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+    tdZ, tY, tX = _t(dZ), _t(Y), _t(X)
+    check(lib.pcadv_gemm_wgrad(_p(tdZ), O, _p(tY), O, _p(tX), K, rows, O, K, _p(dW), K, 0,
+                               _p(ws), nb, stream_ptr()), "wgrad")
+    dz = dZ * (Y > 0)
+    ref = dz.T.astype(np.float64) @ X.astype(np.float64)
+    assert (np.abs(dW.cpu().numpy() - ref) <= _bound(dz.T, X.T) / 20 + 1e-5).all()
+    a = dW.clone()
+    check(lib.pcadv_gemm_wgrad(_p(tdZ), O, _p(tY), O, _p(tX), K, rows, O, K, _p(dW), K, 0,
+                               _p(ws), nb, stream_ptr()), "wgrad")
+    assert torch.equal(a, dW)  # fixed-order slabs: bitwise reproducible
+
+
+def test_colsum_and_group_colsum():
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    M, N = 4096, 77
+    X = rng.standard_normal((M, N)).astype(np.float32)
+    Y = rng.standard_normal((M, N)).astype(np.float32)
+    out = torch.empty(N, device=DEV)
+    nb = lib.pcadv_colsum_workspace_bytes(M, N)
+    ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+    tX, tY = _t(X), _t(Y)
+    check(lib.pcadv_colsum(_p(tX), _p(tY), N, N, M, N, _p(out), 0, _p(ws), nb, stream_ptr()),
+          "colsum")
+    ref = (X * (Y > 0)).astype(np.float64).sum(0)
+    assert np.abs(out.cpu().numpy() - ref).max() < 1e-3
+    g = torch.empty(4, N, device=DEV)
+    check(lib.pcadv_group_colsum(_p(tX), None, N, N, M, N, 1024, _p(g), stream_ptr()), "gcs")
+    ref = X.astype(np.float64).reshape(4, 1024, N).sum(1)
+    assert np.abs(g.cpu().numpy() - ref).max() < 1e-3
+
+
+def _cmx(x, w, b, relu=True):
+    lib = _lib.load()
+    C, N, K = x.shape
+    O = w.shape[0]
+    gmax = torch.empty(C, O, device=DEV)
+    gidx = torch.empty(C, O, device=DEV, dtype=torch.int32)
+    nb = lib.pcadv_conv_max_x3_workspace_bytes(C, N, O)
+    ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+    xt = _t(x.reshape(C * N, K))
+    tw, tb = _t(w), _t(b)
+    check(lib.pcadv_conv_max_x3(_p(xt), K, C, N, K, _p(tw), _p(tb), O, int(relu), _p(gmax),
+                                _p(gidx), _p(ws), nb, stream_ptr()), "conv_max_x3")
+    torch.cuda.synchronize()
+    return gmax.cpu().numpy(), gidx.cpu().numpy(), xt
+
+
+@pytest.mark.parametrize("C,N", [(2, 2048), (3, 300), (1, 97)])
+def test_conv_max_x3_vs_oracle(C, N):
+    rng = np.random.default_rng(C * N)
+    x = np.maximum(rng.standard_normal((C, N, 512)), 0).astype(np.float32)
+    w = (rng.standard_normal((2048, 512)) / 22.6).astype(np.float32)
+    b = (rng.standard_normal(2048) * 0.05).astype(np.float32)
+    gm, gi, _ = _cmx(x, w, b)
+    z = x.astype(np.float64) @ w.T.astype(np.float64) + b          # (C, N, O)
+    ref_val = np.maximum(z.max(1), 0)
+    assert np.abs(gm - ref_val).max() <= 1e-5 * max(1.0, np.abs(ref_val).max())
+    am = z.argmax(1)
+    pos = ref_val > 0
+    bad = (gi != am) & pos
+    for c, o in np.argwhere(bad):  # only at near-ties of the f64 values
+        assert abs(z[c, gi[c, o], o] - z[c, am[c, o], o]) <= 1e-5 * max(1.0, abs(z[c, am[c, o], o]))
+
+
+def test_conv_max_x3_backward_vs_numpy():
+    lib = _lib.load()
+    rng = np.random.default_rng(9)
+    C, N, K, O = 2, 300, 512, 2048
+    x = np.maximum(rng.standard_normal((C, N, K)), 0).astype(np.float32)
+    w = (rng.standard_normal((O, K)) / 22.6).astype(np.float32)
+    b = (rng.standard_normal(O) * 0.05).astype(np.float32)
+    gm, gi, xt = _cmx(x, w, b)
+    dg = rng.standard_normal((C, O)).astype(np.float32)
+    dw = torch.empty(O, K, device=DEV)
+    db = torch.empty(O, device=DEV)
+    base = rng.standard_normal((C * N, K)).astype(np.float32)
+    dx = _t(base)
+    tdg, tgm, tgi, tw = _t(dg), _t(gm), _t(gi, torch.int32), _t(w)
+    check(lib.pcadv_conv_max_x3_bwd(_p(tdg), _p(tgm), _p(tgi), _p(xt), K, C, N, O, K, _p(tw),
+                                    _p(dw), _p(db), _p(dx), K, stream_ptr()), "cmx_bwd")
+    gp = dg * (gm > 0)
+    rdw = np.zeros((O, K))
+    rdx = base.astype(np.float64).reshape(C, N, K).copy()
+    for c in range(C):
+        rdw += gp[c][:, None] * x[c, gi[c]]
+        np.add.at(rdx[c], gi[c], gp[c][:, None] * w)
+    assert np.abs(dw.cpu().numpy() - rdw).max() <= 1e-5 * np.abs(rdw).max()
+    assert np.abs(db.cpu().numpy() - gp.sum(0)).max() <= 1e-5 * np.abs(gp).sum(0).max()
+    assert np.abs(dx.cpu().numpy().reshape(C, N, K) - rdx).max() <= 1e-5 * np.abs(rdx).max()
+
+
+def test_row_ce_vs_oracle():
+    rng = np.random.default_rng(11)
+    B, N, C = 3, 500, 50
+    lg = rng.standard_normal((B, N, C)).astype(np.float32) * 3
+    seg = rng.integers(0, C, (B, N))
+    t = _t(lg).requires_grad_(True)
+    loss = seg_cross_entropy(t, _t(seg, torch.int64))
+    loss.backward()
+    rl, rg = onp.seg_cross_entropy(lg, seg)
+    assert abs(loss.item() - rl) < 1e-5 * max(1, abs(rl))
+    assert np.abs(t.grad.cpu().numpy() - rg).max() <= 1e-6
+
+
+def _seg_model(S):
+    m = PointNetSeg(50)
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in S.items()})
+    return m.to(DEV)
+
+
+def test_seg_forward_golden_g6():
+    """PointNetSeg forward vs the reference capture (B=2, N=2048)."""
+    fx = load("g6_seg_fwd.npz")
+    S = onp.make_params(onp.seg_spec(50), seed=int(fx["s_seed"]))
+    pts = np.random.default_rng(int(fx["pts_seed"])).uniform(-1, 1, (2, 2048, 3)).astype(np.float32)
+    m = _seg_model(S)
+    with torch.no_grad():
+        out, g = m(_t(pts), _t(fx["cls"]))
+    check_tensor_rel(fx, "gmax", g.cpu().numpy()[:, :, 0], tol=1e-3)
+    check_tensor_rel(fx, "out", out.cpu().numpy(), tol=1e-3)
+
+
+def test_seg_step_golden_g8():
+    """run_training_pointnet_seg's step: loss, x_global and every gradient vs the
+    reference capture (B=2, N=512)."""
+    fx = load("g8_seg_step.npz")
+    S = onp.make_params(onp.seg_spec(50), seed=int(fx["s_seed"]))
+    B, N = fx["seg"].shape
+    pts = np.random.default_rng(int(fx["pts_seed"])).uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    m = _seg_model(S)
+    logits, g, _ = m.forward_points(_t(pts), _t(fx["cls"]))
+    loss = seg_cross_entropy(logits, _t(fx["seg"], torch.int64))
+    loss.backward()
+    assert abs(loss.item() - float(fx["loss"])) < 1e-4
+    check_tensor_rel(fx, "gmax", g.detach().cpu().numpy(), tol=1e-3)
+    check_tensor_rel(fx, "logits", logits.detach().cpu().numpy().transpose(0, 2, 1), tol=1e-3)
+    for name, p in m.named_parameters():
+        check_tensor_l2(fx, "grad." + name, p.grad.cpu().numpy(), tol=1e-2)
+
+
+def _oracle_cache(fw, pts, cls):
+    """The oracle's backward cache built from this forward's own activations."""
+    B, N, _ = fw["dims"]
+    loc = fw["xloc"].cpu().numpy().reshape(B, N, 960)
+    offs = [0, 64, 192, 320, 448, 960]
+    xs = [loc[:, :, offs[i]:offs[i + 1]] for i in range(5)] + [None]
+    return dict(pts=pts, xs=xs, am=fw["gidx"].cpu().numpy().astype(np.int64),
+                g=fw["gmax"].cpu().numpy(), loc=loc, cvec=cls.reshape(B, -1),
+                h1=fw["h1"].cpu().numpy().reshape(B, N, 256),
+                h2=fw["h2"].cpu().numpy().reshape(B, N, 256),
+                h3=fw["h3"].cpu().numpy().reshape(B, N, 128))
+
+
+@pytest.mark.parametrize("B,N", [(3, 700), (2, 2048)])
+def test_seg_backward_vs_oracle_same_masks(B, N):
+    """The backward (every parameter gradient) against the oracle's backward
+    evaluated on this forward's activations: 1e-4 of each tensor's max."""
+    S = onp.make_params(onp.seg_spec(50), seed=21 + N)
+    rng = np.random.default_rng(22 + N)
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    cls = np.zeros((B, 1, 16), np.float32)
+    cls[np.arange(B), 0, rng.integers(0, 16, B)] = 1
+    seg = rng.integers(0, 50, (B, N))
+    params = [_t(v) for v in S.values()]
+    with torch.no_grad():
+        fw = seg_forward(_t(pts), _t(cls), params)
+        logits = fw["logits"].cpu().numpy().reshape(B, N, 50)
+        _, dout = onp.seg_cross_entropy(logits, seg)
+        grads = seg_backward(fw, _t(dout.reshape(B * N, 50)))
+    ref = onp.seg_backward(S, _oracle_cache(fw, pts, cls), dout)
+    for (name, r), g in zip(ref.items(), grads):
+        e = np.abs(g.cpu().numpy().reshape(r.shape) - r).max() / max(np.abs(r).max(), 1e-30)
+        assert e < 1e-4, (name, e)
+
+
+def test_seg_step_vs_oracle_ragged():
+    """B=3, N=700 (a ragged last tile) end to end vs the numpy oracle."""
+    S = onp.make_params(onp.seg_spec(50), seed=21)
+    rng = np.random.default_rng(22)
+    B, N = 3, 700
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    cls = np.zeros((B, 1, 16), np.float32)
+    cls[np.arange(B), 0, rng.integers(0, 16, B)] = 1
+    seg = rng.integers(0, 50, (B, N))
+    m = _seg_model(S)
+    logits, g, gi = m.forward_points(_t(pts), _t(cls))
+    loss = seg_cross_entropy(logits, _t(seg, torch.int64))
+    loss.backward()
+    rl, grads, rlog, rg, ram = onp.seg_step(S, pts, cls, seg)
+    assert abs(loss.item() - rl) < 1e-4
+    e = np.abs(logits.detach().cpu().numpy() - rlog).max() / np.abs(rlog).max()
+    assert e < 1e-3, e
+    e = np.abs(g.detach().cpu().numpy() - rg).max() / np.abs(rg).max()
+    assert e < 1e-3, e
+    gi = gi.cpu().numpy()
+    assert ((gi == ram) | (rg <= 0)).all()  # argmax of every positive pooled channel
+    for name, p in m.named_parameters():
+        a, r = p.grad.cpu().numpy(), grads[name]
+        e = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
+        assert e < 1e-2, (name, e)
+
+
+def test_seg_deterministic():
+    S = onp.make_params(onp.seg_spec(50), seed=23)
+    rng = np.random.default_rng(24)
+    pts = _t(rng.uniform(-1, 1, (2, 1024, 3)).astype(np.float32))
+    cls = _t(np.eye(16, dtype=np.float32)[[1, 5]].reshape(2, 1, 16))
+    seg = _t(rng.integers(0, 50, (2, 1024)), torch.int64)
+    out = []
+    for _ in range(2):
+        m = _seg_model(S)
+        lg, _, _ = m.forward_points(pts, cls)
+        seg_cross_entropy(lg, seg).backward()
+        out.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
+    assert torch.equal(out[0], out[1])
