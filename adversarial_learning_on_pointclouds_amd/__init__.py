@@ -5,14 +5,16 @@ Drop-in counterparts of the reference's models and training loop
 (models/pointnet.py), DeepConvDiscNet (models/discriminator.py), load_models
 (utils/model_utils.py), make_D_label (utils/utils.py), ImagePool
 (utils/image_pool.py), run_training / run_testing (utils/trainer.py), plus the
-fused native step AdvTrainStep.  All compute runs in libpcadv.so (C ABI in
+fused native step AdvTrainStep; PointNetSeg (models/pointnet.py:261-317) with
+its native training step SegTrainStep.  All compute runs in libpcadv.so (C ABI in
 include/pcadv.h); there is no CPU fallback.
 """
 from . import _lib
 from .discriminator import DeepConvDiscNet
 from .pointnet import PointNetCls, PointNetfeat, STN3d, STNkd, feature_transform_regularizer
+from .seg import PointNetSeg, SegTrainStep
 from .step import AdvTrainStep
 
 __all__ = ["PointNetCls", "PointNetfeat", "STN3d", "STNkd", "DeepConvDiscNet",
-           "feature_transform_regularizer", "AdvTrainStep"]
+           "feature_transform_regularizer", "AdvTrainStep", "PointNetSeg", "SegTrainStep"]
 __version__ = "0.1.0"

@@ -48,7 +48,8 @@ def init_weights(net, init_type, init_gain=1.0, verbose=True):
 
 
 def load_models(mode, device, args):
-    """utils/model_utils.py:60-140 for the hot path's modes 'cls' and 'disc'.
+    """utils/model_utils.py:60-140 for the hot path's modes 'cls' and 'disc' and
+    the segmentation row's 'seg'.
     The segmentation / stacked discriminators are outside this build's scope."""
     if mode == "cls":
         model = PointNetCls(k=40, feature_transform=False).to(device)
@@ -65,7 +66,15 @@ def load_models(mode, device, args):
     elif mode == "disc":
         model = DeepConvDiscNet(input_dim=args.disc_indim, output_dim=1)
         model = init_net(model, device, init_type=args.init_disc)
-    elif mode in ("seg", "seg_regu", "disc_seg", "disc_dual", "disc_stack"):
+    elif mode == "seg":  # :80-90, PointNetSeg
+        from .seg import PointNetSeg
+        model = PointNetSeg(NUM_SEG_CLASSES=50)
+        model = init_net(model, device, init_type=args.init_disc)
+        if getattr(args, "checkpoint", None):
+            print("Loading pretrained cls model ...")
+            model.load_state_dict(torch.load(args.checkpoint, map_location=device,
+                                             weights_only=True))
+    elif mode in ("seg_regu", "disc_seg", "disc_dual", "disc_stack"):
         raise NotImplementedError(f"mode {mode!r} is outside the adversarial cls hot path")
     else:
         raise ValueError("Invalid mode {}!".format(mode))

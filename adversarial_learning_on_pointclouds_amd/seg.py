@@ -31,7 +31,7 @@ import torch.nn as nn
 from . import _lib
 from ._lib import check, stream_ptr
 
-__all__ = ["PointNetSeg", "seg_cross_entropy"]
+__all__ = ["PointNetSeg", "SegTrainStep", "seg_cross_entropy", "seg_forward", "seg_backward"]
 
 _LOC = 960                       # x1..x5 widths 64 + 128 + 128 + 128 + 512
 _FWD_PRECISE = os.environ.get("PCADV_SEG_PRECISE", "0") == "1"  # diagnostics: six-product forward
@@ -161,9 +161,10 @@ def seg_forward(pts, cls, params):
                 Wf=Wf, logits=logits, dims=(B, N, ncls))
 
 
-def seg_backward(fw, dlogits, dgmax_out=None):
+def seg_backward(fw, dlogits, dgmax_out=None, out=None):
     """Gradients of the 20 parameters (state_dict order) given dL/dlogits
-    (B*N, C) (and optionally dL/dgmax), from the activations of seg_forward."""
+    (B*N, C) (and optionally dL/dgmax), from the activations of seg_forward.
+    `out`: optional list of 20 parameter-shaped tensors written in place."""
     E = _engine()
     pts, cvec, xloc, gmax, gidx = fw["pts"], fw["cvec"], fw["xloc"], fw["gmax"], fw["gidx"]
     h1, h2, h3, W, Wf = fw["h1"], fw["h2"], fw["h3"], fw["W"], fw["Wf"]
@@ -173,30 +174,34 @@ def seg_backward(fw, dlogits, dgmax_out=None):
     dl = torch.zeros(M, ncls, device=dev) if dlogits is None else dlogits.reshape(M, ncls).contiguous()
     g = {}
     # ---- fc4 .. fc2 (dz = dy relu'(y) is applied as A is staged) ---------
-    dW4 = torch.empty_like(Wf[3]); db4 = torch.empty(ncls, device=dev)
+    def _g(k, like):  # the k-th gradient (state_dict order): caller's buffer or a new one
+        if out is not None:
+            return out[k].view(like.shape) if hasattr(like, "shape") else out[k]
+        return torch.empty_like(like) if hasattr(like, "shape") else torch.empty(like, device=dev)
+    dW4 = _g(18, Wf[3]); db4 = _g(19, ncls)
     E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128)
     E.colsum(dl, ncls, M, ncls, db4)
     dh3 = torch.empty(M, 128, device=dev)
     E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, precise=True)
-    dW3 = torch.empty_like(Wf[2]); db3 = torch.empty(128, device=dev)
+    dW3 = _g(16, Wf[2]); db3 = _g(17, 128)
     E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, ymask=h3, ldm=128)
     E.colsum(dh3, 128, M, 128, db3, ymask=h3, ldm=128)
     dh2 = torch.empty(M, 256, device=dev)
     E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, amask=h3, ldm=128, precise=True)
-    dW2 = torch.empty_like(Wf[1]); db2 = torch.empty(256, device=dev)
+    dW2 = _g(14, Wf[1]); db2 = _g(15, 256)
     E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, ymask=h2, ldm=256)
     E.colsum(dh2, 256, M, 256, db2, ymask=h2, ldm=256)
     dh1 = torch.empty(M, 256, device=dev)
     E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, amask=h2, ldm=256, precise=True)
     # ---- fc1: local columns, then the per-cloud (tiled) columns ----------
     W1 = Wf[0]
-    dW1 = torch.empty_like(W1)
+    dW1 = _g(12, W1)
     E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, ymask=h1, ldm=256)
     s1 = torch.empty(B, 256, device=dev)  # per-cloud sums of dz1
     E.group_colsum(dh1, 256, M, 256, N, s1, ymask=h1, ldm=256)
     E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960)
     E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008)
-    db1 = torch.empty(256, device=dev)
+    db1 = _g(13, 256)
     E.colsum(s1, 256, B, 256, db1)
     dloc = torch.empty(M, _LOC, device=dev)
     E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, amask=h1, ldm=256, precise=True)
@@ -205,7 +210,7 @@ def seg_backward(fw, dlogits, dgmax_out=None):
     if dgmax_out is not None:
         dg += dgmax_out.reshape(B, 2048)
     # ---- conv6 + ReLU + max: the gradient reaches the argmax points -------
-    dW6 = torch.empty_like(W[5]); db6 = torch.empty(2048, device=dev)
+    dW6 = _g(10, W[5]); db6 = _g(11, 2048)
     check(E.lib.pcadv_conv_max_x3_bwd(_p(dg), _p(gmax), _p(gidx), _p(xloc, _OFF[4]), _LOC, B,
                                       N, 2048, 512, _p(W[5]), _p(dW6), _p(db6),
                                       _p(dloc, _OFF[4]), _LOC, stream_ptr()),
@@ -216,8 +221,8 @@ def seg_backward(fw, dlogits, dgmax_out=None):
     dWc[5], dbc[5] = dW6, db6
     for i in range(4, -1, -1):
         K, O = _CONV[i]
-        dWc[i] = torch.empty_like(W[i])
-        dbc[i] = torch.empty(O, device=dev)
+        dWc[i] = _g(2 * i, W[i])
+        dbc[i] = _g(2 * i + 1, O)
         if i > 0:
             E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, ymask=xloc, ldm=_LOC,
                     dz_off=_OFF[i], m_off=_OFF[i], x_off=_OFF[i - 1])
@@ -332,3 +337,102 @@ class PointNetSeg(nn.Module):
     def forward(self, x, cls):
         logits, g, _ = self.forward_points(x, cls)
         return logits.permute(0, 2, 1), g.unsqueeze(2)
+
+
+class SegTrainStep:
+    """One iteration of run_training_pointnet_seg (utils/trainer.py:334-349:
+    forward, CrossEntropyLoss over every point, (lambda_seg * l).backward(),
+    optimizer.step() with Adam) as native launches on one stream, capturable
+    into a HIP graph.
+
+    The model's parameters become views of one flat f32 buffer, their .grad
+    views of one flat gradient buffer (written in place by the backward), and
+    the Adam moments are flat too (handed to a torch Adam's state as views, so
+    optimizer.state_dict() stays meaningful); the update is one pcadv_adam
+    launch over the whole network."""
+
+    def __init__(self, model, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
+                 lambda_seg=1.0, device="cuda"):
+        self.lib = _lib.load()
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("SegTrainStep runs on the HIP device only")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device, self.model = dev, model
+        if optimizer is not None:
+            g = optimizer.param_groups[0]
+            lr, betas, eps = g["lr"], tuple(g["betas"]), g["eps"]
+        self.lr, self.betas, self.eps, self.lambda_seg = float(lr), betas, float(eps), float(lambda_seg)
+        named = list(model.named_parameters())
+        offs, n = [], 0
+        for _, p in named:
+            offs.append(n)
+            n += (p.numel() + 63) // 64 * 64  # 256-B aligned views
+        self.numel = n
+        self.param = torch.zeros(n, device=dev)
+        self.grad = torch.zeros(n, device=dev)
+        self.m = torch.zeros(n, device=dev)
+        self.v = torch.zeros(n, device=dev)
+        self.step_count = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.grad_views = []
+        for (name, p), o in zip(named, offs):
+            k = p.numel()
+            self.param[o:o + k].copy_(p.detach().reshape(-1))
+            p.data = self.param[o:o + k].view_as(p)
+            gv = self.grad[o:o + k].view_as(p)
+            p.grad = gv
+            self.grad_views.append(gv)
+            if optimizer is not None:
+                optimizer.state[p] = {"step": torch.zeros((), dtype=torch.float32),
+                                      "exp_avg": self.m[o:o + k].view_as(p),
+                                      "exp_avg_sq": self.v[o:o + k].view_as(p)}
+        self.params = [p for _, p in named]
+        self.optimizer = optimizer
+        self.loss = torch.zeros((), device=dev)
+        self.graph = None
+
+    def __call__(self, pts, cls, seg, apply_adam=True):
+        B, N, _ = pts.shape
+        _check_dev(pts, "pts")
+        if seg.shape != (B, N) or seg.dtype != torch.int64 or not seg.is_contiguous():
+            raise ValueError("seg: expected contiguous int64 (B, N)")
+        fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params)
+        M, ncls = B * N, fw["dims"][2]
+        d = torch.empty(M, ncls, device=self.device)
+        ws = _ws(self.lib.pcadv_row_ce_workspace_bytes(M), self.device)
+        check(self.lib.pcadv_row_ce(_p(fw["logits"]), ncls, _p(seg), M, ncls, self.lambda_seg,
+                                    _p(self.loss), _p(d), _p(ws), ws.numel(), stream_ptr()),
+              "pcadv_row_ce")
+        seg_backward(fw, d, None, out=self.grad_views)
+        if apply_adam:
+            self.adam()
+        return self.loss
+
+    def adam(self):
+        check(self.lib.pcadv_adam(_p(self.param), _p(self.grad), _p(self.m), _p(self.v), self.numel,
+                                  _p(self.step_count), self.lr, self.betas[0], self.betas[1],
+                                  self.eps, stream_ptr()), "pcadv_adam")
+
+    def capture_on(self, pts, cls, seg):
+        """A HIP graph of one step reading the given resident buffers (state is
+        restored to what it was before the warm-up)."""
+        saved = [t.clone() for t in (self.param, self.m, self.v, self.step_count)]
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(pts, cls, seg)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self(pts, cls, seg)
+        torch.cuda.synchronize()
+        for dst, src in zip((self.param, self.m, self.v, self.step_count), saved):
+            dst.copy_(src)
+        return g
+
+    def sync_optimizer_state(self):
+        t = float(self.step_count.item())
+        if self.optimizer is not None:
+            for st in self.optimizer.state.values():
+                st["step"] = torch.tensor(t)

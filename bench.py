@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--config", choices=["adv", "seg"], default="adv",
+                    help="adv: the headline adversarial cls step (default); seg: the "
+                         "PointNetSeg training step of BASELINE configs[3]")
     return ap.parse_args()
 
 
@@ -83,8 +86,65 @@ def cpu_baseline(seconds):
             "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N=1024, fp32) in {dt:.1f}s"}
 
 
+def bench_seg(args):
+    """BASELINE.json configs[3]: PointNetSeg ShapeNet-part B=16, N=2048, one
+    run_training_pointnet_seg iteration (forward, per-point CE, backward, Adam)
+    per step, HIP-graph replayed over resident synthetic batches."""
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd.seg import SegTrainStep
+    from adversarial_learning_on_pointclouds_amd.model_utils import init_weights
+    Bs, Ns = 16, 2048
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = pc.PointNetSeg(50).to(dev)
+    init_weights(model, "xavier", verbose=False)
+    step = SegTrainStep(model, device=dev)
+    pool = []
+    for k in range(2):
+        rng = np.random.default_rng(2000 + k)
+        cls = np.zeros((Bs, 1, 16), np.float32)
+        cls[np.arange(Bs), 0, rng.integers(0, 16, Bs)] = 1
+        pool.append((torch.from_numpy(rng.uniform(-1, 1, (Bs, Ns, 3)).astype(np.float32)).to(dev),
+                     torch.from_numpy(cls).to(dev),
+                     torch.from_numpy(rng.integers(0, 50, (Bs, Ns))).to(dev)))
+    graphs = [step.capture_on(*b) for b in pool]
+    for k in range(args.warmup):
+        graphs[k % 2].replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        graphs[k % 2].replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # algorithmic FLOPs per step (SURVEY 8(d): fc1's tiled part once per cloud;
+    # sparse max backward): forward 2 N (3*64 + 64*128 + 2*128*128 + 128*512 +
+    # 512*2048 + 960*256 + 256*256 + 256*128 + 128*50) per cloud, backward twice
+    # the dense layers except conv6 (sparse) and conv1's input gradient
+    per_pt_fwd = 3 * 64 + 64 * 128 + 2 * 128 * 128 + 128 * 512 + 512 * 2048 + 960 * 256 + \
+        256 * 256 + 256 * 128 + 128 * 50
+    dense_bwd = 2 * (per_pt_fwd - 512 * 2048) - 3 * 64
+    gflop = 2.0 * Bs * Ns * (per_pt_fwd + dense_bwd) / 1e9
+    loss = float(step.loss.item())
+    out = {
+        "metric": "point-clouds/sec (seg train step), B=16 N=2048 ShapeNet-part, 1 GPU",
+        "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded U(-1,1) clouds, one-hot classes, part labels in [0,50))",
+        "config": {"workload": "PointNetSeg(50) + CrossEntropyLoss + Adam, B=16, N=2048 "
+                               "(BASELINE configs[3])", "global_batch": Bs, "points": Ns,
+                   "parallelism": "dp1", "hip_graph": True},
+        "step_flops": {"gflop_per_step": round(gflop, 2),
+                       "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
+        "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "seg":
+        return bench_seg(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
