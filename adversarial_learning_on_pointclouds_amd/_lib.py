@@ -90,10 +90,10 @@ SIGNATURES = {
     "pcadv_conv_max_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "pcadv_tnet_reg_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_tnet_reg_bwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
-    "pcadv_gemm": (_i, [_vp, _i64, _i, _vp, _i64, _vp, _i64, _i, _vp, _i64, _i, _i, _i, _vp, _vp,
-                        _i, _i, _i, _i, _vp]),
-    "pcadv_gemm_wgrad_workspace_bytes": (_sz, [_i, _i, _i]),
-    "pcadv_gemm_wgrad": (_i, [_vp, _i64, _vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp,
+    "pcadv_gemm": (_i, [_vp, _i64, _i, _vp, _i64, _i, _vp, _i64, _i, _i, _i, _vp, _vp, _i, _i, _i,
+                        _vp, _i64, _i, _vp]),
+    "pcadv_gemm_wgrad_workspace_bytes": (_sz, [_i, _i, _i, _i]),
+    "pcadv_gemm_wgrad": (_i, [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _vp, _vp, _i, _i, _vp,
                               _sz, _vp]),
     "pcadv_colsum_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_colsum": (_i, [_vp, _vp, _i64, _i64, _i, _i, _vp, _i, _vp, _sz, _vp]),
@@ -101,7 +101,7 @@ SIGNATURES = {
     "pcadv_conv_max_x3_workspace_bytes": (_sz, [_i, _i, _i]),
     "pcadv_conv_max_x3": (_i, [_vp, _i64, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "pcadv_conv_max_x3_bwd": (_i, [_vp, _vp, _vp, _vp, _i64, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
-                                   _i64, _vp]),
+                                   _i64, _i, _vp]),
     "pcadv_row_ce_workspace_bytes": (_sz, [_i]),
     "pcadv_row_ce": (_i, [_vp, _i64, _vp, _i, _i, _f, _vp, _vp, _vp, _sz, _vp]),
     "pcadv_adv_step_workspace_bytes": (_sz, [_i, _i]),

@@ -63,12 +63,12 @@ int tail_stamps_read(uint64_t* host);
 int launch_head_bwd(const float*, const float*, const float*, int, const float*, const float*,
                     float*, float*, float*, float*, const float*, const float*, float*,
                     hipStream_t);
-int launch_gemm(const float*, long long, int, const float*, long long, const float*, long long,
-                int, float*, long long, int, int, int, const float*, const float*, int, int, int,
+int launch_gemm(const float*, long long, int, const float*, long long, int, float*, long long,
+                int, int, int, const float*, const float*, int, int, int, const float*, long long,
                 int, hipStream_t);
-size_t gemm_wgrad_workspace_bytes(int, int, int);
-int launch_gemm_wgrad(const float*, long long, const float*, long long, const float*, long long,
-                      int, int, int, float*, long long, int, void*, size_t, hipStream_t);
+size_t gemm_wgrad_workspace_bytes(int, int, int, int);
+int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int, int, float*,
+                      long long, float*, float*, int, int, void*, size_t, hipStream_t);
 size_t colsum_workspace_bytes(int, int);
 int launch_colsum(const float*, const float*, long long, long long, int, int, float*, int, void*,
                   size_t, hipStream_t);
@@ -78,7 +78,7 @@ size_t conv_max_x3_workspace_bytes(int, int, int);
 int launch_conv_max_x3(const float*, long long, int, int, int, const float*, const float*, int,
                        int, float*, int32_t*, void*, size_t, hipStream_t);
 int launch_cmx_bwd(const float*, const float*, const int32_t*, const float*, long long, int, int,
-                   int, int, const float*, float*, float*, float*, long long, hipStream_t);
+                   int, int, const float*, float*, float*, float*, long long, int, hipStream_t);
 size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
                   size_t, hipStream_t);
@@ -389,23 +389,23 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
 }
 
 // ---- dense point-wise GEMM engine (segmentation net) -----------------------
-int pcadv_gemm(const float* a, int64_t lda, int ta, const float* amask, int64_t ldm,
-               const float* b, int64_t ldb, int tb, float* c, int64_t ldc, int M, int N, int K,
-               const float* bias, const float* bias_rows, int rows_per_group, int relu,
-               int accumulate, int precise, hipStream_t stream) {
-  return launch_gemm(a, lda, ta, amask, ldm, b, ldb, tb, c, ldc, M, N, K, bias, bias_rows,
-                     rows_per_group, relu, accumulate, precise, stream);
+int pcadv_gemm(const float* a, int64_t lda, int ta, const float* b, int64_t ldb, int tb,
+               float* c, int64_t ldc, int M, int N, int K, const float* bias,
+               const float* bias_rows, int rows_per_group, int relu, int accumulate,
+               const float* cmask, int64_t ldm, int precise, hipStream_t stream) {
+  return launch_gemm(a, lda, ta, b, ldb, tb, c, ldc, M, N, K, bias, bias_rows, rows_per_group,
+                     relu, accumulate, cmask, ldm, precise, stream);
 }
 
-size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin) {
-  return gemm_wgrad_workspace_bytes(rows, O, Kin);
+size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) {
+  return gemm_wgrad_workspace_bytes(rows, O, Kin, rows_per_group);
 }
 
-int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* ymask, int64_t ldm,
-                     const float* x, int64_t ldx, int rows, int O, int Kin, float* dw, int64_t ldo,
+int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows, int O,
+                     int Kin, float* dw, int64_t ldo, float* db, float* gsum, int rows_per_group,
                      int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
-  return launch_gemm_wgrad(dz, ldz, ymask, ldm, x, ldx, rows, O, Kin, dw, ldo, accumulate,
-                           workspace, workspace_bytes, stream);
+  return launch_gemm_wgrad(dz, ldz, x, ldx, rows, O, Kin, dw, ldo, db, gsum, rows_per_group,
+                           accumulate, workspace, workspace_bytes, stream);
 }
 
 size_t pcadv_colsum_workspace_bytes(int M, int N) { return colsum_workspace_bytes(M, N); }
@@ -436,8 +436,9 @@ int pcadv_conv_max_x3(const float* x, int64_t ldx, int C, int Npts, int K, const
 int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* gidx,
                           const float* x, int64_t ldx, int C, int Npts, int O, int K,
                           const float* w, float* dw, float* db, float* dx, int64_t lddx,
-                          hipStream_t stream) {
-  return launch_cmx_bwd(dgmax, gmax, gidx, x, ldx, C, Npts, O, K, w, dw, db, dx, lddx, stream);
+                          int relu_x, hipStream_t stream) {
+  return launch_cmx_bwd(dgmax, gmax, gidx, x, ldx, C, Npts, O, K, w, dw, db, dx, lddx, relu_x,
+                        stream);
 }
 
 size_t pcadv_row_ce_workspace_bytes(int M) { return row_ce_workspace_bytes(M); }

@@ -16,10 +16,12 @@
 // (TA = 1, i.e. A^T stored); B[n][k] at b[n*ldb + k] (TB = 0: a weight [out][in])
 // or b[k*ldb + n] (TB = 1).  Forward: TA = 0, TB = 0.  Data gradient dX = dZ W:
 // TA = 0, TB = 1.  Weight gradient dW = dZ^T X: TA = 1, TB = 1, split over the
-// point axis into fixed-order slabs (k_gemm_slab_sum).
+// point axis into fixed-order slabs (k_slab_sum).
 //
-// An optional activation mask multiplies A as it is staged: A[m][k] * [Y > 0]
-// with Y stored like A (relu' of the layer output, for dZ = dY relu'(Y)).
+// An optional output mask zeroes C where a mask matrix Y (stored like C) is
+// not > 0: relu'(Y) applied by the producer of dZ = dY relu'(Y), so that every
+// consumer (the weight gradient, the next data gradient, the bias sums) reads
+// dZ already masked.
 #include "common.h"
 
 namespace pcadv {
@@ -35,6 +37,7 @@ constexpr int GM_T = 256;   // 4 waves, 2 x 2, each 64 x 64 of C
 constexpr int GM_S = 40;    // bf16 row stride of the staged tiles (80 B: conflict-free b128 reads)
 
 typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4g __attribute__((ext_vector_type(4)));
 
 struct GemmLds {
   alignas(16) __bf16 a[3][GM_BM * GM_S];  // [hi, (mid,) lo][m][k]
@@ -53,17 +56,21 @@ __device__ __forceinline__ void split_planes(float v, __bf16 (&o)[3]) {
 
 struct GemmP {
   const float* a; long long lda;
-  const float* amask; long long ldm;  // nullable: A *= [amask > 0], stored like A (stride ldm)
   const float* b; long long ldb;
   float* c; long long ldc;
+  const float* cmask; long long ldm;  // nullable: C *= [cmask > 0], stored like C (stride ldm)
   const float* bias;               // [N] or null
   const float* bias_rows;          // [M / rows_per_group][N] or null
   int rows_per_group;               // bias_rows groups; mode 2: points per cloud
   int M, N, K;
   int relu, accumulate;
   int avec, bvec;                  // 16-B vector loads allowed (aligned base, ld % 4 == 0)
-  int ksplit_len;                  // k range per grid.z slab (weight gradients)
+  int cvec;                        // the epilogue's C / bias / bias_rows / mask allow 16-B access
+  // k range of slab z (grid.z): group z / zpg of grp rows, piece z % zpg of
+  // ksplit_len rows (weight gradients: the point axis in fixed-order slabs)
+  int grp, zpg, ksplit_len;
   long long slab_stride;           // floats between slabs
+  float* csum;                     // TA = 1: per-slab column sums of A ([z][M]) or null
   // max-over-points screening epilogue (mode 2): per (row tile, column) top-2
   int2* part;                      // [M / BM][N] screening keys
 };
@@ -85,7 +92,14 @@ constexpr int GKEY_NONE = (int)0x80000000;
 
 // NP = 3: three products of hi/lo splits (relative error <= ~1.2e-5 of
 // sum|a b|); NP = 6: six products of hi/mid/lo splits (h h, h m, m h, h l, m m,
-// l h), f32-level accuracy (the gradients, whose sums cancel heavily)
+// l h), f32-level accuracy (the gradients, whose sums cancel heavily).
+//
+// Main loop: the f32 tiles are staged through registers two tiles ahead (two
+// register sets), so two 32 KB tiles per workgroup are in flight while the
+// MFMAs of the current one run; each tile is split into its bf16 planes once,
+// on the way into LDS.  Transposed operands (TA / TB = 1: the reduction axis is
+// the slow one) are read as 4 (k) x 4 (m) blocks per thread and written as
+// 4-k runs (ds_write_b64) of each plane.
 template <int TA, int TB, int MODE, int NP>
 __global__ void __launch_bounds__(GM_T)
 k_gemm_x3(GemmP p) {
@@ -95,152 +109,123 @@ k_gemm_x3(GemmP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.y * GM_BN;
-  // mode 2: blockIdx.x = (cloud, row tile of that cloud); rows never straddle clouds
+  // XCD-aware tile order: the workgroups one XCD runs (linear id = xcd mod 8)
+  // take consecutive tiles with the column tile fastest, so the column tiles
+  // sharing a row tile of A run together on one XCD and read it from its L2
+  int tx, ty, tz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * gridDim.z;
+    const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = lin & 7, q = n >> 3, rr = n & 7;
+    const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (lin >> 3);
+    tz = t / (gx * gy);
+    tx = (t % (gx * gy)) / gy;
+    ty = t % gy;
+  }
+  const int n0 = ty * GM_BN;
+  // mode 2: tx = (cloud, row tile of that cloud); rows never straddle clouds
   const int T2 = MODE == 2 ? (p.rows_per_group + GM_BM - 1) / GM_BM : 1;
-  const int cl = MODE == 2 ? blockIdx.x / T2 : 0;
-  const int m0 = MODE == 2 ? (blockIdx.x % T2) * GM_BM : blockIdx.x * GM_BM;
+  const int cl = MODE == 2 ? tx / T2 : 0;
+  const int m0 = MODE == 2 ? (tx % T2) * GM_BM : tx * GM_BM;
   const int Mlim = MODE == 2 ? p.rows_per_group : p.M;
   const float* Ab = MODE == 2 ? p.a + (size_t)cl * p.rows_per_group * p.lda : p.a;
-  const int kz0 = blockIdx.z * p.ksplit_len;
-  const int kz1 = min(p.K, kz0 + p.ksplit_len);
-  float* C = p.c + (size_t)blockIdx.z * p.slab_stride;
+  const int gz = tz / p.zpg, sz = tz % p.zpg;
+  const int kz0 = gz * p.grp + sz * p.ksplit_len;
+  const int kz1 = min(min(p.K, (gz + 1) * p.grp), kz0 + p.ksplit_len);
+  float* C = p.c + (size_t)tz * p.slab_stride;
+  const bool do_csum = TA == 1 && p.csum != nullptr && ty == 0;
 
-  // staging: the 128 x 32 f32 tile of A (and of B) is 4096 values, 16 per thread
-  f32x4 ra[4], rb[4];
-  auto load_tile = [&](int k0) {
-    if (TA == 0) {  // A[m][k]: thread = (row tid >> 1, 16 k at 16 (tid & 1))
-      const int row = tid >> 1, kk = 16 * (tid & 1);
-      const int m = m0 + row;
+  // one operand tile (128 x 32 f32 = 4096 values, 16 per thread)
+  //   [m][k] layout: thread = (row tid >> 1, 16 k at 16 (tid & 1))
+  //   [k][m] layout: thread = (4 k at 4 (tid & 7), 4 m at 4 (tid >> 3))
+  auto load_rows = [&](f32x4 (&v)[4], const float* base, long long ld, int row0, int rlim, int k0,
+                       bool vec) {
+    const int row = row0 + (tid >> 1), kk = k0 + 16 * (tid & 1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + kk + 4 * j;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (m < Mlim && k < kz1) {
-          const float* src = Ab + (size_t)m * p.lda + k;
-          if (p.avec && k + 3 < kz1) {
-            v = *reinterpret_cast<const f32x4*>(src);
-          } else {
-            for (int t = 0; t < 4 && k + t < kz1; ++t) v[t] = src[t];
-          }
-          if (p.amask) {
-            const float* ms = p.amask + (size_t)m * p.ldm + k;
-            for (int t = 0; t < 4; ++t)
-              if (k + t < kz1 && !(ms[t] > 0.f)) v[t] = 0.f;
-          }
+    for (int j = 0; j < 4; ++j) {
+      const int k = kk + 4 * j;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (row < rlim && k >= kz0 && k < kz1) {
+        const float* src = base + (size_t)row * ld + k;
+        if (vec && k + 3 < kz1) {
+          x = *reinterpret_cast<const f32x4*>(src);
+        } else {
+          for (int t = 0; t < 4 && k + t < kz1; ++t) x[t] = src[t];
         }
-        ra[j] = v;
       }
-    } else {  // A^T stored: a[k * lda + m]; thread = (k tid >> 3, 16 m at 16 (tid & 7))
-      const int kk = tid >> 3, mm = 16 * (tid & 7);
-      const int k = k0 + kk;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + mm + 4 * j;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (k < kz1 && m < Mlim) {
-          const float* src = Ab + (size_t)k * p.lda + m;
-          if (p.avec && m + 3 < Mlim) {
-            v = *reinterpret_cast<const f32x4*>(src);
-          } else {
-            for (int t = 0; t < 4 && m + t < Mlim; ++t) v[t] = src[t];
-          }
-          if (p.amask) {
-            const float* ms = p.amask + (size_t)k * p.ldm + m;
-            for (int t = 0; t < 4; ++t)
-              if (m + t < Mlim && !(ms[t] > 0.f)) v[t] = 0.f;
-          }
-        }
-        ra[j] = v;
-      }
-    }
-    if (TB == 0) {  // B[n][k]
-      const int row = tid >> 1, kk = 16 * (tid & 1);
-      const int n = n0 + row;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + kk + 4 * j;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (n < p.N && k < kz1) {
-          const float* src = p.b + (size_t)n * p.ldb + k;
-          if (p.bvec && k + 3 < kz1) {
-            v = *reinterpret_cast<const f32x4*>(src);
-          } else {
-            for (int t = 0; t < 4 && k + t < kz1; ++t) v[t] = src[t];
-          }
-        }
-        rb[j] = v;
-      }
-    } else {  // b[k * ldb + n]
-      const int kk = tid >> 3, nn = 16 * (tid & 7);
-      const int k = k0 + kk;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + nn + 4 * j;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (k < kz1 && n < p.N) {
-          const float* src = p.b + (size_t)k * p.ldb + n;
-          if (p.bvec && n + 3 < p.N) {
-            v = *reinterpret_cast<const f32x4*>(src);
-          } else {
-            for (int t = 0; t < 4 && n + t < p.N; ++t) v[t] = src[t];
-          }
-        }
-        rb[j] = v;
-      }
+      v[j] = x;
     }
   };
-  auto store_tile = [&]() {
-    if (TA == 0) {
-      const int row = tid >> 1, kk = 16 * (tid & 1);
-      bf16x8g pv[3][2];
+  auto load_cols = [&](f32x4 (&v)[4], const float* base, long long ld, int col0, int clim, int k0,
+                       bool vec) {
+    const int col = col0 + 4 * (tid >> 3), kk = k0 + 4 * (tid & 7);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < 4; ++j) {
+      const int k = kk + j;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (k >= kz0 && k < kz1 && col < clim) {
+        const float* src = base + (size_t)k * ld + col;
+        if (vec && col + 3 < clim) {
+          x = *reinterpret_cast<const f32x4*>(src);
+        } else {
+          for (int t = 0; t < 4 && col + t < clim; ++t) x[t] = src[t];
+        }
+      }
+      v[j] = x;
+    }
+  };
+  auto store_rows = [&](const f32x4 (&v)[4], __bf16 (*planes)[GM_BM * GM_S]) {
+    const int row = tid >> 1, kk = 16 * (tid & 1);
+    bf16x8g pv[3][2];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      __bf16 o[3];
+      split_planes<NPL>(v[j >> 2][j & 3], o);
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) pv[q][j >> 3][j & 7] = o[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      *reinterpret_cast<bf16x8g*>(&planes[q][row * GM_S + kk]) = pv[q][0];
+      *reinterpret_cast<bf16x8g*>(&planes[q][row * GM_S + kk + 8]) = pv[q][1];
+    }
+  };
+  auto store_cols = [&](const f32x4 (&v)[4], __bf16 (*planes)[GM_BM * GM_S]) {
+    const int col = 4 * (tid >> 3), kk = 4 * (tid & 7);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x4g pv[3];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
         __bf16 o[3];
-        split_planes<NPL>(ra[j >> 2][j & 3], o);
+        split_planes<NPL>(v[j][i], o);
 #pragma unroll
-        for (int q = 0; q < NPL; ++q) pv[q][j >> 3][j & 7] = o[q];
+        for (int q = 0; q < NPL; ++q) pv[q][j] = o[q];
       }
 #pragma unroll
-      for (int q = 0; q < NPL; ++q) {
-        *reinterpret_cast<bf16x8g*>(&L.a[q][row * GM_S + kk]) = pv[q][0];
-        *reinterpret_cast<bf16x8g*>(&L.a[q][row * GM_S + kk + 8]) = pv[q][1];
-      }
-    } else {
-      const int kk = tid >> 3, mm = 16 * (tid & 7);
+      for (int q = 0; q < NPL; ++q)
+        *reinterpret_cast<bf16x4g*>(&planes[q][(col + i) * GM_S + kk]) = pv[q];
+    }
+  };
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};  // TA = 1: this thread's column sums of A
+  auto load_tile = [&](f32x4 (&ra)[4], f32x4 (&rb)[4], int k0) {
+    if (TA == 0) load_rows(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
+    else load_cols(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
+    if (TB == 0) load_rows(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
+    else load_cols(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
+  };
+  auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
+    if (TA == 0) store_rows(ra, L.a);
+    else {
+      store_cols(ra, L.a);
+      if (do_csum) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        __bf16 o[3];
-        split_planes<NPL>(ra[j >> 2][j & 3], o);
-#pragma unroll
-        for (int q = 0; q < NPL; ++q) L.a[q][(mm + j) * GM_S + kk] = o[q];
+        for (int i = 0; i < 4; ++i) cs[i] += ((ra[0][i] + ra[1][i]) + ra[2][i]) + ra[3][i];
       }
     }
-    if (TB == 0) {
-      const int row = tid >> 1, kk = 16 * (tid & 1);
-      bf16x8g pv[3][2];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        __bf16 o[3];
-        split_planes<NPL>(rb[j >> 2][j & 3], o);
-#pragma unroll
-        for (int q = 0; q < NPL; ++q) pv[q][j >> 3][j & 7] = o[q];
-      }
-#pragma unroll
-      for (int q = 0; q < NPL; ++q) {
-        *reinterpret_cast<bf16x8g*>(&L.b[q][row * GM_S + kk]) = pv[q][0];
-        *reinterpret_cast<bf16x8g*>(&L.b[q][row * GM_S + kk + 8]) = pv[q][1];
-      }
-    } else {
-      const int kk = tid >> 3, nn = 16 * (tid & 7);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        __bf16 o[3];
-        split_planes<NPL>(rb[j >> 2][j & 3], o);
-#pragma unroll
-        for (int q = 0; q < NPL; ++q) L.b[q][(nn + j) * GM_S + kk] = o[q];
-      }
-    }
+    if (TB == 0) store_rows(rb, L.b);
+    else store_cols(rb, L.b);
   };
 
   f32x16 acc[2][2];
@@ -249,12 +234,7 @@ k_gemm_x3(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
-  load_tile(kz0);
-  for (int k0 = kz0; k0 < kz1; k0 += GM_BK) {
-    __syncthreads();  // every wave is done reading the previous tile
-    store_tile();
-    __syncthreads();
-    if (k0 + GM_BK < kz1) load_tile(k0 + GM_BK);  // in flight during the MFMAs
+  auto mfma_tile = [&]() {
 #pragma unroll
     for (int kb = 0; kb < GM_BK / 16; ++kb) {
       bf16x8g fa[3][2], fb[3][2];  // [plane][tile]
@@ -286,6 +266,42 @@ k_gemm_x3(GemmP p) {
           }
         }
     }
+  };
+
+  // two register sets: tile t+2 is loaded while tile t is multiplied.  The
+  // loop is unrolled by two with straight-line phases (so each store waits
+  // only for its own set's loads); an odd tile count starts one empty tile
+  // early (its loads are all masked to zero).
+  f32x4 ra0[4], rb0[4], ra1[4], rb1[4];
+  const int ntile = (kz1 - kz0 + GM_BK - 1) / GM_BK;
+  const int kb0 = kz0 - (ntile & 1) * GM_BK;  // first (possibly empty) tile
+  load_tile(ra0, rb0, kb0);
+  load_tile(ra1, rb1, kb0 + GM_BK);
+  for (int k0 = kb0; k0 < kz1; k0 += 2 * GM_BK) {
+    __syncthreads();  // every wave is done reading the previous tile
+    store_tile(ra0, rb0);
+    __syncthreads();
+    load_tile(ra0, rb0, k0 + 2 * GM_BK);
+    mfma_tile();
+    __syncthreads();
+    store_tile(ra1, rb1);
+    __syncthreads();
+    load_tile(ra1, rb1, k0 + 3 * GM_BK);
+    mfma_tile();
+  }
+
+  if (do_csum) {  // fixed-order reduction over the 8 k-lanes of each column group
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cs[i] += __shfl_xor(cs[i], 1);
+      cs[i] += __shfl_xor(cs[i], 2);
+      cs[i] += __shfl_xor(cs[i], 4);
+    }
+    const int col = m0 + 4 * (tid >> 3);
+    if ((tid & 7) == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (col + i < Mlim) p.csum[(size_t)tz * p.M + col + i] = cs[i];
   }
 
   if constexpr (MODE == 2) {
@@ -319,42 +335,185 @@ k_gemm_x3(GemmP p) {
       const int2 x = red[0][c], y = red[1][c];
       const int b2 = max(min(x.x, y.x), max(x.y, y.y));
       const int b1 = max(x.x, y.x);
-      p.part[(size_t)blockIdx.x * p.N + n] = make_int2(b1, b2);
+      p.part[(size_t)tx * p.N + n] = make_int2(b1, b2);
     }
   } else {
+    // epilogue through LDS, one 128 x 64 half of the tile at a time (each
+    // wave's 32-column block j): rows are then written by 16 lanes x 4
+    // consecutive columns, so C, the per-group bias and the mask move as
+    // coalesced 16-B accesses with one address per row
+    float* stage = reinterpret_cast<float*>(smem);
+    constexpr int ES = 68;  // row stride (floats) of the staged half tile
+    const bool vec = p.cvec;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int n = n0 + 64 * wn + 32 * j + r;
-      if (n >= p.N) continue;
-      const float bias = p.bias ? p.bias[n] : 0.f;
+      __syncthreads();  // the MFMA operands / the previous half are no longer read
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + 64 * wm + 32 * i + acc_row(e, lane);
-          if (m >= p.M) continue;
-          float v = acc[i][j][e] + bias;
-          if (p.bias_rows) v += p.bias_rows[(size_t)(m / p.rows_per_group) * p.N + n];
-          float* dst = C + (size_t)m * p.ldc + n;
-          if (MODE == 1) v += *dst;
-          if (p.relu) v = v > 0.f ? v : 0.f;
-          *dst = v;
+        for (int e = 0; e < 16; ++e)
+          stage[(64 * wm + 32 * i + acc_row(e, lane)) * ES + 32 * wn + r] = acc[i][j][e];
+      __syncthreads();
+      const int c4 = 4 * (tid & 15);                 // staged column (0..60)
+      const int n = n0 + 64 * (c4 >> 5) + 32 * j + (c4 & 31);
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) {
+        const int row = (tid >> 4) + 16 * it;
+        const int m = m0 + row;
+        if (m >= p.M) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(&stage[row * ES + c4]);
+        float* dst = C + (size_t)m * p.ldc + n;
+        const float* br = p.bias_rows ? p.bias_rows + (size_t)(m / p.rows_per_group) * p.N + n : nullptr;
+        const float* mk = p.cmask ? p.cmask + (size_t)m * p.ldm + n : nullptr;
+        if (vec && n + 3 < p.N) {
+          if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+          if (br) v += *reinterpret_cast<const f32x4*>(br);
+          if (MODE == 1) v += *reinterpret_cast<const f32x4*>(dst);
+          const f32x4 mv = mk ? *reinterpret_cast<const f32x4*>(mk) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (p.relu) v[t] = v[t] > 0.f ? v[t] : 0.f;
+            if (!(mv[t] > 0.f)) v[t] = 0.f;
+          }
+          *reinterpret_cast<f32x4*>(dst) = v;
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (n + t >= p.N) break;
+            float x = v[t];
+            if (p.bias) x += p.bias[n + t];
+            if (br) x += br[t];
+            if (MODE == 1) x += dst[t];
+            if (p.relu) x = x > 0.f ? x : 0.f;
+            if (mk && !(mk[t] > 0.f)) x = 0.f;
+            dst[t] = x;
+          }
         }
+      }
     }
   }
 }
 
-// fixed-order sum of nz slabs of M x N (row stride ld) into out (+ column sums)
+// Skinny GEMM (M <= 16 rows per workgroup: one row per cloud, e.g. fc1's
+// per-cloud bias gmax W1g^T and the per-cloud gradient s1 W1g) in exact f32
+// FMAs on the vector ALUs, with the same epilogue as k_gemm_x3.  The 16 rows
+// of A are read by every lane (clamped to the last row, so no per-row
+// branches), the reduction axis is spread over the workgroup and combined in a
+// fixed order (bitwise reproducible).
+//   TB = 0 (B[n][k], k contiguous): a workgroup per column n, 256 lanes
+//          across k (16-B loads when aligned);
+//   TB = 1 (B[k][n], n contiguous): a workgroup per 16 columns, 16 k-lanes
+//          per column.
+template <int TB>
 __global__ void __launch_bounds__(256)
-k_gemm_slab_sum(const float* __restrict__ slabs, long long slab_stride, int nz, int M, int N,
-                long long ld, float* __restrict__ out, long long ldo, int accumulate) {
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long long)M * N) return;
-  const int m = (int)(e / N), n = (int)(e % N);
+k_gemm_small(GemmP p) {
+  const int tid = threadIdx.x;
+  const int m0 = blockIdx.y * 16;
+  const int mrows = min(16, p.M - m0);
+  const float* arow[16];
+#pragma unroll
+  for (int mm = 0; mm < 16; ++mm) arow[mm] = p.a + (size_t)(m0 + min(mm, mrows - 1)) * p.lda;
+  float acc[16];
+#pragma unroll
+  for (int mm = 0; mm < 16; ++mm) acc[mm] = 0.f;
+  __shared__ float red[16][257];
+  int n, part;  // this thread's column and its slot among the column's partial sums
+  if (TB == 0) {
+    n = blockIdx.x;
+    part = tid;
+    const float* brow = p.b + (size_t)n * p.ldb;
+    if (p.avec && p.bvec) {
+      for (int k = 4 * tid; k + 3 < p.K; k += 1024) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(brow + k);
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(arow[mm] + k);
+          acc[mm] = fmaf(a[3], b[3], fmaf(a[2], b[2], fmaf(a[1], b[1], fmaf(a[0], b[0], acc[mm]))));
+        }
+      }
+      for (int k = (p.K & ~3) + tid; k < p.K; k += 256) {  // K % 4 tail
+        const float b = brow[k];
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) acc[mm] = fmaf(arow[mm][k], b, acc[mm]);
+      }
+    } else {
+      for (int k = tid; k < p.K; k += 256) {
+        const float b = brow[k];
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) acc[mm] = fmaf(arow[mm][k], b, acc[mm]);
+      }
+    }
+  } else {
+    n = blockIdx.x * 16 + (tid & 15);
+    part = tid >> 4;
+    if (n < p.N) {
+#pragma unroll 4
+      for (int k = part; k < p.K; k += 16) {
+        const float b = p.b[(size_t)k * p.ldb + n];
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) acc[mm] = fmaf(arow[mm][k], b, acc[mm]);
+      }
+    }
+  }
+  // partial sums -> LDS [row][slot], then a fixed-order sum per (row, column)
+  const int nslot = TB == 0 ? 256 : 16;
+  const int col = TB == 0 ? 0 : (tid & 15);
+#pragma unroll
+  for (int mm = 0; mm < 16; ++mm) red[mm][TB == 0 ? part : col * 16 + part] = acc[mm];
+  __syncthreads();
+  int mm, cc;
+  if (TB == 0) {
+    if (tid >= 16) return;
+    mm = tid; cc = 0;
+  } else {
+    mm = tid >> 4; cc = tid & 15;
+    n = blockIdx.x * 16 + cc;
+  }
+  if (mm >= mrows || n >= p.N) return;
+  float v = 0.f;
+  const float* src = &red[mm][TB == 0 ? 0 : cc * 16];
+  for (int q = 0; q < nslot; ++q) v += src[q];
+  const int m = m0 + mm;
+  float* dst = p.c + (size_t)m * p.ldc + n;
+  v += p.bias ? p.bias[n] : 0.f;
+  if (p.bias_rows) v += p.bias_rows[(size_t)(m / p.rows_per_group) * p.N + n];
+  if (p.accumulate) v += *dst;
+  if (p.relu) v = v > 0.f ? v : 0.f;
+  if (p.cmask && !(p.cmask[(size_t)m * p.ldm + n] > 0.f)) v = 0.f;
+  *dst = v;
+}
+
+// out[g][e] (+)= sum over z < nz of in[(g nz + z) * stride + e], e < E, in a
+// fixed order (bitwise reproducible): a workgroup takes 32 consecutive e
+// (coalesced) x 8 interleaved z-subsets (one per half-wave), combined through
+// LDS.  The output index is 2-D: out + g * ldg + (e / N) * ldo + e % N.
+__global__ void __launch_bounds__(256)
+k_slab_sum(const float* __restrict__ in, long long stride, int nz, long long E,
+           float* __restrict__ out, long long ldg, int N, long long ldo, int accumulate) {
+  const int tid = threadIdx.x, el = tid & 31, zs = tid >> 5;
+  const long long e = (long long)blockIdx.x * 32 + el;
+  const int g = blockIdx.y;
+  __shared__ float part[8][33];
   float s = 0.f;
-  for (int z = 0; z < nz; ++z) s += slabs[(size_t)z * slab_stride + (size_t)m * ld + n];
-  float* dst = out + (size_t)m * ldo + n;
-  *dst = accumulate ? *dst + s : s;
+  if (e < E) {
+    const float* src = in + (size_t)g * nz * stride + e;
+    int z = zs;
+    for (; z + 24 < nz; z += 32) {  // four independent loads in flight
+      const float a0 = src[(size_t)z * stride], a1 = src[(size_t)(z + 8) * stride];
+      const float a2 = src[(size_t)(z + 16) * stride], a3 = src[(size_t)(z + 24) * stride];
+      s += ((a0 + a1) + a2) + a3;
+    }
+    for (; z < nz; z += 8) s += src[(size_t)z * stride];
+  }
+  part[zs][el] = s;
+  __syncthreads();
+  if (zs == 0 && e < E) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += part[q][el];
+    float* dst = out + (size_t)g * ldg + (size_t)(e / N) * ldo + (e % N);
+    *dst = accumulate ? *dst + t : t;
+  }
 }
 
 // column sums of an M x N matrix (row stride ld), optionally masked by [Y > 0]
@@ -527,26 +686,37 @@ static int gemm_launch(const GemmP& p, int nz, hipStream_t s) {
 }
 
 // C[M][N] (+)= op(A) op(B)^T: see the header comment for ta / tb.
-int launch_gemm(const float* a, long long lda, int ta, const float* amask, long long ldm,
-                const float* b,
-                long long ldb, int tb, float* c, long long ldc, int M, int N, int K,
-                const float* bias, const float* bias_rows, int rows_per_group, int relu,
-                int accumulate, int precise, hipStream_t s) {
+int launch_gemm(const float* a, long long lda, int ta, const float* b, long long ldb, int tb,
+                float* c, long long ldc, int M, int N, int K, const float* bias,
+                const float* bias_rows, int rows_per_group, int relu, int accumulate,
+                const float* cmask, long long ldm, int precise, hipStream_t s) {
   PC_REQUIRE(a && b && c && M > 0 && N > 0 && K > 0, "gemm: bad shape M=%d N=%d K=%d", M, N, K);
   PC_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M), "gemm: bad lda %lld (ta=%d)", lda, ta);
   PC_REQUIRE((tb == 0 && ldb >= K) || (tb == 1 && ldb >= N), "gemm: bad ldb %lld (tb=%d)", ldb, tb);
   PC_REQUIRE(((uintptr_t)a & 3) == 0 && ((uintptr_t)b & 3) == 0 && ((uintptr_t)c & 3) == 0,
              "gemm: operands must be float aligned");
   PC_REQUIRE(ldc >= N, "gemm: bad ldc %lld", ldc);
+  PC_REQUIRE(!cmask || ldm >= N, "gemm: bad ldm %lld", ldm);
   PC_REQUIRE(!bias_rows || rows_per_group > 0, "gemm: bias_rows needs rows_per_group");
   PC_REQUIRE(ta == 0 || tb == 1, "gemm: A^T needs B^T (the weight-gradient form)");
   GemmP p{};
-  p.a = a; p.lda = lda; p.amask = amask; p.ldm = ldm; p.b = b; p.ldb = ldb; p.c = c; p.ldc = ldc;
+  p.a = a; p.lda = lda; p.b = b; p.ldb = ldb; p.c = c; p.ldc = ldc;
+  p.cmask = cmask; p.ldm = ldm;
   p.bias = bias; p.bias_rows = bias_rows; p.rows_per_group = rows_per_group;
   p.M = M; p.N = N; p.K = K; p.relu = relu; p.accumulate = accumulate;
   p.avec = lda % 4 == 0 && ((uintptr_t)a & 15) == 0;
   p.bvec = ldb % 4 == 0 && ((uintptr_t)b & 15) == 0;
-  p.ksplit_len = K;
+  p.cvec = ldc % 4 == 0 && ((uintptr_t)c & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0) &&
+           (!bias_rows || (N % 4 == 0 && ((uintptr_t)bias_rows & 15) == 0)) &&
+           (!cmask || (ldm % 4 == 0 && ((uintptr_t)cmask & 15) == 0));
+  p.grp = K; p.zpg = 1; p.ksplit_len = K;
+  if (ta == 0 && M <= 32) {  // per-cloud rows: exact f32 on the vector ALUs
+    const dim3 grid(tb ? (N + 15) / 16 : N, (M + 15) / 16);
+    if (tb) hipLaunchKernelGGL(k_gemm_small<1>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_gemm_small<0>, grid, dim3(256), 0, s, p);
+    PC_HIP_CHECK_LAUNCH("k_gemm_small");
+    return PCADV_OK;
+  }
   if (precise) {
     if (ta == 0 && tb == 0) return accumulate ? gemm_launch<0, 0, 1, 6>(p, 1, s) : gemm_launch<0, 0, 0, 6>(p, 1, s);
     if (ta == 0 && tb == 1) return accumulate ? gemm_launch<0, 1, 1, 6>(p, 1, s) : gemm_launch<0, 1, 0, 6>(p, 1, s);
@@ -557,40 +727,85 @@ int launch_gemm(const float* a, long long lda, int ta, const float* amask, long 
   return accumulate ? gemm_launch<1, 1, 1, 3>(p, 1, s) : gemm_launch<1, 1, 0, 3>(p, 1, s);
 }
 
-// weight gradient dW[N][K'] (+)= sum over M' points of dZ[m][n] X[m][k]:
-// A = dZ^T (stored [M'][N], row stride ldz), B = X^T (stored [M'][K'], ldx),
-// the point axis split into nz fixed-order slabs in the workspace.
-size_t gemm_wgrad_workspace_bytes(int rows, int O, int Kin) {
-  const int nz = rows >= 4096 ? min(32, rows / 1024) : 1;
-  return (size_t)nz * O * Kin * sizeof(float) + 256;
+// weight gradient dW[O][Kin] (+)= sum over the rows of dZ[row][o] X[row][k]:
+// A = dZ^T (stored [rows][O], row stride ldz), B = X^T (stored [rows][Kin],
+// ldx); the row axis is cut into fixed-order slabs (zpg per group of
+// rows_per_group rows, or of all rows) reduced by k_slab_sum, which also
+// forms db[o] (+)= sum dZ[.][o] and the per-group sums gsum[g][o] from the
+// column sums the slabs take of the staged dZ.  Enough slabs to give the
+// launch ~768 workgroups, each slab at least 128 rows.
+struct WgradPlan { int groups, grp, zpg, len, nz; };
+static WgradPlan wgrad_plan(int rows, int O, int Kin, int rows_per_group) {
+  WgradPlan w{};
+  w.grp = rows_per_group > 0 ? rows_per_group : rows;
+  w.groups = rows / w.grp;
+  const int tiles = ((O + GM_BM - 1) / GM_BM) * ((Kin + GM_BN - 1) / GM_BN);
+  const int want = (768 + tiles * w.groups - 1) / (tiles * w.groups);
+  w.zpg = max(1, min(want, (w.grp + 127) / 128));
+  w.len = (w.grp + w.zpg - 1) / w.zpg;
+  w.zpg = (w.grp + w.len - 1) / w.len;
+  w.nz = w.groups * w.zpg;
+  return w;
 }
 
-int launch_gemm_wgrad(const float* dz, long long ldz, const float* ymask, long long ldm,
-                      const float* x, long long ldx, int rows, int O, int Kin, float* dw,
-                      long long ldo, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
-  PC_REQUIRE(dz && x && dw && rows > 0 && O > 0 && Kin > 0 && ldo >= Kin, "gemm_wgrad: bad shape");
+size_t gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) {
+  if (rows <= 0 || O <= 0 || Kin <= 0 || (rows_per_group > 0 && rows % rows_per_group)) return 0;
+  const WgradPlan w = wgrad_plan(rows, O, Kin, rows_per_group);
+  return ((size_t)w.nz * O * Kin + (size_t)w.nz * O + (size_t)w.groups * O) * sizeof(float) + 512;
+}
 
-  const int nz = rows >= 4096 ? min(32, rows / 1024) : 1;
-  PC_REQUIRE(ws && ws_bytes >= gemm_wgrad_workspace_bytes(rows, O, Kin), "gemm_wgrad: workspace");
+int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long ldx, int rows,
+                      int O, int Kin, float* dw, long long ldo, float* db, float* gsum,
+                      int rows_per_group, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+  PC_REQUIRE(dz && x && dw && rows > 0 && O > 0 && Kin > 0 && ldo >= Kin && ldz >= O && ldx >= Kin,
+             "gemm_wgrad: bad shape rows=%d O=%d Kin=%d", rows, O, Kin);
+  PC_REQUIRE(!gsum || (rows_per_group > 0 && rows % rows_per_group == 0),
+             "gemm_wgrad: per-group sums need rows %% rows_per_group == 0");
+  PC_REQUIRE(rows_per_group <= 0 || rows % rows_per_group == 0, "gemm_wgrad: rows %% rows_per_group");
+  const WgradPlan w = wgrad_plan(rows, O, Kin, rows_per_group);
+  PC_REQUIRE(ws && ws_bytes >= gemm_wgrad_workspace_bytes(rows, O, Kin, rows_per_group),
+             "gemm_wgrad: workspace");
+  float* slabs = static_cast<float*>(ws);
+  float* csum = (db || gsum) ? slabs + (size_t)w.nz * O * Kin : nullptr;
   GemmP p{};
-  p.a = dz; p.lda = ldz; p.amask = ymask; p.ldm = ldm; p.b = x; p.ldb = ldx;
-  p.c = static_cast<float*>(ws); p.ldc = Kin;
+  p.a = dz; p.lda = ldz; p.b = x; p.ldb = ldx;
+  p.c = slabs; p.ldc = Kin;
   p.M = O; p.N = Kin; p.K = rows;
   p.avec = ldz % 4 == 0 && ((uintptr_t)dz & 15) == 0;
   p.bvec = ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
-  p.ksplit_len = ((rows + nz - 1) / nz + GM_BK - 1) / GM_BK * GM_BK;
+  p.cvec = Kin % 4 == 0;
+  p.grp = w.grp; p.zpg = w.zpg; p.ksplit_len = w.len;
   p.slab_stride = (long long)O * Kin;
-  PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(p, nz, s)));
-  const long long tot = (long long)O * Kin;
-  hipLaunchKernelGGL(k_gemm_slab_sum, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
-                     static_cast<const float*>(ws), p.slab_stride, nz, O, Kin, (long long)Kin, dw,
-                     ldo, accumulate);
-  PC_HIP_CHECK_LAUNCH("k_gemm_slab_sum");
+  p.csum = csum;
+  PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(p, w.nz, s)));
+  const long long E = (long long)O * Kin;
+  hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((E + 31) / 32), 1), dim3(256), 0, s,
+                     static_cast<const float*>(slabs), E, w.nz, E, dw, 0LL, Kin, ldo, accumulate);
+  PC_HIP_CHECK_LAUNCH("k_slab_sum (dw)");
+  if (csum) {
+    // per-group sums of the slabs' column sums, then their total
+    float* gs = gsum ? gsum : csum + (size_t)w.nz * O;
+    if (w.groups > 1 || gsum) {
+      hipLaunchKernelGGL(k_slab_sum, dim3((O + 31) / 32, w.groups), dim3(256), 0, s,
+                         static_cast<const float*>(csum), (long long)O, w.zpg, (long long)O, gs,
+                         (long long)O, O, 0LL, 0);
+      PC_HIP_CHECK_LAUNCH("k_slab_sum (groups)");
+    }
+    if (db) {
+      const bool from_groups = w.groups > 1 || gsum;
+      hipLaunchKernelGGL(k_slab_sum, dim3((O + 31) / 32, 1), dim3(256), 0, s,
+                         static_cast<const float*>(from_groups ? gs : csum), (long long)O,
+                         from_groups ? w.groups : w.nz, (long long)O, db, 0LL, O, 0LL, accumulate);
+      PC_HIP_CHECK_LAUNCH("k_slab_sum (db)");
+    }
+  }
   return PCADV_OK;
 }
 
+constexpr int CS_ROWS = 128;  // rows per colsum chunk (enough workgroups to fill the chip)
+
 size_t colsum_workspace_bytes(int M, int N) {
-  const int nchunk = (M + 1023) / 1024;
+  const int nchunk = (M + CS_ROWS - 1) / CS_ROWS;
   return (size_t)nchunk * N * sizeof(float) + 256;
 }
 
@@ -608,11 +823,11 @@ int launch_group_colsum(const float* x, const float* ymask, long long ld, long l
 int launch_colsum(const float* x, const float* ymask, long long ld, long long ldm, int M, int N,
                   float* out, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
   PC_REQUIRE(x && out && M > 0 && N > 0, "colsum: bad shape");
-  const int nchunk = (M + 1023) / 1024;
+  const int nchunk = (M + CS_ROWS - 1) / CS_ROWS;
   PC_REQUIRE(ws && ws_bytes >= colsum_workspace_bytes(M, N), "colsum: workspace");
   float* part = static_cast<float*>(ws);
   hipLaunchKernelGGL(k_colsum_part, dim3((N + 63) / 64, nchunk), dim3(256), 0, s, x, ymask, ld,
-                     ldm, M, N, 1024, part);
+                     ldm, M, N, CS_ROWS, part);
   PC_HIP_CHECK_LAUNCH("k_colsum_part");
   hipLaunchKernelGGL(k_colsum_fin, dim3((N + 255) / 256), dim3(256), 0, s, part, nchunk, N, out,
                      accumulate);
@@ -643,7 +858,7 @@ int launch_conv_max_x3(const float* x, long long ldx, int C, int Npts, int K, co
     p.avec = ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
     p.bvec = K % 4 == 0 && ((uintptr_t)w & 15) == 0;
     p.rows_per_group = Npts;
-    p.M = C * Npts; p.N = O; p.K = K; p.ksplit_len = K;
+    p.M = C * Npts; p.N = O; p.K = K; p.grp = K; p.zpg = 1; p.ksplit_len = K;
     p.part = part;
     static bool attr = false;
     if (!attr) {
@@ -753,106 +968,169 @@ k_cmx_dw(const float* __restrict__ g, const float* __restrict__ gmax,
   if (blockIdx.y == 0 && threadIdx.x == 0 && db) db[o] = sb;
 }
 
-// One workgroup per (cloud, 256-column block of K).  The cloud's live hits
-// (g' != 0) are bucketed by argmax point (counting sort in LDS), each bucket is
-// ordered by o, and each thread then walks the hits for its column, adding one
-// sum per point: a fixed summation order, bitwise reproducible.
-constexpr int CMX_MAXO = 4096, CMX_MAXP = 4096;
+// One workgroup (8 waves) per (64-point range, cloud).  The cloud's live hits
+// (g' != 0) whose argmax falls in the range are marked in a per-point bit set
+// over the channels (LDS atomicOr: order-free), flattened into one list sorted
+// by (point, o) (popcount prefixes), and the list is cut into 8 equal pieces,
+// one per wave, so a point that wins hundreds of channels (a hull point) is
+// spread over the waves instead of serialising one.  A wave walks its piece
+// with its lanes across the K columns (4 per lane per 256), eight hits' loads
+// in flight, and writes a point when the point changes; a point cut by a piece
+// boundary is finished by the wave that holds its first hit, adding the later
+// waves' partial sums in wave order.  Fixed summation order: bitwise
+// reproducible.  relu_x: the additions are masked by [x > 0] at (point,
+// column), the relu' of the layer that produced x (x = relu(previous conv)).
+constexpr int CMX_PTS = 64, CMX_MAXO = 4096, CMX_MAXK = 512, CMX_W = 8, CMX_U = 8;
+constexpr int CMX_T = CMX_MAXK / 256;  // f32x4 column groups per lane
 struct CmxLds {
-  int cnt[CMX_MAXP];   // hits per point, then bucket starts
-  int fill[CMX_MAXP];
-  int ho[CMX_MAXO];    // o of each hit, bucketed by point
-  int hp[CMX_MAXO];    // point of each hit
-  int part[256];
-  int n;
+  unsigned bits[CMX_PTS][CMX_MAXO / 32];
+  int start[CMX_PTS + 1];
+  int list[CMX_MAXO];                 // (point in range) << 16 | o, sorted
+  float carry[CMX_W][CMX_MAXK];       // a wave's partial sum of the point it starts inside
+  int carry_pt[CMX_W];
 };
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(CMX_W * 64)
 k_cmx_dx(const float* __restrict__ g, const float* __restrict__ gmax,
          const int32_t* __restrict__ gidx, int Npts, int O, int K, const float* __restrict__ w,
-         float* __restrict__ dx, long long lddx) {
+         const float* __restrict__ x, long long ldx, int relu_x, float* __restrict__ dx,
+         long long lddx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CmxLds& L = *reinterpret_cast<CmxLds*>(smem);
-  const int c = blockIdx.x, tid = threadIdx.x, col = blockIdx.y * 256 + tid;
-  for (int p = tid; p < Npts; p += 256) {
-    L.cnt[p] = 0;
-    L.fill[p] = 0;
-  }
+  const int c = blockIdx.y, p0 = blockIdx.x * CMX_PTS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = (O + 31) / 32;
+  for (int i = tid; i < CMX_PTS * nw; i += CMX_W * 64) L.bits[i / nw][i % nw] = 0u;
   __syncthreads();
-  for (int o = tid; o < O; o += 256)
-    if (gmax[(size_t)c * O + o] > 0.f && g[(size_t)c * O + o] != 0.f)
-      atomicAdd(&L.cnt[gidx[(size_t)c * O + o]], 1);
-  __syncthreads();
-  // exclusive scan of cnt over the points: per-thread runs, then the run totals
-  const int per = (Npts + 255) / 256, p0 = tid * per;
-  int run = 0;
-  for (int p = p0; p < min(Npts, p0 + per); ++p) run += L.cnt[p];
-  L.part[tid] = run;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int t = 0; t < 256; ++t) {
-      const int v = L.part[t];
-      L.part[t] = acc;
-      acc += v;
+  for (int o = tid; o < O; o += CMX_W * 64) {
+    const size_t co = (size_t)c * O + o;
+    if (gmax[co] > 0.f && g[co] != 0.f) {
+      const int pl = gidx[co] - p0;
+      if (pl >= 0 && pl < CMX_PTS) atomicOr(&L.bits[pl][o >> 5], 1u << (o & 31));
     }
-    L.n = acc;
   }
   __syncthreads();
-  int off = L.part[tid];
-  for (int p = p0; p < min(Npts, p0 + per); ++p) {
-    const int v = L.cnt[p];
-    L.cnt[p] = off;
-    off += v;
-  }
-  __syncthreads();
-  for (int o = tid; o < O; o += 256)
-    if (gmax[(size_t)c * O + o] > 0.f && g[(size_t)c * O + o] != 0.f) {
-      const int p = gidx[(size_t)c * O + o];
-      const int pos = L.cnt[p] + atomicAdd(&L.fill[p], 1);
-      L.ho[pos] = o;
-      L.hp[pos] = p;
+  // hits per point (wave 0, a lane per point), exclusive scan -> start[]
+  if (wave == 0) {
+    int cnt = 0;
+    for (int i = 0; i < nw; ++i) cnt += __popc(L.bits[lane][i]);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
     }
+    L.start[lane] = incl - cnt;
+    if (lane == 63) L.start[CMX_PTS] = incl;
+  }
   __syncthreads();
-  // order each bucket by o (buckets are short: insertion sort, a thread per point)
-  for (int p = tid; p < Npts; p += 256) {
-    const int s0 = L.cnt[p], len = L.fill[p];
-    for (int i = s0 + 1; i < s0 + len; ++i) {
-      const int v = L.ho[i];
-      int j = i - 1;
-      while (j >= s0 && L.ho[j] > v) {
-        L.ho[j + 1] = L.ho[j];
-        --j;
+  // flatten: wave w lists the points w, w + 8, ... (their o in increasing order)
+  for (int pl = wave; pl < CMX_PTS; pl += CMX_W) {
+    int pos0 = L.start[pl];
+    for (int w0 = 0; w0 < nw; w0 += 64) {
+      const unsigned word = w0 + lane < nw ? L.bits[pl][w0 + lane] : 0u;
+      const int cnt = __popc(word);
+      int incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
       }
-      L.ho[j + 1] = v;
+      int pos = pos0 + incl - cnt;
+      for (unsigned bw = word; bw; bw &= bw - 1)
+        L.list[pos++] = (pl << 16) | ((w0 + lane) * 32 + __builtin_ctz(bw));
+      pos0 += __shfl(incl, 63);
     }
   }
+  if (tid < CMX_W) L.carry_pt[tid] = -1;
   __syncthreads();
-  if (col >= K) return;
-  const int n = L.n;
-  float acc = 0.f;
-  int cur = n > 0 ? L.hp[0] : -1;
-  for (int i = 0; i < n; ++i) {
-    const int p = L.hp[i], o = L.ho[i];
-    if (p != cur) {
-      float* d = dx + (size_t)(c * Npts + cur) * lddx + col;
-      *d += acc;
-      acc = 0.f;
-      cur = p;
+  const int H = L.start[CMX_PTS];
+  const int chunk = (H + CMX_W - 1) / CMX_W;
+  const int lo = min(H, wave * chunk), hi = min(H, lo + chunk);
+  const bool has = lo < hi;
+  const int lead = has ? L.list[lo] >> 16 : -1;
+  const bool lead_cut = has && lo > 0 && (L.list[lo - 1] >> 16) == lead;  // started in an earlier piece
+  const bool tail_cut = has && hi < H && (L.list[hi] >> 16) == (L.list[hi - 1] >> 16);  // continues
+  f32x4 acc[CMX_T];
+#pragma unroll
+  for (int t = 0; t < CMX_T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto write_point = [&](int pl) {  // dx[point] += acc (masked), or hand acc on as a carry
+    if (pl == lead && lead_cut) {
+#pragma unroll
+      for (int t = 0; t < CMX_T; ++t)
+        *reinterpret_cast<f32x4*>(&L.carry[wave][256 * t + 4 * lane]) = acc[t];
+      if (lane == 0) L.carry_pt[wave] = pl;
+      return;
     }
-    acc = fmaf(g[(size_t)c * O + o], w[(size_t)o * K + col], acc);
+    const size_t row = (size_t)c * Npts + p0 + pl;
+#pragma unroll
+    for (int t = 0; t < CMX_T; ++t) {
+      const int col = 256 * t + 4 * lane;
+      if (col >= K) continue;
+      f32x4* d = reinterpret_cast<f32x4*>(dx + row * lddx + col);
+      f32x4 v = *d, a = acc[t];
+      if (relu_x) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(x + row * ldx + col);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = xv[u] > 0.f ? a[u] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] += a[u];
+      *d = v;
+    }
+  };
+  int cur = lead;
+  for (int i0 = lo; i0 < hi; i0 += CMX_U) {
+    int e[CMX_U];
+    float gv[CMX_U];
+    f32x4 wv[CMX_U][CMX_T];
+#pragma unroll
+    for (int u = 0; u < CMX_U; ++u) {  // every load of the group first
+      const int i = min(i0 + u, hi - 1);
+      e[u] = L.list[i];
+      const int o = e[u] & 0xffff;
+      gv[u] = i0 + u < hi ? g[(size_t)c * O + o] : 0.f;
+#pragma unroll
+      for (int t = 0; t < CMX_T; ++t) {
+        const int col = min(256 * t + 4 * lane, K - 4);
+        wv[u][t] = *reinterpret_cast<const f32x4*>(w + (size_t)o * K + col);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CMX_U; ++u) {
+      if (i0 + u >= hi) break;
+      const int pl = e[u] >> 16;
+      if (pl != cur) {
+        write_point(cur);
+#pragma unroll
+        for (int t = 0; t < CMX_T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        cur = pl;
+      }
+#pragma unroll
+      for (int t = 0; t < CMX_T; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[t][q] = fmaf(gv[u], wv[u][t][q], acc[t][q]);
+    }
   }
-  if (n > 0) {
-    float* d = dx + (size_t)(c * Npts + cur) * lddx + col;
-    *d += acc;
-  }
+  const bool owner_of_tail = tail_cut && !(cur == lead && lead_cut);
+  if (has && !owner_of_tail) write_point(cur);
+  __syncthreads();  // carries written
+  if (!owner_of_tail) return;
+  for (int w2 = wave + 1; w2 < CMX_W && L.carry_pt[w2] == cur; ++w2)
+#pragma unroll
+    for (int t = 0; t < CMX_T; ++t) {
+      const f32x4 cv = *reinterpret_cast<const f32x4*>(&L.carry[w2][256 * t + 4 * lane]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[t][q] += cv[q];
+    }
+  write_point(cur);
 }
 
 int launch_cmx_bwd(const float* g, const float* gmax, const int32_t* gidx, const float* x,
                    long long ldx, int C, int Npts, int O, int K, const float* w, float* dw,
-                   float* db, float* dx, long long lddx, hipStream_t s) {
-  PC_REQUIRE(g && gmax && gidx && x && w && C > 0 && Npts > 0 && Npts <= CMX_MAXP && O > 0 &&
-                 O <= CMX_MAXO && K > 0 && K % 4 == 0 && ldx % 4 == 0,
+                   float* db, float* dx, long long lddx, int relu_x, hipStream_t s) {
+  PC_REQUIRE(g && gmax && gidx && x && w && C > 0 && Npts > 0 && O > 0 && O <= CMX_MAXO && K > 0 &&
+                 O < 65536 && K % 4 == 0 && ldx % 4 == 0 && (!dx || (K <= CMX_MAXK && lddx % 4 == 0)),
              "cmx_bwd: bad shape C=%d N=%d O=%d K=%d", C, Npts, O, K);
   if (dw) {
     hipLaunchKernelGGL(k_cmx_dw, dim3(O, (K + 511) / 512), dim3(128), 0, s, g, gmax, gidx, x, ldx,
@@ -870,8 +1148,8 @@ int launch_cmx_bwd(const float* g, const float* gmax, const int32_t* gidx, const
       }
       attr = true;
     }
-    hipLaunchKernelGGL(k_cmx_dx, dim3(C, (K + 255) / 256), dim3(256), sizeof(CmxLds), s, g, gmax,
-                       gidx, Npts, O, K, w, dx, lddx);
+    hipLaunchKernelGGL(k_cmx_dx, dim3((Npts + CMX_PTS - 1) / CMX_PTS, C), dim3(CMX_W * 64), sizeof(CmxLds),
+                       s, g, gmax, gidx, Npts, O, K, w, x, ldx, relu_x, dx, lddx);
     PC_HIP_CHECK_LAUNCH("k_cmx_dx");
   }
   return PCADV_OK;

@@ -35,6 +35,10 @@ __all__ = ["PointNetSeg", "SegTrainStep", "seg_cross_entropy", "seg_forward", "s
 
 _LOC = 960                       # x1..x5 widths 64 + 128 + 128 + 128 + 512
 _FWD_PRECISE = os.environ.get("PCADV_SEG_PRECISE", "0") == "1"  # diagnostics: six-product forward
+# data gradients dX = dZ W: three products (sums over <= 960 terms; 1.2e-5 of
+# sum|a b|) unless PCADV_SEG_DGRAD_PRECISE=1 (six); weight gradients (sums over
+# all B*N points, heavy cancellation) always take six
+_DGRAD_PRECISE = os.environ.get("PCADV_SEG_DGRAD_PRECISE", "0") == "1"
 _OFF = [0, 64, 192, 320, 448, 960]
 _CONV = [(3, 64), (64, 128), (128, 128), (128, 128), (128, 512), (512, 2048)]
 
@@ -53,24 +57,25 @@ class _Engine:
     def __init__(self):
         self.lib = _lib.load()
 
-    def gemm(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, amask=None, ldm=0, bias=None,
+    def gemm(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, cmask=None, ldm=0, bias=None,
              bias_rows=None, rows_per_group=0, relu=False, accumulate=False, precise=False,
              a_off=0, b_off=0, c_off=0, m_off=0):
-        check(self.lib.pcadv_gemm(_p(a, a_off), lda, ta, None if amask is None else _p(amask, m_off),
-                                  ldm, _p(b, b_off), ldb, tb, _p(c, c_off), ldc, M, N, K,
-                                  None if bias is None else _p(bias),
+        check(self.lib.pcadv_gemm(_p(a, a_off), lda, ta, _p(b, b_off), ldb, tb, _p(c, c_off), ldc,
+                                  M, N, K, None if bias is None else _p(bias),
                                   None if bias_rows is None else _p(bias_rows), rows_per_group,
-                                  int(relu), int(accumulate), int(precise), stream_ptr()),
+                                  int(relu), int(accumulate),
+                                  None if cmask is None else _p(cmask, m_off), ldm, int(precise),
+                                  stream_ptr()),
               "pcadv_gemm")
 
-    def wgrad(self, dz, ldz, x, ldx, rows, O, K, dw, ldo, *, ymask=None, ldm=0, dz_off=0,
-              x_off=0, m_off=0, dw_off=0):
-        nb = self.lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K)
+    def wgrad(self, dz, ldz, x, ldx, rows, O, K, dw, ldo, *, db=None, gsum=None, rpg=0, dz_off=0,
+              x_off=0, dw_off=0):
+        nb = self.lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K, rpg)
         ws = _ws(nb, dz.device)
-        check(self.lib.pcadv_gemm_wgrad(_p(dz, dz_off), ldz,
-                                        None if ymask is None else _p(ymask, m_off), ldm,
-                                        _p(x, x_off), ldx, rows, O, K, _p(dw, dw_off), ldo, 0,
-                                        _p(ws), ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
+        check(self.lib.pcadv_gemm_wgrad(_p(dz, dz_off), ldz, _p(x, x_off), ldx, rows, O, K,
+                                        _p(dw, dw_off), ldo, None if db is None else _p(db),
+                                        None if gsum is None else _p(gsum), rpg, 0, _p(ws),
+                                        ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
 
     def colsum(self, x, ld, M, N, out, *, ymask=None, ldm=0, x_off=0, m_off=0):
         nb = self.lib.pcadv_colsum_workspace_bytes(M, N)
@@ -172,48 +177,44 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
     M = B * N
     dev = xloc.device
     dl = torch.zeros(M, ncls, device=dev) if dlogits is None else dlogits.reshape(M, ncls).contiguous()
-    g = {}
-    # ---- fc4 .. fc2 (dz = dy relu'(y) is applied as A is staged) ---------
+    # Every data-gradient GEMM applies the relu' of the layer below in its
+    # epilogue (cmask), so each dz is stored masked once and read as is by the
+    # weight gradient (which also forms the bias gradient) and the next GEMM.
     def _g(k, like):  # the k-th gradient (state_dict order): caller's buffer or a new one
         if out is not None:
             return out[k].view(like.shape) if hasattr(like, "shape") else out[k]
         return torch.empty_like(like) if hasattr(like, "shape") else torch.empty(like, device=dev)
+    # ---- fc4 .. fc2 -------------------------------------------------------
     dW4 = _g(18, Wf[3]); db4 = _g(19, ncls)
-    E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128)
-    E.colsum(dl, ncls, M, ncls, db4)
+    E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128, db=db4)
     dh3 = torch.empty(M, 128, device=dev)
-    E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, precise=True)
+    E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3, ldm=128, precise=_DGRAD_PRECISE)
     dW3 = _g(16, Wf[2]); db3 = _g(17, 128)
-    E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, ymask=h3, ldm=128)
-    E.colsum(dh3, 128, M, 128, db3, ymask=h3, ldm=128)
+    E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, db=db3)
     dh2 = torch.empty(M, 256, device=dev)
-    E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, amask=h3, ldm=128, precise=True)
+    E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2, ldm=256, precise=_DGRAD_PRECISE)
     dW2 = _g(14, Wf[1]); db2 = _g(15, 256)
-    E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, ymask=h2, ldm=256)
-    E.colsum(dh2, 256, M, 256, db2, ymask=h2, ldm=256)
+    E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, db=db2)
     dh1 = torch.empty(M, 256, device=dev)
-    E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, amask=h2, ldm=256, precise=True)
-    # ---- fc1: local columns, then the per-cloud (tiled) columns ----------
+    E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1, ldm=256, precise=_DGRAD_PRECISE)
+    # ---- fc1: local columns (+ per-cloud sums s1), then the tiled columns --
     W1 = Wf[0]
-    dW1 = _g(12, W1)
-    E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, ymask=h1, ldm=256)
+    dW1 = _g(12, W1); db1 = _g(13, 256)
     s1 = torch.empty(B, 256, device=dev)  # per-cloud sums of dz1
-    E.group_colsum(dh1, 256, M, 256, N, s1, ymask=h1, ldm=256)
+    E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N)
     E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960)
     E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008)
-    db1 = _g(13, 256)
-    E.colsum(s1, 256, B, 256, db1)
     dloc = torch.empty(M, _LOC, device=dev)
-    E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, amask=h1, ldm=256, precise=True)
+    E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc, ldm=_LOC, precise=_DGRAD_PRECISE)
     dg = torch.empty(B, 2048, device=dev)
-    E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=True)
+    E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=_DGRAD_PRECISE)
     if dgmax_out is not None:
         dg += dgmax_out.reshape(B, 2048)
     # ---- conv6 + ReLU + max: the gradient reaches the argmax points -------
     dW6 = _g(10, W[5]); db6 = _g(11, 2048)
     check(E.lib.pcadv_conv_max_x3_bwd(_p(dg), _p(gmax), _p(gidx), _p(xloc, _OFF[4]), _LOC, B,
                                       N, 2048, 512, _p(W[5]), _p(dW6), _p(db6),
-                                      _p(dloc, _OFF[4]), _LOC, stream_ptr()),
+                                      _p(dloc, _OFF[4]), _LOC, 1, stream_ptr()),
           "pcadv_conv_max_x3_bwd")
     # ---- conv5 .. conv1 (each layer's output gradient also carries fc1's) --
     dWc = [None] * 6
@@ -224,16 +225,13 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         dWc[i] = _g(2 * i, W[i])
         dbc[i] = _g(2 * i + 1, O)
         if i > 0:
-            E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, ymask=xloc, ldm=_LOC,
-                    dz_off=_OFF[i], m_off=_OFF[i], x_off=_OFF[i - 1])
-        else:
-            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, ymask=xloc, ldm=_LOC,
-                    dz_off=_OFF[i], m_off=_OFF[i])
-        E.colsum(dloc, _LOC, M, O, dbc[i], ymask=xloc, ldm=_LOC, x_off=_OFF[i], m_off=_OFF[i])
-        if i > 0:
-            E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, amask=xloc, ldm=_LOC,
-                   accumulate=True, precise=True, a_off=_OFF[i], m_off=_OFF[i],
+            E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i],
+                    x_off=_OFF[i - 1])
+            E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, cmask=xloc, ldm=_LOC,
+                   accumulate=True, precise=_DGRAD_PRECISE, a_off=_OFF[i], m_off=_OFF[i - 1],
                    c_off=_OFF[i - 1])
+        else:
+            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i])
     grads = []
     for i in range(6):
         grads += [dWc[i].view(O_shape(i)), dbc[i]]

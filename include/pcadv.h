@@ -199,21 +199,28 @@ int pcadv_linear_bwd(const float* dy, const float* y, int act,
  * pcadv_gemm: C[m][n] (+)= sum_k A[m][k] B[n][k] (+ bias[n] + bias_rows[m /
  * rows_per_group][n]), ReLU optional.  A[m][k] = a[m*lda + k] (ta = 0) or
  * a[k*lda + m] (ta = 1, only with tb = 1); B[n][k] = b[n*ldb + k] (tb = 0: a
- * weight [out][in], the forward) or b[k*ldb + n] (tb = 1: dX = dZ W).  amask
- * (nullable, stored like A with stride ldm) zeroes A where amask <= 0 (relu'
- * of a layer output).  accumulate = 1 adds into C.  precise = 1 multiplies six
- * products of hi/mid/lo splits instead (f32-level accuracy; the gradients). */
-int pcadv_gemm(const float* a, int64_t lda, int ta, const float* amask, int64_t ldm,
-               const float* b, int64_t ldb, int tb, float* c, int64_t ldc, int M, int N, int K,
-               const float* bias, const float* bias_rows, int rows_per_group, int relu,
-               int accumulate, int precise, hipStream_t stream);
+ * weight [out][in], the forward) or b[k*ldb + n] (tb = 1: dX = dZ W).
+ * accumulate = 1 adds into C.  cmask (nullable, stored like C with stride ldm)
+ * then zeroes C where cmask <= 0: the producer of a data gradient applies the
+ * relu' of the layer below, so every consumer reads dZ = dY relu'(Y) already
+ * masked.  precise = 1 multiplies six products of hi/mid/lo splits instead
+ * (f32-level accuracy; the gradients). */
+int pcadv_gemm(const float* a, int64_t lda, int ta, const float* b, int64_t ldb, int tb,
+               float* c, int64_t ldc, int M, int N, int K, const float* bias,
+               const float* bias_rows, int rows_per_group, int relu, int accumulate,
+               const float* cmask, int64_t ldm, int precise, hipStream_t stream);
 
 /* Weight gradient dw[o][k] (row stride ldo) (+)= sum over `rows` points of
- * dz[p][o] [ymask[p][o] > 0] x[p][k]: six-product (f32-level) GEMM over
- * fixed-order slabs of the point axis. */
-size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin);
-int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* ymask, int64_t ldm,
-                     const float* x, int64_t ldx, int rows, int O, int Kin, float* dw, int64_t ldo,
+ * dz[p][o] x[p][k]: six-product (f32-level) GEMM over fixed-order slabs of the
+ * point axis.  db (nullable) (+)= the column sums of dz (the bias gradient);
+ * gsum (nullable, needs rows_per_group > 0 dividing rows) = the sums of dz over
+ * each group of rows_per_group rows ([rows / rows_per_group][O], overwritten:
+ * fc1's per-cloud sums).  Both come from the staged dz, no second pass.
+ * rows_per_group (0 = one group) also sets the slab plan, so pass the same
+ * value to the workspace query. */
+size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group);
+int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows, int O,
+                     int Kin, float* dw, int64_t ldo, float* db, float* gsum, int rows_per_group,
                      int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Column sums (bias gradients): out[n] (+)= sum_m x[m][n] [ymask[m][n] > 0];
@@ -235,11 +242,13 @@ int pcadv_conv_max_x3(const float* x, int64_t ldx, int C, int Npts, int K, const
                       const float* b, int O, int relu, float* gmax, int32_t* gidx,
                       void* workspace, size_t workspace_bytes, hipStream_t stream);
 /* Its backward: g' = dgmax [gmax > 0]; dw [O][K] and db [O] overwritten
- * (nullable), dx rows (stride lddx, nullable) accumulated: deterministic. */
+ * (nullable), dx rows (stride lddx, nullable, K <= 512) accumulated:
+ * deterministic.  relu_x = 1 masks the dx additions by [x > 0] (x the output
+ * of a ReLU layer: the gradient leaves already multiplied by its relu'). */
 int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* gidx,
                           const float* x, int64_t ldx, int C, int Npts, int O, int K,
                           const float* w, float* dw, float* db, float* dx, int64_t lddx,
-                          hipStream_t stream);
+                          int relu_x, hipStream_t stream);
 
 /* CrossEntropyLoss over rows (the per-point segmentation loss, mean over M
  * points): *loss, and dlogits = scale * dL/dlogits (same stride ld). */

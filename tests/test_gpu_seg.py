@@ -56,56 +56,66 @@ def test_gemm_forward_vs_fp64(M, N, K):
     C = torch.empty(M, N, device=DEV)
     rpg = (M + 1) // 2
     tA, tW, tb, tbr = _t(A), _t(W), _t(b), _t(br)  # alive across the launch
-    check(lib.pcadv_gemm(_p(tA), K, 0, None, 0, _p(tW), K, 0, _p(C), N, M, N, K, _p(tb), _p(tbr),
-                         rpg, 1, 0, 0, stream_ptr()), "gemm")
+    check(lib.pcadv_gemm(_p(tA), K, 0, _p(tW), K, 0, _p(C), N, M, N, K, _p(tb), _p(tbr),
+                         rpg, 1, 0, None, 0, 0, stream_ptr()), "gemm")
     ref = A.astype(np.float64) @ W.astype(np.float64).T + b + br[np.arange(M) // rpg]
     ref = np.maximum(ref, 0)
     assert (np.abs(C.cpu().numpy() - ref) <= _bound(A, W) + 1e-6).all()
 
 
 def test_gemm_data_grad_masked_accumulate():
-    """dX (+)= (dY * [Y > 0]) W with a strided, offset output (the seg backward's form)."""
+    """dX = [Y > 0] (dX + dZ W) with a strided, offset output and a mask stored
+    like it (the seg backward's form: the producer applies the next relu')."""
     lib = _lib.load()
     rng = np.random.default_rng(3)
     M, O, K = 517, 128, 64
-    dY = rng.standard_normal((M, O)).astype(np.float32)
-    Y = rng.standard_normal((M, O)).astype(np.float32)
+    dZ = rng.standard_normal((M, O)).astype(np.float32)
+    Y = rng.standard_normal((M, 200)).astype(np.float32)
     W = rng.standard_normal((O, K)).astype(np.float32)
     base = rng.standard_normal((M, 200)).astype(np.float32)
     out = _t(base)
-    tdY, tY, tW = _t(dY), _t(Y), _t(W)
-    check(lib.pcadv_gemm(_p(tdY), O, 0, _p(tY), O, _p(tW), K, 1, _p(out, 64), 200, M, K, O,
-                         None, None, 0, 0, 1, 1, stream_ptr()), "gemm")
-    dz = dY * (Y > 0)
+    tdZ, tY, tW = _t(dZ), _t(Y), _t(W)
+    check(lib.pcadv_gemm(_p(tdZ), O, 0, _p(tW), K, 1, _p(out, 64), 200, M, K, O, None, None, 0, 0,
+                         1, _p(tY, 64), 200, 1, stream_ptr()), "gemm")
     ref = base.astype(np.float64).copy()
-    ref[:, 64:128] += dz.astype(np.float64) @ W.astype(np.float64)
+    ref[:, 64:128] = (ref[:, 64:128] + dZ.astype(np.float64) @ W.astype(np.float64)) * (Y[:, 64:128] > 0)
     got = out.cpu().numpy()
     # six-product (precise) form: f32-level, 1e-6 of sum|a b|
-    assert (np.abs(got[:, 64:128] - ref[:, 64:128]) <= _bound(dz, W.T) / 20 + 1e-5).all()
+    assert (np.abs(got[:, 64:128] - ref[:, 64:128]) <= _bound(dZ, W.T) / 20 + 1e-5).all()
+    assert (got[:, 64:128][Y[:, 64:128] <= 0] == 0).all()
     assert np.array_equal(got[:, :64], base[:, :64]) and np.array_equal(got[:, 128:], base[:, 128:])
 
 
-@pytest.mark.parametrize("rows", [300, 32768])
-def test_gemm_weight_grad(rows):
+@pytest.mark.parametrize("rows,rpg,O,K", [(300, 100, 96, 40), (32768, 2048, 96, 40),
+                                          (32768, 0, 256, 960), (16, 0, 256, 2048),
+                                          (4096, 0, 64, 3)])
+def test_gemm_weight_grad(rows, rpg, O, K):
+    """dW = dZ^T X over fixed-order slabs, with the bias gradient and the
+    per-group (per-cloud) sums taken from the staged dZ."""
     lib = _lib.load()
-    rng = np.random.default_rng(rows)
-    O, K = 96, 40
-    dZ = rng.standard_normal((rows, O)).astype(np.float32)
-    Y = rng.standard_normal((rows, O)).astype(np.float32)
+    rng = np.random.default_rng(rows + O)
+    dZ = rng.standard_normal((rows, O)).astype(np.float32) * (rng.random((rows, O)) > 0.5)
     X = rng.standard_normal((rows, K)).astype(np.float32)
     dW = torch.empty(O, K, device=DEV)
-    nb = lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K)
+    db = torch.empty(O, device=DEV)
+    G = rows // rpg if rpg else 1
+    gs = torch.empty(G, O, device=DEV)
+    nb = lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K, rpg)
     ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
-    tdZ, tY, tX = _t(dZ), _t(Y), _t(X)
-    check(lib.pcadv_gemm_wgrad(_p(tdZ), O, _p(tY), O, _p(tX), K, rows, O, K, _p(dW), K, 0,
-                               _p(ws), nb, stream_ptr()), "wgrad")
-    dz = dZ * (Y > 0)
-    ref = dz.T.astype(np.float64) @ X.astype(np.float64)
-    assert (np.abs(dW.cpu().numpy() - ref) <= _bound(dz.T, X.T) / 20 + 1e-5).all()
-    a = dW.clone()
-    check(lib.pcadv_gemm_wgrad(_p(tdZ), O, _p(tY), O, _p(tX), K, rows, O, K, _p(dW), K, 0,
-                               _p(ws), nb, stream_ptr()), "wgrad")
-    assert torch.equal(a, dW)  # fixed-order slabs: bitwise reproducible
+    tdZ, tX = _t(dZ), _t(X)
+    args = (_p(tdZ), O, _p(tX), K, rows, O, K, _p(dW), K, _p(db), _p(gs) if rpg else None, rpg, 0,
+            _p(ws), nb, stream_ptr())
+    check(lib.pcadv_gemm_wgrad(*args), "wgrad")
+    ref = dZ.T.astype(np.float64) @ X.astype(np.float64)
+    assert (np.abs(dW.cpu().numpy() - ref) <= _bound(dZ.T, X.T) / 20 + 1e-5).all()
+    d64 = dZ.astype(np.float64)
+    assert np.abs(db.cpu().numpy() - d64.sum(0)).max() <= 1e-5 * max(1.0, np.abs(d64).sum(0).max())
+    if rpg:
+        rg = d64.reshape(G, rpg, O).sum(1)
+        assert np.abs(gs.cpu().numpy() - rg).max() <= 1e-5 * max(1.0, np.abs(d64).sum(0).max())
+    a, a_db = dW.clone(), db.clone()
+    check(lib.pcadv_gemm_wgrad(*args), "wgrad")
+    assert torch.equal(a, dW) and torch.equal(a_db, db)  # fixed-order slabs: bitwise reproducible
 
 
 def test_colsum_and_group_colsum():
@@ -161,7 +171,8 @@ def test_conv_max_x3_vs_oracle(C, N):
         assert abs(z[c, gi[c, o], o] - z[c, am[c, o], o]) <= 1e-5 * max(1.0, abs(z[c, am[c, o], o]))
 
 
-def test_conv_max_x3_backward_vs_numpy():
+@pytest.mark.parametrize("relu_x", [0, 1])
+def test_conv_max_x3_backward_vs_numpy(relu_x):
     lib = _lib.load()
     rng = np.random.default_rng(9)
     C, N, K, O = 2, 300, 512, 2048
@@ -176,16 +187,57 @@ def test_conv_max_x3_backward_vs_numpy():
     dx = _t(base)
     tdg, tgm, tgi, tw = _t(dg), _t(gm), _t(gi, torch.int32), _t(w)
     check(lib.pcadv_conv_max_x3_bwd(_p(tdg), _p(tgm), _p(tgi), _p(xt), K, C, N, O, K, _p(tw),
-                                    _p(dw), _p(db), _p(dx), K, stream_ptr()), "cmx_bwd")
+                                    _p(dw), _p(db), _p(dx), K, relu_x, stream_ptr()), "cmx_bwd")
     gp = dg * (gm > 0)
     rdw = np.zeros((O, K))
     rdx = base.astype(np.float64).reshape(C, N, K).copy()
     for c in range(C):
         rdw += gp[c][:, None] * x[c, gi[c]]
-        np.add.at(rdx[c], gi[c], gp[c][:, None] * w)
+        add = np.zeros((N, K))
+        np.add.at(add, gi[c], gp[c][:, None] * w)
+        rdx[c] += add * (x[c] > 0) if relu_x else add
     assert np.abs(dw.cpu().numpy() - rdw).max() <= 1e-5 * np.abs(rdw).max()
     assert np.abs(db.cpu().numpy() - gp.sum(0)).max() <= 1e-5 * np.abs(gp).sum(0).max()
     assert np.abs(dx.cpu().numpy().reshape(C, N, K) - rdx).max() <= 1e-5 * np.abs(rdx).max()
+
+
+@pytest.mark.parametrize("pattern", ["hull", "one_point", "sparse"])
+def test_conv_max_x3_backward_heavy_points(pattern):
+    """The sparse max backward when a few points win most channels (hull
+    points of a cloud; every channel on one point) or only a few channels are
+    live: the hit list of a 64-point range is cut across the 8 waves and the
+    cut points are finished in wave order.  Bitwise reproducible."""
+    lib = _lib.load()
+    rng = np.random.default_rng({"hull": 1, "one_point": 2, "sparse": 3}[pattern])
+    C, N, K, O = 3, 700, 512, 2048
+    x = np.maximum(rng.standard_normal((C * N, K)), 0).astype(np.float32)
+    w = rng.standard_normal((O, K)).astype(np.float32)
+    gm = rng.random((C, O)).astype(np.float32) + 0.1
+    if pattern == "hull":
+        gi = rng.choice([3, 64, 65, 130, 699], size=(C, O)).astype(np.int32)
+    elif pattern == "one_point":
+        gi = np.full((C, O), 70, np.int32)
+    else:
+        gi = rng.integers(0, N, (C, O)).astype(np.int32)
+        gm[rng.random((C, O)) < 0.95] = -1.0  # relu'd away
+    dg = rng.standard_normal((C, O)).astype(np.float32)
+    base = rng.standard_normal((C * N, K)).astype(np.float32)
+    tdg, tgm, tgi, tw, tx = _t(dg), _t(gm), _t(gi, torch.int32), _t(w), _t(x)
+    outs = []
+    for _ in range(2):
+        dx = _t(base)
+        check(lib.pcadv_conv_max_x3_bwd(_p(tdg), _p(tgm), _p(tgi), _p(tx), K, C, N, O, K, _p(tw),
+                                        None, None, _p(dx), K, 1, stream_ptr()), "cmx_bwd")
+        outs.append(dx.cpu())
+    assert torch.equal(outs[0], outs[1])
+    gp = (dg * (gm > 0)).astype(np.float64)
+    rdx = base.astype(np.float64).reshape(C, N, K).copy()
+    for c in range(C):
+        add = np.zeros((N, K))
+        np.add.at(add, gi[c], gp[c][:, None] * w)
+        rdx[c] += add * (x.reshape(C, N, K)[c] > 0)
+    err = np.abs(outs[0].numpy().reshape(C, N, K) - rdx).max()
+    assert err <= 1e-5 * np.abs(rdx).max(), err
 
 
 def test_row_ce_vs_oracle():
