@@ -86,6 +86,39 @@ def cpu_baseline(seconds):
             "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N=1024, fp32) in {dt:.1f}s"}
 
 
+def cpu_baseline_seg(seconds, Bs, Ns):
+    """The numpy oracle's PointNetSeg training step (forward, per-point CE,
+    backward, Adam) on a bounded sample of the seg workload: B=2 clouds of
+    N=2048 points per step, timed on this host's cores."""
+    from oracle import pointnet_np as onp
+    P = onp.make_params(onp.seg_spec(50), seed=8, init="xavier")
+    opt = onp.Adam(P)
+    rng = np.random.default_rng(2000)
+    b = 2
+    pts = rng.uniform(-1, 1, (b, Ns, 3)).astype(np.float32)
+    cls = np.zeros((b, 1, 16), np.float32)
+    cls[np.arange(b), 0, rng.integers(0, 16, b)] = 1
+    seg = rng.integers(0, 50, (b, Ns))
+
+    def one():
+        _, grads, _, _, _ = onp.seg_step(P, pts, cls, seg)
+        opt.step(grads)
+
+    one()  # warm-up
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        one()
+        steps += 1
+        if time.perf_counter() - t0 >= seconds and steps >= 2:
+            break
+    dt = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"value": round(b * steps / dt, 2), "unit": "clouds/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} numpy-oracle seg steps (B={b}, N={Ns}, fp32, forward+CE+backward+Adam) "
+                      f"in {dt:.1f}s"}
+
+
 def bench_seg(args):
     """BASELINE.json configs[3]: PointNetSeg ShapeNet-part B=16, N=2048, one
     run_training_pointnet_seg iteration (forward, per-point CE, backward, Adam)
@@ -125,6 +158,40 @@ def bench_seg(args):
     dense_bwd = 2 * (per_pt_fwd - 512 * 2048) - 3 * 64
     gflop = 2.0 * Bs * Ns * (per_pt_fwd + dense_bwd) / 1e9
     loss = float(step.loss.item())
+    # dominant kernel: conv6 + ReLU + max over points (pcadv_conv_max_x3: the
+    # screened GEMM k_gemm_x3<0,0,2,3> + the exact re-evaluation k_max_combine),
+    # timed with HIP events on the current stream over the last batch's x5
+    from adversarial_learning_on_pointclouds_amd import seg as segmod
+    from adversarial_learning_on_pointclouds_amd._lib import check, stream_ptr
+    import ctypes
+    params = [p for p in model.parameters()]
+    fw = segmod.seg_forward(pool[(args.steps - 1) % 2][0], pool[(args.steps - 1) % 2][1], params)
+    lib = segmod._engine().lib
+    gmax = torch.empty(Bs, 2048, device=dev)
+    gidx = torch.empty(Bs, 2048, device=dev, dtype=torch.int32)
+    wsb = lib.pcadv_conv_max_x3_workspace_bytes(Bs, Ns, 2048)
+    ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+    W6 = fw["W"][5]
+    b6 = params[11]
+    x5 = ctypes.c_void_p(fw["xloc"].data_ptr() + 4 * segmod._OFF[4])
+
+    def cmx():
+        check(lib.pcadv_conv_max_x3(x5, segmod._LOC, Bs, Ns, 512, ctypes.c_void_p(W6.data_ptr()),
+                                    ctypes.c_void_p(b6.data_ptr()), 2048, 1,
+                                    ctypes.c_void_p(gmax.data_ptr()), ctypes.c_void_p(gidx.data_ptr()),
+                                    ctypes.c_void_p(ws.data_ptr()), wsb, stream_ptr()), "conv_max_x3")
+    for _ in range(3):
+        cmx()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    ev0.record()
+    for _ in range(reps):
+        cmx()
+    ev1.record()
+    torch.cuda.synchronize()
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
+    kflops = 2.0 * Bs * Ns * 512 * 2048
+    kpeak = 2500.0 / 3.0  # three bf16 MFMA products per f32 product (hi/lo splits)
     out = {
         "metric": "point-clouds/sec (seg train step), B=16 N=2048 ShapeNet-part, 1 GPU",
         "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
@@ -134,10 +201,21 @@ def bench_seg(args):
         "config": {"workload": "PointNetSeg(50) + CrossEntropyLoss + Adam, B=16, N=2048 "
                                "(BASELINE configs[3])", "global_batch": Bs, "points": Ns,
                    "parallelism": "dp1", "hip_graph": True},
+        "roofline": {"bound": "mfma",
+                     "kernel": "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3> (conv6 512->2048 screened "
+                               "top-2 per 128-point tile) + k_max_combine (exact f32 re-evaluation)",
+                     "achieved": round(kflops / kern_s / 1e12, 2), "peak": round(kpeak, 1),
+                     "unit": "TFLOP/s", "frac": round(kflops / kern_s / 1e12 / kpeak, 4),
+                     "traffic": None, "avg_launch_us": round(kern_s * 1e6, 2),
+                     "algorithmic_flops_per_launch": kflops,
+                     "algorithmic_bytes_per_launch": Bs * Ns * 512 * 4 + 2048 * 512 * 4 + Bs * 2048 * 8,
+                     "peak_basis": "bf16 2500 TF dense / 3 split products"},
         "step_flops": {"gflop_per_step": round(gflop, 2),
                        "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
     }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_seg(args.cpu_seconds, Bs, Ns)
     print(json.dumps(out), flush=True)
 
 
