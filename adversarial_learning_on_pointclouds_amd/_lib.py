@@ -66,6 +66,7 @@ class AdvArgs(ctypes.Structure):
         ("apply_adam", _i),
         ("losses", _vp), ("logits", _vp),
         ("workspace", _vp), ("workspace_bytes", _sz),
+        ("semi", _i), ("lambda_semi", _f), ("semi_th", _f),
     ]
 
 

@@ -56,13 +56,13 @@ int launch_head_fwd(const float*, const float*, const float*, const int64_t*, in
                     float*, float*, const float*, const float*, float*, float*, hipStream_t);
 int launch_disc_tail(const float*, int, const float*, const float*, const float*, const float*,
                      const float*, const float*, const float*, const float*, const int32_t*,
-                     uint64_t, float, float*, float*, float*, hipStream_t);
+                     uint64_t, float, float*, float*, float*, float*, hipStream_t);
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
 #endif
 int launch_head_bwd(const float*, const float*, const float*, int, const float*, const float*,
-                    float*, float*, float*, float*, const float*, const float*, float*,
-                    hipStream_t);
+                    float*, float*, float*, float*, const float*, const float*, float*, int, float,
+                    float, const float*, const float*, hipStream_t);
 int launch_gemm(const float*, long long, int, const float*, long long, int, float*, long long,
                 int, int, int, const float*, const float*, int, int, int, const float*, long long,
                 int, hipStream_t);
@@ -89,7 +89,7 @@ struct StepWs {
   float *din, *d1, *d2, *d3;
   float *dd3, *dd2, *dd1;
   float *mask;
-  float *lpart, *lpart3, *dslabs;
+  float *lpart, *lpart3, *dslabs, *dout;
   int32_t* gidx;
   void* feat_ws;
   size_t feat_ws_bytes;
@@ -128,6 +128,7 @@ static StepWs carve(int B, int N, char* base) {
   w.lpart = take(head_rowblocks(B));
   w.lpart3 = take(3 * (size_t)disc_rowblocks(B));
   w.dslabs = take((size_t)disc_rowblocks(B) * disc_tail_slab_floats());
+  w.dout = take(R);
   w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
   if (feat_fwd_workspace_bytes((int)C, N) > w.feat_ws_bytes)
     w.feat_ws_bytes = feat_fwd_workspace_bytes((int)C, N);
@@ -204,7 +205,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_TRY(launch_disc_tail(w.d3, B, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, D + PCADV_D_CONV5_W,
                           D + PCADV_D_CONV5_B, D + PCADV_D_FC_W, D + PCADV_D_FC_B, a->soft_gt,
                           a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
-                          s));
+                          w.dout, s));
   // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
   //      input grads of all rows (rows [2B,3B) feed the generator, D frozen) ---
   const int MW = 2 * B;
@@ -225,7 +226,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   //      fc3 input grad; D conv1 weight grad; the four losses -----------------
   PC_TRY(launch_head_bwd(w.dd1, w.d1, w.din, B, D + PCADV_D_CONV1_W, G + PCADV_G_FC3_W, w.dlogits,
                          w.dh2, gD + PCADV_D_CONV1_W, gD + PCADV_D_CONV1_B, w.lpart, w.lpart3,
-                         a->losses, s));
+                         a->losses, a->semi, a->lambda_semi, a->semi_th, logits, w.dout, s));
   // ---- generator head backward (:520); fc3's weight grad rides along -------
   {
     LinBwdExtra ex{};
@@ -265,7 +266,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 2; }
+int pcadv_abi_version(void) { return 3; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 

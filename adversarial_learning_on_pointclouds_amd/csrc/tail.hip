@@ -26,6 +26,13 @@ namespace pcadv {
 
 constexpr int TR = 16;     // rows per workgroup
 constexpr int TT = 1024;   // 16 waves
+
+struct SemiArgs {           // run_training_semi's pseudo-label term (k_head_bwd)
+  int on;
+  float lambda, th;
+  const float* logits;      // [2B][40] generator logits (no-GT rows [B, 2B))
+  const float* dout;        // [3B] D logits (adversarial rows [2B, 3B))
+};
 constexpr int TW = TT / 64;
 
 typedef float f32x4t __attribute__((ext_vector_type(4)));
@@ -289,7 +296,7 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
             const float* __restrict__ bf, const float* __restrict__ soft_gt,
             const float* __restrict__ soft_nogt, const int32_t* __restrict__ step, uint64_t seed,
             float lambda_adv, float* __restrict__ dd3, float* __restrict__ slabs,
-            float* __restrict__ lpart3) {
+            float* __restrict__ lpart3, float* __restrict__ dout) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DiscTailLds& L = *reinterpret_cast<DiscTailLds*>(smem);
   const int tid = threadIdx.x;
@@ -326,6 +333,7 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
     float g = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
     if (m < R) {
       const float x = L.out[tid * 4];
+      if (dout) dout[m] = x;  // the D logits (run_training_semi's confidence, trainer.py:717)
       float y, f;
       if (m < B) {
         y = soft_gt ? ysoft : 0.7f + 0.35f * rng_uniform(seed, stepv, RNG_LABEL_GT, (uint32_t)m);
@@ -404,6 +412,36 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
 // ---------------------------------------------------------------------------
 // k_head_bwd: rows m of the 2B generator outputs (+ conv1 weight-grad blocks)
 // ---------------------------------------------------------------------------
+// run_training_semi's pseudo-label loss (utils/trainer.py:716-728):
+//   ignore = D(lsm_nogt) <= semi_TH, semi_gt = argmax(pred_nogt) (first index),
+//   l_semi = CrossEntropyLoss(ignore_index=255)(pred_nogt, semi_gt): the mean of
+//   -log_softmax(pred_nogt)[semi_gt] over the kept clouds, none when all are
+//   ignored; its gradient lambda_semi (softmax - onehot) / kept reaches the
+//   no-GT logits next to the adversarial one.
+__device__ __forceinline__ void wave_argmax40(float v, int lane, float& mx, int& am) {
+  // (value, index) max over the lanes < 40, lower index on equal values
+  float bv = lane < 40 ? v : -INFINITY;
+  int bi = lane < 40 ? lane : 64;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  mx = bv;
+  am = bi;
+}
+
+__device__ __forceinline__ int semi_kept(const float* dout, int B, float th, int lane) {
+  int c = 0;
+  for (int j = lane; j < B; j += 64) c += dout[2 * B + j] > th ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  return c;
+}
 struct HeadBwdLds {
   float w1[512 * 48];          // discriminator conv1 weight [512][40], rows padded to 48
   alignas(16) float z1[TR * 516];
@@ -417,7 +455,8 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
            const float* __restrict__ din, int B, const float* __restrict__ dw1,
            const float* __restrict__ w3, float* __restrict__ dlogits, float* __restrict__ dh2,
            float* __restrict__ gw1, float* __restrict__ gb1, const float* __restrict__ lpart,
-           int nlp, const float* __restrict__ lpart3, int nlp3, float* __restrict__ losses) {
+           int nlp, const float* __restrict__ lpart3, int nlp3, float* __restrict__ losses,
+           SemiArgs semi) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   HeadBwdLds& L = *reinterpret_cast<HeadBwdLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -504,10 +543,18 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
       float s = g;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-      if (lane < 40) {
-        dl = g - expf(lsm_or_dl) * s;
-        dlogits[(size_t)m * 40 + lane] = dl;
+      if (lane < 40) dl = g - expf(lsm_or_dl) * s;
+      if (semi.on) {
+        const int kept = semi_kept(semi.dout, B, semi.th, lane);
+        if (kept > 0 && semi.dout[m + B] > semi.th) {
+          float mx;
+          int am;
+          wave_argmax40(lane < 40 ? semi.logits[(size_t)m * 40 + lane] : 0.f, lane, mx, am);
+          if (lane < 40)
+            dl += semi.lambda / (float)kept * (expf(lsm_or_dl) - (lane == am ? 1.f : 0.f));
+        }
       }
+      if (lane < 40) dlogits[(size_t)m * 40 + lane] = dl;
     } else if (m < B && lane < 40) {
       dl = lsm_or_dl;
     }
@@ -518,6 +565,26 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
   rows_layer<40, 256, B_KO, ACT_NONE>(L.dl, 44, w3, 256, nullptr, dh2 + (size_t)r0 * 256, 256,
                                       nullptr, nrows);
   TSTAMP(2, 4);
+  if (semi.on && blockIdx.x == 0 && wave == 0) {
+    // l_semi and the kept ratio (losses[4], losses[5]), rows in order
+    const int kept = semi_kept(semi.dout, B, semi.th, lane);
+    float sum = 0.f;
+    for (int j = 0; j < B; ++j) {
+      if (!(semi.dout[2 * B + j] > semi.th)) continue;
+      const float x = lane < 40 ? semi.logits[(size_t)(B + j) * 40 + lane] : -INFINITY;
+      float mx;
+      int am;
+      wave_argmax40(x, lane, mx, am);
+      float e = lane < 40 ? expf(x - mx) : 0.f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o);
+      sum += logf(e);  // -log_softmax at the argmax = log sum exp(x - max)
+    }
+    if (lane == 0) {
+      losses[4] = kept > 0 ? sum / (float)kept : 0.f;
+      losses[5] = (float)kept / (float)B;
+    }
+  }
   if (blockIdx.x == 0 && tid == 0) {
     // losses: CE mean, adversarial BCE mean, 0.5 x D-loss means (row-block order)
     float s = 0.f;
@@ -570,7 +637,7 @@ int launch_head_fwd(const float* h2, const float* w3, const float* b3, const int
 int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, const float* w5,
                      const float* b5, const float* wf, const float* bf, const float* soft_gt,
                      const float* soft_nogt, const int32_t* step, uint64_t seed, float lambda_adv,
-                     float* dd3, float* slabs, float* lpart3, hipStream_t s) {
+                     float* dd3, float* slabs, float* lpart3, float* dout, hipStream_t s) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_disc_tail, sizeof(DiscTailLds), "disc_tail") != PCADV_OK) return PCADV_EHIP;
@@ -578,23 +645,27 @@ int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, c
   }
   hipLaunchKernelGGL(k_disc_tail, dim3(disc_rowblocks(B)), dim3(TT), sizeof(DiscTailLds), s, d3, B,
                      w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3, slabs,
-                     lpart3);
+                     lpart3, dout);
   PC_HIP_CHECK_LAUNCH("k_disc_tail");
   return PCADV_OK;
 }
 
 int launch_head_bwd(const float* dd1, const float* d1, const float* din, int B, const float* dw1,
                     const float* w3, float* dlogits, float* dh2, float* gw1, float* gb1,
-                    const float* lpart, const float* lpart3, float* losses, hipStream_t s) {
+                    const float* lpart, const float* lpart3, float* losses, int semi,
+                    float lambda_semi, float semi_th, const float* logits, const float* dout,
+                    hipStream_t s) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_head_bwd, sizeof(HeadBwdLds), "head_bwd") != PCADV_OK) return PCADV_EHIP;
     once = true;
   }
   const int nrb = head_rowblocks(B), nwb = (32 * 3 + TW - 1) / TW;
+  const SemiArgs sa{semi, lambda_semi, semi_th, logits, dout};
+  PC_REQUIRE(!semi || (logits && dout), "head_bwd: the semi term needs the logits and D outputs");
   hipLaunchKernelGGL(k_head_bwd, dim3(nrb + nwb), dim3(TT), sizeof(HeadBwdLds), s, dd1, d1, din, B,
                      dw1, w3, dlogits, dh2, gw1, gb1, lpart, nrb, lpart3, disc_rowblocks(B),
-                     losses);
+                     losses, sa);
   PC_HIP_CHECK_LAUNCH("k_head_bwd");
   return PCADV_OK;
 }

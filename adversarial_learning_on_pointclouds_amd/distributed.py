@@ -32,8 +32,11 @@ class DataParallelAdvStep:
             dist.broadcast(step.g_param, src=0, group=group)
             dist.broadcast(step.d_param, src=0, group=group)
 
-    def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None):
-        self.step.grads(pts_gt, labels, pts_nogt, masks, soft)
+    def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, semi=False):
+        # semi: each rank's pseudo-label CE is the mean over its own kept clouds,
+        # so the averaged gradient weights ranks equally (the global-batch mean
+        # would weight them by their kept counts)
+        self.step.grads(pts_gt, labels, pts_nogt, masks, soft, semi=semi)
         _avg_(self.step.grad_flat, self.group)
         self.step.adam()
         return self.step.losses

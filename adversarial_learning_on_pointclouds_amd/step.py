@@ -53,13 +53,16 @@ class AdvTrainStep:
     (B, N, 3) f32.  Dropout masks and soft D labels are drawn on device from
     Philox keyed by (seed, step) unless given explicitly (parity mode:
     masks=(gt, nogt) each (B, 256) {0,1}; soft=(gt, nogt) each (B,)).
-    Returns the device tensor [loss_cls, loss_adv, loss_D_gt, loss_D_nogt]
-    (no host sync: read it when you log, trainer.py:561-572).
+    Returns the device tensor [loss_cls, loss_adv, loss_D_gt, loss_D_nogt,
+    loss_semi, semi_ratio] (no host sync: read it when you log,
+    trainer.py:561-572).  semi=True adds run_training_semi's pseudo-label term
+    (utils/trainer.py:716-743: lambda_semi x CrossEntropyLoss(ignore_index=255)
+    of the no-GT logits against their argmax, clouds with D <= semi_th ignored).
     """
 
     def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
                  lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
-                 seed=0, device="cuda"):
+                 seed=0, device="cuda", lambda_semi=1.0, semi_th=0.8):
         self.lib = _lib.load()
         self.model, self.model_D = model, model_D
         self.B, self.N = int(B), int(N)
@@ -76,7 +79,8 @@ class AdvTrainStep:
             lr_D = optimizer_D.param_groups[0]["lr"]
         self.hp = dict(lr=float(lr), lr_D=float(lr_D), betas=betas, eps=float(eps),
                        lambda_cls=float(lambda_cls), lambda_adv=float(lambda_adv),
-                       p=float(model.dropout.p))
+                       p=float(model.dropout.p), lambda_semi=float(lambda_semi),
+                       semi_th=float(semi_th))
         self.g_param = flatten_params(model, G_LAYOUT, G_NUMEL, dev)
         self.d_param = flatten_params(model_D, D_LAYOUT, D_NUMEL, dev)
         self.grad_flat = torch.zeros(D_GRAD_OFFSET + D_NUMEL, device=dev)
@@ -97,7 +101,7 @@ class AdvTrainStep:
                     opt.state[p] = {"step": torch.zeros((), dtype=torch.float32),
                                     "exp_avg": mv[name], "exp_avg_sq": vv[name]}
         self.optimizers = (optimizer, optimizer_D)
-        self.losses = torch.zeros(4, device=dev)
+        self.losses = torch.zeros(6, device=dev)
         self.logits = torch.zeros(2 * self.B, 40, device=dev)
         nbytes = self.lib.pcadv_adv_step_workspace_bytes(self.B, self.N)
         self.workspace = torch.empty(nbytes, device=dev, dtype=torch.uint8)
@@ -106,7 +110,7 @@ class AdvTrainStep:
         self._keep = []
 
     # ------------------------------------------------------------------
-    def _args(self, pts_gt, labels, pts_nogt, masks, soft, apply_adam):
+    def _args(self, pts_gt, labels, pts_nogt, masks, soft, apply_adam, semi=False):
         B, N = int(pts_gt.shape[0]), self.N
         if not 0 < B <= self.B:
             raise ValueError(f"batch of {B} clouds; this step was built for at most {self.B}")
@@ -145,17 +149,20 @@ class AdvTrainStep:
         a.logits = self.logits.data_ptr()
         a.workspace = self.workspace.data_ptr()
         a.workspace_bytes = self.workspace.numel()
+        a.semi = int(bool(semi))
+        a.lambda_semi, a.semi_th = hp["lambda_semi"], hp["semi_th"]
         return a
 
-    def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, apply_adam=True):
+    def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, apply_adam=True,
+                 semi=False):
         """Whole iteration: forward, losses, backward, both Adam steps."""
-        a = self._args(pts_gt, labels, pts_nogt, masks, soft, apply_adam)
+        a = self._args(pts_gt, labels, pts_nogt, masks, soft, apply_adam, semi)
         check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step")
         return self.losses
 
-    def grads(self, pts_gt, labels, pts_nogt, masks=None, soft=None):
+    def grads(self, pts_gt, labels, pts_nogt, masks=None, soft=None, semi=False):
         """Forward + backward only (gradients in grad_flat; step counter advanced)."""
-        return self(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False)
+        return self(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=semi)
 
     def adam(self):
         """optimizer.step(); optimizer_D.step() on the current gradients."""
@@ -179,17 +186,17 @@ class AdvTrainStep:
                              self.step_count), saved):
             dst.copy_(src)
 
-    def capture_on(self, pts_gt, labels, pts_nogt, apply_adam=True):
+    def capture_on(self, pts_gt, labels, pts_nogt, apply_adam=True, semi=False):
         """Capture one step reading the given (resident) input buffers into a
         HIP graph; state is left as it was before the capture."""
         saved = self._snapshot()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam)  # warm-up outside capture
+            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam, semi=semi)  # warm-up
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        a = self._args(pts_gt, labels, pts_nogt, None, None, apply_adam)
+        a = self._args(pts_gt, labels, pts_nogt, None, None, apply_adam, semi)
         self._keep.append(a)
         with torch.cuda.graph(g):
             check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (capture)")

@@ -1,6 +1,6 @@
 """Training / evaluation loops with the reference's signatures
 (utils/trainer.py:30-69 run_testing, :222-308 run_training_pointnet_cls,
-:403-608 run_training).
+:403-608 run_training, :611-847 run_training_semi).
 
 run_training runs each iteration through the fused native step
 (AdvTrainStep: one C-ABI call, no per-op Python) whenever the configuration is
@@ -84,15 +84,25 @@ def _save(model, model_D, args, tag):
     torch.save(model_D.state_dict(), os.path.join(args.exp_dir, "modelD_{}.pth".format(tag)))
 
 
-def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloader_nogt_iter,
-                 testloader, model, model_D, gan_loss, cls_loss, optimizer, optimizer_D,
-                 history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args):
-    """utils/trainer.py:403-608."""
+def _semi_fusable(semi_loss):
+    return (type(semi_loss) is torch.nn.CrossEntropyLoss and semi_loss.weight is None
+            and semi_loss.reduction == "mean" and semi_loss.ignore_index == 255
+            and semi_loss.label_smoothing == 0.0)
+
+
+def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloader_nogt_iter,
+              testloader, model, model_D, gan_loss, cls_loss, optimizer, optimizer_D,
+              history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args,
+              semi_loss=None):
+    """The iteration loop shared by run_training (semi_loss None) and
+    run_training_semi (pseudo-label term from iteration semi_start + 1)."""
     gt_label, nogt_label = 1, 0
     max_test_accu = float("-inf")
     max_train_epoch = 0
     fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss,
                      (history_pool_gt, history_pool_nogt), args)
+    if semi_loss is not None:
+        fused = fused and _semi_fusable(semi_loss)
     step = None
     log_every = int(getattr(args, "log_every", 1))
 
@@ -105,6 +115,7 @@ def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetlo
         pts = pts.float().to(args.device).contiguous()
         cls = cls.long().to(args.device).contiguous()
         pts_nogt = pts_nogt.float().to(args.device).contiguous()
+        semi_on = semi_loss is not None and args.semi_start > 0 and i_iter > args.semi_start
 
         if fused and pts.shape == pts_nogt.shape:
             if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
@@ -112,12 +123,15 @@ def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetlo
                                     optimizer=optimizer, optimizer_D=optimizer_D,
                                     lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
                                     seed=int(getattr(args, "seed", 0)) + i_iter,
-                                    device=args.device)
-            losses = step(pts, cls, pts_nogt)
+                                    device=args.device,
+                                    lambda_semi=float(getattr(args, "lambda_semi", 1.0)),
+                                    semi_th=float(getattr(args, "semi_TH", 0.8)))
+            losses = step(pts, cls, pts_nogt, semi=semi_on)
             vals = losses.tolist() if (i_iter % log_every == 0) else None
             if vals is not None:
                 loss_cls_value, loss_adv_value = vals[0], vals[1]
                 loss_D_value = vals[2] + vals[3]
+                loss_semi_value = vals[4] if semi_on else 0.0
         else:
             optimizer.zero_grad()
             optimizer_D.zero_grad()
@@ -131,6 +145,15 @@ def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetlo
             D_out = model_D(pred_nogt_softmax)
             loss_adv = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=False))
             loss = args.lambda_cls * l + args.lambda_adv * loss_adv
+            loss_semi_value = 0.0
+            if semi_on:  # utils/trainer.py:716-743
+                ignore = (D_out <= args.semi_TH).squeeze(1)
+                semi_gt = torch.argmax(pred_nogt.detach(), dim=1)
+                semi_gt[ignore] = 255
+                if int(ignore.sum().item()) < ignore.numel():
+                    l_semi = semi_loss(pred_nogt, semi_gt)
+                    loss_semi_value = l_semi.item()
+                    loss = loss + args.lambda_semi * l_semi
             loss.backward()
             for param in model_D.parameters():
                 param.requires_grad = True
@@ -155,11 +178,17 @@ def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetlo
                 writer.add_scalar("Loss/train_cls", loss_cls_value, i_iter)
                 writer.add_scalar("Loss/train_adv", loss_adv_value, i_iter)
                 writer.add_scalar("Loss/train_disc", loss_D_value, i_iter)
+                if semi_loss is not None:
+                    writer.add_scalar("Loss/train_semi", loss_semi_value, i_iter)
 
         if i_iter % args.iter_save_epoch == 0:
             if step is not None:
                 step.sync_optimizer_state()
-            _save(model, model_D, args, "train_epoch_{}".format(i_iter // args.iter_save_epoch))
+            if semi_loss is None:
+                tag = i_iter // args.iter_save_epoch
+            else:  # trainer.py:789
+                tag = int(round(i_iter / len(trainloader_gt)))
+            _save(model, model_D, args, "train_epoch_{}".format(tag))
         if i_iter % args.iter_test_epoch == 0:
             curr_accu, _ = run_testing(testloader, model, cls_loss, test_logger, i_iter, writer, args)
             if max_test_accu < curr_accu:
@@ -174,6 +203,30 @@ def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetlo
     train_logger.info("Max test accuracy: {:.4f}".format(max_test_accu))
     train_logger.info("Train model is at epoch: {}".format(max_train_epoch))
     return max_test_accu
+
+
+def run_training(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloader_nogt_iter,
+                 testloader, model, model_D, gan_loss, cls_loss, optimizer, optimizer_D,
+                 history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args):
+    """utils/trainer.py:403-608."""
+    return _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloader_nogt_iter,
+                     testloader, model, model_D, gan_loss, cls_loss, optimizer, optimizer_D,
+                     history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args)
+
+
+def run_training_semi(trainloader_gt, trainloader_nogt, trainloader_gt_iter,
+                      targetloader_nogt_iter, testloader, model, model_D, gan_loss, cls_loss,
+                      semi_loss, optimizer, optimizer_D, history_pool_gt, history_pool_nogt,
+                      train_logger, test_logger, writer, args):
+    """utils/trainer.py:611-847: run_training plus, for i_iter > args.semi_start
+    (> 0), lambda_semi x semi_loss(pred_nogt, argmax(pred_nogt)) over the no-GT
+    clouds the frozen discriminator scores above args.semi_TH (the rest are
+    ignore_index 255; no term when all are ignored).  The fused step computes
+    the term on device (k_head_bwd)."""
+    return _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloader_nogt_iter,
+                     testloader, model, model_D, gan_loss, cls_loss, optimizer, optimizer_D,
+                     history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args,
+                     semi_loss=semi_loss)
 
 
 def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, model, cls_loss,

@@ -286,11 +286,18 @@ typedef struct pcadv_adv_args {
   uint64_t rng_seed;
   int apply_adam;           /* 0: stop after the gradients (parity tests) */
   /* outputs */
-  float* losses;            /* [4]: loss_cls, loss_adv, loss_D_gt, loss_D_nogt */
+  float* losses;            /* [4]: loss_cls, loss_adv, loss_D_gt, loss_D_nogt
+                               ([6] with semi: + loss_semi, kept ratio) */
   float* logits;            /* [2B][40] or NULL */
   /* scratch */
   void* workspace;
   size_t workspace_bytes;
+  /* run_training_semi (utils/trainer.py:611-847, :716-743): when semi != 0 the
+   * generator loss gains lambda_semi * CrossEntropyLoss(ignore_index=255) of
+   * the no-GT logits against their own argmax, the clouds with
+   * D(log_softmax(pred_nogt)) <= semi_th ignored (no term when all are) */
+  int semi;
+  float lambda_semi, semi_th;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

@@ -360,12 +360,36 @@ class Adam:
 # the adversarial step (utils/trainer.py:426-559)
 # --------------------------------------------------------------------------
 
+def semi_ce(logits_ng, d_ng, semi_th):
+    """run_training_semi's pseudo-label loss (utils/trainer.py:716-728):
+    ignore = D_out <= semi_TH, semi_gt = argmax(pred_nogt) (first index),
+    CrossEntropyLoss(ignore_index=255) = mean over the kept rows of
+    -log_softmax[semi_gt].  Returns (loss or None, dloss/dlogits, kept ratio)."""
+    keep = ~(d_ng[:, 0] <= F32(semi_th))
+    kept = int(keep.sum())
+    ratio = kept / float(keep.size)
+    if kept == 0:
+        return None, np.zeros_like(logits_ng), ratio
+    am = logits_ng.argmax(1)
+    lsm = log_softmax(logits_ng)
+    rows = np.nonzero(keep)[0]
+    loss = -float(np.mean(lsm[rows, am[rows]].astype(np.float64)))
+    grad = np.zeros_like(logits_ng)
+    p = np.exp(lsm[rows])
+    p[np.arange(rows.size), am[rows]] -= 1.0
+    grad[rows] = p / F32(kept)
+    return loss, grad.astype(F32), ratio
+
+
 def adv_step(G, D, optG, optD, pts_gt, labels, pts_nogt, mask_gt, mask_nogt,
-             y_gt, y_nogt, lambda_cls=1.0, lambda_adv=0.001, apply_adam=True):
-    """One run_training iteration.  The stochastic parts are inputs: dropout
-    masks (B, 256) for the two G passes and the U(0.7,1.05) / U(0,0.305) soft
-    D labels drawn by make_D_label(random=True) (utils/utils.py:22-31).
-    ImagePool(0).query is the identity (utils/image_pool.py:35-36)."""
+             y_gt, y_nogt, lambda_cls=1.0, lambda_adv=0.001, apply_adam=True,
+             semi=False, semi_th=0.8, lambda_semi=1.0):
+    """One run_training iteration (semi=True: one run_training_semi iteration
+    past semi_start, utils/trainer.py:611-847).  The stochastic parts are
+    inputs: dropout masks (B, 256) for the two G passes and the U(0.7,1.05) /
+    U(0,0.305) soft D labels drawn by make_D_label(random=True)
+    (utils/utils.py:22-31).  ImagePool(0).query is the identity
+    (utils/image_pool.py:35-36)."""
     logits_gt, _, c_gt = cls_forward(G, pts_gt, mask_gt)             # :468
     l, dce = cross_entropy(logits_gt, labels)                          # :469
     lsm_gt = log_softmax(logits_gt)                                    # :472
@@ -376,6 +400,10 @@ def adv_step(G, D, optG, optD, pts_gt, labels, pts_nogt, mask_gt, mask_nogt,
     # G backward (:510-520); D frozen -> only the input gradient
     _, dlsm = disc_backward(D, acts_ng, F32(lambda_adv) * dadv, need_params=False)
     dlog_ng = log_softmax_bwd(lsm_ng, dlsm)
+    loss_semi, semi_ratio = None, None
+    if semi:                                                           # :716-743
+        loss_semi, dsemi, semi_ratio = semi_ce(logits_ng, d_ng, semi_th)
+        dlog_ng = (dlog_ng + F32(lambda_semi) * dsemi).astype(F32)
     ga = cls_backward(G, c_gt, F32(lambda_cls) * dce)
     gb = cls_backward(G, c_ng, dlog_ng)
     gG = OrderedDict((k, (ga[k] + gb[k]).astype(F32)) for k in G)
@@ -390,7 +418,8 @@ def adv_step(G, D, optG, optD, pts_gt, labels, pts_nogt, mask_gt, mask_nogt,
         optG.step(gG)                                                   # :558
         optD.step(gD)                                                   # :559
     losses = dict(loss_cls=l, loss_adv=loss_adv, loss_D=0.5 * lD1 + 0.5 * lD2,
-                  loss_D_gt=0.5 * lD1, loss_D_nogt=0.5 * lD2)
+                  loss_D_gt=0.5 * lD1, loss_D_nogt=0.5 * lD2, loss_semi=loss_semi,
+                  semi_ratio=semi_ratio)
     aux = dict(logits_gt=logits_gt, logits_nogt=logits_ng, d_nogt=d_ng, d_gt=d_gt,
                am_gt=c_gt["am"], am_nogt=c_ng["am"], gmax_gt=c_gt["gmax"],
                gmax_nogt=c_ng["gmax"])

@@ -175,6 +175,109 @@ def main(ref_root, only=None):
             summarize("param." + name, p.detach().numpy(), out)
         np.savez_compressed(os.path.join(HERE, "g8_seg_step.npz"), **out)
 
+    # ---------------- G9: run_training_semi (pseudo-label step) ----------------
+    # utils/trainer.py:611-847 for 3 iterations with semi_start = 1, so the
+    # pseudo-label CE (ignore_index=255) joins the generator loss at i_iter 2.
+    # semi_TH is set between the middle two D scores of that iteration's no-GT
+    # clouds (found with the oracle, which tracks the reference to ~1e-6), so
+    # half the clouds are kept and half ignored.
+    def g9():
+        iters, B, data_seed = 3, 8, 91
+        Gp = onp.make_params(onp.cls_spec(40), seed=1)
+        Dp = onp.make_params(onp.disc_spec(40, 1), seed=2, init="xavier")
+        rng = np.random.default_rng(data_seed)
+        batches_gt, batches_ng, masks, soft = [], [], [], []
+        for _ in range(iters):
+            batches_gt.append((rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32),
+                               rng.integers(0, 40, B).astype(np.int64)))
+            batches_ng.append(rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32))
+            masks.append(make_mask(rng, B))
+            masks.append(make_mask(rng, B))
+            soft.append(rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32))
+            soft.append(rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32))
+        # threshold from the oracle's D scores at i_iter 2
+        oG = {k: v.copy() for k, v in Gp.items()}
+        oD = {k: v.copy() for k, v in Dp.items()}
+        aG, aD = onp.Adam(oG), onp.Adam(oD)
+        for it in range(2):
+            onp.adv_step(oG, oD, aG, aD, batches_gt[it][0], batches_gt[it][1], batches_ng[it],
+                         masks[2 * it], masks[2 * it + 1], soft[2 * it], soft[2 * it + 1])
+        _, _, _, aux = onp.adv_step(oG, oD, aG, aD, batches_gt[2][0], batches_gt[2][1],
+                                    batches_ng[2], masks[4], masks[5], soft[4], soft[5],
+                                    apply_adam=False)
+        d = np.sort(aux["d_nogt"][:, 0])
+        semi_th = float((d[B // 2 - 1] + d[B // 2]) / 2)
+
+        model = load(PointNetCls(k=40, feature_transform=False), Gp)
+        model.dropout = MaskDropout([m.copy() for m in masks])
+        model_D = load(DeepConvDiscNet(40, 1), Dp)
+        soft_q = [x.copy() for x in soft]
+        orig = rtrainer.make_D_label
+
+        def make_D_label(input, value, device, random=False):
+            if random:
+                return torch.from_numpy(soft_q.pop(0)).to(device)
+            return orig(input, value, device, random=False)
+
+        rec = {"cls": [], "gan": [], "semi": []}
+
+        class Rec(nn.Module):
+            def __init__(self, inner, key):
+                super().__init__()
+                self.inner, self.key = inner, key
+
+            def forward(self, a, b):
+                r = self.inner(a, b)
+                rec[self.key].append(float(r.item()))
+                return r
+
+        optimizer = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        optimizer_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        tmp = tempfile.mkdtemp(prefix="golden_")
+        args = argparse.Namespace(device=torch.device("cpu"), total_iterations=iters,
+                                  lambda_cls=1.0, lambda_adv=0.001, lambda_semi=1.0,
+                                  semi_start=1, semi_TH=semi_th,
+                                  iter_save_epoch=10 ** 9, iter_test_epoch=10 ** 9,
+                                  exp_dir=tmp, tensorboard=False, batch_size=B)
+        gt_list = [(torch.from_numpy(a), torch.from_numpy(b)) for a, b in batches_gt]
+        ng_list = [torch.from_numpy(a) for a in batches_ng]
+        logger = logging.getLogger("golden")
+        logger.addHandler(logging.NullHandler())
+        logger.propagate = False
+        rtrainer.make_D_label = make_D_label
+        try:
+            rtrainer.run_training_semi(
+                trainloader_gt=gt_list, trainloader_nogt=ng_list,
+                trainloader_gt_iter=enumerate(list(gt_list)),
+                targetloader_nogt_iter=enumerate(list(ng_list)),
+                testloader=[gt_list[0]], model=model, model_D=model_D,
+                gan_loss=Rec(nn.BCEWithLogitsLoss(), "gan"),
+                cls_loss=Rec(nn.CrossEntropyLoss(), "cls"),
+                semi_loss=Rec(nn.CrossEntropyLoss(ignore_index=255), "semi"),
+                optimizer=optimizer, optimizer_D=optimizer_D,
+                history_pool_gt=ImagePool(0), history_pool_nogt=ImagePool(0),
+                train_logger=logger, test_logger=logger, writer=None, args=args)
+        finally:
+            rtrainer.make_D_label = orig
+        out = dict(iters=iters, data_seed=data_seed, g_seed=1, d_seed=2, B=B, N=N_PTS,
+                   semi_start=1, semi_th=np.float64(semi_th), lambda_semi=1.0,
+                   semi_ratio=np.float64(0.5))
+        cls_train = [rec["cls"][0]] + rec["cls"][2:]
+        gan = np.array(rec["gan"]).reshape(iters, 3)
+        out["loss_cls"] = np.array(cls_train)
+        out["loss_adv"] = gan[:, 0]
+        out["loss_D_gt"] = gan[:, 1] * 0.5
+        out["loss_D_nogt"] = gan[:, 2] * 0.5
+        out["loss_semi"] = np.array(rec["semi"])  # one term: i_iter 2
+        for name, p in model.named_parameters():
+            summarize("paramG." + name, p.detach().numpy(), out)
+        for name, p in model_D.named_parameters():
+            summarize("paramD." + name, p.detach().numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g9_semi_step3.npz"), **out)
+
+    if only == "g9":
+        g9()
+        return
     if only == "g7":
         g7()
         return
@@ -346,6 +449,7 @@ def main(ref_root, only=None):
     summarize("out", so.numpy(), out)
     np.savez_compressed(os.path.join(HERE, "g6_seg_fwd.npz"), **out)
     g8()
+    g9()
 
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
@@ -355,6 +459,6 @@ def main(ref_root, only=None):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("ref_root", nargs="?", default="/root/reference")
-    ap.add_argument("--only", default=None, help="g7 or g8: regenerate only that fixture")
+    ap.add_argument("--only", default=None, help="g7, g8 or g9: regenerate only that fixture")
     a = ap.parse_args()
     main(a.ref_root, a.only)

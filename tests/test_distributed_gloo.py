@@ -70,9 +70,10 @@ class OracleStep:
             out[k] = view[off:off + v.size].reshape(v.shape)  # shares memory with flat
         return out
 
-    def grads(self, pts_gt, labels, pts_nogt, masks, soft):
+    def grads(self, pts_gt, labels, pts_nogt, masks, soft, semi=False):
         losses, gG, gD, _ = O.adv_step(self.G, self.D, None, None, pts_gt, labels, pts_nogt,
-                                       masks[0], masks[1], soft[0], soft[1], apply_adam=False)
+                                       masks[0], masks[1], soft[0], soft[1], apply_adam=False,
+                                       semi=semi)
         g = self.grad_flat.numpy()
         for k, v in gG.items():
             g[self.g_lay[k]:self.g_lay[k] + v.size] = v.reshape(-1)

@@ -240,6 +240,64 @@ def test_adv_step_golden_g3(name):
         check_tensor(fx, "paramD." + nm, p.detach().cpu().numpy(), tol=1e-5)
 
 
+def test_semi_step_golden_g9():
+    """run_training_semi: 3 fused steps, the pseudo-label term
+    on device from i_iter 2 (half the no-GT clouds kept by the D threshold)."""
+    fx = load("g9_semi_step3.npz")
+    B = int(fx["B"])
+    step, model, model_D = _make_step(B, int(fx["N"]))
+    step.hp["semi_th"], step.hp["lambda_semi"] = float(fx["semi_th"]), float(fx["lambda_semi"])
+    semi_start = int(fx["semi_start"])
+    for i, (pg, lab, pn, m1, m2, y1, y2) in enumerate(_adv_inputs(fx)):
+        on = semi_start > 0 and i > semi_start
+        losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                      soft=(_t(y1), _t(y2)), semi=on).cpu().numpy()
+        assert abs(losses[0] - fx["loss_cls"][i]) < 1e-4
+        assert abs(losses[1] - fx["loss_adv"][i]) < 1e-4
+        assert abs(losses[2] - fx["loss_D_gt"][i]) < 1e-4
+        assert abs(losses[3] - fx["loss_D_nogt"][i]) < 1e-4
+        if on:
+            assert abs(losses[4] - fx["loss_semi"][0]) < 1e-4
+            assert losses[5] == float(fx["semi_ratio"])
+    for nm, p in model.named_parameters():
+        check_tensor(fx, "paramG." + nm, p.detach().cpu().numpy(), tol=1e-5)
+    for nm, p in model_D.named_parameters():
+        check_tensor(fx, "paramD." + nm, p.detach().cpu().numpy(), tol=1e-5)
+
+
+@pytest.mark.parametrize("keep", ["half", "none", "all"])
+def test_semi_step_full_size_vs_oracle(keep):
+    """B=32 fused semi step vs the oracle's gradients, with the D threshold
+    keeping half, none (no term) or all of the no-GT clouds."""
+    B, N = 32, 1024
+    step, model, model_D = _make_step(B, N, g_seed=3, d_seed=4)
+    rng = np.random.default_rng(1001)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+    G = onp.make_params(onp.cls_spec(40), seed=3)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=4, init="xavier")
+    _, _, _, aux = onp.adv_step(dict(G), dict(D), None, None, pg, lab, pn, m1, m2, y1, y2,
+                                apply_adam=False)
+    d = np.sort(aux["d_nogt"][:, 0])
+    th = {"half": float((d[B // 2 - 1] + d[B // 2]) / 2), "none": 1e9, "all": -1e9}[keep]
+    losses_ref, gG, gD, _ = onp.adv_step(G, D, None, None, pg, lab, pn, m1, m2, y1, y2,
+                                         apply_adam=False, semi=True, semi_th=th, lambda_semi=0.7)
+    step.hp["semi_th"], step.hp["lambda_semi"] = th, 0.7
+    losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                  soft=(_t(y1), _t(y2)), apply_adam=False, semi=True).cpu().numpy()
+    assert losses[5] == losses_ref["semi_ratio"]
+    assert abs(losses[4] - (losses_ref["loss_semi"] or 0.0)) < 1e-4
+    for nm, p in model.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), gG[nm]) < TOL, nm
+    for nm, p in model_D.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), gD[nm]) < TOL, nm
+
+
 def test_adv_step_full_size_vs_oracle():
     """Bench configuration (B=32, N=1024): one step, gradients vs the oracle."""
     B, N = 32, 1024

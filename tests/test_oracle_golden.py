@@ -76,6 +76,33 @@ def test_g3_adv_step(name):
         check_tensor(fx, "paramD." + k, D[k], tol=1e-5)
 
 
+def test_g9_semi_step():
+    """run_training_semi (utils/trainer.py:611-847), 3 iterations, the
+    pseudo-label term on from i_iter 2 with half the no-GT clouds kept."""
+    fx = load("g9_semi_step3.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    D = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
+    oG, oD = onp.Adam(G), onp.Adam(D)
+    semi_start, th = int(fx["semi_start"]), float(fx["semi_th"])
+    semi_losses = []
+    for i, (pg, lab, pn, m1, m2, y1, y2) in enumerate(_adv_inputs(fx)):
+        on = semi_start > 0 and i > semi_start
+        losses, _, _, _ = onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2, semi=on,
+                                       semi_th=th, lambda_semi=float(fx["lambda_semi"]))
+        assert abs(losses["loss_cls"] - fx["loss_cls"][i]) < 1e-4
+        assert abs(losses["loss_adv"] - fx["loss_adv"][i]) < 1e-4
+        assert abs(losses["loss_D_gt"] - fx["loss_D_gt"][i]) < 1e-4
+        assert abs(losses["loss_D_nogt"] - fx["loss_D_nogt"][i]) < 1e-4
+        if on:
+            assert losses["semi_ratio"] == float(fx["semi_ratio"])
+            semi_losses.append(losses["loss_semi"])
+    assert np.allclose(semi_losses, fx["loss_semi"], atol=1e-4)
+    for k in G:
+        check_tensor(fx, "paramG." + k, G[k], tol=1e-5)
+    for k in D:
+        check_tensor(fx, "paramD." + k, D[k], tol=1e-5)
+
+
 def test_g4_disc():
     fx = load("g4_disc.npz")
     D = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
