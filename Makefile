@@ -5,7 +5,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := adversarial_learning_on_pointclouds_amd
 SRC := $(wildcard $(PKG)/csrc/*.hip)
-OBJ := $(patsubst $(PKG)/csrc/%.hip,build/obj/%.o,$(SRC))
+CPP := $(wildcard $(PKG)/csrc/*.cpp)
+OBJ := $(patsubst $(PKG)/csrc/%.hip,build/obj/%.o,$(SRC)) $(patsubst $(PKG)/csrc/%.cpp,build/obj/%.host.o,$(CPP))
 HDR := $(wildcard $(PKG)/csrc/*.h) include/pcadv.h
 LIB := $(PKG)/lib/libpcadv.so
 HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
@@ -16,9 +17,14 @@ build/obj/%.o: $(PKG)/csrc/%.hip $(HDR)
 	@mkdir -p build/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# host-only C++ (the dataset reader)
+build/obj/%.host.o: $(PKG)/csrc/%.cpp $(HDR)
+	@mkdir -p build/obj
+	$(HIPCC) -O2 -fPIC -std=c++17 -Wall -Iinclude -c $< -o $@
+
 $(LIB): $(OBJ)
 	@mkdir -p $(PKG)/lib
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ) -lz
 
 asm: $(SRC)
 	@mkdir -p build/asm
@@ -33,5 +39,5 @@ clean:
 STAMPS_LIB := build/stamps/libpcadv_stamps.so
 stamps: $(SRC) $(HDR)
 	@mkdir -p build/stamps
-	$(HIPCC) $(HIPFLAGS) -DPCADV_STAMPS -shared -o $(STAMPS_LIB) $(SRC)
+	$(HIPCC) $(HIPFLAGS) -DPCADV_STAMPS -shared -o $(STAMPS_LIB) $(SRC) $(CPP) -lz
 .PHONY: stamps

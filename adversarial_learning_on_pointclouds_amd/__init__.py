@@ -6,8 +6,10 @@ Drop-in counterparts of the reference's models and training loop
 (utils/model_utils.py), make_D_label (utils/utils.py), ImagePool
 (utils/image_pool.py), run_training / run_testing (utils/trainer.py), plus the
 fused native step AdvTrainStep; PointNetSeg (models/pointnet.py:261-317) with
-its native training step SegTrainStep.  All compute runs in libpcadv.so (C ABI in
-include/pcadv.h); there is no CPU fallback.
+its native training step SegTrainStep; run_training_semi; the HDF5 datasets of
+dataset/modelNetData.py and dataset/shapeNetData.py without h5py, with a
+device-resident batch loader (dataset.DeviceCloudLoader).  All compute runs in
+libpcadv.so (C ABI in include/pcadv.h); there is no CPU fallback.
 """
 from . import _lib
 from .discriminator import DeepConvDiscNet

@@ -103,6 +103,12 @@ SIGNATURES = {
     "pcadv_conv_max_x3": (_i, [_vp, _i64, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "pcadv_conv_max_x3_bwd": (_i, [_vp, _vp, _vp, _vp, _i64, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
                                    _i64, _i, _vp]),
+    "pcadv_h5_info": (_i, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(_i),
+                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_i)]),
+    "pcadv_h5_read": (_i, [ctypes.c_char_p, ctypes.c_char_p, _i, _i64, _vp, _sz]),
+    "pcadv_gather_clouds": (_i, [_vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, ctypes.c_double,
+                                 ctypes.c_double, _vp, _u64, _vp,
+                                 _vp, _vp, _vp, _vp]),
     "pcadv_row_ce_workspace_bytes": (_sz, [_i]),
     "pcadv_row_ce": (_i, [_vp, _i64, _vp, _i, _i, _f, _vp, _vp, _vp, _sz, _vp]),
     "pcadv_adv_step_workspace_bytes": (_sz, [_i, _i]),

@@ -79,6 +79,9 @@ int launch_conv_max_x3(const float*, long long, int, int, int, const float*, con
                        int, float*, int32_t*, void*, size_t, hipStream_t);
 int launch_cmx_bwd(const float*, const float*, const int32_t*, const float*, long long, int, int,
                    int, int, const float*, float*, float*, float*, long long, int, hipStream_t);
+int launch_gather_clouds(const float*, int64_t, int, int, const int64_t*, int, const int64_t*, int,
+                         const int64_t*, double, double, const double*, uint64_t, const int32_t*,
+                         float*, int64_t*, int64_t*, hipStream_t);
 size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
                   size_t, hipStream_t);
@@ -440,6 +443,15 @@ int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* 
                           int relu_x, hipStream_t stream) {
   return launch_cmx_bwd(dgmax, gmax, gidx, x, ldx, C, Npts, O, K, w, dw, db, dx, lddx, relu_x,
                         stream);
+}
+
+int pcadv_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
+                        const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
+                        const int64_t* src_seg, double sigma, double clip, const double* noise,
+                        uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
+                        int64_t* out_seg, hipStream_t stream) {
+  return launch_gather_clouds(src, n_src, npts, src_npts, idx, B, src_lab, lab_width, src_seg,
+                              sigma, clip, noise, seed, step, out, out_lab, out_seg, stream);
 }
 
 size_t pcadv_row_ce_workspace_bytes(int M) { return row_ce_workspace_bytes(M); }

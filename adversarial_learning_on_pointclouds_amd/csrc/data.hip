@@ -1,0 +1,84 @@
+// Batch assembly on the device for the data path: the whole
+// split stays resident in HBM and each batch is a gather of B clouds by index
+// plus the reference's per-point jitter (dataset/modelNetData.py:80-91,
+// jitter_point_cloud: data + clip(sigma * randn(N, 3), -clip, clip), applied in
+// __getitem__ when data_augmentation is on, :73-78), the labels and part ids
+// gathered alongside.  Replaces the host DataLoader + H2D copy per step.
+//
+// One thread per point (3 floats), coalesced along the point axis.  Noise:
+// explicit f64 standard-normal draws (parity with numpy, which jitters in f64
+// and rounds to f32 in __getitem__), or Philox-4x32 draws keyed by (seed,
+// device step counter, RNG_JITTER, point) turned into normals by Box-Muller, so
+// a captured graph jitters differently on every replay.
+#include "common.h"
+
+namespace pcadv {
+
+constexpr uint32_t RNG_JITTER = 4;
+
+__global__ void __launch_bounds__(256)
+k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_npts,
+                const int64_t* __restrict__ idx, int B, const int64_t* __restrict__ src_lab,
+                int lab_width, const int64_t* __restrict__ src_seg, double sigma_d, double clip_d,
+                const double* __restrict__ noise, uint64_t seed, const int32_t* __restrict__ step,
+                float* __restrict__ out, int64_t* __restrict__ out_lab,
+                int64_t* __restrict__ out_seg) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * npts) return;
+  const int b = (int)(t / npts), p = (int)(t % npts);
+  const int64_t c = idx[b];
+  if (c < 0 || c >= n_src) return;  // validated on the host; never reads out of range
+  const float* s = src + ((size_t)c * src_npts + p) * 3;
+  float* o = out + (size_t)t * 3;
+  const float x0 = s[0], x1 = s[1], x2 = s[2];
+  const float sigma = (float)sigma_d, clip = (float)clip_d;
+  if (sigma_d > 0.0) {
+    if (noise) {  // f64 like numpy (sigma, clip are Python floats there)
+      const double* z = noise + (size_t)t * 3;
+      const double sg = sigma_d, cl = clip_d;
+      o[0] = (float)((double)x0 + fmin(fmax(sg * z[0], -cl), cl));
+      o[1] = (float)((double)x1 + fmin(fmax(sg * z[1], -cl), cl));
+      o[2] = (float)((double)x2 + fmin(fmax(sg * z[2], -cl), cl));
+    } else {
+      const uint32_t st = step ? (uint32_t)*step : 0u;
+      const u32x4 r = philox((uint32_t)t, st, RNG_JITTER, (uint32_t)(t >> 32), (uint32_t)seed,
+                             (uint32_t)(seed >> 32));
+      // Box-Muller on two uniform pairs -> 4 normals (3 used)
+      const float u1 = fmaxf(u01(r.x), 1e-7f), u2 = u01(r.y);
+      const float u3 = fmaxf(u01(r.z), 1e-7f), u4 = u01(r.w);
+      const float m1 = sqrtf(-2.f * logf(u1)), m2 = sqrtf(-2.f * logf(u3));
+      const float a1 = 6.28318530718f * u2, a2 = 6.28318530718f * u4;
+      const float z0 = m1 * cosf(a1), z1 = m1 * sinf(a1), z2 = m2 * cosf(a2);
+      o[0] = x0 + fminf(fmaxf(sigma * z0, -clip), clip);
+      o[1] = x1 + fminf(fmaxf(sigma * z1, -clip), clip);
+      o[2] = x2 + fminf(fmaxf(sigma * z2, -clip), clip);
+    }
+  } else {
+    o[0] = x0;
+    o[1] = x1;
+    o[2] = x2;
+  }
+  if (out_seg && src_seg) out_seg[t] = src_seg[(size_t)c * src_npts + p];
+  if (p < lab_width && out_lab && src_lab) out_lab[(size_t)b * lab_width + p] = src_lab[(size_t)c * lab_width + p];
+}
+
+int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
+                         const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
+                         const int64_t* src_seg, double sigma, double clip, const double* noise,
+                         uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
+                         int64_t* out_seg, hipStream_t s) {
+  PC_REQUIRE(src && idx && out && n_src > 0 && B > 0 && npts > 0 && src_npts >= npts,
+             "gather_clouds: bad arguments (n_src=%lld B=%d npts=%d src_npts=%d)",
+             (long long)n_src, B, npts, src_npts);
+  PC_REQUIRE(sigma >= 0.0 && (sigma == 0.0 || clip > 0.0), "gather_clouds: clip must be > 0");
+  PC_REQUIRE(!src_lab || (lab_width > 0 && lab_width <= npts && out_lab), "gather_clouds: labels");
+  PC_REQUIRE(!src_seg || out_seg, "gather_clouds: part ids");
+  const int64_t n = (int64_t)B * npts;
+  hipLaunchKernelGGL(k_gather_clouds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src,
+                     n_src, npts, src_npts, idx, B, src_lab, lab_width, src_seg, sigma, clip, noise,
+                     seed, step, out, out_lab, out_seg);
+  PC_HIP_CHECK_LAUNCH("k_gather_clouds");
+  return PCADV_OK;
+}
+
+}  // namespace pcadv

@@ -1,6 +1,7 @@
 """Training / evaluation loops with the reference's signatures
-(utils/trainer.py:30-69 run_testing, :222-308 run_training_pointnet_cls,
-:403-608 run_training, :611-847 run_training_semi).
+(utils/trainer.py:30-69 run_testing, :72-143 run_testing_seg, :222-308
+run_training_pointnet_cls, :310-400 run_training_pointnet_seg, :403-608
+run_training, :611-847 run_training_semi).
 
 run_training runs each iteration through the fused native step
 (AdvTrainStep: one C-ABI call, no per-op Python) whenever the configuration is
@@ -17,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from .discriminator import DeepConvDiscNet
+from .metric import batch_get_iou, object_names
 from .pointnet import PointNetCls, feature_transform_regularizer
 from .step import AdvTrainStep
 from .utils import make_D_label
@@ -263,3 +265,108 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
     train_logger.info("Max test accuracy: {:.4f}".format(max_test_accu))
     train_logger.info("Train model is at epoch: {}".format(max_train_epoch))
     return max_test_accu
+
+
+def run_testing_seg(dataloader, dataset, model, criterion, logger, test_iter, writer, args):
+    """utils/trainer.py:72-143: point accuracy, loss and the category / all-shape
+    mean part IoU (the reference's np.object container, removed from numpy,
+    becomes a list of lists)."""
+    model.eval()
+    total_accuracy = 0.0
+    total_loss = 0.0
+    shape_ious = [[] for _ in object_names]
+    for batch_idx, data in enumerate(dataloader):
+        pts, cls, seg = data
+        pts, cls, seg = pts.float().to(args.device), cls.to(args.device), seg.long().to(args.device)
+        with torch.set_grad_enabled(False):
+            pred, _ = model(pts, cls)
+            loss = criterion(pred, seg)
+        pred_seg = pred.max(1)[1]
+        total_accuracy += pred_seg.eq(seg).cpu().numpy().sum() / float(args.input_pts)
+        total_loss += loss.item()
+        p, s_, c = pred_seg.cpu().numpy(), seg.cpu().numpy(), cls[:, 0, :].cpu().numpy()
+        for b, iou in enumerate(batch_get_iou(batch_pred=p, batch_seg=s_, batch_cls=c)):
+            shape_ious[int(np.argmax(c[b, :]))].append(iou)
+    mean_cat = float(np.mean([np.mean(i) for i in shape_ious]))
+    mean_all = float(np.mean([i for s in shape_ious for i in s]))
+    n = float(len(dataset))
+    logger.info("Test accuracy: {:.4f}\tloss: {:.3f}\tcat_iou: {:.4f}\tall_iou: {:.4f}".format(
+        total_accuracy / n, total_loss / n, mean_cat, mean_all))
+    if getattr(args, "tensorboard", False) and writer is not None:
+        writer.add_scalar("Loss/test_cls", total_loss / n, test_iter)
+        writer.add_scalar("Accuracy/test", total_accuracy / n, test_iter)
+        writer.add_scalar("IoU/test_cat_iou", mean_cat, test_iter)
+        writer.add_scalar("IoU/test_all_iou", mean_all, test_iter)
+    return total_accuracy / n, total_loss / n, mean_cat, mean_all
+
+
+def run_training_pointnet_seg(trainloader_gt, trainloader_gt_iter, testloader, testdataset, model,
+                              seg_loss, optimizer, train_logger, test_logger, writer, args):
+    """utils/trainer.py:310-400.  With PointNetSeg + CrossEntropyLoss + Adam on
+    the HIP device each iteration is one SegTrainStep (forward, per-point CE,
+    backward into a flat gradient buffer, one Adam launch); otherwise the
+    reference's body runs through autograd over the same kernels."""
+    from .seg import PointNetSeg, SegTrainStep
+    max_test_accu = max_test_cat_iou = max_test_all_iou = float("-inf")
+    max_train_epoch = max_train_cat_epoch = max_train_all_epoch = 0
+    fused = (isinstance(model, PointNetSeg) and type(optimizer) is torch.optim.Adam
+             and len(optimizer.param_groups) == 1
+             and not optimizer.param_groups[0].get("weight_decay", 0)
+             and not optimizer.param_groups[0].get("amsgrad")
+             and type(seg_loss) is torch.nn.CrossEntropyLoss and seg_loss.weight is None
+             and seg_loss.reduction == "mean" and seg_loss.ignore_index < 0
+             and seg_loss.label_smoothing == 0.0 and str(args.device).split(":")[0] == "cuda")
+    step = None
+    for i_iter in range(args.total_iterations):
+        model.train()
+        batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
+        pts, cls, seg = batch
+        pts = pts.float().to(args.device).contiguous()
+        cls = cls.float().to(args.device).contiguous()
+        seg = seg.long().to(args.device).contiguous()
+        if fused:
+            if step is None:
+                step = SegTrainStep(model, optimizer=optimizer, lambda_seg=args.lambda_seg,
+                                    device=args.device)
+            loss_seg_value = float(step(pts, cls, seg).item())
+        else:
+            optimizer.zero_grad()
+            pred, global_gt = model(pts, cls)
+            l = seg_loss(pred, seg)
+            loss_seg_value = l.item()
+            (args.lambda_seg * l).backward()
+            optimizer.step()
+        train_logger.info("iter = {0:8d}/{1:8d} loss_seg = {2:.3f} ".format(
+            i_iter, args.total_iterations, loss_seg_value))
+        if getattr(args, "tensorboard", False) and writer is not None:
+            writer.add_scalar("Loss/train_seg", loss_seg_value, i_iter)
+        if i_iter % args.iter_save_epoch == 0:
+            if step is not None:
+                step.sync_optimizer_state()
+            torch.save(model.state_dict(), os.path.join(
+                args.exp_dir, "model_train_epoch_{}.pth".format(i_iter // len(trainloader_gt))))
+        if i_iter % args.iter_test_epoch == 0:
+            accu, _, cat_iou, all_iou = run_testing_seg(testloader, testdataset, model, seg_loss,
+                                                        test_logger, i_iter, writer, args)
+            for tag, val in (("accu", accu), ("cat_iou", cat_iou), ("all_iou", all_iou)):
+                best = {"accu": max_test_accu, "cat_iou": max_test_cat_iou,
+                        "all_iou": max_test_all_iou}[tag]
+                if best < val:
+                    ep = i_iter // args.iter_test_epoch
+                    if tag == "accu":
+                        max_test_accu, max_train_epoch = val, ep
+                    elif tag == "cat_iou":
+                        max_test_cat_iou, max_train_cat_epoch = val, ep
+                    else:
+                        max_test_all_iou, max_train_all_epoch = val, ep
+                    torch.save(model.state_dict(),
+                               os.path.join(args.exp_dir, "model_train_best_{}.pth".format(tag)))
+    if step is not None:
+        step.sync_optimizer_state()
+    if getattr(args, "tensorboard", False) and writer is not None:
+        writer.close()
+    train_logger.info("=========================")
+    train_logger.info("Max test accuracy: {:.4f}, at epoch: {}".format(max_test_accu, max_train_epoch))
+    train_logger.info("Max cat mIoU: {:.4f}, at epoch: {}".format(max_test_cat_iou, max_train_cat_epoch))
+    train_logger.info("Max all mIoU: {:.4f}, at epoch: {}".format(max_test_all_iou, max_train_all_epoch))
+    return max_test_accu, max_test_cat_iou, max_test_all_iou

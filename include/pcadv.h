@@ -250,6 +250,38 @@ int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* 
                           const float* w, float* dw, float* db, float* dx, int64_t lddx,
                           int relu_x, hipStream_t stream);
 
+/* ---- data path: HDF5-free dataset reader -------------------
+ * Replaces h5py's f['data'][:, 0:npts, :], f['label'][:], f['pid'][:, 0:npts]
+ * in dataset/modelNetData.py:43-47 and dataset/shapeNetData.py:176-181 (host
+ * code; no HDF5 library).  pcadv_h5_info: rank, dims[<= 8] and the stored type
+ * (PCADV_H5_F32 / _F64, or PCADV_H5_INT / _UINT | byte size << 4).
+ * pcadv_h5_read: the whole dataset converted to f32 or int64 (row-major), the
+ * second dimension cut to its first keep1 entries when 0 < keep1 < dims[1]. */
+#define PCADV_H5_F32 1
+#define PCADV_H5_F64 2
+#define PCADV_H5_INT 3
+#define PCADV_H5_UINT 4
+#define PCADV_H5_OUT_F32 0
+#define PCADV_H5_OUT_I64 1
+int pcadv_h5_info(const char* path, const char* name, int* rank, int64_t* dims, int* dtype);
+int pcadv_h5_read(const char* path, const char* name, int out_type, int64_t keep1, void* out,
+                  size_t out_bytes);
+
+/* Batch assembly on the device: out[b] = src[idx[b]][0:npts] (+ jitter), with
+ * src [n_src][src_npts][3] resident in HBM (the whole split), labels
+ * src_lab [n_src][lab_width] and part ids src_seg [n_src][src_npts] (both
+ * nullable) gathered alongside.  Jitter (dataset/modelNetData.py:80-91):
+ * + clip(sigma * z, -clip, clip) per coordinate (sigma = 0: none), z from
+ * `noise` ([B][npts][3] f64 standard normals, computed in f64 like numpy) or,
+ * when noise is NULL, Philox normals keyed by (seed, *step, point).  Indices
+ * must lie in [0, n_src) (checked by the caller; out-of-range rows are left
+ * untouched). */
+int pcadv_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
+                        const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
+                        const int64_t* src_seg, double sigma, double clip, const double* noise,
+                        uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
+                        int64_t* out_seg, hipStream_t stream);
+
 /* CrossEntropyLoss over rows (the per-point segmentation loss, mean over M
  * points): *loss, and dlogits = scale * dL/dlogits (same stride ld). */
 size_t pcadv_row_ce_workspace_bytes(int M);
