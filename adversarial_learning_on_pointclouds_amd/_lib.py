@@ -114,6 +114,7 @@ SIGNATURES = {
     "pcadv_adv_step_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_adv_step": (_i, [ctypes.POINTER(AdvArgs), _vp]),
     "pcadv_adv_step_adam": (_i, [ctypes.POINTER(AdvArgs), _vp]),
+    "pcadv_cls_step": (_i, [ctypes.POINTER(AdvArgs), _vp]),
 }
 
 _lib = None

@@ -262,6 +262,74 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   return PCADV_OK;
 }
 
+// run_training_pointnet_cls's iteration (utils/trainer.py:222-268,
+// feature_transform=False; BASELINE configs[1]): PointNetCls on B labelled
+// clouds, loss = lambda_cls * CE, backward, Adam on the generator only.  The
+// same kernels as the adversarial step minus the discriminator: the feature
+// forward over C = B clouds, fc1, fc2 + dropout, fc3 (k_linear_fwd), the CE and
+// its gradient (k_row_ce), the head backward (k_linear_bwd x3), the sparse
+// feature backward and one Adam launch.
+static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
+  PC_REQUIRE(a && a->B > 0 && a->B <= 256 && a->N > 0 && a->pts_gt && a->labels && a->g_param &&
+                 a->g_grad && a->step_count && a->losses,
+             "cls_step: bad arguments");
+  const int B = a->B, N = a->N, C = B;
+  PC_REQUIRE(a->workspace && a->workspace_bytes >= carve(B, N, nullptr).total,
+             "cls_step: workspace too small (need %zu bytes)", carve(B, N, nullptr).total);
+  StepWs w = carve(B, N, static_cast<char*>(a->workspace));
+  const float* G = a->g_param;
+  float* gG = a->g_grad;
+  const int32_t* st = a->step_count;
+  float* logits = a->logits ? a->logits : w.logits;
+  const float* mask = nullptr;
+  if (a->drop_mask_gt) {
+    if (hipMemcpyAsync(w.mask, a->drop_mask_gt, sizeof(float) * B * 256, hipMemcpyDeviceToDevice,
+                       s) != hipSuccess) {
+      set_error("cls_step: mask staging copy failed");
+      return PCADV_EHIP;
+    }
+    mask = w.mask;
+  }
+  const int32_t* rstep = mask ? nullptr : st;
+  PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
+                               G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                               G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
+                               G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
+                               w.feat_ws, w.feat_ws_bytes, s));
+  PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
+                           PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
+  PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
+                           PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s, 0,
+                           mask ? nullptr : w.mask));
+  PC_TRY(launch_linear_fwd(w.h2, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, logits, C, 40, 256,
+                           PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, s));
+  // CrossEntropyLoss (train_classification.py:199) and lambda_cls * dCE/dlogits
+  PC_TRY(launch_row_ce(logits, 40, a->labels, B, 40, a->lambda_cls, a->losses, w.dlogits,
+                       w.dslabs, (size_t)disc_rowblocks(B) * disc_tail_slab_floats() * sizeof(float),
+                       s));
+  PC_TRY(launch_linear_bwd(w.dlogits, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h2,
+                           G + PCADV_G_FC3_W, w.dh2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, C,
+                           40, 256, s));
+  PC_TRY(launch_linear_bwd(w.dh2, w.h2, PCADV_ACT_RELU, w.mask, nullptr, 0, a->drop_p, w.h1,
+                           G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C, C,
+                           256, 512, s));
+  PC_TRY(launch_linear_bwd(w.dh1, w.h1, PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, w.gmax,
+                           G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
+                           C, 512, 1024, s));
+  PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
+                         G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                         G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
+                         gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
+                         gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
+                         gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
+                         s));
+  if (!a->apply_adam) return PCADV_OK;
+  PC_REQUIRE(a->g_m && a->g_v, "cls_step: Adam moments");
+  return launch_adam2(a->g_param, a->g_grad, a->g_m, a->g_v, PCADV_G_NUMEL, a->lr_g, nullptr,
+                      nullptr, nullptr, nullptr, 0, 0.f, a->step_count, 0, a->beta1, a->beta2,
+                      a->eps, s);
+}
+
 }  // namespace pcadv
 
 using namespace pcadv;
@@ -470,5 +538,7 @@ int pcadv_adv_step(const pcadv_adv_args* args, hipStream_t stream) { return adv_
 int pcadv_adv_step_adam(const pcadv_adv_args* args, hipStream_t stream) {
   return adv_adam(args, stream);
 }
+
+int pcadv_cls_step(const pcadv_adv_args* args, hipStream_t stream) { return cls_step(args, stream); }
 
 }  // extern "C"

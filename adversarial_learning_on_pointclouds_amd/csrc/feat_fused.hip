@@ -125,6 +125,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     const int c = tile / T, p0 = (tile % T) * PM_P;
     if (tid < PM_P * 3) L.pts[(tid / 3) * 4 + tid % 3] = pv;
     __syncthreads();  // (also: every wave is past the previous tile's conv3 reads)
+    STAMP(3 + 5 * it);
     if (it + 1 < PM_TPW && tile + 1 < ntiles) pv = pts_load(tile + 1);  // in flight during this tile
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -133,6 +134,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
     }
     __syncthreads();
+    STAMP(4 + 5 * it);
     {  // conv2 + ReLU, written to LDS split three ways for conv3
       const int pt = wave >> 1, col = 32 * (wave & 1) + r;
       f32x16 acc = {};
@@ -146,6 +148,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       }
     }
     __syncthreads();
+    STAMP(5 + 5 * it);
     {  // conv3 (64 -> 128) + ReLU -> x3 (HBM): wave = channel tile, both point tiles
       f32x16 acc[2] = {{}, {}};
 #pragma unroll
@@ -164,6 +167,10 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
           acc[pt] = mfma_bf16(xh, w3h[kb], acc[pt]);
         }
       }
+#ifdef PCADV_STAMPS
+      asm volatile("s_nop 0" ::"v"(acc[0][0]), "v"(acc[1][15]));
+#endif
+      STAMP(6 + 5 * it);
       float* xg = x3g + ((size_t)c * N + p0) * 128 + 32 * wave + r;
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt)
@@ -173,6 +180,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
           const float v = acc[pt][i] + bias3;
           if (p0 + row < N) xg[(size_t)row * 128] = v > 0.f ? v : 0.f;
         }
+      STAMP(7 + 5 * it);
     }
   }
   STAMP(2);

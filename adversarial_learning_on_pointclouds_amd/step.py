@@ -233,3 +233,109 @@ class AdvTrainStep:
             if opt is not None:
                 for st in opt.state.values():
                     st["step"] = torch.tensor(t)
+
+
+class ClsTrainStep:
+    """run_training_pointnet_cls's iteration (utils/trainer.py:222-268) for
+    PointNetCls(k=40, feature_transform=False): forward on B labelled clouds,
+    lambda_cls * CrossEntropyLoss, backward, Adam - one pcadv_cls_step call
+    (BASELINE configs[1]).  Parameters, gradients and Adam moments are flat
+    buffers as in AdvTrainStep; returns the device tensor [loss_cls]."""
+
+    def __init__(self, model, B, N, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
+                 lambda_cls=1.0, seed=0, device="cuda"):
+        self.lib = _lib.load()
+        self.model = model
+        self.B, self.N = int(B), int(N)
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("ClsTrainStep runs on the HIP device only")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        if getattr(model, "feature_transform", False):
+            raise NotImplementedError("ClsTrainStep: feature_transform=True trains through "
+                                      "run_training_pointnet_cls's autograd path")
+        if optimizer is not None:
+            g = optimizer.param_groups[0]
+            lr, betas, eps = g["lr"], tuple(g["betas"]), g["eps"]
+        self.hp = dict(lr=float(lr), betas=betas, eps=float(eps), lambda_cls=float(lambda_cls),
+                       p=float(model.dropout.p))
+        self.g_param = flatten_params(model, G_LAYOUT, G_NUMEL, dev)
+        self.g_grad = torch.zeros(G_NUMEL, device=dev)
+        self.g_m = torch.zeros_like(self.g_param)
+        self.g_v = torch.zeros_like(self.g_param)
+        self.step_count = torch.zeros(1, device=dev, dtype=torch.int32)
+        mv, vv, gv = (_views(self.g_m, model, G_LAYOUT), _views(self.g_v, model, G_LAYOUT),
+                      _views(self.g_grad, model, G_LAYOUT))
+        for name, p in model.named_parameters():
+            p.grad = gv[name]
+            if optimizer is not None:
+                optimizer.state[p] = {"step": torch.zeros((), dtype=torch.float32),
+                                      "exp_avg": mv[name], "exp_avg_sq": vv[name]}
+        self.optimizer = optimizer
+        self.losses = torch.zeros(1, device=dev)
+        self.logits = torch.zeros(self.B, 40, device=dev)
+        nbytes = self.lib.pcadv_adv_step_workspace_bytes(self.B, self.N)
+        self.workspace = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._keep = []
+
+    def _args(self, pts, labels, mask, apply_adam):
+        B, N = int(pts.shape[0]), self.N
+        if not 0 < B <= self.B:
+            raise ValueError(f"batch of {B} clouds; this step was built for at most {self.B}")
+        for t, nm, shape, dt in ((pts, "pts", (B, N, 3), torch.float32),
+                                 (labels, "labels", (B,), torch.int64)):
+            if (tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous()
+                    or t.device != self.device):
+                raise ValueError(f"{nm}: expected contiguous {dt} {shape} on {self.device}")
+        a = AdvArgs()
+        a.B, a.N = B, N
+        a.pts_gt, a.labels = pts.data_ptr(), labels.data_ptr()
+        if mask is not None:
+            if tuple(mask.shape) != (B, 256) or mask.dtype != torch.float32 or not mask.is_contiguous():
+                raise ValueError("dropout mask must be contiguous float32 (B, 256)")
+            a.drop_mask_gt = mask.data_ptr()
+        a.g_param, a.g_grad = self.g_param.data_ptr(), self.g_grad.data_ptr()
+        a.g_m, a.g_v = self.g_m.data_ptr(), self.g_v.data_ptr()
+        a.step_count = self.step_count.data_ptr()
+        hp = self.hp
+        a.lr_g, a.beta1, a.beta2, a.eps = hp["lr"], hp["betas"][0], hp["betas"][1], hp["eps"]
+        a.lambda_cls, a.drop_p = hp["lambda_cls"], hp["p"]
+        a.rng_seed = self.seed
+        a.apply_adam = int(bool(apply_adam))
+        a.losses = self.losses.data_ptr()
+        a.logits = self.logits.data_ptr()
+        a.workspace = self.workspace.data_ptr()
+        a.workspace_bytes = self.workspace.numel()
+        return a
+
+    def __call__(self, pts, labels, mask=None, apply_adam=True):
+        a = self._args(pts, labels, mask, apply_adam)
+        check(self.lib.pcadv_cls_step(ctypes.byref(a), stream_ptr()), "pcadv_cls_step")
+        return self.losses
+
+    def capture_on(self, pts, labels):
+        """A HIP graph of one step over resident buffers (state restored)."""
+        saved = [t.clone() for t in (self.g_param, self.g_m, self.g_v, self.step_count)]
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(pts, labels)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        a = self._args(pts, labels, None, True)
+        self._keep.append(a)
+        with torch.cuda.graph(g):
+            check(self.lib.pcadv_cls_step(ctypes.byref(a), stream_ptr()), "pcadv_cls_step (capture)")
+        torch.cuda.synchronize()
+        for dst, src in zip((self.g_param, self.g_m, self.g_v, self.step_count), saved):
+            dst.copy_(src)
+        return g
+
+    def sync_optimizer_state(self):
+        if self.optimizer is not None:
+            t = float(self.step_count.item())
+            for st in self.optimizer.state.values():
+                st["step"] = torch.tensor(t)

@@ -233,27 +233,51 @@ def run_training_semi(trainloader_gt, trainloader_nogt, trainloader_gt_iter,
 
 def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, model, cls_loss,
                               optimizer, train_logger, test_logger, writer, args):
-    """utils/trainer.py:222-308 (supervised baseline, no discriminator)."""
+    """utils/trainer.py:222-308 (supervised baseline, no discriminator).  With
+    PointNetCls(k=40, feature_transform=False), CrossEntropyLoss and Adam on the
+    HIP device each iteration is one ClsTrainStep (pcadv_cls_step); otherwise
+    (e.g. feature_transform=True, whose regulariser joins the loss) the
+    reference's body runs through autograd over the same kernels."""
+    from .step import ClsTrainStep
     max_test_accu = float("-inf")
     max_train_epoch = 0
+    fused = (isinstance(model, PointNetCls) and not model.feature_transform
+             and model.fc3.out_features == 40 and type(optimizer) is torch.optim.Adam
+             and len(optimizer.param_groups) == 1
+             and not optimizer.param_groups[0].get("weight_decay", 0)
+             and not optimizer.param_groups[0].get("amsgrad")
+             and type(cls_loss) is torch.nn.CrossEntropyLoss and cls_loss.weight is None
+             and cls_loss.reduction == "mean" and cls_loss.label_smoothing == 0.0
+             and str(args.device).split(":")[0] == "cuda")
+    step = None
     for i_iter in range(args.total_iterations):
         model.train()
-        optimizer.zero_grad()
         batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
         pts, cls = batch
-        pts, cls = pts.float().to(args.device), cls.long().to(args.device)
-        pred, global_gt, high_feat = model(pts)
-        l = cls_loss(pred, cls)
-        loss = args.lambda_cls * l
+        pts, cls = pts.float().to(args.device).contiguous(), cls.long().to(args.device).contiguous()
         l_regu = None
-        if high_feat is not None:  # feature_transform=True (:256-268)
-            l_regu = feature_transform_regularizer(high_feat)
-            loss = loss + args.lambda_regu * l_regu
-        loss.backward()
-        optimizer.step()
+        if fused:
+            if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
+                step = ClsTrainStep(model, pts.shape[0], pts.shape[1], optimizer=optimizer,
+                                    lambda_cls=args.lambda_cls,
+                                    seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)
+            l_value = float(step(pts, cls)[0].item())
+        else:
+            optimizer.zero_grad()
+            pred, global_gt, high_feat = model(pts)
+            l = cls_loss(pred, cls)
+            loss = args.lambda_cls * l
+            if high_feat is not None:  # feature_transform=True (:256-268)
+                l_regu = feature_transform_regularizer(high_feat)
+                loss = loss + args.lambda_regu * l_regu
+            loss.backward()
+            optimizer.step()
+            l_value = l.item()
         train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
-            i_iter, args.total_iterations, l.item(), 0.0 if l_regu is None else l_regu.item()))
+            i_iter, args.total_iterations, l_value, 0.0 if l_regu is None else l_regu.item()))
         if i_iter % args.iter_save_epoch == 0:
+            if step is not None:
+                step.sync_optimizer_state()
             torch.save(model.state_dict(), os.path.join(
                 args.exp_dir, "model_train_epoch_{}.pth".format(i_iter // len(trainloader_gt))))
         if i_iter % args.iter_test_epoch == 0:
@@ -262,6 +286,8 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
                 max_test_accu = curr_accu
                 max_train_epoch = i_iter // args.iter_test_epoch
                 torch.save(model.state_dict(), os.path.join(args.exp_dir, "model_train_best.pth"))
+    if step is not None:
+        step.sync_optimizer_state()
     train_logger.info("Max test accuracy: {:.4f}".format(max_test_accu))
     train_logger.info("Train model is at epoch: {}".format(max_train_epoch))
     return max_test_accu

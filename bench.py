@@ -40,9 +40,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--config", choices=["adv", "seg"], default="adv",
+    ap.add_argument("--config", choices=["adv", "seg", "cls"], default="adv",
                     help="adv: the headline adversarial cls step (default); seg: the "
-                         "PointNetSeg training step of BASELINE configs[3]")
+                         "PointNetSeg training step of BASELINE configs[3]; cls: the "
+                         "supervised PointNetCls step of configs[1]")
     return ap.parse_args()
 
 
@@ -117,6 +118,81 @@ def cpu_baseline_seg(seconds, Bs, Ns):
     return {"value": round(b * steps / dt, 2), "unit": "clouds/s", "cores": cores, "kind": "port",
             "sample": f"{steps} numpy-oracle seg steps (B={b}, N={Ns}, fp32, forward+CE+backward+Adam) "
                       f"in {dt:.1f}s"}
+
+
+def cpu_baseline_cls(seconds):
+    """The numpy oracle's run_training_pointnet_cls iteration (B=32, N=1024:
+    forward with a dropout mask, CE, backward, Adam) timed on the host cores."""
+    from oracle import pointnet_np as onp
+    G = onp.make_params(onp.cls_spec(40), seed=3)
+    opt = onp.Adam(G)
+    rng = np.random.default_rng(3000)
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    m = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+
+    def one():
+        logits, _, cache = onp.cls_forward(G, pts, m)
+        _, dlog = onp.cross_entropy(logits, lab)
+        opt.step(onp.cls_backward(G, cache, dlog))
+
+    one()
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        one()
+        steps += 1
+        if time.perf_counter() - t0 >= seconds and steps >= 2:
+            break
+    dt = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"value": round(B * steps / dt, 2), "unit": "clouds/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} numpy-oracle cls steps (B=32, N=1024, fp32) in {dt:.1f}s"}
+
+
+def bench_cls(args):
+    """BASELINE.json configs[1]: PointNetCls ModelNet40 B=32, N=1024, no
+    discriminator - one run_training_pointnet_cls iteration per step
+    (pcadv_cls_step), HIP-graph replayed over resident batches."""
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd.step import ClsTrainStep
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = pc.PointNetCls(k=40).to(dev)
+    step = ClsTrainStep(model, B, N, seed=7, device=dev)
+    pool = []
+    for k in range(POOL):
+        rng = np.random.default_rng(3000 + k)
+        pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
+                     torch.from_numpy(rng.integers(0, 40, B)).to(dev)))
+    graphs = [step.capture_on(*b) for b in pool]
+    for k in range(args.warmup):
+        graphs[k % POOL].replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        graphs[k % POOL].replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gflop = 11.18  # SURVEY.md 8(d): algorithmic FLOPs of one cfg-2 step
+    loss = float(step.losses[0].item())
+    out = {
+        "metric": "point-clouds/sec (cls train step, no discriminator), B=32 N=1024 ModelNet40, 1 GPU",
+        "value": round(B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32 (conv4 as three bf16 MFMA products, f32-level; configs[1] allows bf16)",
+        "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
+        "config": {"workload": "run_training_pointnet_cls: PointNetCls(k=40), CE, Adam, B=32, "
+                               "N=1024 (BASELINE configs[1])", "global_batch": B, "points": N,
+                   "parallelism": "dp1", "hip_graph": True},
+        "step_flops": {"gflop_per_step": gflop,
+                       "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
+        "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
+    }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_cls(args.cpu_seconds)
+    print(json.dumps(out), flush=True)
 
 
 def bench_seg(args):
@@ -223,6 +299,8 @@ def main():
     args = parse()
     if args.config == "seg":
         return bench_seg(args)
+    if args.config == "cls":
+        return bench_cls(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -341,6 +341,15 @@ int pcadv_adv_step(const pcadv_adv_args* args, hipStream_t stream);
  * Uses the step counter already advanced by that pcadv_adv_step. */
 int pcadv_adv_step_adam(const pcadv_adv_args* args, hipStream_t stream);
 
+/* One iteration of run_training_pointnet_cls (utils/trainer.py:222-268,
+ * feature_transform=False; BASELINE configs[1]): PointNetCls forward on the B
+ * clouds of pts_gt (labels), loss = lambda_cls * CrossEntropyLoss, backward,
+ * and (apply_adam) the generator's Adam step.  Uses the generator fields of
+ * pcadv_adv_args (pts_nogt, d_*, soft_*, lambda_adv, semi ignored);
+ * drop_mask_gt optional (else device-drawn); losses[0] = CE; workspace as
+ * pcadv_adv_step_workspace_bytes(B, N). */
+int pcadv_cls_step(const pcadv_adv_args* args, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
