@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--points", type=int, default=1024,
+                    help="points per cloud of the adv step (1024: the metric's config; 2048: "
+                         "BASELINE configs[4]'s per-rank shape)")
     ap.add_argument("--config", choices=["adv", "seg", "cls"], default="adv",
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
@@ -84,7 +87,7 @@ def cpu_baseline(seconds):
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     return {"value": round(2 * B * steps / dt, 2), "unit": "clouds/s", "cores": cores,
             "kind": "port",
-            "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N=1024, fp32) in {dt:.1f}s"}
+            "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N={N}, fp32) in {dt:.1f}s"}
 
 
 def cpu_baseline_seg(seconds, Bs, Ns):
@@ -296,7 +299,9 @@ def bench_seg(args):
 
 
 def main():
+    global N
     args = parse()
+    N = args.points
     if args.config == "seg":
         return bench_seg(args)
     if args.config == "cls":
@@ -405,11 +410,12 @@ def main():
         if all(n in kern for n in names):
             traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
             traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))
-    step_gflop = 22.47  # algorithmic FLOPs of one B=32 adversarial step
+    # algorithmic FLOPs of one B=32 adversarial step (44.53 at N=2048)
+    step_gflop = 22.47 if N == 1024 else 22.47 * N / 1024.0
     step_tf = step_gflop * world * args.steps / dt / 1e3
 
     result = {
-        "metric": "point-clouds/sec (adv train step), B=32 N=1024 ModelNet40, 1/2/4/8 GPU",
+        "metric": f"point-clouds/sec (adv train step), B=32 N={N} ModelNet40, 1/2/4/8 GPU",
         "value": round(2 * B * args.steps * world / dt, 1),
         "unit": "clouds/s",
         "n_gpus": world,
@@ -422,7 +428,7 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
         "config": {"workload": "adversarial cls step: PointNetCls(k=40)+DeepConvDiscNet(40,1), "
-                               "B=32 GT + 32 noGT clouds/GPU, N=1024, Adam x2",
+                               f"B=32 GT + 32 noGT clouds/GPU, N={N}, Adam x2",
                    "global_batch": 2 * B * world, "points": N,
                    "parallelism": f"dp{world}", "hip_graph": use_graph},
         "roofline": {"bound": "mfma",

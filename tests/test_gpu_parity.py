@@ -329,6 +329,33 @@ def test_adv_step_full_size_vs_oracle():
         assert rel_err(p.detach().cpu().numpy(), D[nm]) < 1e-5, nm
 
 
+def test_adv_step_cfg5_shape_vs_oracle():
+    """BASELINE configs[4]'s per-rank shape (B=32 GT + 32 no-GT, N=2048): one
+    step's gradients against the oracle."""
+    B, N = 32, 2048
+    step, model, model_D = _make_step(B, N, g_seed=5, d_seed=6)
+    rng = np.random.default_rng(4004)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+    G = onp.make_params(onp.cls_spec(40), seed=5)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=6, init="xavier")
+    losses_ref, gG, gD, _ = onp.adv_step(G, D, None, None, pg, lab, pn, m1, m2, y1, y2,
+                                         apply_adam=False)
+    losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                  soft=(_t(y1), _t(y2)), apply_adam=False).cpu().numpy()
+    for i, k in enumerate(["loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt"]):
+        assert abs(losses[i] - losses_ref[k]) < 1e-4, (k, losses[i], losses_ref[k])
+    for nm, p in model.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), gG[nm]) < TOL, nm
+    for nm, p in model_D.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), gD[nm]) < TOL, nm
+
+
 def test_adv_step_graph_replay_matches_eager():
     B, N = 8, 1024
     s1, m1, _ = _make_step(B, N, seed=77)
