@@ -92,7 +92,12 @@ SIGNATURES = {
     "pcadv_tnet_reg_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_tnet_reg_bwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_gemm": (_i, [_vp, _i64, _i, _vp, _i64, _i, _vp, _i64, _i, _i, _i, _vp, _vp, _i, _i, _i,
-                        _vp, _i64, _i, _vp]),
+                        _vp, _i64, _i, _vp, _vp, _i64, _vp]),
+    "pcadv_gemm_bf2": (_i, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i, _i, _i,
+                            _vp, _vp, _i, _i, _i, _vp, _i64, _vp]),
+    "pcadv_split_bf2": (_i, [_vp, _i64, _i, _i, _vp, _vp, _i64, _vp]),
+    "pcadv_conv_max_bf2": (_i, [_vp, _i64, _vp, _vp, _i64, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i,
+                                _vp, _vp, _vp, _sz, _vp]),
     "pcadv_gemm_wgrad_workspace_bytes": (_sz, [_i, _i, _i, _i]),
     "pcadv_gemm_wgrad": (_i, [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _vp, _vp, _i, _i, _vp,
                               _sz, _vp]),

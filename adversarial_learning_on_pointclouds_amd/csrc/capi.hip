@@ -65,7 +65,11 @@ int launch_head_bwd(const float*, const float*, const float*, int, const float*,
                     float, const float*, const float*, hipStream_t);
 int launch_gemm(const float*, long long, int, const float*, long long, int, float*, long long,
                 int, int, int, const float*, const float*, int, int, int, const float*, long long,
-                int, hipStream_t);
+                int, void*, void*, long long, hipStream_t);
+int launch_gemm_bf2(const void*, const void*, long long, const void*, const void*, long long, float*,
+                    long long, void*, void*, long long, int, int, int, const float*, const float*,
+                    int, int, int, const float*, long long, hipStream_t);
+int launch_split_bf2(const float*, long long, int, int, void*, void*, long long, hipStream_t);
 size_t gemm_wgrad_workspace_bytes(int, int, int, int);
 int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int, int, float*,
                       long long, float*, float*, int, int, void*, size_t, hipStream_t);
@@ -76,7 +80,8 @@ int launch_group_colsum(const float*, const float*, long long, long long, int, i
                         hipStream_t);
 size_t conv_max_x3_workspace_bytes(int, int, int);
 int launch_conv_max_x3(const float*, long long, int, int, int, const float*, const float*, int,
-                       int, float*, int32_t*, void*, size_t, hipStream_t);
+                       int, float*, int32_t*, void*, size_t, hipStream_t, const void*, const void*,
+                       long long, const void*, const void*);
 int launch_cmx_bwd(const float*, const float*, const int32_t*, const float*, long long, int, int,
                    int, int, const float*, float*, float*, float*, long long, int, hipStream_t);
 int launch_gather_clouds(const float*, int64_t, int, int, const int64_t*, int, const int64_t*, int,
@@ -464,9 +469,24 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
 int pcadv_gemm(const float* a, int64_t lda, int ta, const float* b, int64_t ldb, int tb,
                float* c, int64_t ldc, int M, int N, int K, const float* bias,
                const float* bias_rows, int rows_per_group, int relu, int accumulate,
-               const float* cmask, int64_t ldm, int precise, hipStream_t stream) {
+               const float* cmask, int64_t ldm, int precise, void* c_hi, void* c_lo, int64_t ldcp,
+               hipStream_t stream) {
   return launch_gemm(a, lda, ta, b, ldb, tb, c, ldc, M, N, K, bias, bias_rows, rows_per_group,
-                     relu, accumulate, cmask, ldm, precise, stream);
+                     relu, accumulate, cmask, ldm, precise, c_hi, c_lo, ldcp, stream);
+}
+
+int pcadv_gemm_bf2(const void* a_hi, const void* a_lo, int64_t lda, const void* b_hi,
+                   const void* b_lo, int64_t ldb, float* c, int64_t ldc, void* c_hi, void* c_lo,
+                   int64_t ldcp, int M, int N, int K, const float* bias, const float* bias_rows,
+                   int rows_per_group, int relu, int accumulate, const float* cmask, int64_t ldm,
+                   hipStream_t stream) {
+  return launch_gemm_bf2(a_hi, a_lo, lda, b_hi, b_lo, ldb, c, ldc, c_hi, c_lo, ldcp, M, N, K, bias,
+                         bias_rows, rows_per_group, relu, accumulate, cmask, ldm, stream);
+}
+
+int pcadv_split_bf2(const float* x, int64_t ld, int rows, int cols, void* hi, void* lo,
+                    int64_t ldo, hipStream_t stream) {
+  return launch_split_bf2(x, ld, rows, cols, hi, lo, ldo, stream);
 }
 
 size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) {
@@ -502,7 +522,17 @@ int pcadv_conv_max_x3(const float* x, int64_t ldx, int C, int Npts, int K, const
                       const float* b, int O, int relu, float* gmax, int32_t* gidx,
                       void* workspace, size_t workspace_bytes, hipStream_t stream) {
   return launch_conv_max_x3(x, ldx, C, Npts, K, w, b, O, relu, gmax, gidx, workspace,
-                            workspace_bytes, stream);
+                            workspace_bytes, stream, nullptr, nullptr, 0, nullptr, nullptr);
+}
+
+int pcadv_conv_max_bf2(const float* x, int64_t ldx, const void* x_hi, const void* x_lo,
+                       int64_t ldxp, int C, int Npts, int K, const float* w, const void* w_hi,
+                       const void* w_lo, const float* b, int O, int relu, float* gmax,
+                       int32_t* gidx, void* workspace, size_t workspace_bytes,
+                       hipStream_t stream) {
+  PC_REQUIRE(x_hi && x_lo && w_hi && w_lo, "conv_max_bf2: planes required");
+  return launch_conv_max_x3(x, ldx, C, Npts, K, w, b, O, relu, gmax, gidx, workspace,
+                            workspace_bytes, stream, x_hi, x_lo, ldxp, w_hi, w_lo);
 }
 
 int pcadv_conv_max_x3_bwd(const float* dgmax, const float* gmax, const int32_t* gidx,

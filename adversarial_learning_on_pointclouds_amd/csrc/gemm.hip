@@ -71,6 +71,12 @@ struct GemmP {
   int grp, zpg, ksplit_len;
   long long slab_stride;           // floats between slabs
   float* csum;                     // TA = 1: per-slab column sums of A ([z][M]) or null
+  // TA / TB = 2: the operand given as its bf16 hi / lo planes ([m][k] / [n][k],
+  // row stride in elements), split once by its producer: staged as plain
+  // copies (no VALU split per tile)
+  const __bf16* ap[2]; long long ldap;
+  const __bf16* bp[2]; long long ldbp;
+  __bf16* cp[2]; long long ldcp;    // nullable: the epilogue also writes C's hi / lo planes
   // max-over-points screening epilogue (mode 2): per (row tile, column) top-2
   int2* part;                      // [M / BM][N] screening keys
 };
@@ -129,7 +135,8 @@ k_gemm_x3(GemmP p) {
   const int cl = MODE == 2 ? tx / T2 : 0;
   const int m0 = MODE == 2 ? (tx % T2) * GM_BM : tx * GM_BM;
   const int Mlim = MODE == 2 ? p.rows_per_group : p.M;
-  const float* Ab = MODE == 2 ? p.a + (size_t)cl * p.rows_per_group * p.lda : p.a;
+  const float* Ab = MODE == 2 && TA != 2 ? p.a + (size_t)cl * p.rows_per_group * p.lda : p.a;
+  const size_t aoff2 = MODE == 2 ? (size_t)cl * p.rows_per_group * p.ldap : 0;
   const int gz = tz / p.zpg, sz = tz % p.zpg;
   const int kz0 = gz * p.grp + sz * p.ksplit_len;
   const int kz1 = min(min(p.K, (gz + 1) * p.grp), kz0 + p.ksplit_len);
@@ -208,15 +215,39 @@ k_gemm_x3(GemmP p) {
         *reinterpret_cast<bf16x4g*>(&planes[q][(col + i) * GM_S + kk]) = pv[q];
     }
   };
+  // planes: thread = (row tid >> 1, 16 k at 16 (tid & 1)); v[0..1] = hi, v[2..3]
+  // = lo, each 8 bf16 carried as 16 raw bytes (K % 16 == 0, ld % 8 == 0)
+  auto load_planes = [&](f32x4 (&v)[4], const __bf16* const (&pl)[2], size_t off, long long ld,
+                         int row0, int rlim, int k0) {
+    const int row = row0 + (tid >> 1), k = k0 + 16 * (tid & 1);
+    const bool ok = row < rlim && k >= kz0 && k < kz1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const __bf16* src = pl[q] + off + (size_t)row * ld + k;
+      v[2 * q] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[2 * q + 1] = ok ? *reinterpret_cast<const f32x4*>(src + 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_planes = [&](const f32x4 (&v)[4], __bf16 (*planes)[GM_BM * GM_S]) {
+    const int row = tid >> 1, kk = 16 * (tid & 1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk]) = v[2 * q];
+      *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk + 8]) = v[2 * q + 1];
+    }
+  };
   float cs[4] = {0.f, 0.f, 0.f, 0.f};  // TA = 1: this thread's column sums of A
   auto load_tile = [&](f32x4 (&ra)[4], f32x4 (&rb)[4], int k0) {
-    if (TA == 0) load_rows(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
+    if (TA == 2) load_planes(ra, p.ap, aoff2, p.ldap, m0, Mlim, k0);
+    else if (TA == 0) load_rows(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
     else load_cols(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
-    if (TB == 0) load_rows(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
+    if (TB == 2) load_planes(rb, p.bp, 0, p.ldbp, n0, p.N, k0);
+    else if (TB == 0) load_rows(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
     else load_cols(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
   };
   auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
-    if (TA == 0) store_rows(ra, L.a);
+    if (TA == 2) store_planes(ra, L.a);
+    else if (TA == 0) store_rows(ra, L.a);
     else {
       store_cols(ra, L.a);
       if (do_csum) {
@@ -224,7 +255,8 @@ k_gemm_x3(GemmP p) {
         for (int i = 0; i < 4; ++i) cs[i] += ((ra[0][i] + ra[1][i]) + ra[2][i]) + ra[3][i];
       }
     }
-    if (TB == 0) store_rows(rb, L.b);
+    if (TB == 2) store_planes(rb, L.b);
+    else if (TB == 0) store_rows(rb, L.b);
     else store_cols(rb, L.b);
   };
 
@@ -376,6 +408,17 @@ k_gemm_x3(GemmP p) {
             if (!(mv[t] > 0.f)) v[t] = 0.f;
           }
           *reinterpret_cast<f32x4*>(dst) = v;
+          if (p.cp[0]) {  // the hi / lo planes the next layer stages (ldcp % 4 == 0)
+            bf16x4g hv, lv;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              hv[t] = (__bf16)v[t];
+              lv[t] = (__bf16)(v[t] - (float)hv[t]);
+            }
+            const size_t pofs = (size_t)m * p.ldcp + n;
+            *reinterpret_cast<bf16x4g*>(p.cp[0] + pofs) = hv;
+            *reinterpret_cast<bf16x4g*>(p.cp[1] + pofs) = lv;
+          }
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
@@ -387,6 +430,11 @@ k_gemm_x3(GemmP p) {
             if (p.relu) x = x > 0.f ? x : 0.f;
             if (mk && !(mk[t] > 0.f)) x = 0.f;
             dst[t] = x;
+            if (p.cp[0]) {
+              const __bf16 hx = (__bf16)x;
+              p.cp[0][(size_t)m * p.ldcp + n + t] = hx;
+              p.cp[1][(size_t)m * p.ldcp + n + t] = (__bf16)(x - (float)hx);
+            }
           }
         }
       }
@@ -689,7 +737,8 @@ static int gemm_launch(const GemmP& p, int nz, hipStream_t s) {
 int launch_gemm(const float* a, long long lda, int ta, const float* b, long long ldb, int tb,
                 float* c, long long ldc, int M, int N, int K, const float* bias,
                 const float* bias_rows, int rows_per_group, int relu, int accumulate,
-                const float* cmask, long long ldm, int precise, hipStream_t s) {
+                const float* cmask, long long ldm, int precise, void* c_hi, void* c_lo,
+                long long ldcp, hipStream_t s) {
   PC_REQUIRE(a && b && c && M > 0 && N > 0 && K > 0, "gemm: bad shape M=%d N=%d K=%d", M, N, K);
   PC_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M), "gemm: bad lda %lld (ta=%d)", lda, ta);
   PC_REQUIRE((tb == 0 && ldb >= K) || (tb == 1 && ldb >= N), "gemm: bad ldb %lld (tb=%d)", ldb, tb);
@@ -710,6 +759,11 @@ int launch_gemm(const float* a, long long lda, int ta, const float* b, long long
            (!bias_rows || (N % 4 == 0 && ((uintptr_t)bias_rows & 15) == 0)) &&
            (!cmask || (ldm % 4 == 0 && ((uintptr_t)cmask & 15) == 0));
   p.grp = K; p.zpg = 1; p.ksplit_len = K;
+  PC_REQUIRE(!c_hi == !c_lo && (!c_hi || (ldcp >= N && ldcp % 4 == 0 && N % 4 == 0 && p.cvec &&
+                                         ((uintptr_t)c_hi & 7) == 0 && ((uintptr_t)c_lo & 7) == 0)),
+             "gemm: output planes need N %% 4, ldcp %% 4 and 16-B aligned C");
+  p.cp[0] = static_cast<__bf16*>(c_hi); p.cp[1] = static_cast<__bf16*>(c_lo); p.ldcp = ldcp;
+  PC_REQUIRE(!c_hi || !(ta == 0 && M <= 32), "gemm: output planes need M > 32");
   if (ta == 0 && M <= 32) {  // per-cloud rows: exact f32 on the vector ALUs
     const dim3 grid(tb ? (N + 15) / 16 : N, (M + 15) / 16);
     if (tb) hipLaunchKernelGGL(k_gemm_small<1>, grid, dim3(256), 0, s, p);
@@ -725,6 +779,64 @@ int launch_gemm(const float* a, long long lda, int ta, const float* b, long long
   if (ta == 0 && tb == 0) return accumulate ? gemm_launch<0, 0, 1, 3>(p, 1, s) : gemm_launch<0, 0, 0, 3>(p, 1, s);
   if (ta == 0 && tb == 1) return accumulate ? gemm_launch<0, 1, 1, 3>(p, 1, s) : gemm_launch<0, 1, 0, 3>(p, 1, s);
   return accumulate ? gemm_launch<1, 1, 1, 3>(p, 1, s) : gemm_launch<1, 1, 0, 3>(p, 1, s);
+}
+
+// Both operands as bf16 hi / lo planes (the 2-way splits of f32 matrices, made
+// once by their producers): the three-product forward GEMM with no per-tile
+// splitting; C (f32) and optionally C's own planes for the next layer.
+int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const void* b_hi,
+                    const void* b_lo, long long ldb, float* c, long long ldc, void* c_hi,
+                    void* c_lo, long long ldcp, int M, int N, int K, const float* bias,
+                    const float* bias_rows, int rows_per_group, int relu, int accumulate,
+                    const float* cmask, long long ldm, hipStream_t s) {
+  PC_REQUIRE(a_hi && a_lo && b_hi && b_lo && c && M > 0 && N > 0 && K > 0,
+             "gemm_bf2: bad shape M=%d N=%d K=%d", M, N, K);
+  PC_REQUIRE(K % 16 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K,
+             "gemm_bf2: K %% 16 and lda, ldb %% 8 required (K=%d lda=%lld ldb=%lld)", K, lda, ldb);
+  PC_REQUIRE((((uintptr_t)a_hi | (uintptr_t)a_lo | (uintptr_t)b_hi | (uintptr_t)b_lo) & 15) == 0,
+             "gemm_bf2: planes must be 16-B aligned");
+  PC_REQUIRE(ldc >= N && (!cmask || ldm >= N) && (!bias_rows || rows_per_group > 0),
+             "gemm_bf2: bad ldc / ldm / bias_rows");
+  GemmP p{};
+  p.ap[0] = static_cast<const __bf16*>(a_hi); p.ap[1] = static_cast<const __bf16*>(a_lo);
+  p.ldap = lda;
+  p.bp[0] = static_cast<const __bf16*>(b_hi); p.bp[1] = static_cast<const __bf16*>(b_lo);
+  p.ldbp = ldb;
+  p.c = c; p.ldc = ldc; p.cmask = cmask; p.ldm = ldm;
+  p.bias = bias; p.bias_rows = bias_rows; p.rows_per_group = rows_per_group;
+  p.M = M; p.N = N; p.K = K; p.relu = relu; p.accumulate = accumulate;
+  p.cvec = ldc % 4 == 0 && ((uintptr_t)c & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0) &&
+           (!bias_rows || (N % 4 == 0 && ((uintptr_t)bias_rows & 15) == 0)) &&
+           (!cmask || (ldm % 4 == 0 && ((uintptr_t)cmask & 15) == 0));
+  PC_REQUIRE(!c_hi == !c_lo && (!c_hi || (ldcp >= N && ldcp % 4 == 0 && N % 4 == 0 && p.cvec)),
+             "gemm_bf2: output planes need N %% 4, ldcp %% 4 and 16-B aligned C");
+  p.cp[0] = static_cast<__bf16*>(c_hi); p.cp[1] = static_cast<__bf16*>(c_lo); p.ldcp = ldcp;
+  p.grp = K; p.zpg = 1; p.ksplit_len = K;
+  return accumulate ? gemm_launch<2, 2, 1, 3>(p, 1, s) : gemm_launch<2, 2, 0, 3>(p, 1, s);
+}
+
+// f32 [rows][cols] (row stride ld) -> bf16 hi / lo planes (row stride ldo)
+__global__ void __launch_bounds__(256)
+k_split_bf2(const float* __restrict__ x, long long ld, int rows, int cols, __bf16* __restrict__ hi,
+            __bf16* __restrict__ lo, long long ldo) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)rows * cols) return;
+  const int r = (int)(e / cols), c = (int)(e % cols);
+  const float v = x[(size_t)r * ld + c];
+  const __bf16 h = (__bf16)v;
+  hi[(size_t)r * ldo + c] = h;
+  lo[(size_t)r * ldo + c] = (__bf16)(v - (float)h);
+}
+
+int launch_split_bf2(const float* x, long long ld, int rows, int cols, void* hi, void* lo,
+                     long long ldo, hipStream_t s) {
+  PC_REQUIRE(x && hi && lo && rows > 0 && cols > 0 && ld >= cols && ldo >= cols,
+             "split_bf2: bad arguments");
+  const long long n = (long long)rows * cols;
+  hipLaunchKernelGGL(k_split_bf2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ld, rows,
+                     cols, static_cast<__bf16*>(hi), static_cast<__bf16*>(lo), ldo);
+  PC_HIP_CHECK_LAUNCH("k_split_bf2");
+  return PCADV_OK;
 }
 
 // weight gradient dW[O][Kin] (+)= sum over the rows of dZ[row][o] X[row][k]:
@@ -844,11 +956,17 @@ size_t conv_max_x3_workspace_bytes(int C, int Npts, int O) {
 
 int launch_conv_max_x3(const float* x, long long ldx, int C, int Npts, int K, const float* w,
                        const float* b, int O, int relu, float* gmax, int32_t* gidx, void* ws,
-                       size_t ws_bytes, hipStream_t s) {
+                       size_t ws_bytes, hipStream_t s, const void* x_hi = nullptr,
+                       const void* x_lo = nullptr, long long ldxp = 0, const void* w_hi = nullptr,
+                       const void* w_lo = nullptr) {
   PC_REQUIRE(x && w && gmax && gidx && C > 0 && Npts > 0 && K > 0 && O > 0,
              "conv_max_x3: bad shape");
   PC_REQUIRE(K % 32 == 0 && ldx % 4 == 0, "conv_max_x3: K %% 32 and ldx %% 4 required");
   PC_REQUIRE(ws && ws_bytes >= conv_max_x3_workspace_bytes(C, Npts, O), "conv_max_x3: workspace");
+  const bool planes = x_hi != nullptr;
+  PC_REQUIRE(!planes || (x_lo && w_hi && w_lo && ldxp % 8 == 0 && ldxp >= K &&
+                         ((((uintptr_t)x_hi | (uintptr_t)x_lo | (uintptr_t)w_hi | (uintptr_t)w_lo) & 15) == 0)),
+             "conv_max_x3: planes need ldxp %% 8 and 16-B alignment");
   const int T = (Npts + GM_BM - 1) / GM_BM;
   int2* part = static_cast<int2*>(ws);
   {
@@ -857,21 +975,41 @@ int launch_conv_max_x3(const float* x, long long ldx, int C, int Npts, int K, co
     p.c = gmax; p.ldc = O;
     p.avec = ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
     p.bvec = K % 4 == 0 && ((uintptr_t)w & 15) == 0;
+    if (planes) {
+      p.ap[0] = static_cast<const __bf16*>(x_hi); p.ap[1] = static_cast<const __bf16*>(x_lo);
+      p.ldap = ldxp;
+      p.bp[0] = static_cast<const __bf16*>(w_hi); p.bp[1] = static_cast<const __bf16*>(w_lo);
+      p.ldbp = K;
+    }
     p.rows_per_group = Npts;
     p.M = C * Npts; p.N = O; p.K = K; p.grp = K; p.zpg = 1; p.ksplit_len = K;
     p.part = part;
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<0, 0, 2, 3>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(GemmLds)) != hipSuccess) {
-        set_error("conv_max_x3: cannot reserve LDS");
-        return PCADV_EHIP;
+    const dim3 grid(C * T, (O + GM_BN - 1) / GM_BN, 1);
+    if (planes) {
+      static bool attr2 = false;
+      if (!attr2) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<2, 2, 2, 3>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(GemmLds)) != hipSuccess) {
+          set_error("conv_max_x3: cannot reserve LDS");
+          return PCADV_EHIP;
+        }
+        attr2 = true;
       }
-      attr = true;
+      hipLaunchKernelGGL((k_gemm_x3<2, 2, 2, 3>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
+    } else {
+      static bool attr = false;
+      if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<0, 0, 2, 3>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(GemmLds)) != hipSuccess) {
+          set_error("conv_max_x3: cannot reserve LDS");
+          return PCADV_EHIP;
+        }
+        attr = true;
+      }
+      hipLaunchKernelGGL((k_gemm_x3<0, 0, 2, 3>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
     }
-    hipLaunchKernelGGL((k_gemm_x3<0, 0, 2, 3>), dim3(C * T, (O + GM_BN - 1) / GM_BN, 1), dim3(GM_T),
-                       sizeof(GemmLds), s, p);
     PC_HIP_CHECK_LAUNCH("k_gemm_x3 (max)");
   }
   const int pairs = C * O;

@@ -35,6 +35,9 @@ __all__ = ["PointNetSeg", "SegTrainStep", "seg_cross_entropy", "seg_forward", "s
 
 _LOC = 960                       # x1..x5 widths 64 + 128 + 128 + 128 + 512
 _FWD_PRECISE = os.environ.get("PCADV_SEG_PRECISE", "0") == "1"  # diagnostics: six-product forward
+# the forward's operands as bf16 hi / lo planes written once by their producers
+# (pcadv_gemm_bf2; bitwise the f32-staged result); PCADV_SEG_PLANES=0 stages f32
+_PLANES = os.environ.get("PCADV_SEG_PLANES", "1") == "1" and not _FWD_PRECISE
 # data gradients dX = dZ W: three products (sums over <= 960 terms; 1.2e-5 of
 # sum|a b|) unless PCADV_SEG_DGRAD_PRECISE=1 (six); weight gradients (sums over
 # all B*N points, heavy cancellation) always take six
@@ -45,6 +48,10 @@ _CONV = [(3, 64), (64, 128), (128, 128), (128, 128), (128, 512), (512, 2048)]
 
 def _p(t, off=0):
     return ctypes.c_void_p(t.data_ptr() + 4 * off)
+
+
+def _pb(t, off=0):  # bf16 tensors: element offsets of 2 bytes
+    return ctypes.c_void_p(t.data_ptr() + 2 * off)
 
 
 def _ws(nbytes, dev):
@@ -59,14 +66,34 @@ class _Engine:
 
     def gemm(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, cmask=None, ldm=0, bias=None,
              bias_rows=None, rows_per_group=0, relu=False, accumulate=False, precise=False,
-             a_off=0, b_off=0, c_off=0, m_off=0):
+             a_off=0, b_off=0, c_off=0, m_off=0, cp=None, ldcp=0, cp_off=0):
         check(self.lib.pcadv_gemm(_p(a, a_off), lda, ta, _p(b, b_off), ldb, tb, _p(c, c_off), ldc,
                                   M, N, K, None if bias is None else _p(bias),
                                   None if bias_rows is None else _p(bias_rows), rows_per_group,
                                   int(relu), int(accumulate),
                                   None if cmask is None else _p(cmask, m_off), ldm, int(precise),
-                                  stream_ptr()),
+                                  None if cp is None else _pb(cp[0], cp_off),
+                                  None if cp is None else _pb(cp[1], cp_off), ldcp, stream_ptr()),
               "pcadv_gemm")
+
+    def gemm_bf2(self, ap, lda, bp, ldb, c, ldc, M, N, K, *, bias=None, bias_rows=None,
+                 rows_per_group=0, relu=False, a_off=0, b_off=0, c_off=0, cp=None, ldcp=0,
+                 cp_off=0):
+        """A, B as (hi, lo) bf16 plane pairs; C f32 (+ its planes)."""
+        check(self.lib.pcadv_gemm_bf2(_pb(ap[0], a_off), _pb(ap[1], a_off), lda, _pb(bp[0], b_off),
+                                      _pb(bp[1], b_off), ldb, _p(c, c_off), ldc,
+                                      None if cp is None else _pb(cp[0], cp_off),
+                                      None if cp is None else _pb(cp[1], cp_off), ldcp, M, N, K,
+                                      None if bias is None else _p(bias),
+                                      None if bias_rows is None else _p(bias_rows),
+                                      rows_per_group, int(relu), 0, None, 0, stream_ptr()),
+              "pcadv_gemm_bf2")
+
+    def split(self, x, hi, lo):
+        """x (rows, cols) f32 contiguous -> hi, lo bf16 of the same shape."""
+        r, c = (1, x.numel()) if x.dim() == 1 else (x.shape[0], x.shape[1])
+        check(self.lib.pcadv_split_bf2(_p(x), c, r, c, _pb(hi), _pb(lo), c, stream_ptr()),
+              "pcadv_split_bf2")
 
     def wgrad(self, dz, ldz, x, ldx, rows, O, K, dw, ldo, *, db=None, gsum=None, rpg=0, dz_off=0,
               x_off=0, dw_off=0):
@@ -113,10 +140,29 @@ def _check_dev(t, name, shape=None, dtype=torch.float32):
         raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
 
 
-def seg_forward(pts, cls, params):
+def _weight_planes(W, Wf, wplanes=None):
+    """(hi, lo) bf16 planes of conv2..conv6 and fc1..fc4, from ``wplanes`` (the
+    caller's split of its flat parameter buffer: a list of 20 (hi, lo) pairs in
+    state_dict order) or split here."""
+    if wplanes is not None:
+        return ([None] + [tuple(t.view(W[i].shape) for t in wplanes[2 * i]) for i in range(1, 6)],
+                [tuple(t.view(Wf[i].shape) for t in wplanes[12 + 2 * i]) for i in range(4)])
+    E = _engine()
+    out = []
+    for w in W[1:] + Wf:
+        hi = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+        lo = torch.empty_like(hi)
+        E.split(w, hi, lo)
+        out.append((hi, lo))
+    return [None] + out[:5], out[5:]
+
+
+def seg_forward(pts, cls, params, wplanes=None):
     """PointNetSeg forward (pointnet.py:282-317) on the engine.  Returns a dict
     with logits (B*N, C) point-major, gmax (B, 2048), gidx (B, 2048) and every
-    activation the backward needs."""
+    activation the backward needs.  Each layer's epilogue also writes its
+    output's bf16 hi / lo planes, which the next layer's GEMM stages as they
+    are (no per-tile splitting)."""
     E = _engine()
     B, N, _ = pts.shape
     M = B * N
@@ -128,22 +174,39 @@ def seg_forward(pts, cls, params):
     Wf = [params[12 + 2 * i].contiguous() for i in range(4)]
     bf = [params[13 + 2 * i].contiguous() for i in range(4)]
     ncls = Wf[3].shape[0]
+    planes = _PLANES
     xloc = torch.empty(M, _LOC, device=dev)
+    pl = lambda rows, cols: (torch.empty(rows, cols, device=dev, dtype=torch.bfloat16),  # noqa: E731
+                             torch.empty(rows, cols, device=dev, dtype=torch.bfloat16))
+    if planes:
+        Wp, Wfp = _weight_planes(W, Wf, wplanes)
+        xp = pl(M, _LOC)
     # conv1..conv5 + ReLU into the column blocks of xloc
-    src, ld, off = pts, 3, 0
-    for i in range(5):
+    E.gemm(pts, 3, W[0], 3, xloc, _LOC, M, 64, 3, bias=bc[0], relu=True, c_off=_OFF[0],
+           precise=_FWD_PRECISE, cp=xp if planes else None, ldcp=_LOC, cp_off=_OFF[0])
+    for i in range(1, 5):
         K, O = _CONV[i]
-        E.gemm(src, ld, W[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True, a_off=off,
-               c_off=_OFF[i], precise=_FWD_PRECISE)
-        src, ld, off = xloc, _LOC, _OFF[i]
+        if planes:
+            E.gemm_bf2(xp, _LOC, Wp[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
+                       a_off=_OFF[i - 1], c_off=_OFF[i], cp=xp, ldcp=_LOC, cp_off=_OFF[i])
+        else:
+            E.gemm(xloc, _LOC, W[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
+                   a_off=_OFF[i - 1], c_off=_OFF[i], precise=_FWD_PRECISE)
     # conv6 + ReLU + max over the points of each cloud
     gmax = torch.empty(B, 2048, device=dev)
     gidx = torch.empty(B, 2048, device=dev, dtype=torch.int32)
     nb = E.lib.pcadv_conv_max_x3_workspace_bytes(B, N, 2048)
     ws = _ws(nb, dev)
-    check(E.lib.pcadv_conv_max_x3(_p(xloc, _OFF[4]), _LOC, B, N, 512, _p(W[5]), _p(bc[5]),
-                                  2048, 1, _p(gmax), _p(gidx), _p(ws), ws.numel(),
-                                  stream_ptr()), "pcadv_conv_max_x3")
+    if planes:
+        check(E.lib.pcadv_conv_max_bf2(_p(xloc, _OFF[4]), _LOC, _pb(xp[0], _OFF[4]),
+                                       _pb(xp[1], _OFF[4]), _LOC, B, N, 512, _p(W[5]),
+                                       _pb(Wp[5][0]), _pb(Wp[5][1]), _p(bc[5]), 2048, 1,
+                                       _p(gmax), _p(gidx), _p(ws), ws.numel(), stream_ptr()),
+              "pcadv_conv_max_bf2")
+    else:
+        check(E.lib.pcadv_conv_max_x3(_p(xloc, _OFF[4]), _LOC, B, N, 512, _p(W[5]), _p(bc[5]),
+                                      2048, 1, _p(gmax), _p(gidx), _p(ws), ws.numel(),
+                                      stream_ptr()), "pcadv_conv_max_x3")
     # fc1: per-cloud bias from the tiled global feature and class vector
     W1 = Wf[0]
     cb = torch.empty(B, 256, device=dev)
@@ -152,18 +215,29 @@ def seg_forward(pts, cls, params):
     E.gemm(cvec, cvec.shape[1], W1, 3024, cb, 256, B, 256, cvec.shape[1], b_off=3008,
            accumulate=True)
     h1 = torch.empty(M, 256, device=dev)
-    E.gemm(xloc, _LOC, W1, 3024, h1, 256, M, 256, _LOC, bias_rows=cb, rows_per_group=N,
-           relu=True, precise=_FWD_PRECISE)
     h2 = torch.empty(M, 256, device=dev)
-    E.gemm(h1, 256, Wf[1], 256, h2, 256, M, 256, 256, bias=bf[1], relu=True,
-           precise=_FWD_PRECISE)
     h3 = torch.empty(M, 128, device=dev)
-    E.gemm(h2, 256, Wf[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True,
-           precise=_FWD_PRECISE)
     logits = torch.empty(M, ncls, device=dev)
-    E.gemm(h3, 128, Wf[3], 128, logits, ncls, M, ncls, 128, bias=bf[3], precise=_FWD_PRECISE)
+    if planes:
+        h1p, h2p, h3p = pl(M, 256), pl(M, 256), pl(M, 128)
+        E.gemm_bf2(xp, _LOC, Wfp[0], 3024, h1, 256, M, 256, _LOC, bias_rows=cb,
+                   rows_per_group=N, relu=True, cp=h1p, ldcp=256)
+        E.gemm_bf2(h1p, 256, Wfp[1], 256, h2, 256, M, 256, 256, bias=bf[1], relu=True, cp=h2p,
+                   ldcp=256)
+        E.gemm_bf2(h2p, 256, Wfp[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True, cp=h3p,
+                   ldcp=128)
+        E.gemm_bf2(h3p, 128, Wfp[3], 128, logits, ncls, M, ncls, 128, bias=bf[3])
+    else:
+        E.gemm(xloc, _LOC, W1, 3024, h1, 256, M, 256, _LOC, bias_rows=cb, rows_per_group=N,
+               relu=True, precise=_FWD_PRECISE)
+        E.gemm(h1, 256, Wf[1], 256, h2, 256, M, 256, 256, bias=bf[1], relu=True,
+               precise=_FWD_PRECISE)
+        E.gemm(h2, 256, Wf[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True,
+               precise=_FWD_PRECISE)
+        E.gemm(h3, 128, Wf[3], 128, logits, ncls, M, ncls, 128, bias=bf[3], precise=_FWD_PRECISE)
     return dict(pts=pts, cvec=cvec, xloc=xloc, gmax=gmax, gidx=gidx, h1=h1, h2=h2, h3=h3, W=W,
-                Wf=Wf, logits=logits, dims=(B, N, ncls))
+                Wf=Wf, logits=logits, dims=(B, N, ncls), xp=xp if planes else None,
+                W6p=Wp[5] if planes else None)
 
 
 def seg_backward(fw, dlogits, dgmax_out=None, out=None):
@@ -386,6 +460,12 @@ class SegTrainStep:
                                       "exp_avg": self.m[o:o + k].view_as(p),
                                       "exp_avg_sq": self.v[o:o + k].view_as(p)}
         self.params = [p for _, p in named]
+        # bf16 hi / lo planes of all parameters: one split per step feeds every
+        # forward GEMM's weight operand
+        self.wph = torch.empty(n, device=dev, dtype=torch.bfloat16)
+        self.wpl = torch.empty(n, device=dev, dtype=torch.bfloat16)
+        self.wplanes = [(self.wph[o:o + p.numel()], self.wpl[o:o + p.numel()])
+                        for (_, p), o in zip(named, offs)]
         self.optimizer = optimizer
         self.loss = torch.zeros((), device=dev)
         self.graph = None
@@ -395,7 +475,11 @@ class SegTrainStep:
         _check_dev(pts, "pts")
         if seg.shape != (B, N) or seg.dtype != torch.int64 or not seg.is_contiguous():
             raise ValueError("seg: expected contiguous int64 (B, N)")
-        fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params)
+        wpl = None
+        if _PLANES:
+            _engine().split(self.param, self.wph, self.wpl)
+            wpl = self.wplanes
+        fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params, wplanes=wpl)
         M, ncls = B * N, fw["dims"][2]
         d = torch.empty(M, ncls, device=self.device)
         ws = _ws(self.lib.pcadv_row_ce_workspace_bytes(M), self.device)

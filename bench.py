@@ -237,9 +237,10 @@ def bench_seg(args):
     dense_bwd = 2 * (per_pt_fwd - 512 * 2048) - 3 * 64
     gflop = 2.0 * Bs * Ns * (per_pt_fwd + dense_bwd) / 1e9
     loss = float(step.loss.item())
-    # dominant kernel: conv6 + ReLU + max over points (pcadv_conv_max_x3: the
-    # screened GEMM k_gemm_x3<0,0,2,3> + the exact re-evaluation k_max_combine),
-    # timed with HIP events on the current stream over the last batch's x5
+    # dominant kernel: conv6 + ReLU + max over points as the step runs it
+    # (pcadv_conv_max_bf2: the screened GEMM k_gemm_x3<2,2,2,3> on the bf16 planes
+    # conv5's epilogue wrote + the exact re-evaluation k_max_combine), timed with
+    # HIP events on the current stream over the last batch's x5
     from adversarial_learning_on_pointclouds_amd import seg as segmod
     from adversarial_learning_on_pointclouds_amd._lib import check, stream_ptr
     import ctypes
@@ -254,7 +255,18 @@ def bench_seg(args):
     b6 = params[11]
     x5 = ctypes.c_void_p(fw["xloc"].data_ptr() + 4 * segmod._OFF[4])
 
+    xp, w6p = fw["xp"], fw["W6p"]
+    kname = "pcadv_conv_max_bf2: k_gemm_x3<2,2,2,3>" if xp is not None else "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3>"
+
     def cmx():
+        if xp is not None:
+            check(lib.pcadv_conv_max_bf2(x5, segmod._LOC, segmod._pb(xp[0], segmod._OFF[4]),
+                                         segmod._pb(xp[1], segmod._OFF[4]), segmod._LOC, Bs, Ns, 512,
+                                         ctypes.c_void_p(W6.data_ptr()), segmod._pb(w6p[0]),
+                                         segmod._pb(w6p[1]), ctypes.c_void_p(b6.data_ptr()), 2048, 1,
+                                         ctypes.c_void_p(gmax.data_ptr()), ctypes.c_void_p(gidx.data_ptr()),
+                                         ctypes.c_void_p(ws.data_ptr()), wsb, stream_ptr()), "conv_max_bf2")
+            return
         check(lib.pcadv_conv_max_x3(x5, segmod._LOC, Bs, Ns, 512, ctypes.c_void_p(W6.data_ptr()),
                                     ctypes.c_void_p(b6.data_ptr()), 2048, 1,
                                     ctypes.c_void_p(gmax.data_ptr()), ctypes.c_void_p(gidx.data_ptr()),
@@ -281,8 +293,8 @@ def bench_seg(args):
                                "(BASELINE configs[3])", "global_batch": Bs, "points": Ns,
                    "parallelism": "dp1", "hip_graph": True},
         "roofline": {"bound": "mfma",
-                     "kernel": "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3> (conv6 512->2048 screened "
-                               "top-2 per 128-point tile) + k_max_combine (exact f32 re-evaluation)",
+                     "kernel": kname + " (conv6 512->2048 screened top-2 per 128-point tile) "
+                               "+ k_max_combine (exact f32 re-evaluation)",
                      "achieved": round(kflops / kern_s / 1e12, 2), "peak": round(kpeak, 1),
                      "unit": "TFLOP/s", "frac": round(kflops / kern_s / 1e12 / kpeak, 4),
                      "traffic": None, "avg_launch_us": round(kern_s * 1e6, 2),

@@ -204,11 +204,28 @@ int pcadv_linear_bwd(const float* dy, const float* y, int act,
  * then zeroes C where cmask <= 0: the producer of a data gradient applies the
  * relu' of the layer below, so every consumer reads dZ = dY relu'(Y) already
  * masked.  precise = 1 multiplies six products of hi/mid/lo splits instead
- * (f32-level accuracy; the gradients). */
+ * (f32-level accuracy; the gradients).  c_hi / c_lo (nullable, bf16, row
+ * stride ldcp): the epilogue also writes C's hi / lo planes, the operand form
+ * pcadv_gemm_bf2 stages without splitting. */
 int pcadv_gemm(const float* a, int64_t lda, int ta, const float* b, int64_t ldb, int tb,
                float* c, int64_t ldc, int M, int N, int K, const float* bias,
                const float* bias_rows, int rows_per_group, int relu, int accumulate,
-               const float* cmask, int64_t ldm, int precise, hipStream_t stream);
+               const float* cmask, int64_t ldm, int precise, void* c_hi, void* c_lo, int64_t ldcp,
+               hipStream_t stream);
+
+/* The forward GEMM with both operands given as bf16 hi / lo planes (A [M][K],
+ * B [N][K], the 2-way splits of f32 matrices made once by their producers:
+ * hi = bf16(v), lo = bf16(v - hi)); bitwise the result pcadv_gemm computes
+ * from the f32 matrices (precise = 0), without re-splitting every tile.
+ * K % 16, lda % 8, ldb % 8, 16-B aligned planes. */
+int pcadv_gemm_bf2(const void* a_hi, const void* a_lo, int64_t lda, const void* b_hi,
+                   const void* b_lo, int64_t ldb, float* c, int64_t ldc, void* c_hi, void* c_lo,
+                   int64_t ldcp, int M, int N, int K, const float* bias, const float* bias_rows,
+                   int rows_per_group, int relu, int accumulate, const float* cmask, int64_t ldm,
+                   hipStream_t stream);
+/* f32 [rows][cols] (stride ld) -> its bf16 hi / lo planes (stride ldo). */
+int pcadv_split_bf2(const float* x, int64_t ld, int rows, int cols, void* hi, void* lo,
+                    int64_t ldo, hipStream_t stream);
 
 /* Weight gradient dw[o][k] (row stride ldo) (+)= sum over `rows` points of
  * dz[p][o] x[p][k]: six-product (f32-level) GEMM over fixed-order slabs of the
@@ -241,6 +258,13 @@ size_t pcadv_conv_max_x3_workspace_bytes(int C, int Npts, int O);
 int pcadv_conv_max_x3(const float* x, int64_t ldx, int C, int Npts, int K, const float* w,
                       const float* b, int O, int relu, float* gmax, int32_t* gidx,
                       void* workspace, size_t workspace_bytes, hipStream_t stream);
+/* The same with the screened GEMM staging x and w from their bf16 hi / lo
+ * planes (x still given in f32 for the exact re-evaluation). */
+int pcadv_conv_max_bf2(const float* x, int64_t ldx, const void* x_hi, const void* x_lo,
+                       int64_t ldxp, int C, int Npts, int K, const float* w, const void* w_hi,
+                       const void* w_lo, const float* b, int O, int relu, float* gmax,
+                       int32_t* gidx, void* workspace, size_t workspace_bytes,
+                       hipStream_t stream);
 /* Its backward: g' = dgmax [gmax > 0]; dw [O][K] and db [O] overwritten
  * (nullable), dx rows (stride lddx, nullable, K <= 512) accumulated:
  * deterministic.  relu_x = 1 masks the dx additions by [x > 0] (x the output

@@ -57,7 +57,7 @@ def test_gemm_forward_vs_fp64(M, N, K):
     rpg = (M + 1) // 2
     tA, tW, tb, tbr = _t(A), _t(W), _t(b), _t(br)  # alive across the launch
     check(lib.pcadv_gemm(_p(tA), K, 0, _p(tW), K, 0, _p(C), N, M, N, K, _p(tb), _p(tbr),
-                         rpg, 1, 0, None, 0, 0, stream_ptr()), "gemm")
+                         rpg, 1, 0, None, 0, 0, None, None, 0, stream_ptr()), "gemm")
     ref = A.astype(np.float64) @ W.astype(np.float64).T + b + br[np.arange(M) // rpg]
     ref = np.maximum(ref, 0)
     assert (np.abs(C.cpu().numpy() - ref) <= _bound(A, W) + 1e-6).all()
@@ -76,7 +76,7 @@ def test_gemm_data_grad_masked_accumulate():
     out = _t(base)
     tdZ, tY, tW = _t(dZ), _t(Y), _t(W)
     check(lib.pcadv_gemm(_p(tdZ), O, 0, _p(tW), K, 1, _p(out, 64), 200, M, K, O, None, None, 0, 0,
-                         1, _p(tY, 64), 200, 1, stream_ptr()), "gemm")
+                         1, _p(tY, 64), 200, 1, None, None, 0, stream_ptr()), "gemm")
     ref = base.astype(np.float64).copy()
     ref[:, 64:128] = (ref[:, 64:128] + dZ.astype(np.float64) @ W.astype(np.float64)) * (Y[:, 64:128] > 0)
     got = out.cpu().numpy()
@@ -84,6 +84,59 @@ def test_gemm_data_grad_masked_accumulate():
     assert (np.abs(got[:, 64:128] - ref[:, 64:128]) <= _bound(dZ, W.T) / 20 + 1e-5).all()
     assert (got[:, 64:128][Y[:, 64:128] <= 0] == 0).all()
     assert np.array_equal(got[:, :64], base[:, :64]) and np.array_equal(got[:, 128:], base[:, 128:])
+
+
+def _pb(t, off=0):
+    return ctypes.c_void_p(t.data_ptr() + 2 * off)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 64, 64), (1000, 256, 960), (4096, 128, 128)])
+def test_gemm_bf2_is_bitwise_the_f32_staged_gemm(M, N, K):
+    """Operands as bf16 hi / lo planes (split once; pcadv_gemm_bf2) give the
+    three-product GEMM bit for bit, and the epilogue's own output planes are
+    the split of its f32 output."""
+    lib = _lib.load()
+    rng = np.random.default_rng(M + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((N, K)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    tA, tW, tb = _t(A), _t(W), _t(b)
+    ref = torch.empty(M, N, device=DEV)
+    check(lib.pcadv_gemm(_p(tA), K, 0, _p(tW), K, 0, _p(ref), N, M, N, K, _p(tb), None, 0, 1, 0,
+                         None, 0, 0, None, None, 0, stream_ptr()), "gemm")
+    ah, al = torch.empty(M, K, device=DEV, dtype=torch.bfloat16), torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    wh, wl = torch.empty(N, K, device=DEV, dtype=torch.bfloat16), torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    check(lib.pcadv_split_bf2(_p(tA), K, M, K, _pb(ah), _pb(al), K, stream_ptr()), "split")
+    check(lib.pcadv_split_bf2(_p(tW), K, N, K, _pb(wh), _pb(wl), K, stream_ptr()), "split")
+    assert torch.equal(ah.float() + al.float(), (tA.to(torch.bfloat16).float()
+                                                 + (tA - tA.to(torch.bfloat16).float()).to(torch.bfloat16).float()))
+    C = torch.empty(M, N, device=DEV)
+    ch, cl = torch.empty(M, N, device=DEV, dtype=torch.bfloat16), torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    check(lib.pcadv_gemm_bf2(_pb(ah), _pb(al), K, _pb(wh), _pb(wl), K, _p(C), N, _pb(ch), _pb(cl), N,
+                             M, N, K, _p(tb), None, 0, 1, 0, None, 0, stream_ptr()), "gemm_bf2")
+    assert torch.equal(C, ref)
+    assert torch.equal(ch, C.to(torch.bfloat16))
+    assert torch.equal(cl, (C - ch.float()).to(torch.bfloat16))
+
+
+def test_seg_forward_planes_path_is_bitwise_the_f32_path():
+    from adversarial_learning_on_pointclouds_amd import seg as segmod
+    torch.manual_seed(4)
+    m = PointNetSeg(50).to(DEV)
+    params = list(m.parameters())
+    pts = torch.rand(2, 700, 3, device=DEV) * 2 - 1
+    cls = torch.zeros(2, 1, 16, device=DEV)
+    cls[0, 0, 3] = cls[1, 0, 9] = 1
+    saved = segmod._PLANES
+    try:
+        segmod._PLANES = True
+        a = seg_forward(pts, cls, params)
+        segmod._PLANES = False
+        b = seg_forward(pts, cls, params)
+    finally:
+        segmod._PLANES = saved
+    for k in ("xloc", "gmax", "gidx", "h1", "h2", "h3", "logits"):
+        assert torch.equal(a[k], b[k]), k
 
 
 @pytest.mark.parametrize("rows,rpg,O,K", [(300, 100, 96, 40), (32768, 2048, 96, 40),
