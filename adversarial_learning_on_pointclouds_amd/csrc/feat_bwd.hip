@@ -460,40 +460,64 @@ __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __r
 }
 
 // dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :];  db4[o] = sum_c g[c,o].
-// One wave per channel, lanes hold two of the 128 columns.
-__device__ void dw4_wave(int o, const float* __restrict__ dg, const int32_t* __restrict__ gidx,
-                         int C, int N, int O, const float* __restrict__ x3,
-                         float* __restrict__ dw4, float* __restrict__ db4) {
-  const int lane = threadIdx.x & 63;
-  if (o >= O) return;
+// Four channels per 1024-thread block (256 blocks: every CU takes a share of
+// the 33.5 MB of gathered rows); four waves per channel, each summing a quarter
+// of the clouds in cloud order, the quarters then added in order (fixed).
+// Lanes hold two of the 128 columns.  Per group of 64 clouds, lane c fetches
+// (g, gidx) of cloud c once and the row addresses are broadcast with
+// v_readlane (scalar base + lane offset), so the row loads are all in flight
+// together: two memory round trips per wave.
+constexpr int DW4_CPB = 4;  // channels per block
+__device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__ dg,
+                          const int32_t* __restrict__ gidx, int C, int N, int O,
+                          const float* __restrict__ x3, float* __restrict__ dw4,
+                          float* __restrict__ db4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int o = blk * DW4_CPB + (wave >> 2), qq = wave & 3;
+  const int ca = C * qq / 4, cb = C * (qq + 1) / 4;
   float ax = 0.f, ay = 0.f, ab = 0.f;
-  int c = 0;
-  for (; c + 8 <= C; c += 8) {
-    float g[8];
-    float2 v[8];
+  if (o < O) {
+    for (int c0 = ca; c0 < cb; c0 += 64) {
+      const int cl = c0 + lane, cnt = min(64, cb - c0);
+      const bool vl = lane < cnt;
+      const float gl = vl ? dg[(size_t)cl * O + o] : 0.f;
+      const int nl = vl ? gidx[(size_t)cl * O + o] : 0;
+      constexpr int U = 16;
+      for (int u0 = 0; u0 < cnt; u0 += U) {
+        float2 v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      g[u] = dg[(size_t)(c + u) * O + o];
-      const int n = gidx[(size_t)(c + u) * O + o];
-      v[u] = *reinterpret_cast<const float2*>(x3 + ((size_t)(c + u) * N + n) * 128 + 2 * lane);
-    }
+        for (int u = 0; u < U; ++u) {
+          const int cu = min(u0 + u, cnt - 1);  // clamped: loads past cnt are discarded
+          const int n = __builtin_amdgcn_readlane(nl, cu);
+          v[u] = *reinterpret_cast<const float2*>(x3 + ((size_t)(c0 + cu) * N + n) * 128 + 2 * lane);
+        }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      ax = fmaf(g[u], v[u].x, ax);
-      ay = fmaf(g[u], v[u].y, ay);
-      ab += g[u];
+        for (int u = 0; u < U; ++u) {
+          if (u0 + u < cnt) {
+            const float g = __builtin_bit_cast(
+                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gl), u0 + u));
+            ax = fmaf(g, v[u].x, ax);
+            ay = fmaf(g, v[u].y, ay);
+            ab += g;
+          }
+        }
+      }
     }
   }
-  for (; c < C; ++c) {
-    const float g = dg[(size_t)c * O + o];
-    const int n = gidx[(size_t)c * O + o];
-    const float2 v = *reinterpret_cast<const float2*>(x3 + ((size_t)c * N + n) * 128 + 2 * lane);
-    ax = fmaf(g, v.x, ax);
-    ay = fmaf(g, v.y, ay);
-    ab += g;
+  part[wave][lane] = make_float4(ax, ay, ab, 0.f);
+  __syncthreads();
+  if (qq == 0 && o < O) {
+    float4 t = part[wave][lane];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 p = part[wave + k][lane];
+      t.x += p.x;
+      t.y += p.y;
+      t.z += p.z;
+    }
+    *reinterpret_cast<float2*>(dw4 + (size_t)o * 128 + 2 * lane) = make_float2(t.x, t.y);
+    if (lane == 0) db4[o] = t.z;
   }
-  *reinterpret_cast<float2*>(dw4 + (size_t)o * 128 + 2 * lane) = make_float2(ax, ay);
-  if (lane == 0) db4[o] = ab;
 }
 
 // One launch after k_feat_bwd_chunk: blocks [0, nred) reduce the slabs
@@ -504,13 +528,15 @@ __global__ void __launch_bounds__(1024)
 k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
                   float* db2, float* dw3, float* db3, const float* __restrict__ dg,
                   const int32_t* __restrict__ gidx, int C, int N, int O,
-                  const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4) {
-  __shared__ float2 part[16][64];
-  if ((int)blockIdx.x < FIN_NRED)
-    reduce_slabs_block(blockIdx.x, part, slabs, nslabs, dw1, db1, dw2, db2, dw3, db3);
+                  const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4,
+                  int blk0) {
+  __shared__ float4 part[16][64];
+  const int blk = (int)blockIdx.x + blk0;
+  if (blk < FIN_NRED)
+    reduce_slabs_block(blk, reinterpret_cast<float2(*)[64]>(part), slabs, nslabs, dw1, db1, dw2,
+                       db2, dw3, db3);
   else
-    dw4_wave(((int)blockIdx.x - FIN_NRED) * 16 + (threadIdx.x >> 6), dg, gidx, C, N, O, x3, dw4,
-             db4);
+    dw4_block(blk - FIN_NRED, part, dg, gidx, C, N, O, x3, dw4, db4);
 }
 
 size_t feat_bwd_workspace_bytes(int C, int N) {
@@ -542,8 +568,17 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                      pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   PC_REQUIRE(dw4 && db4, "feat_bwd: dw4/db4 required");
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + (O + 15) / 16), dim3(1024), 0, s, slabs,
-                     C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4);
+#ifdef PCADV_STAMPS
+  // diagnostic build: the slab reduction and the dW4 gather as separate launches
+  // so a kernel trace times each part
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED), dim3(1024), 0, s, slabs, C * nchunk, dw1,
+                     db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0);
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3((O + DW4_CPB - 1) / DW4_CPB), dim3(1024), 0, s, slabs, C * nchunk,
+                     dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, FIN_NRED);
+#else
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + (O + DW4_CPB - 1) / DW4_CPB), dim3(1024), 0, s, slabs,
+                     C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0);
+#endif
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
   return PCADV_OK;
 }

@@ -209,7 +209,10 @@ __device__ void weight_job(const GemmArgs& g, int tile, int ntiles_total) {
   const int r0 = (tile / ctiles) * 16, c0 = (tile % ctiles) * 16;
   const int nch = (g.m_w + 15) / 16;
   float s;
-  f32x4v acc = wave_tile<OP_BWD_WEIGHT, MAXC, ACT, DM>(g, r0, c0, 0, nch, lane, step, &s);
+  // the load count follows the chunk count (m_w <= 64 at B = 32: half the loads)
+  const f32x4v acc = nch <= MAXC / 2
+                         ? wave_tile<OP_BWD_WEIGHT, MAXC / 2, ACT, DM>(g, r0, c0, 0, nch, lane, step, &s)
+                         : wave_tile<OP_BWD_WEIGHT, MAXC, ACT, DM>(g, r0, c0, 0, nch, lane, step, &s);
   const int col = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
