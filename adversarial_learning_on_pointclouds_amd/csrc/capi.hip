@@ -60,9 +60,10 @@ int launch_disc_tail(const float*, int, const float*, const float*, const float*
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
 #endif
-int launch_head_bwd(const float*, const float*, const float*, int, const float*, const float*,
-                    float*, float*, float*, float*, const float*, const float*, float*, int, float,
-                    float, const float*, const float*, hipStream_t);
+int launch_head_bwd(const float*, const float*, const float*, float, const float*, int,
+                    const float*, const float*, float*, float*, float*, float*, const float*,
+                    const float*, float*, int, float, float, const float*, const float*,
+                    hipStream_t);
 int launch_gemm(const float*, long long, int, const float*, long long, int, float*, long long,
                 int, int, int, const float*, const float*, int, int, int, const float*, long long,
                 int, void*, void*, long long, hipStream_t);
@@ -215,7 +216,11 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
                           a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
                           w.dout, s));
   // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
-  //      input grads of all rows (rows [2B,3B) feed the generator, D frozen) ---
+  //      input grads of all rows (rows [2B,3B) feed the generator, D frozen).
+  //      Every data gradient is stored as the layer below's dz (its activation
+  //      derivative, and fc2's dropout, applied by the producer), so each
+  //      backward launch reads dz as is: dd3 (k_disc_tail) -> dd2 -> dd1 ->
+  //      (k_head_bwd) dh2 -> dh1 -> dgmax (raw: the max-pool has no activation)
   const int MW = 2 * B;
   {
     LinBwdExtra ex{};  // + sum of the conv4/conv5/fc partial-gradient slabs
@@ -223,18 +228,24 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
     ex.red_dst = gD + PCADV_D_CONV4_W;
     ex.red_n = (int)disc_tail_slab_floats();
     ex.red_cnt = disc_rowblocks(B);
-    PC_TRY(launch_linear_bwd(w.dd3, w.d3, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d2,
+    ex.dx_act = PCADV_ACT_LRELU;  // x = conv2 output
+    PC_TRY(launch_linear_bwd(w.dd3, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.d2,
                              D + PCADV_D_CONV3_W, w.dd2, gD + PCADV_D_CONV3_W,
                              gD + PCADV_D_CONV3_B, R, MW, 256, 256, s, &ex));
   }
-  PC_TRY(launch_linear_bwd(w.dd2, w.d2, PCADV_ACT_LRELU, nullptr, nullptr, 0, 0.f, w.d1,
-                           D + PCADV_D_CONV2_W, w.dd1, gD + PCADV_D_CONV2_W, gD + PCADV_D_CONV2_B,
-                           R, MW, 256, 512, s));
+  {
+    LinBwdExtra ex{};
+    ex.dx_act = PCADV_ACT_LRELU;  // x = conv1 output
+    PC_TRY(launch_linear_bwd(w.dd2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.d1,
+                             D + PCADV_D_CONV2_W, w.dd1, gD + PCADV_D_CONV2_W,
+                             gD + PCADV_D_CONV2_B, R, MW, 256, 512, s, &ex));
+  }
   // ---- D conv1 input grad of the adversarial rows -> log_softmax backward ->
-  //      fc3 input grad; D conv1 weight grad; the four losses -----------------
-  PC_TRY(launch_head_bwd(w.dd1, w.d1, w.din, B, D + PCADV_D_CONV1_W, G + PCADV_G_FC3_W, w.dlogits,
-                         w.dh2, gD + PCADV_D_CONV1_W, gD + PCADV_D_CONV1_B, w.lpart, w.lpart3,
-                         a->losses, a->semi, a->lambda_semi, a->semi_th, logits, w.dout, s));
+  //      fc3 input grad (stored as fc2's dz); D conv1 weight grad; the losses -
+  PC_TRY(launch_head_bwd(w.dd1, w.h2, bmask, a->drop_p, w.din, B, D + PCADV_D_CONV1_W,
+                         G + PCADV_G_FC3_W, w.dlogits, w.dh2, gD + PCADV_D_CONV1_W,
+                         gD + PCADV_D_CONV1_B, w.lpart, w.lpart3, a->losses, a->semi,
+                         a->lambda_semi, a->semi_th, logits, w.dout, s));
   // ---- generator head backward (:520); fc3's weight grad rides along -------
   {
     LinBwdExtra ex{};
@@ -247,11 +258,12 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
     ex.m_w = C;
     ex.N = 40;
     ex.K = 256;
-    PC_TRY(launch_linear_bwd(w.dh2, w.h2, PCADV_ACT_RELU, bmask, nullptr, 0, a->drop_p,
-                             w.h1, G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W,
-                             gG + PCADV_G_FC2_B, C, C, 256, 512, s, &ex));
+    ex.dx_act = PCADV_ACT_RELU;  // x = fc1 output
+    PC_TRY(launch_linear_bwd(w.dh2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h1,
+                             G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,
+                             C, 256, 512, s, &ex));
   }
-  PC_TRY(launch_linear_bwd(w.dh1, w.h1, PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, w.gmax,
+  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
   // ---- PointNetfeat backward (sparse max-pool) -----------------------------
@@ -312,13 +324,24 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_TRY(launch_row_ce(logits, 40, a->labels, B, 40, a->lambda_cls, a->losses, w.dlogits,
                        w.dslabs, (size_t)disc_rowblocks(B) * disc_tail_slab_floats() * sizeof(float),
                        s));
-  PC_TRY(launch_linear_bwd(w.dlogits, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h2,
-                           G + PCADV_G_FC3_W, w.dh2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, C,
-                           40, 256, s));
-  PC_TRY(launch_linear_bwd(w.dh2, w.h2, PCADV_ACT_RELU, w.mask, nullptr, 0, a->drop_p, w.h1,
-                           G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C, C,
-                           256, 512, s));
-  PC_TRY(launch_linear_bwd(w.dh1, w.h1, PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, w.gmax,
+  // data gradients stored as the layer below's dz (see adv_step)
+  {
+    LinBwdExtra ex{};
+    ex.dx_act = PCADV_ACT_RELU;  // x = fc2 output, with its dropout
+    ex.dx_mask = w.mask;
+    ex.dx_keep = 1.0f / (1.0f - a->drop_p);
+    PC_TRY(launch_linear_bwd(w.dlogits, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h2,
+                             G + PCADV_G_FC3_W, w.dh2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C,
+                             C, 40, 256, s, &ex));
+  }
+  {
+    LinBwdExtra ex{};
+    ex.dx_act = PCADV_ACT_RELU;  // x = fc1 output
+    PC_TRY(launch_linear_bwd(w.dh2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h1,
+                             G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,
+                             C, 256, 512, s, &ex));
+  }
+  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
   PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,

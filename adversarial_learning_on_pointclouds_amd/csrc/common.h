@@ -140,6 +140,11 @@ struct LinBwdExtra {
   const float* red_src;
   float* red_dst;
   int red_n, red_cnt;
+  // data-gradient output mask: dx *= act'(x) (* dx_mask * dx_keep), dx then
+  // being the layer below's dz (its backward runs with act NONE, no dropout)
+  int dx_act;
+  const float* dx_mask;
+  float dx_keep;
 };
 int launch_linear_bwd(const float* dy, const float* y, int act, const float* mask,
                       const int32_t* step, uint64_t seed, float p, const float* x, const float* w,

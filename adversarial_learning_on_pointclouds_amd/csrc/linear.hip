@@ -52,6 +52,11 @@ struct GemmArgs {
   int M, N, K, m_w;
   int diag;  // forward: add the k x k identity to the flattened output (0: off)
   float* mask_out;  // forward, device-drawn dropout: store the {0,1} mask here
+  // backward-data output mask: dx *= act'(x) (* ox_mask * ox_keep), i.e. dx is
+  // stored as the layer below's dz, so its backward reads one operand as is
+  int ox_act;
+  const float* ox_mask;
+  float ox_keep;
 };
 
 // dropout scale s at (m, n) of an [M][N] output
@@ -102,10 +107,21 @@ __device__ __forceinline__ void load_ab(const GemmArgs& g, int r0, int c0, int r
   } else if (OP == OP_BWD_DATA) {
     // dx[m][k] = sum_n dz[m][n] w[n][k]
     const int m = r0 + r, k = c0 + r;
+    if (ACT == ACT_NONE && DM == DM_NONE && (g.N & 3) == 0) {
+      // dz stored as is (the producer applied the masks): one 16-B load
+      const bool va = cv && m < g.M && kk < g.N;
+      const f32x4v av = *reinterpret_cast<const f32x4v*>(
+          g.dy + (size_t)(va ? m : 0) * g.N + (va ? kk : 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = va ? av[j] : 0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        a[j] = dz_at<ACT, DM>(g, m, kk + j, cv && m < g.M && kk + j < g.N, step);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = kk + j;
-      a[j] = dz_at<ACT, DM>(g, m, n, cv && m < g.M && n < g.N, step);
       const bool vb = cv && n < g.N && k < g.K;
       const float wv = g.w[(size_t)(vb ? n : 0) * g.K + (vb ? k : 0)];
       b[j] = vb ? wv : 0.f;
@@ -192,7 +208,10 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
         if (g.diag && n % (g.diag + 1) == 0) o += 1.f;
         g.y[i] = o;
       } else {
-        g.dx[(size_t)m * g.K + n] = v;
+        const size_t i = (size_t)m * g.K + n;
+        if (g.ox_act != ACT_NONE) v *= act_bwd(g.x[i], g.ox_act);
+        if (g.ox_mask) v *= g.ox_mask[i] * g.ox_keep;
+        g.dx[i] = v;
       }
     }
   }
@@ -249,9 +268,9 @@ struct BwdExtra {
 // then the extra weight tiles; then the slab reduction
 template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
-k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex) {
+k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0) {
   __shared__ float red[16 * 256];
-  const int b = blockIdx.x, nbw = (nwt + S - 1) / S, nbw2 = (ex.nwt2 + S - 1) / S;
+  const int b = blockIdx.x + blk0, nbw = (nwt + S - 1) / S, nbw2 = (ex.nwt2 + S - 1) / S;
   if (b < nbx) {
     split_job<OP_BWD_DATA, ACT, DM>(g, b, g.M, g.K, g.N, S, L, red);
   } else if (b < nbx + nbw) {
@@ -334,6 +353,15 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   g.drop = DropSpec{mask, step, seed, p};
   g.dx = dx; g.dw = dw; g.db = db;
   g.M = M; g.N = N; g.K = K; g.m_w = m_w;
+  if (extra) {
+    PC_REQUIRE(extra->dx_act == ACT_NONE || extra->dx_act == ACT_RELU || extra->dx_act == ACT_LRELU,
+               "linear_bwd: bad dx_act %d", extra->dx_act);
+    PC_REQUIRE(!(extra->dx_act != ACT_NONE || extra->dx_mask) || (dx && x),
+               "linear_bwd: the dx output mask needs dx and the layer input x");
+    g.ox_act = extra->dx_act;
+    g.ox_mask = extra->dx_mask;
+    g.ox_keep = extra->dx_keep;
+  }
   int S, L;
   split_cfg(N, &S, &L);
   const int nbx = dx ? ((M + 15) / 16) * ((K + 15) / 16) : 0;
@@ -366,8 +394,17 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   }
   if (nbx + nbw + nbe == 0) return PCADV_OK;
   PC_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU, "linear_bwd: bad act %d", act);
+#ifdef PCADV_STAMPS
+  // diagnostic build: data-gradient tiles and the rest as separate launches
+  if (nbx > 0)
+    launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx), dim3(64 * S), s, g, S, L, nbx, nwt, ex, 0);
+  if (nbw + nbe > 0)
+    launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbw + nbe), dim3(64 * S), s, g, S, L, nbx, nwt,
+                         ex, nbx);
+#else
   launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx + nbw + nbe), dim3(64 * S), s, g, S, L,
-                       nbx, nwt, ex);
+                       nbx, nwt, ex, 0);
+#endif
   PC_HIP_CHECK_LAUNCH("k_linear_bwd");
   return PCADV_OK;
 }

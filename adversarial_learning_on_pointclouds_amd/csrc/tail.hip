@@ -59,11 +59,25 @@ enum BMode { B_OK = 0, B_KO = 1 };  // B[k][j] = W[j * ldw + k]  |  W[k * ldw + 
 // of the discriminator input).
 // KC0: reduction chunk per work item (default min(K, 128)); smaller chunks
 // spread a narrow layer over more waves at the cost of a partial-sum pass.
-template <int K, int NC, int MODE, int ACT, int KC0 = 128>
+// Output mask (backward layers): with `om`, each output is multiplied by
+// act'(om[row][j]) for OM_ACT, then by om_drop[row][j] * om_keep when given, so
+// it is stored as the next backward layer's dz.
+struct OutMask {
+  const float* om;      // [rows][oms] activations of the layer below (LDS or global)
+  int oms;
+  const float* drop;    // [rows][oms] {0,1} dropout mask or nullptr
+  float keep;
+};
+template <int K, int NC, int MODE, int ACT, int KC0 = 128, int OM_ACT = ACT_NONE>
 __device__ __forceinline__ void rows_layer(const float* A, int as, const float* W, int ldw,
                                            const float* __restrict__ bias, float* out, int os,
                                            float* scratch, int nrows = TR, int dup_row = TR,
-                                           long dup_off = 0) {
+                                           long dup_off = 0, OutMask msk = OutMask{}) {
+  auto masked = [&](float o, int row, int j) {
+    if (OM_ACT != ACT_NONE) o *= act_bwd(msk.om[row * msk.oms + j], OM_ACT);
+    if (msk.drop) o *= msk.drop[row * msk.oms + j] * msk.keep;
+    return o;
+  };
   constexpr int KC = K < KC0 ? K : KC0;
   constexpr int C = (K + KC - 1) / KC, T = (NC + 15) / 16, ITEMS = T * C;
   constexpr int NS = (KC + 3) / 4;
@@ -93,7 +107,7 @@ __device__ __forceinline__ void rows_layer(const float* A, int as, const float* 
         for (int v = 0; v < 4; ++v) {
           const int row = 4 * q + v;
           if (row < nrows) {
-            const float o = act_fwd(acc[v] + bj, ACT);
+            const float o = masked(act_fwd(acc[v] + bj, ACT), row, j);
             out[row * os + j] = o;
             if (row >= dup_row) out[row * os + j + dup_off] = o;
           }
@@ -112,7 +126,7 @@ __device__ __forceinline__ void rows_layer(const float* A, int as, const float* 
 #pragma unroll
       for (int c = 0; c < C; ++c) v += scratch[(t * C + c) * 256 + row * 16 + (col & 15)];
       if (bias) v += bias[col];
-      const float o = act_fwd(v, ACT);
+      const float o = masked(act_fwd(v, ACT), row, col);
       out[row * os + col] = o;
       if (row >= dup_row) out[row * os + col + dup_off] = o;
     }
@@ -379,8 +393,10 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
     L.z4[row * 68 + col] *= act_bwd(L.a4[row * 68 + col], ACT_LRELU);
   }
   __syncthreads();
-  rows_layer<64, 256, B_KO, ACT_NONE>(L.z4, 68, L.w4, 260, nullptr, dd3 + (size_t)r0 * 256, 256,
-                                      L.scratch, nrows);
+  // stored as D conv3's dz: times lrelu'(conv3 output), which is this block's x3 rows
+  rows_layer<64, 256, B_KO, ACT_NONE, 128, ACT_LRELU>(L.z4, 68, L.w4, 260, nullptr,
+                                                      dd3 + (size_t)r0 * 256, 256, L.scratch,
+                                                      nrows, TR, 0, OutMask{L.x3, 260, nullptr, 1.f});
   TSTAMP(1, 8);
   // partial weight gradients over this block's D-loss rows (m < 2B; the
   // adversarial rows train only the generator)
@@ -451,7 +467,8 @@ struct HeadBwdLds {
 };
 
 __global__ void __launch_bounds__(TT)
-k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
+k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
+           const float* __restrict__ drop_mask, float drop_keep,
            const float* __restrict__ din, int B, const float* __restrict__ dw1,
            const float* __restrict__ w3, float* __restrict__ dlogits, float* __restrict__ dh2,
            float* __restrict__ gw1, float* __restrict__ gb1, const float* __restrict__ lpart,
@@ -463,7 +480,8 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
   const int C = 2 * B, nrb = (C + TR - 1) / TR;
   if ((int)blockIdx.x >= nrb) {
     // discriminator conv1 weight gradient over the D-loss rows [0, 2B):
-    // dW[o][k] = sum_m dz[m][o] din[m][k], dz = dd1 * lrelu'(d1); wave = 16x16 tile
+    // dW[o][k] = sum_m dz[m][o] din[m][k] (dz1 stored masked by D conv2's
+    // backward); wave = 16x16 tile
     const int t = ((int)blockIdx.x - nrb) * TW + wave;
     constexpr int TK = 3;  // 40 columns in 3 tiles
     if (t >= 32 * TK) return;
@@ -477,7 +495,7 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
         const int m = m0 + 4 * u + q;
         const bool vm = m < C;
         const size_t ia = (size_t)(vm ? m : 0) * 512 + o0 + r;
-        const float z = dd1[ia] * act_bwd(d1[ia], ACT_LRELU);
+        const float z = dz1[ia];
         a[u] = vm ? z : 0.f;
         const bool vb = vm && k0 + r < 40;
         const float xv = din[(size_t)(vm ? m : 0) * 40 + (vb ? k0 + r : 0)];
@@ -509,14 +527,13 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
   }
   // dz of the adversarial D rows m + B (m in [B, 2B)); zero for GT rows.  The
   // row loads are issued together with the conv1 weight staging.
-  f32x4 zd[2], zy[2];
+  f32x4 zd[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
     const bool v = m >= B && m < C;
     const size_t i = v ? (size_t)(m + B) * 512 + 4 * c4 : 0;
-    zd[u] = *reinterpret_cast<const f32x4*>(dd1 + i);
-    zy[u] = *reinterpret_cast<const f32x4*>(d1 + i);
+    zd[u] = *reinterpret_cast<const f32x4*>(dz1 + i);
   }
   {
     const Fill f[1] = {{L.w1, 48, dw1, 512, 40, 512}};
@@ -528,7 +545,7 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
     const bool v = m >= B && m < C;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      L.z1[row * 516 + 4 * c4 + i] = v ? zd[u][i] * act_bwd(zy[u][i], ACT_LRELU) : 0.f;
+      L.z1[row * 516 + 4 * c4 + i] = v ? zd[u][i] : 0.f;
   }
   __syncthreads();
   TSTAMP(2, 1);
@@ -562,8 +579,11 @@ k_head_bwd(const float* __restrict__ dd1, const float* __restrict__ d1,
   }
   __syncthreads();
   TSTAMP(2, 3);
-  rows_layer<40, 256, B_KO, ACT_NONE>(L.dl, 44, w3, 256, nullptr, dh2 + (size_t)r0 * 256, 256,
-                                      nullptr, nrows);
+  // stored as fc2's dz: times relu'(h2) and the dropout mask x 1/(1-p)
+  rows_layer<40, 256, B_KO, ACT_NONE, 128, ACT_RELU>(
+      L.dl, 44, w3, 256, nullptr, dh2 + (size_t)r0 * 256, 256, nullptr, nrows, TR, 0,
+      OutMask{h2 + (size_t)r0 * 256, 256, drop_mask ? drop_mask + (size_t)r0 * 256 : nullptr,
+              drop_keep});
   TSTAMP(2, 4);
   if (semi.on && blockIdx.x == 0 && wave == 0) {
     // l_semi and the kept ratio (losses[4], losses[5]), rows in order
@@ -650,7 +670,8 @@ int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, c
   return PCADV_OK;
 }
 
-int launch_head_bwd(const float* dd1, const float* d1, const float* din, int B, const float* dw1,
+int launch_head_bwd(const float* dz1, const float* h2, const float* drop_mask, float drop_p,
+                    const float* din, int B, const float* dw1,
                     const float* w3, float* dlogits, float* dh2, float* gw1, float* gb1,
                     const float* lpart, const float* lpart3, float* losses, int semi,
                     float lambda_semi, float semi_th, const float* logits, const float* dout,
@@ -663,8 +684,9 @@ int launch_head_bwd(const float* dd1, const float* d1, const float* din, int B, 
   const int nrb = head_rowblocks(B), nwb = (32 * 3 + TW - 1) / TW;
   const SemiArgs sa{semi, lambda_semi, semi_th, logits, dout};
   PC_REQUIRE(!semi || (logits && dout), "head_bwd: the semi term needs the logits and D outputs");
-  hipLaunchKernelGGL(k_head_bwd, dim3(nrb + nwb), dim3(TT), sizeof(HeadBwdLds), s, dd1, d1, din, B,
-                     dw1, w3, dlogits, dh2, gw1, gb1, lpart, nrb, lpart3, disc_rowblocks(B),
+  const float keep = 1.0f / (1.0f - drop_p);  // as the linear kernels' dropout scale
+  hipLaunchKernelGGL(k_head_bwd, dim3(nrb + nwb), dim3(TT), sizeof(HeadBwdLds), s, dz1, h2,
+                     drop_mask, keep, din, B, dw1, w3, dlogits, dh2, gw1, gb1, lpart, nrb, lpart3, disc_rowblocks(B),
                      losses, sa);
   PC_HIP_CHECK_LAUNCH("k_head_bwd");
   return PCADV_OK;
