@@ -535,6 +535,15 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
     const size_t i = v ? (size_t)(m + B) * 512 + 4 * c4 : 0;
     zd[u] = *reinterpret_cast<const f32x4*>(dz1 + i);
   }
+  // this block's h2 and dropout-mask rows (the output mask of the last layer),
+  // fetched now and parked in LDS once z1 is consumed: one float4 each
+  f32x4 hv, mv = {1.f, 1.f, 1.f, 1.f};
+  {
+    const int row = tid >> 6, c4 = tid & 63, m = r0 + row;
+    const size_t i = (size_t)(m < C ? m : 0) * 256 + 4 * c4;
+    hv = *reinterpret_cast<const f32x4*>(h2 + i);
+    if (drop_mask) mv = *reinterpret_cast<const f32x4*>(drop_mask + i);
+  }
   {
     const Fill f[1] = {{L.w1, 48, dw1, 512, 40, 512}};
     lds_fill(f);  // 5120 float4: 5 per thread
@@ -551,6 +560,10 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
   TSTAMP(2, 1);
   rows_layer<512, 40, B_KO, ACT_NONE>(L.z1, 516, L.w1, 48, nullptr, L.ddin, 44, L.scratch);
   TSTAMP(2, 2);
+  float* h2s = L.z1;             // [16][256], z1 is free now
+  float* ms = L.z1 + TR * 256;   // [16][256]
+  *reinterpret_cast<f32x4*>(h2s + 4 * tid) = hv;
+  *reinterpret_cast<f32x4*>(ms + 4 * tid) = mv;
   // log_softmax backward (noGT rows) / the CE gradient of the GT rows
   {
     const int row = wave, m = r0 + row;
@@ -582,8 +595,7 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
   // stored as fc2's dz: times relu'(h2) and the dropout mask x 1/(1-p)
   rows_layer<40, 256, B_KO, ACT_NONE, 128, ACT_RELU>(
       L.dl, 44, w3, 256, nullptr, dh2 + (size_t)r0 * 256, 256, nullptr, nrows, TR, 0,
-      OutMask{h2 + (size_t)r0 * 256, 256, drop_mask ? drop_mask + (size_t)r0 * 256 : nullptr,
-              drop_keep});
+      OutMask{h2s, 256, drop_mask ? ms : nullptr, drop_keep});
   TSTAMP(2, 4);
   if (semi.on && blockIdx.x == 0 && wave == 0) {
     // l_semi and the kept ratio (losses[4], losses[5]), rows in order
