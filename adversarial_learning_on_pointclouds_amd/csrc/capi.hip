@@ -26,7 +26,8 @@ size_t feat_bwd_workspace_bytes(int C, int N);
 int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
                     const float*, const float*, const float*, const float*, const float*,
                     const float*, const float*, float*, float*, float*, float*, float*, float*,
-                    float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr);
+                    float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr,
+                    const FinAdam* adam = nullptr);
 size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
@@ -152,6 +153,26 @@ static StepWs carve(int B, int N, char* base) {
     if (rc_ != PCADV_OK) return rc_; \
   } while (0)
 
+// Adam fused into the feature backward's finishing launch (apply_adam): G's
+// conv1..conv4 as their gradients are formed there, the rest of G and all of D
+// in extra blocks of the same launch (their gradients are final by then).
+static FinAdam fused_adam(const pcadv_adv_args* a, bool with_d) {
+  FinAdam f{};
+  f.on = 1;
+  f.gp = a->g_param; f.gm = a->g_m; f.gv = a->g_v; f.gg = a->g_grad;
+  f.g_rest0 = PCADV_G_FC1_W;
+  f.g_n = PCADV_G_NUMEL;
+  if (with_d) {
+    f.dp = a->d_param; f.dm = a->d_m; f.dv = a->d_v; f.dg = a->d_grad;
+    f.d_n = PCADV_D_NUMEL;
+  }
+  f.lr_g = a->lr_g; f.lr_d = a->lr_d;
+  f.b1 = a->beta1; f.b2 = a->beta2; f.eps = a->eps;
+  f.step_count = a->step_count;
+  f.step_offset = 0;  // the step already advanced the counter (k_point_mlp)
+  return f;
+}
+
 static int adv_adam(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(a && a->g_param && a->d_param && a->step_count, "adv_step_adam: bad arguments");
   return launch_adam2(a->g_param, a->g_grad, a->g_m, a->g_v, PCADV_G_NUMEL, a->lr_g, a->d_param,
@@ -266,17 +287,18 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
-  // ---- PointNetfeat backward (sparse max-pool) -----------------------------
-  PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
+  // ---- PointNetfeat backward (sparse max-pool), then optimizer.step();
+  //      optimizer_D.step() (:558-559) fused into its finishing launch --------
+  PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v && a->d_param && a->d_m && a->d_v),
+             "adv_step: Adam buffers");
+  const FinAdam fa = fused_adam(a, true);
+  return launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
                          G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                          G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s));
-  // ---- optimizer.step(); optimizer_D.step() (:558-559) ----------------------
-  if (a->apply_adam) return adv_adam(a, s);
-  return PCADV_OK;
+                         s, nullptr, a->apply_adam ? &fa : nullptr);
 }
 
 // run_training_pointnet_cls's iteration (utils/trainer.py:222-268,
@@ -344,18 +366,16 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
-  PC_TRY(launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
+  // feature backward; Adam (generator only) fused into its finishing launch
+  PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v), "cls_step: Adam moments");
+  const FinAdam fa = fused_adam(a, false);
+  return launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
                          G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                          G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s));
-  if (!a->apply_adam) return PCADV_OK;
-  PC_REQUIRE(a->g_m && a->g_v, "cls_step: Adam moments");
-  return launch_adam2(a->g_param, a->g_grad, a->g_m, a->g_v, PCADV_G_NUMEL, a->lr_g, nullptr,
-                      nullptr, nullptr, nullptr, 0, 0.f, a->step_count, 0, a->beta1, a->beta2,
-                      a->eps, s);
+                         s, nullptr, a->apply_adam ? &fa : nullptr);
 }
 
 }  // namespace pcadv

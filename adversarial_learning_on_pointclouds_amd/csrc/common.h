@@ -127,6 +127,46 @@ __device__ __forceinline__ float conv1_point(float wa, float wb, float wc, float
 // Work added to a linear-backward launch (linear.hip): an extra weight-gradient
 // job dw[N][K] (+ db) = sum over the first m_w rows of dy^T x (no activation,
 // no dropout), and a fixed-order sum of red_cnt slabs of red_n floats.
+// torch.optim.Adam, single-tensor path (train_classification.py:110-122):
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)
+//   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, value=-lr/(1-b1^t))
+struct AdamHp {
+  float w1, b2, w2, bc2s, eps, step;
+};
+__device__ __forceinline__ AdamHp adam_hp(const int32_t* step_count, int step_offset, float b1,
+                                          float b2, float eps, float lr) {
+  const double t = (double)(*step_count + step_offset);
+  const float bc1 = (float)(1.0 - pow((double)b1, t));
+  AdamHp h;
+  h.bc2s = (float)sqrt(1.0 - pow((double)b2, t));
+  h.step = (float)((double)lr / (double)bc1);
+  h.w1 = 1.f - b1;
+  h.w2 = 1.f - b2;
+  h.b2 = b2;
+  h.eps = eps;
+  return h;
+}
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamHp& h) {
+  m = m + h.w1 * (g - m);
+  v = v * h.b2 + h.w2 * (g * g);
+  const float denom = sqrtf(v) / h.bc2s + h.eps;
+  p = p - h.step * (m / denom);
+}
+
+// Adam riding along the launch that finishes the gradients (k_feat_bwd_finish):
+// the generator's conv1..conv4 parameters as their gradients are formed, plus
+// the parameters whose gradients are already final (G from fc1 on, all of D).
+struct FinAdam {
+  int on;
+  float* gp; float* gm; float* gv; const float* gg;  // generator flat buffers
+  int64_t g_rest0, g_n;                             // G [g_rest0, g_n) in the extra blocks
+  float* dp; float* dm; float* dv; const float* dg;  // discriminator (d_n = 0: none)
+  int64_t d_n;
+  float lr_g, lr_d, b1, b2, eps;
+  const int32_t* step_count;
+  int step_offset;
+};
+
 struct LinBwdExtra {
   const float* dy;
   const float* y;

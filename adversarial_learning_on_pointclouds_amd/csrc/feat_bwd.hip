@@ -420,7 +420,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 // order through LDS.
 __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __restrict__ slabs,
                                    int nslabs, float* dw1, float* db1, float* dw2, float* db2,
-                                   float* dw3, float* db3) {
+                                   float* dw3, float* db3, const FinAdam& fa) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = blk * 128 + 2 * lane;  // SLAB is even: j, j+1 both valid or both not
   const int s0 = wave * nslabs / 16, s1 = (wave + 1) * nslabs / 16;
@@ -456,6 +456,17 @@ __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __r
       else if (jj < SL_DB3) dw3[jj - SL_DW3] = x;
       else db3[jj - SL_DB3] = x;
     }
+    if (fa.on) {  // the slab order is the generator's flat order (PCADV_G_CONV1_W = 0 ..)
+      const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g);
+      float2 p = *reinterpret_cast<const float2*>(fa.gp + j);
+      float2 m = *reinterpret_cast<const float2*>(fa.gm + j);
+      float2 w = *reinterpret_cast<const float2*>(fa.gv + j);
+      adam_elem(p.x, v.x, m.x, w.x, h);
+      adam_elem(p.y, v.y, m.y, w.y, h);
+      *reinterpret_cast<float2*>(fa.gp + j) = p;
+      *reinterpret_cast<float2*>(fa.gm + j) = m;
+      *reinterpret_cast<float2*>(fa.gv + j) = w;
+    }
   }
 }
 
@@ -471,7 +482,7 @@ constexpr int DW4_CPB = 4;  // channels per block
 __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__ dg,
                           const int32_t* __restrict__ gidx, int C, int N, int O,
                           const float* __restrict__ x3, float* __restrict__ dw4,
-                          float* __restrict__ db4) {
+                          float* __restrict__ db4, const FinAdam& fa) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int o = blk * DW4_CPB + (wave >> 2), qq = wave & 3;
   const int ca = C * qq / 4, cb = C * (qq + 1) / 4;
@@ -517,7 +528,62 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
     }
     *reinterpret_cast<float2*>(dw4 + (size_t)o * 128 + 2 * lane) = make_float2(t.x, t.y);
     if (lane == 0) db4[o] = t.z;
+    if (fa.on) {
+      const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g);
+      const size_t j = PCADV_G_CONV4_W + (size_t)o * 128 + 2 * lane;
+      float2 p = *reinterpret_cast<const float2*>(fa.gp + j);
+      float2 m = *reinterpret_cast<const float2*>(fa.gm + j);
+      float2 w = *reinterpret_cast<const float2*>(fa.gv + j);
+      adam_elem(p.x, t.x, m.x, w.x, h);
+      adam_elem(p.y, t.y, m.y, w.y, h);
+      *reinterpret_cast<float2*>(fa.gp + j) = p;
+      *reinterpret_cast<float2*>(fa.gm + j) = m;
+      *reinterpret_cast<float2*>(fa.gv + j) = w;
+      if (lane == 0) {
+        const size_t jb = PCADV_G_CONV4_B + o;
+        adam_elem(fa.gp[jb], t.z, fa.gm[jb], fa.gv[jb], h);
+      }
+    }
   }
+}
+
+// Adam over the parameters whose gradients are final before this launch: the
+// generator from fc1 on (segment 0) and the discriminator (segment 1); one
+// float4 per thread and pass, blocks [0, nb0) on segment 0.
+constexpr int FIN_ADAM_V4 = 2;  // float4 per thread
+__device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
+  const bool first = blk < nb0;
+  float* p = first ? fa.gp + fa.g_rest0 : fa.dp;
+  float* m = first ? fa.gm + fa.g_rest0 : fa.dm;
+  float* v = first ? fa.gv + fa.g_rest0 : fa.dv;
+  const float* g = first ? fa.gg + fa.g_rest0 : fa.dg;
+  const int64_t n = first ? fa.g_n - fa.g_rest0 : fa.d_n;
+  const int b = first ? blk : blk - nb0, nb = first ? nb0 : nb1;
+  const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps,
+                           first ? fa.lr_g : fa.lr_d);
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)b * 1024 + threadIdx.x; i < n4; i += (int64_t)nb * 1024) {
+    const f32x4 p4 = reinterpret_cast<f32x4*>(p)[i];
+    const f32x4 g4 = reinterpret_cast<const f32x4*>(g)[i];
+    const f32x4 m4 = reinterpret_cast<f32x4*>(m)[i];
+    const f32x4 v4 = reinterpret_cast<f32x4*>(v)[i];
+    float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w};
+    float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], h);
+    reinterpret_cast<f32x4*>(p)[i] = f32x4{pp[0], pp[1], pp[2], pp[3]};
+    reinterpret_cast<f32x4*>(m)[i] = f32x4{mm[0], mm[1], mm[2], mm[3]};
+    reinterpret_cast<f32x4*>(v)[i] = f32x4{vv[0], vv[1], vv[2], vv[3]};
+  }
+  if (b == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    adam_elem(p[i], g[i], m[i], v[i], h);
+  }
+}
+static int fin_adam_blocks(int64_t n) {
+  int64_t b = (n / 4 + 1024 * FIN_ADAM_V4 - 1) / (1024 * FIN_ADAM_V4);
+  return (int)(b < 1 ? 1 : b);
 }
 
 // One launch after k_feat_bwd_chunk: blocks [0, nred) reduce the slabs
@@ -529,14 +595,16 @@ k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float
                   float* db2, float* dw3, float* db3, const float* __restrict__ dg,
                   const int32_t* __restrict__ gidx, int C, int N, int O,
                   const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4,
-                  int blk0) {
+                  int blk0, FinAdam fa, int nb_adam0, int nb_adam1) {
   __shared__ float4 part[16][64];
-  const int blk = (int)blockIdx.x + blk0;
+  const int blk = (int)blockIdx.x + blk0, ndw4 = (O + DW4_CPB - 1) / DW4_CPB;
   if (blk < FIN_NRED)
     reduce_slabs_block(blk, reinterpret_cast<float2(*)[64]>(part), slabs, nslabs, dw1, db1, dw2,
-                       db2, dw3, db3);
+                       db2, dw3, db3, fa);
+  else if (blk < FIN_NRED + ndw4)
+    dw4_block(blk - FIN_NRED, part, dg, gidx, C, N, O, x3, dw4, db4, fa);
   else
-    dw4_block(blk - FIN_NRED, part, dg, gidx, C, N, O, x3, dw4, db4);
+    adam_block(blk - FIN_NRED - ndw4, nb_adam0, nb_adam1, fa);
 }
 
 size_t feat_bwd_workspace_bytes(int C, int N) {
@@ -549,7 +617,7 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                     const float* b2, const float* w3, const float* w4, const float* x3,
                     float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
                     float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s,
-                    uint64_t* stamps) {
+                    uint64_t* stamps, const FinAdam* adam) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
@@ -568,16 +636,34 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                      pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   PC_REQUIRE(dw4 && db4, "feat_bwd: dw4/db4 required");
+  FinAdam fa{};
+  int nba0 = 0, nba1 = 0;
+  if (adam && adam->on) {
+    fa = *adam;
+    PC_REQUIRE(fa.gp && fa.gm && fa.gv && fa.gg && fa.step_count && fa.g_n > fa.g_rest0 &&
+                   fa.g_rest0 % 4 == 0 && (fa.d_n == 0 || (fa.dp && fa.dm && fa.dv && fa.dg)) &&
+                   dw1 == fa.gg + PCADV_G_CONV1_W && dw4 == fa.gg + PCADV_G_CONV4_W &&
+                   db4 == fa.gg + PCADV_G_CONV4_B,
+               "feat_bwd: the fused Adam needs the generator's flat buffers");
+    nba0 = fin_adam_blocks(fa.g_n - fa.g_rest0);
+    nba1 = fa.d_n > 0 ? fin_adam_blocks(fa.d_n) : 0;
+  }
+  const int ndw4 = (O + DW4_CPB - 1) / DW4_CPB;
 #ifdef PCADV_STAMPS
-  // diagnostic build: the slab reduction and the dW4 gather as separate launches
-  // so a kernel trace times each part
+  // diagnostic build: the slab reduction, the dW4 gather and the Adam blocks as
+  // separate launches so a kernel trace times each part
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED), dim3(1024), 0, s, slabs, C * nchunk, dw1,
-                     db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0);
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3((O + DW4_CPB - 1) / DW4_CPB), dim3(1024), 0, s, slabs, C * nchunk,
-                     dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, FIN_NRED);
+                     db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0, fa, nba0, nba1);
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(ndw4), dim3(1024), 0, s, slabs, C * nchunk, dw1, db1,
+                     dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, FIN_NRED, fa, nba0, nba1);
+  if (nba0 + nba1 > 0)
+    hipLaunchKernelGGL(k_feat_bwd_finish, dim3(nba0 + nba1), dim3(1024), 0, s, slabs, C * nchunk,
+                       dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4,
+                       FIN_NRED + ndw4, fa, nba0, nba1);
 #else
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + (O + DW4_CPB - 1) / DW4_CPB), dim3(1024), 0, s, slabs,
-                     C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0);
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + ndw4 + nba0 + nba1), dim3(1024), 0, s,
+                     slabs, C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4,
+                     db4, 0, fa, nba0, nba1);
 #endif
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
   return PCADV_OK;

@@ -5,10 +5,8 @@
 
 namespace pcadv {
 
-// torch.optim.Adam, single-tensor path:
-//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)
-//   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, value=-lr/(1-b1^t))
-// Up to two segments (generator, discriminator) per launch.
+// torch.optim.Adam (adam_elem, common.h) over up to two segments (generator,
+// discriminator) per launch.
 struct AdamSeg {
   float* p;
   const float* g;
@@ -18,14 +16,6 @@ struct AdamSeg {
   float lr;
 };
 
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1,
-                                          float b2, float w2, float bc2s, float eps, float step) {
-  m = m + w1 * (g - m);
-  v = v * b2 + w2 * (g * g);
-  const float denom = sqrtf(v) / bc2s + eps;
-  p = p - step * (m / denom);
-}
-
 __global__ void __launch_bounds__(256)
 k_adam(AdamSeg s0, AdamSeg s1, int nblk0, const int32_t* __restrict__ step_count, int step_offset,
        float b1, float b2, float eps) {
@@ -33,11 +23,7 @@ k_adam(AdamSeg s0, AdamSeg s1, int nblk0, const int32_t* __restrict__ step_count
   const AdamSeg s = first ? s0 : s1;
   const int blk = first ? blockIdx.x : blockIdx.x - nblk0;
   const int nblk = first ? nblk0 : gridDim.x - nblk0;
-  const double t = (double)(*step_count + step_offset);
-  const float bc1 = (float)(1.0 - pow((double)b1, t));
-  const float bc2s = (float)sqrt(1.0 - pow((double)b2, t));
-  const float stepsz = (float)((double)s.lr / (double)bc1);
-  const float w1 = 1.f - b1, w2 = 1.f - b2;
+  const AdamHp h = adam_hp(step_count, step_offset, b1, b2, eps, s.lr);
   const int64_t n4 = s.n / 4;
   for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < n4; i += (int64_t)nblk * 256) {
     const f32x4 p4 = reinterpret_cast<f32x4*>(s.p)[i];
@@ -47,14 +33,14 @@ k_adam(AdamSeg s0, AdamSeg s1, int nblk0, const int32_t* __restrict__ step_count
     float p[4] = {p4.x, p4.y, p4.z, p4.w}, g[4] = {g4.x, g4.y, g4.z, g4.w};
     float m[4] = {m4.x, m4.y, m4.z, m4.w}, v[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) adam_elem(p[e], g[e], m[e], v[e], w1, b2, w2, bc2s, eps, stepsz);
+    for (int e = 0; e < 4; ++e) adam_elem(p[e], g[e], m[e], v[e], h);
     reinterpret_cast<f32x4*>(s.p)[i] = f32x4{p[0], p[1], p[2], p[3]};
     reinterpret_cast<f32x4*>(s.m)[i] = f32x4{m[0], m[1], m[2], m[3]};
     reinterpret_cast<f32x4*>(s.v)[i] = f32x4{v[0], v[1], v[2], v[3]};
   }
   if (blk == 0 && threadIdx.x < (s.n & 3)) {
     const int64_t i = n4 * 4 + threadIdx.x;
-    adam_elem(s.p[i], s.g[i], s.m[i], s.v[i], w1, b2, w2, bc2s, eps, stepsz);
+    adam_elem(s.p[i], s.g[i], s.m[i], s.v[i], h);
   }
 }
 
