@@ -424,6 +424,17 @@ __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __r
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = blk * 128 + 2 * lane;  // SLAB is even: j, j+1 both valid or both not
   const int s0 = wave * nslabs / 16, s1 = (wave + 1) * nslabs / 16;
+  // Adam state of this lane's two parameters, in flight during the reduction
+  const bool adam = fa.on && wave == 0 && j < SLAB;
+  float2 ap = make_float2(0.f, 0.f), am = ap, av = ap;
+  if (adam) {
+    ap = *reinterpret_cast<const float2*>(fa.gp + j);
+    am = *reinterpret_cast<const float2*>(fa.gm + j);
+    av = *reinterpret_cast<const float2*>(fa.gv + j);
+  }
+  // bias corrections (f64 pow) computed while the loads are in flight
+  const AdamHp h = adam ? adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g)
+                        : AdamHp{};
   float2 acc = make_float2(0.f, 0.f);
   if (j < SLAB) {
     int s = s0;
@@ -456,16 +467,12 @@ __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __r
       else if (jj < SL_DB3) dw3[jj - SL_DW3] = x;
       else db3[jj - SL_DB3] = x;
     }
-    if (fa.on) {  // the slab order is the generator's flat order (PCADV_G_CONV1_W = 0 ..)
-      const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g);
-      float2 p = *reinterpret_cast<const float2*>(fa.gp + j);
-      float2 m = *reinterpret_cast<const float2*>(fa.gm + j);
-      float2 w = *reinterpret_cast<const float2*>(fa.gv + j);
-      adam_elem(p.x, v.x, m.x, w.x, h);
-      adam_elem(p.y, v.y, m.y, w.y, h);
-      *reinterpret_cast<float2*>(fa.gp + j) = p;
-      *reinterpret_cast<float2*>(fa.gm + j) = m;
-      *reinterpret_cast<float2*>(fa.gv + j) = w;
+    if (adam) {  // the slab order is the generator's flat order (PCADV_G_CONV1_W = 0 ..)
+      adam_elem(ap.x, v.x, am.x, av.x, h);
+      adam_elem(ap.y, v.y, am.y, av.y, h);
+      *reinterpret_cast<float2*>(fa.gp + j) = ap;
+      *reinterpret_cast<float2*>(fa.gm + j) = am;
+      *reinterpret_cast<float2*>(fa.gv + j) = av;
     }
   }
 }
@@ -486,6 +493,22 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int o = blk * DW4_CPB + (wave >> 2), qq = wave & 3;
   const int ca = C * qq / 4, cb = C * (qq + 1) / 4;
+  // Adam state of the row (and bias) this wave finishes, in flight during the gather
+  const bool adam = fa.on && qq == 0 && o < O;
+  const size_t jw = PCADV_G_CONV4_W + (size_t)(o < O ? o : 0) * 128 + 2 * lane;
+  const size_t jb = PCADV_G_CONV4_B + (o < O ? o : 0);
+  float2 ap = make_float2(0.f, 0.f), am = ap, av = ap;
+  float bp = 0.f, bm = 0.f, bv = 0.f;
+  if (adam) {
+    ap = *reinterpret_cast<const float2*>(fa.gp + jw);
+    am = *reinterpret_cast<const float2*>(fa.gm + jw);
+    av = *reinterpret_cast<const float2*>(fa.gv + jw);
+    bp = fa.gp[jb];
+    bm = fa.gm[jb];
+    bv = fa.gv[jb];
+  }
+  const AdamHp h = adam ? adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g)
+                        : AdamHp{};
   float ax = 0.f, ay = 0.f, ab = 0.f;
   if (o < O) {
     for (int c0 = ca; c0 < cb; c0 += 64) {
@@ -528,20 +551,17 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
     }
     *reinterpret_cast<float2*>(dw4 + (size_t)o * 128 + 2 * lane) = make_float2(t.x, t.y);
     if (lane == 0) db4[o] = t.z;
-    if (fa.on) {
-      const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g);
-      const size_t j = PCADV_G_CONV4_W + (size_t)o * 128 + 2 * lane;
-      float2 p = *reinterpret_cast<const float2*>(fa.gp + j);
-      float2 m = *reinterpret_cast<const float2*>(fa.gm + j);
-      float2 w = *reinterpret_cast<const float2*>(fa.gv + j);
-      adam_elem(p.x, t.x, m.x, w.x, h);
-      adam_elem(p.y, t.y, m.y, w.y, h);
-      *reinterpret_cast<float2*>(fa.gp + j) = p;
-      *reinterpret_cast<float2*>(fa.gm + j) = m;
-      *reinterpret_cast<float2*>(fa.gv + j) = w;
+    if (adam) {
+      adam_elem(ap.x, t.x, am.x, av.x, h);
+      adam_elem(ap.y, t.y, am.y, av.y, h);
+      *reinterpret_cast<float2*>(fa.gp + jw) = ap;
+      *reinterpret_cast<float2*>(fa.gm + jw) = am;
+      *reinterpret_cast<float2*>(fa.gv + jw) = av;
       if (lane == 0) {
-        const size_t jb = PCADV_G_CONV4_B + o;
-        adam_elem(fa.gp[jb], t.z, fa.gm[jb], fa.gv[jb], h);
+        adam_elem(bp, t.z, bm, bv, h);
+        fa.gp[jb] = bp;
+        fa.gm[jb] = bm;
+        fa.gv[jb] = bv;
       }
     }
   }
