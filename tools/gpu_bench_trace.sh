@@ -9,4 +9,4 @@ rc=$?; echo "bench rc=$rc"; grep metric gpurun_out/q_bench.log | cut -c1-300
 rm -rf gpurun_out/q_trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/q_trace -o run --output-format csv -- python bench.py --no-cpu --steps 30 --warmup 5 > gpurun_out/q_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"
-python tools/kstats.py gpurun_out/q_trace/run_kernel_trace.csv | head -18
+python tools/kstats.py gpurun_out/q_trace/run_kernel_trace.csv > gpurun_out/q_kstats.txt; head -18 gpurun_out/q_kstats.txt
