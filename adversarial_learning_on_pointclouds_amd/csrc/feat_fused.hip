@@ -90,35 +90,42 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     return (tid < PM_P * 3 && p0 + p < N) ? pts[(size_t)p0 * 3 + tid] : 0.f;
   };
   int tile = blockIdx.x * PM_TPW;
+  // loads in the order they are consumed (the memory counter waits in issue
+  // order): the first tile's points and conv1's weights, then conv2's B
+  // fragments, then W3 (split three ways only after conv1 of the first tile)
   float pv = tile < ntiles ? pts_load(tile) : 0.f;
-
+  // conv1: thread = (channel tid & 63, 16-point group tid >> 6)
+  const int c1 = tid & 63, pg = tid >> 6;
+  const float wa = w1[c1 * 3 + 0], wb = w1[c1 * 3 + 1], wc = w1[c1 * 3 + 2], bb1 = b1[c1];
   // conv2: wave = (point tile wave >> 1, channel tile wave & 1), f32 B fragments
   f32x4 bf2[8];
   load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
   const float bias2 = b2[32 * (wave & 1) + r];
   // conv3: wave = channel tile (32 channels), W3 rows split three ways:
   // lane (r, h) holds k = 16 kb + 8 h .. + 8 of channel 32 wave + r
-  bf16x8 w3h[4], w3m[4], w3l[4];
+  f32x4 w3raw[8];
   {
     const float* wrow = w3 + (size_t)(32 * wave + r) * 64 + 8 * h;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb);
-      const f32x4 u1 = *reinterpret_cast<const f32x4*>(wrow + 16 * kb + 4);
+      w3raw[2 * kb] = *reinterpret_cast<const f32x4*>(wrow + 16 * kb);
+      w3raw[2 * kb + 1] = *reinterpret_cast<const f32x4*>(wrow + 16 * kb + 4);
+    }
+  }
+  const float bias3 = b3[32 * wave + r];
+  bf16x8 w3h[4], w3m[4], w3l[4];
+  auto split_w3 = [&]() {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         __bf16 a, m, l;
-        split3(j < 4 ? u0[j] : u1[j - 4], a, m, l);
+        split3(j < 4 ? w3raw[2 * kb][j] : w3raw[2 * kb + 1][j - 4], a, m, l);
         w3h[kb][j] = a;
         w3m[kb][j] = m;
         w3l[kb][j] = l;
       }
-    }
-  }
-  const float bias3 = b3[32 * wave + r];
-  // conv1: thread = (channel tid & 63, 16-point group tid >> 6)
-  const int c1 = tid & 63, pg = tid >> 6;
-  const float wa = w1[c1 * 3 + 0], wb = w1[c1 * 3 + 1], wc = w1[c1 * 3 + 2], bb1 = b1[c1];
+  };
   STAMP(1);
 
   for (int it = 0; it < PM_TPW && tile < ntiles; ++it, ++tile) {
@@ -133,6 +140,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       const f32x4 q = *reinterpret_cast<const f32x4*>(&L.pts[p * 4]);
       L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
     }
+    if (it == 0) split_w3();  // W3 has landed by now (after conv1 of the first tile)
     __syncthreads();
     STAMP(4 + 5 * it);
     {  // conv2 + ReLU, written to LDS split three ways for conv3
