@@ -67,6 +67,7 @@ class AdvArgs(ctypes.Structure):
         ("losses", _vp), ("logits", _vp),
         ("workspace", _vp), ("workspace_bytes", _sz),
         ("semi", _i), ("lambda_semi", _f), ("semi_th", _f),
+        ("part", _i),
     ]
 
 

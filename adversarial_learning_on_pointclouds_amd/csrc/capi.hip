@@ -180,18 +180,44 @@ static int adv_adam(const pcadv_adv_args* a, hipStream_t s) {
                       a->beta1, a->beta2, a->eps, s);
 }
 
+static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w, float* logits);
+
 static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(a && a->B > 0 && a->B <= 256 && a->N > 0, "adv_step: bad B/N");
-  const int B = a->B, N = a->N, C = 2 * B, R = 3 * B;
+  const int B = a->B, N = a->N, C = 2 * B;
   PC_REQUIRE(a->workspace && a->workspace_bytes >= carve(B, N, nullptr).total,
              "adv_step: workspace too small (need %zu bytes)", carve(B, N, nullptr).total);
   StepWs w = carve(B, N, static_cast<char*>(a->workspace));
   const float* G = a->g_param;
   float* gG = a->g_grad;
+  float* logits = a->logits ? a->logits : w.logits;
+  PC_REQUIRE(a->part >= 0 && a->part <= 2, "adv_step: part %d (0 whole, 1 head, 2 feature bwd)",
+             a->part);
+  PC_REQUIRE(!(a->part == 1 && a->apply_adam), "adv_step: part 1 cannot apply Adam");
+  if (a->part != 2) PC_TRY(adv_head_part(a, s, w, logits));
+  if (a->part == 1) return PCADV_OK;
+  // ---- PointNetfeat backward (sparse max-pool), then optimizer.step();
+  //      optimizer_D.step() (:558-559) fused into its finishing launch --------
+  PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v && a->d_param && a->d_m && a->d_v),
+             "adv_step: Adam buffers");
+  const FinAdam fa = fused_adam(a, true);
+  return launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
+                         G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                         G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
+                         gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
+                         gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
+                         gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
+                         s, nullptr, a->apply_adam ? &fa : nullptr);
+}
+
+// Part 1 of adv_step: everything before the feature backward.
+static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w, float* logits) {
+  const int B = a->B, N = a->N, C = 2 * B, R = 3 * B;
+  const float* G = a->g_param;
+  float* gG = a->g_grad;
   const float* D = a->d_param;
   float* gD = a->d_grad;
   const int32_t* st = a->step_count;
-  float* logits = a->logits ? a->logits : w.logits;
 
   // dropout: explicit masks (parity mode) are staged as one [2B][256] array
   const float* mask = nullptr;
@@ -287,18 +313,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
                            G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
-  // ---- PointNetfeat backward (sparse max-pool), then optimizer.step();
-  //      optimizer_D.step() (:558-559) fused into its finishing launch --------
-  PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v && a->d_param && a->d_m && a->d_v),
-             "adv_step: Adam buffers");
-  const FinAdam fa = fused_adam(a, true);
-  return launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
-                         G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
-                         G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
-                         gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
-                         gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
-                         gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr);
+  return PCADV_OK;
 }
 
 // run_training_pointnet_cls's iteration (utils/trainer.py:222-268,
@@ -385,7 +400,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 3; }
+int pcadv_abi_version(void) { return 4; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 

@@ -3,10 +3,15 @@
 The reference is single-process (train_classification.py:93); the north star
 adds data parallelism.  Clouds are independent, so each rank runs the fused
 step on its own B-cloud shards of the GT and noGT batches; the only exchange
-is ONE all-reduce(AVG) of the concatenated generator + discriminator gradient
+is an all-reduce(AVG) of the concatenated generator + discriminator gradient
 buffer (811 240 + 238 785 fp32 = 4.2 MB) between backward and the replicated
 Adam updates.  With equal shards this equals the single-process step on the
 global batch, since CE/BCE are batch means (mean of per-rank means).
+
+The buffer goes in two buckets, overlapped with backward: the head and
+discriminator gradients (3.6 MB, final before the feature backward) are
+all-reduced on RCCL's stream while the feature backward runs (step part 2);
+the generator's conv1..conv4 gradients (0.58 MB) follow it.
 """
 from __future__ import annotations
 
@@ -15,36 +20,66 @@ import torch.distributed as dist
 
 
 def _avg_(t, group=None):
+    _avg_async(t, group)()
+
+
+def _avg_async(t, group=None):
+    """Start all-reduce(AVG) of t; returns the wait() that completes it."""
     if dist.get_backend(group) == "nccl":
-        dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group)
-    else:  # gloo has no AVG
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        t.div_(dist.get_world_size(group))
+        work = dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=True)
+        return work.wait
+    work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)  # gloo: no AVG
+    world = dist.get_world_size(group)
+
+    def done():
+        work.wait()
+        t.div_(world)
+    return done
 
 
 class DataParallelAdvStep:
     """Wraps an AdvTrainStep-like object exposing grads(), adam(), grad_flat,
     g_param, d_param and losses."""
 
-    def __init__(self, step, group=None, broadcast_params=True):
+    def __init__(self, step, group=None, broadcast_params=True, overlap=None):
+        """overlap: bucket the all-reduce around the feature backward (default:
+        when the step supports parts and the backend is RCCL)."""
         self.step, self.group = step, group
+        self.overlap = overlap
         if broadcast_params:  # identical initial weights on every rank
             dist.broadcast(step.g_param, src=0, group=group)
             dist.broadcast(step.d_param, src=0, group=group)
+
+    def _split(self):
+        if self.overlap is not None:
+            return bool(self.overlap)
+        return getattr(self.step, "supports_parts", False) and dist.get_backend(self.group) == "nccl"
 
     def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, semi=False):
         # semi: each rank's pseudo-label CE is the mean over its own kept clouds,
         # so the averaged gradient weights ranks equally (the global-batch mean
         # would weight them by their kept counts)
-        self.step.grads(pts_gt, labels, pts_nogt, masks, soft, semi=semi)
-        _avg_(self.step.grad_flat, self.group)
-        self.step.adam()
-        return self.step.losses
+        s = self.step
+        if self._split():
+            s(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=semi, part=1)
+            done = _avg_async(s.early_grads(), self.group)
+            s(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=semi, part=2)
+            done()
+            _avg_(s.late_grads(), self.group)
+        else:
+            s.grads(pts_gt, labels, pts_nogt, masks, soft, semi=semi)
+            _avg_(s.grad_flat, self.group)
+        s.adam()
+        return s.losses
 
     def capture(self, pts_gt, labels, pts_nogt):
         """HIP graphs for the compute halves around the (eager) all-reduce."""
         s = self.step
-        g_fwd = s.capture_on(pts_gt, labels, pts_nogt, apply_adam=False)
+        if self._split():
+            g_fwd = (s.capture_on(pts_gt, labels, pts_nogt, apply_adam=False, part=1),
+                     s.capture_on(pts_gt, labels, pts_nogt, apply_adam=False, part=2))
+        else:
+            g_fwd = s.capture_on(pts_gt, labels, pts_nogt, apply_adam=False)
         saved = s._snapshot()
         g_adam = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=s.device)
@@ -64,7 +99,15 @@ class _DPGraph:
         self.g_fwd, self.g_adam, self.step, self.group = g_fwd, g_adam, step, group
 
     def replay(self):
-        self.g_fwd.replay()
-        _avg_(self.step.grad_flat, self.group)
+        s = self.step
+        if isinstance(self.g_fwd, tuple):  # bucketed, overlapped with the feature backward
+            self.g_fwd[0].replay()
+            done = _avg_async(s.early_grads(), self.group)
+            self.g_fwd[1].replay()
+            done()
+            _avg_(s.late_grads(), self.group)
+        else:
+            self.g_fwd.replay()
+            _avg_(s.grad_flat, self.group)
         self.g_adam.replay()
-        return self.step.losses
+        return s.losses

@@ -19,6 +19,7 @@ from . import _lib
 from ._lib import AdvArgs, D_LAYOUT, D_NUMEL, G_LAYOUT, G_NUMEL, check, stream_ptr
 
 D_GRAD_OFFSET = (G_NUMEL + 63) // 64 * 64  # D grads start 256-B aligned
+G_LATE_END = G_LAYOUT["fc1.weight"]  # grad_flat[:G_LATE_END]: the feature backward's (part 2)
 
 
 def flatten_params(module, layout, numel, device):
@@ -110,7 +111,7 @@ class AdvTrainStep:
         self._keep = []
 
     # ------------------------------------------------------------------
-    def _args(self, pts_gt, labels, pts_nogt, masks, soft, apply_adam, semi=False):
+    def _args(self, pts_gt, labels, pts_nogt, masks, soft, apply_adam, semi=False, part=0):
         B, N = int(pts_gt.shape[0]), self.N
         if not 0 < B <= self.B:
             raise ValueError(f"batch of {B} clouds; this step was built for at most {self.B}")
@@ -151,12 +152,25 @@ class AdvTrainStep:
         a.workspace_bytes = self.workspace.numel()
         a.semi = int(bool(semi))
         a.lambda_semi, a.semi_th = hp["lambda_semi"], hp["semi_th"]
+        a.part = int(part)
         return a
 
+    # gradients that are final before the feature backward: g_grad[G_FC1_W:] and
+    # all of D, contiguous in grad_flat (part 1 of a split step)
+    supports_parts = True
+
+    def early_grads(self):
+        return self.grad_flat[G_LATE_END:]
+
+    def late_grads(self):
+        return self.grad_flat[:G_LATE_END]
+
     def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, apply_adam=True,
-                 semi=False):
-        """Whole iteration: forward, losses, backward, both Adam steps."""
-        a = self._args(pts_gt, labels, pts_nogt, masks, soft, apply_adam, semi)
+                 semi=False, part=0):
+        """Whole iteration: forward, losses, backward, both Adam steps.  part=1
+        stops before the feature backward, part=2 runs only the feature backward
+        (and Adam when apply_adam) on the state part 1 left."""
+        a = self._args(pts_gt, labels, pts_nogt, masks, soft, apply_adam, semi, part)
         check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step")
         return self.losses
 
@@ -186,17 +200,18 @@ class AdvTrainStep:
                              self.step_count), saved):
             dst.copy_(src)
 
-    def capture_on(self, pts_gt, labels, pts_nogt, apply_adam=True, semi=False):
-        """Capture one step reading the given (resident) input buffers into a
-        HIP graph; state is left as it was before the capture."""
+    def capture_on(self, pts_gt, labels, pts_nogt, apply_adam=True, semi=False, part=0):
+        """Capture one step (or one part of it) reading the given (resident)
+        input buffers into a HIP graph; state is left as it was before the
+        capture."""
         saved = self._snapshot()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam, semi=semi)  # warm-up
+        with torch.cuda.stream(side):  # warm-up: the whole step (part 2 needs part 1's state)
+            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam, semi=semi)
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        a = self._args(pts_gt, labels, pts_nogt, None, None, apply_adam, semi)
+        a = self._args(pts_gt, labels, pts_nogt, None, None, apply_adam, semi, part)
         self._keep.append(a)
         with torch.cuda.graph(g):
             check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (capture)")

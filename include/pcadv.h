@@ -354,6 +354,13 @@ typedef struct pcadv_adv_args {
    * D(log_softmax(pred_nogt)) <= semi_th ignored (no term when all are) */
   int semi;
   float lambda_semi, semi_th;
+  /* 0: the whole step.  A data-parallel step may split it so the gradients
+   * that are final early are all-reduced while the feature backward runs:
+   * 1 = forward, losses, discriminator and head backward (every gradient
+   *     except the generator's conv1..conv4, g_grad[0, PCADV_G_FC1_W));
+   * 2 = the feature backward (those conv1..conv4 gradients; and both Adam
+   *     updates when apply_adam) on the state part 1 left in the workspace. */
+  int part;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

@@ -14,6 +14,7 @@ import socket
 from collections import OrderedDict
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -81,6 +82,30 @@ class OracleStep:
             g[self.d_off + self.d_lay[k]:self.d_off + self.d_lay[k] + v.size] = v.reshape(-1)
         self.losses = losses
 
+    # the split step of the overlapped all-reduce (AdvTrainStep parts 1 / 2):
+    # part 1 leaves the early gradients, part 2 the generator's conv1..conv4
+    supports_parts = True
+
+    def early_grads(self):
+        from adversarial_learning_on_pointclouds_amd.step import G_LATE_END
+        return self.grad_flat[G_LATE_END:]
+
+    def late_grads(self):
+        from adversarial_learning_on_pointclouds_amd.step import G_LATE_END
+        return self.grad_flat[:G_LATE_END]
+
+    def __call__(self, pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=False,
+                 part=0):
+        assert not apply_adam
+        if part == 1:
+            self.grads(pts_gt, labels, pts_nogt, masks, soft, semi)
+            self._late = self.late_grads().clone()
+            self.late_grads().fill_(float("nan"))  # part 2 has not run yet
+        elif part == 2:
+            self.late_grads().copy_(self._late)
+        else:
+            self.grads(pts_gt, labels, pts_nogt, masks, soft, semi)
+
     def adam(self):
         g = self.grad_flat.numpy()
         self.optG.step(OrderedDict((k, g[self.g_lay[k]:self.g_lay[k] + v.size].reshape(v.shape))
@@ -90,14 +115,14 @@ class OracleStep:
             for k, v in self.D.items()))
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, overlap=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
         from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
         # rank 1 starts from different weights: the wrapper's broadcast must fix that
         step = OracleStep(seed_g=11 + rank, seed_d=12 + rank)
-        dp = DataParallelAdvStep(step)
+        dp = DataParallelAdvStep(step, overlap=overlap)
         sl = slice(rank * B_RANK, (rank + 1) * B_RANK)
         for t in range(STEPS):
             pg, lab, pn, mg, mn, yg, yn = _inputs(t)
@@ -108,8 +133,11 @@ def _worker(rank, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_dp_gloo_matches_global_batch(tmp_path):
-    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_gloo_matches_global_batch(tmp_path, overlap):
+    """overlap: the bucketed all-reduce (head/D gradients while the feature
+    backward runs, then the conv1..conv4 bucket)."""
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path), overlap), nprocs=WORLD, join=True)
     g0, g1 = np.load(tmp_path / "g0.npy"), np.load(tmp_path / "g1.npy")
     d0, d1 = np.load(tmp_path / "d0.npy"), np.load(tmp_path / "d1.npy")
     # replicas stay bit-identical: same averaged gradient, same Adam
