@@ -283,6 +283,17 @@ def bench_seg(args):
     kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
     kflops = 2.0 * Bs * Ns * 512 * 2048
     kpeak = 2500.0 / 3.0  # three bf16 MFMA products per f32 product (hi/lo splits)
+    # HBM traffic of the same launch pair from the committed PMC passes of
+    # `bench.py --config seg` (tools/gpu_round.sh, tools/pmc_traffic.py)
+    traffic, traffic_src = None, None
+    here = os.path.dirname(os.path.abspath(__file__))
+    prof = sorted(glob.glob(os.path.join(here, "profiles", "r*_seg_pmc_traffic.json")))
+    if prof:
+        kern = json.load(open(prof[-1]))["kernels"]
+        names = ("pcadv::k_gemm_x3<2, 2, 2, 3>", "pcadv::k_max_combine")
+        if all(n in kern for n in names):
+            traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
+            traffic_src = os.path.relpath(prof[-1], here)
     out = {
         "metric": "point-clouds/sec (seg train step), B=16 N=2048 ShapeNet-part, 1 GPU",
         "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
@@ -297,7 +308,9 @@ def bench_seg(args):
                                "+ k_max_combine (exact f32 re-evaluation)",
                      "achieved": round(kflops / kern_s / 1e12, 2), "peak": round(kpeak, 1),
                      "unit": "TFLOP/s", "frac": round(kflops / kern_s / 1e12 / kpeak, 4),
-                     "traffic": None, "avg_launch_us": round(kern_s * 1e6, 2),
+                     "traffic": traffic,
+                     "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
+                     "traffic_source": traffic_src, "avg_launch_us": round(kern_s * 1e6, 2),
                      "algorithmic_flops_per_launch": kflops,
                      "algorithmic_bytes_per_launch": Bs * Ns * 512 * 4 + 2048 * 512 * 4 + Bs * 2048 * 8,
                      "peak_basis": "bf16 2500 TF dense / 3 split products"},
@@ -321,12 +334,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PCADV_BENCH_BACKEND", "nccl") != "nccl":  # rehearsal: ranks may share a GPU
+        local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=dev)
+        # RCCL; PCADV_BENCH_BACKEND=gloo rehearses the multi-rank path with several
+        # ranks on one GPU (RCCL needs a device per rank) - never for measurements
+        backend = os.environ.get("PCADV_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=dev)
+        else:
+            tdist.init_process_group(backend)
         dist = tdist
 
     from adversarial_learning_on_pointclouds_amd import ops
@@ -414,8 +435,9 @@ def main():
     t_min = f12 / 157.3e12 + f3 / (2500e12 / 6.0) + f4 / (2500e12 / 3.0)
     peak = flops / t_min / 1e12
     traffic, traffic_src = None, None
-    prof = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                         "profiles", "r*_pmc_traffic.json")))
+    prof = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                     "profiles", "r*_pmc_traffic.json"))
+                  if "_seg_" not in os.path.basename(p))
     if prof:
         kern = json.load(open(prof[-1]))["kernels"]
         names = ("pcadv::k_point_mlp", "pcadv::k_conv4_max")
