@@ -52,10 +52,16 @@ constexpr int PM_T = 256;   // 4 waves; 2 workgroups per CU (register-bound)
 constexpr int PM_TPW = 2;   // tiles per workgroup (the next tile's points are prefetched)
 constexpr int X2S = 72;     // bf16 row stride of the x2 planes (144 B: conflict-free b128 reads)
 
+constexpr int X3S = 136;     // f32 row stride of the x3 store staging (the two half-waves' rows 32 banks apart)
 struct MlpLds {
   alignas(16) float pts[PM_P * 4];
-  alignas(16) float x1[PM_P * S64];
-  alignas(16) __bf16 x2[3][PM_P * X2S];  // conv2 output split in bf16 hi / mid / lo
+  union {
+    struct {
+      alignas(16) float x1[PM_P * S64];
+      alignas(16) __bf16 x2[3][PM_P * X2S];  // conv2 output split in bf16 hi / mid / lo
+    };
+    alignas(16) float x3[PM_P * X3S];  // the tile's conv3 output, staged for 16-B stores
+  };
 };
 
 // conv1 and conv2 run in exact f32 (VALU, then v_mfma_f32_32x32x2_f32 in the k
@@ -179,15 +185,26 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       asm volatile("s_nop 0" ::"v"(acc[0][0]), "v"(acc[1][15]));
 #endif
       STAMP(6 + 5 * it);
-      float* xg = x3g + ((size_t)c * N + p0) * 128 + 32 * wave + r;
+      // stage the 64 x 128 tile through LDS (over x1 / x2: every wave is past
+      // conv3's reads after the barrier), then write it as the contiguous 32 KB
+      // it is in HBM with 16-B stores: a quarter of the store instructions
+      __syncthreads();
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int row = 32 * pt + acc_row(i, lane);
           const float v = acc[pt][i] + bias3;
-          if (p0 + row < N) xg[(size_t)row * 128] = v > 0.f ? v : 0.f;
+          L.x3[(32 * pt + acc_row(i, lane)) * X3S + 32 * wave + r] = v > 0.f ? v : 0.f;
         }
+      __syncthreads();
+      float* xg = x3g + ((size_t)c * N + p0) * 128;
+#pragma unroll
+      for (int u = 0; u < PM_P * 32 / PM_T; ++u) {
+        const int e = tid + PM_T * u, row = e >> 5, c4 = e & 31;
+        if (p0 + row < N)
+          *reinterpret_cast<f32x4*>(xg + (size_t)row * 128 + 4 * c4) =
+              *reinterpret_cast<const f32x4*>(&L.x3[row * X3S + 4 * c4]);
+      }
       STAMP(7 + 5 * it);
     }
   }
