@@ -126,8 +126,19 @@ k_gemm_x3(GemmP p) {
     const int xcd = lin & 7, q = n >> 3, rr = n & 7;
     const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (lin >> 3);
     tz = t / (gx * gy);
-    tx = (t % (gx * gy)) / gy;
-    ty = t % gy;
+    const int rem = t % (gx * gy);
+    // wide outputs (>= 16 column tiles: conv6's 2048) go column-group-major in
+    // groups of 8, so the B tiles a group shares stay in L2 while A streams by
+    // (all 16 at once plus the A tiles in flight overflow one XCD's 4 MB)
+    constexpr int CG = 8;
+    if (gy >= 2 * CG && gy % CG == 0) {
+      const int g = rem / (gx * CG), w = rem % (gx * CG);
+      tx = w / CG;
+      ty = g * CG + w % CG;
+    } else {
+      tx = rem / gy;
+      ty = rem % gy;
+    }
   }
   const int n0 = ty * GM_BN;
   // mode 2: tx = (cloud, row tile of that cloud); rows never straddle clouds
