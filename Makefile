@@ -41,3 +41,11 @@ stamps: $(SRC) $(HDR)
 	@mkdir -p build/stamps
 	$(HIPCC) $(HIPFLAGS) -DPCADV_STAMPS -shared -o $(STAMPS_LIB) $(SRC) $(CPP) -lz
 .PHONY: stamps
+
+# A/B variant library (tools/gpu_ab.sh): the same sources with ABDEFS, e.g.
+#   make ab ABDEFS=-DPCADV_K2_PRIO=0
+ABDEFS ?=
+ab: $(SRC) $(HDR)
+	@mkdir -p build/ab
+	$(HIPCC) $(HIPFLAGS) $(ABDEFS) -shared -o build/ab/libA.so $(SRC) $(CPP) -lz
+.PHONY: ab

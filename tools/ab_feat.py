@@ -1,0 +1,55 @@
+"""A/B timing of the feature forward pair (pcadv_feat_fwd: k_point_mlp +
+k_conv4_max) and of the whole adversarial step graph, for the library named by
+PCADV_LIB.  Run the variants alternately in one gpurun call (box-to-box
+variation is several %; within one box it is well under 1 %).
+
+    PCADV_LIB=path python tools/ab_feat.py TAG
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+import adversarial_learning_on_pointclouds_amd as pc  # noqa: E402
+from adversarial_learning_on_pointclouds_amd import ops  # noqa: E402
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "?"
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model, model_D = pc.PointNetCls(k=40).to(dev), pc.DeepConvDiscNet(40, 1).to(dev)
+    B, N = 32, 1024
+    g = torch.Generator().manual_seed(1)
+    pg = (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dev)
+    pn = (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dev)
+    lab = torch.randint(0, 40, (B,), generator=g).to(dev)
+    pts = torch.cat([pg, pn], 0).contiguous()
+    f = model.feat
+    fw = [f.conv1.weight, f.conv1.bias, f.conv2.weight, f.conv2.bias, f.conv3.weight,
+          f.conv3.bias, f.conv4.weight, f.conv4.bias]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(20):
+        ops.feat_fwd(pts, *fw)
+    e0.record()
+    for _ in range(300):
+        ops.feat_fwd(pts, *fw)
+    e1.record()
+    torch.cuda.synchronize()
+    pair = e0.elapsed_time(e1) / 300 * 1e3
+    step = pc.AdvTrainStep(model, model_D, B, N, device=dev)
+    gr = step.capture_on(pg, lab, pn)
+    for _ in range(20):
+        gr.replay()
+    e0.record()
+    for _ in range(300):
+        gr.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    st = e0.elapsed_time(e1) / 300 * 1e3
+    print(f"AB {tag}: feature pair {pair:7.2f} us   step {st:7.2f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
