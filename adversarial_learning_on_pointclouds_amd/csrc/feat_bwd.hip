@@ -582,19 +582,33 @@ __device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
   const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps,
                            first ? fa.lr_g : fa.lr_d);
   const int64_t n4 = n / 4;
-  for (int64_t i = (int64_t)b * 1024 + threadIdx.x; i < n4; i += (int64_t)nb * 1024) {
-    const f32x4 p4 = reinterpret_cast<f32x4*>(p)[i];
-    const f32x4 g4 = reinterpret_cast<const f32x4*>(g)[i];
-    const f32x4 m4 = reinterpret_cast<f32x4*>(m)[i];
-    const f32x4 v4 = reinterpret_cast<f32x4*>(v)[i];
-    float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w};
-    float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-    const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+  // FIN_ADAM_V4 float4 per thread, all loads issued before any update: one
+  // memory round trip per pass
+  const int64_t stride = (int64_t)nb * 1024;
+  for (int64_t i0 = (int64_t)b * 1024 + threadIdx.x; i0 < n4; i0 += stride * FIN_ADAM_V4) {
+    f32x4 p4[FIN_ADAM_V4], g4[FIN_ADAM_V4], m4[FIN_ADAM_V4], v4[FIN_ADAM_V4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], h);
-    reinterpret_cast<f32x4*>(p)[i] = f32x4{pp[0], pp[1], pp[2], pp[3]};
-    reinterpret_cast<f32x4*>(m)[i] = f32x4{mm[0], mm[1], mm[2], mm[3]};
-    reinterpret_cast<f32x4*>(v)[i] = f32x4{vv[0], vv[1], vv[2], vv[3]};
+    for (int u = 0; u < FIN_ADAM_V4; ++u) {
+      const int64_t i = i0 + u * stride < n4 ? i0 + u * stride : i0;  // clamped, not stored
+      p4[u] = reinterpret_cast<f32x4*>(p)[i];
+      g4[u] = reinterpret_cast<const f32x4*>(g)[i];
+      m4[u] = reinterpret_cast<f32x4*>(m)[i];
+      v4[u] = reinterpret_cast<f32x4*>(v)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_ADAM_V4; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n4) continue;
+      float pp[4] = {p4[u].x, p4[u].y, p4[u].z, p4[u].w};
+      float mm[4] = {m4[u].x, m4[u].y, m4[u].z, m4[u].w};
+      float vv[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
+      const float gg[4] = {g4[u].x, g4[u].y, g4[u].z, g4[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], h);
+      reinterpret_cast<f32x4*>(p)[i] = f32x4{pp[0], pp[1], pp[2], pp[3]};
+      reinterpret_cast<f32x4*>(m)[i] = f32x4{mm[0], mm[1], mm[2], mm[3]};
+      reinterpret_cast<f32x4*>(v)[i] = f32x4{vv[0], vv[1], vv[2], vv[3]};
+    }
   }
   if (b == 0 && threadIdx.x < (n & 3)) {
     const int64_t i = n4 * 4 + threadIdx.x;
