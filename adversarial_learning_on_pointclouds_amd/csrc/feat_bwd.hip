@@ -437,7 +437,17 @@ __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __r
                         : AdamHp{};
   float2 acc = make_float2(0.f, 0.f);
   if (j < SLAB) {
+    // 32 slabs in flight per lane (a block is alone on its CU at this kernel's
+    // register use, so the registers are free): one round trip per 32 slabs
     int s = s0;
+    constexpr int RD = 32;
+    for (; s + RD <= s1; s += RD) {
+      float2 v[RD];
+#pragma unroll
+      for (int u = 0; u < RD; ++u) v[u] = *reinterpret_cast<const float2*>(slabs + (size_t)(s + u) * SLAB + j);
+#pragma unroll
+      for (int u = 0; u < RD; ++u) { acc.x += v[u].x; acc.y += v[u].y; }
+    }
     for (; s + 8 <= s1; s += 8) {
       float2 v[8];
 #pragma unroll
