@@ -24,9 +24,11 @@ step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/${tag}_pmc_fetch" -
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/${tag}_pmc_write" -o run --output-format csv -- python bench.py --no-cpu --steps 3 --warmup 1
 step bench 600 python bench.py
 grep '"metric"' "gpurun_out/${tag}_bench.log"
-step bench_seg 600 python bench.py --config seg --steps 20 --warmup 3
 step trace_seg 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_trace_seg" -o run --output-format csv -- python bench.py --config seg --no-cpu --steps 5 --warmup 1
 step pmc_fetch_seg 600 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/${tag}_pmc_fetch_seg" -o run --output-format csv -- python bench.py --config seg --no-cpu --steps 2 --warmup 1
 step pmc_write_seg 600 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/${tag}_pmc_write_seg" -o run --output-format csv -- python bench.py --config seg --no-cpu --steps 2 --warmup 1
+# the seg bench line reads its traffic from the committed summary of these passes
+python tools/pmc_traffic.py "gpurun_out/${tag}_pmc_fetch_seg" "gpurun_out/${tag}_pmc_write_seg" "profiles/${tag}_seg_pmc_traffic.json" > /dev/null
+step bench_seg 600 python bench.py --config seg --steps 20 --warmup 3
 step bench_cls 600 python bench.py --config cls
 step bench_n2048 600 python bench.py --points 2048 --no-cpu --steps 100 --warmup 10
