@@ -444,7 +444,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   // unit are issued in the same scheduling regions as the screening of the
   // previous unit (the other accumulator) and a share of the staging work, so
   // one wave's matrix and vector work overlap.
-  f32x16 accA, accB;  // units of half 0 / half 1 of a step
+  f32x16 accA = {}, accB = {};  // units of half 0 / half 1 of a step
   auto unit = [&](int s, int pt, f32x16& cur, const f32x16& prev, auto SCREEN, auto MASKED) {
     const int buf = s & 1;
     const __bf16* xh = &L.x[buf][0][(32 * pt + r) * C4_SB + 8 * h];
