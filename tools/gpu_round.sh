@@ -19,6 +19,7 @@ step() {  # step <name> <seconds> <cmd...>
 }
 
 step pytest 900 python -m pytest tests -m gpu -q --timeout 300 -rf
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step trace 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_trace" -o run --output-format csv -- python bench.py --no-cpu --steps 50 --warmup 10
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/${tag}_pmc_fetch" -o run --output-format csv -- python bench.py --no-cpu --steps 3 --warmup 1
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/${tag}_pmc_write" -o run --output-format csv -- python bench.py --no-cpu --steps 3 --warmup 1
