@@ -175,9 +175,17 @@ static FinAdam fused_adam(const pcadv_adv_args* a, bool with_d) {
 
 static int adv_adam(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(a && a->g_param && a->d_param && a->step_count, "adv_step_adam: bad arguments");
-  return launch_adam2(a->g_param, a->g_grad, a->g_m, a->g_v, PCADV_G_NUMEL, a->lr_g, a->d_param,
-                      a->d_grad, a->d_m, a->d_v, PCADV_D_NUMEL, a->lr_d, a->step_count, 0,
-                      a->beta1, a->beta2, a->eps, s);
+  PC_REQUIRE(a->part >= 0 && a->part <= 2, "adv_step_adam: part %d not in 0..2", a->part);
+  if (a->part == 2)  // the generator's conv1..conv4 (the late all-reduce bucket)
+    return launch_adam2(a->g_param, a->g_grad, a->g_m, a->g_v, PCADV_G_FC1_W, a->lr_g, nullptr,
+                        nullptr, nullptr, nullptr, 0, 0.f, a->step_count, 0, a->beta1, a->beta2,
+                        a->eps, s);
+  // part 1 starts at fc1 (a multiple of 4 floats: the vector loads stay aligned)
+  static_assert(PCADV_G_FC1_W % 4 == 0, "fc1 offset alignment");
+  const int64_t g0 = a->part == 1 ? PCADV_G_FC1_W : 0;
+  return launch_adam2(a->g_param + g0, a->g_grad + g0, a->g_m + g0, a->g_v + g0,
+                      PCADV_G_NUMEL - g0, a->lr_g, a->d_param, a->d_grad, a->d_m, a->d_v,
+                      PCADV_D_NUMEL, a->lr_d, a->step_count, 0, a->beta1, a->beta2, a->eps, s);
 }
 
 static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w, float* logits);

@@ -11,7 +11,10 @@ global batch, since CE/BCE are batch means (mean of per-rank means).
 The buffer goes in two buckets, overlapped with backward: the head and
 discriminator gradients (3.6 MB, final before the feature backward) are
 all-reduced on RCCL's stream while the feature backward runs (step part 2);
-the generator's conv1..conv4 gradients (0.58 MB) follow it.
+the generator's conv1..conv4 gradients (0.58 MB) follow it, and while that
+small all-reduce is in flight the parameters of the first bucket take their
+Adam update (Adam is elementwise: the split update equals the whole one
+bitwise), so only conv1..conv4's update waits for the last collective.
 """
 from __future__ import annotations
 
@@ -65,6 +68,12 @@ class DataParallelAdvStep:
             done = _avg_async(s.early_grads(), self.group)
             s(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=semi, part=2)
             done()
+            if getattr(s, "supports_split_adam", False):
+                done_late = _avg_async(s.late_grads(), self.group)
+                s.adam(part=1)  # the early bucket's parameters, beside the late all-reduce
+                done_late()
+                s.adam(part=2)
+                return s.losses
             _avg_(s.late_grads(), self.group)
         else:
             s.grads(pts_gt, labels, pts_nogt, masks, soft, semi=semi)
@@ -80,15 +89,20 @@ class DataParallelAdvStep:
                      s.capture_on(pts_gt, labels, pts_nogt, apply_adam=False, part=2))
         else:
             g_fwd = s.capture_on(pts_gt, labels, pts_nogt, apply_adam=False)
+        parts = (1, 2) if self._split() and getattr(s, "supports_split_adam", False) else (0,)
         saved = s._snapshot()
-        g_adam = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=s.device)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            s.adam()
+        with torch.cuda.stream(side):  # warm-up outside the capture
+            for part in parts:
+                s.adam(part=part)
         torch.cuda.current_stream().wait_stream(side)
-        with torch.cuda.graph(g_adam):
-            s.adam()
+        g_adam = []
+        for part in parts:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                s.adam(part=part)
+            g_adam.append(g)
         torch.cuda.synchronize()
         s._restore(saved)
         return _DPGraph(g_fwd, g_adam, s, self.group)
@@ -105,9 +119,15 @@ class _DPGraph:
             done = _avg_async(s.early_grads(), self.group)
             self.g_fwd[1].replay()
             done()
+            if len(self.g_adam) == 2:  # early bucket's Adam beside the late all-reduce
+                done_late = _avg_async(s.late_grads(), self.group)
+                self.g_adam[0].replay()
+                done_late()
+                self.g_adam[1].replay()
+                return s.losses
             _avg_(s.late_grads(), self.group)
         else:
             self.g_fwd.replay()
             _avg_(s.grad_flat, self.group)
-        self.g_adam.replay()
+        self.g_adam[0].replay()
         return s.losses

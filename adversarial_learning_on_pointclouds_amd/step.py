@@ -178,9 +178,15 @@ class AdvTrainStep:
         """Forward + backward only (gradients in grad_flat; step counter advanced)."""
         return self(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=semi)
 
-    def adam(self):
-        """optimizer.step(); optimizer_D.step() on the current gradients."""
+    # adam(part=1) / adam(part=2): the parameters of the early / late gradient
+    # bucket (Adam is elementwise: both together are adam() bitwise)
+    supports_split_adam = True
+
+    def adam(self, part=0):
+        """optimizer.step(); optimizer_D.step() on the current gradients
+        (part 1: g_param[G_LATE_END:] and D; part 2: g_param[:G_LATE_END])."""
         a = AdvArgs()
+        a.part = int(part)
         a.g_param, a.g_grad = self.g_param.data_ptr(), self.g_grad.data_ptr()
         a.g_m, a.g_v = self.g_m.data_ptr(), self.g_v.data_ptr()
         a.d_param, a.d_grad = self.d_param.data_ptr(), self.d_grad.data_ptr()

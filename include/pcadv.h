@@ -369,7 +369,12 @@ int pcadv_adv_step(const pcadv_adv_args* args, hipStream_t stream);
 /* The two Adam updates of pcadv_adv_step alone (optimizer.step() and
  * optimizer_D.step(), trainer.py:558-559), for a step that ran with
  * apply_adam = 0 and whose gradients were then all-reduced across ranks.
- * Uses the step counter already advanced by that pcadv_adv_step. */
+ * Uses the step counter already advanced by that pcadv_adv_step.  args->part
+ * selects the parameters (Adam is elementwise, so parts 1 + 2 equal part 0
+ * bitwise): 0 = all; 1 = those whose gradients part 1 of the step finalises
+ * (g_param[PCADV_G_FC1_W, PCADV_G_NUMEL) and all of D), so they can update
+ * while the conv1..conv4 bucket is still being all-reduced; 2 = the rest
+ * (g_param[0, PCADV_G_FC1_W)). */
 int pcadv_adv_step_adam(const pcadv_adv_args* args, hipStream_t stream);
 
 /* One iteration of run_training_pointnet_cls (utils/trainer.py:222-268,

@@ -54,6 +54,31 @@ def test_parts_equal_whole_step():
         assert torch.equal(a, b)
 
 
+def test_split_adam_equals_whole_adam():
+    """adam(part=1) then adam(part=2) (the early bucket's parameters updated
+    beside the late all-reduce) equals adam() bitwise, over three steps."""
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+    dev = torch.device("cuda:0")
+    outs = []
+    for split in (False, True):
+        m, d = _models(dev)
+        st = AdvTrainStep(m, d, B, N, seed=7, device=dev)
+        for k in range(3):
+            st.grads(*_batch(dev, 20 + k))
+            if split:
+                st.adam(part=1)
+                st.adam(part=2)
+            else:
+                st.adam()
+        torch.cuda.synchronize()
+        outs.append((st.g_param.clone(), st.g_m.clone(), st.g_v.clone(), st.d_param.clone(),
+                     st.d_m.clone(), st.d_v.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    with pytest.raises(RuntimeError):
+        st.adam(part=3)
+
+
 def test_part_graphs_equal_whole_graph():
     from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
     dev = torch.device("cuda:0")
