@@ -356,7 +356,9 @@ def main():
 
     model, model_D = make_models(dev, seed=0)
     step = AdvTrainStep(model, model_D, B, N, seed=1234 + rank, device=dev)
-    runner = DataParallelAdvStep(step) if dist is not None else None
+    # PCADV_BENCH_OVERLAP=1 forces the bucketed all-reduce (the RCCL default) in a gloo rehearsal
+    overlap = {"1": True, "0": False}.get(os.environ.get("PCADV_BENCH_OVERLAP", ""))
+    runner = DataParallelAdvStep(step, overlap=overlap) if dist is not None else None
 
     # resident synthetic inputs: rank-specific shards of the global batch
     pool = []
