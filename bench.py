@@ -406,7 +406,9 @@ def main():
 
     # dominant kernels: the PointNetfeat forward (k_point_mlp: conv1..conv3;
     # k_conv4_max: conv4 + max with the exact re-evaluation), timed with HIP events on
-    # the stream they are launched on, same inputs as the step (the last resident batch)
+    # the stream they are launched on, same inputs as the step (the last resident batch).
+    # The pairs run back to back from one HIP graph, as they do inside the step graph
+    # (eager calls would add host launch gaps between pairs to the events' interval).
     pg, lab, pn = pool[(args.steps - 1) % POOL]
     pts_all = torch.cat([pg, pn], 0).contiguous()
     fw = [model.feat.conv1.weight, model.feat.conv1.bias, model.feat.conv2.weight,
@@ -415,10 +417,16 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
         ops.feat_fwd(pts_all, *fw)
+    torch.cuda.synchronize()
     reps = 50
+    pair_graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(pair_graph):
+        for _ in range(reps):
+            ops.feat_fwd(pts_all, *fw)
+    pair_graph.replay()  # warm
+    torch.cuda.synchronize()
     ev0.record()
-    for _ in range(reps):
-        ops.feat_fwd(pts_all, *fw)
+    pair_graph.replay()
     ev1.record()
     torch.cuda.synchronize()
     kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
