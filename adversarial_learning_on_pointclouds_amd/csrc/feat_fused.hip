@@ -523,6 +523,17 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     else unit(s, 1, accB, accA, T_{}, T_{});
     __syncthreads();
   }
+  // W4 rows of the exact re-evaluation (eight lanes per row, see below): they
+  // do not depend on the winners, so they are fetched while the last unit is
+  // screened and merged (the W4 fragments' registers are free by now)
+  const int oc = lane >> 3, part = lane & 7;
+  const float* wbase = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128 + 16 * part;
+  f32x4 wv[4][4];
+#pragma unroll
+  for (int G = 0; G < 4; ++G)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)(8 * G + oc) * 128 + 4 * u);
   {  // the last unit
     int k1 = KEY_NONE, k2 = KEY_NONE;
     screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2);
@@ -575,16 +586,13 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     // 8 G + (l >> 3) and terms 16 (l & 7) .. + 16, so a load instruction reads
     // eight 128-B lines whole (a lane-per-row layout would touch 64 lines) and
     // the partial sums meet in three DPP steps within the lane octet.
-    const int oc = lane >> 3, part = lane & 7;
-    const float* wbase = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128 + 16 * part;
-    f32x4 wv[4][4], av[4][4], bv[4][4];
+    f32x4 av[4][4], bv[4][4];
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
       const int ch = 8 * G + oc;
       const int p1 = __shfl(a1, ch), p2 = __shfl(b2, ch);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)ch * 128 + 4 * u);
         av[G][u] = *reinterpret_cast<const f32x4*>(xc + (size_t)p1 * 128 + 16 * part + 4 * u);
         bv[G][u] = *reinterpret_cast<const f32x4*>(xc + (size_t)p2 * 128 + 16 * part + 4 * u);
       }
