@@ -146,11 +146,14 @@ __device__ __forceinline__ AdamHp adam_hp(const int32_t* step_count, int step_of
   h.eps = eps;
   return h;
 }
+// Every rounding is explicit (no contraction left to the compiler), so the Adam
+// fused into k_feat_bwd_finish and the standalone k_adam of the data-parallel
+// path give bitwise the same parameters whatever code surrounds them.
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamHp& h) {
-  m = m + h.w1 * (g - m);
-  v = v * h.b2 + h.w2 * (g * g);
-  const float denom = sqrtf(v) / h.bc2s + h.eps;
-  p = p - h.step * (m / denom);
+  m = __fmaf_rn(h.w1, __fsub_rn(g, m), m);
+  v = __fmaf_rn(v, h.b2, __fmul_rn(h.w2, __fmul_rn(g, g)));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), h.bc2s), h.eps);
+  p = __fmaf_rn(-h.step, __fdiv_rn(m, denom), p);
 }
 
 // Adam riding along the launch that finishes the gradients (k_feat_bwd_finish):

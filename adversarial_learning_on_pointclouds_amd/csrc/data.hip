@@ -27,7 +27,10 @@ k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_
   if (t >= (int64_t)B * npts) return;
   const int b = (int)(t / npts), p = (int)(t % npts);
   const int64_t c = idx[b];
-  if (c < 0 || c >= n_src) return;  // validated on the host; never reads out of range
+  // DeviceCloudLoader.gather() rejects out-of-range indices on the host before
+  // the launch (its own epoch order is in range by construction); this guard
+  // only keeps a bad index from reading outside the split
+  if (c < 0 || c >= n_src) return;
   const float* s = src + ((size_t)c * src_npts + p) * 3;
   float* o = out + (size_t)t * 3;
   const float x0 = s[0], x1 = s[1], x2 = s[2];

@@ -201,9 +201,17 @@ class DeviceCloudLoader:
     ShapeNet sets - all on the device, each batch one pcadv_gather_clouds
     launch (jitter from device Philox draws when the dataset augments).
     ``noise``: optional callable(b, npts) -> f64 standard normals (host numpy),
-    for parity runs against the reference's jitter."""
+    for parity runs against the reference's jitter.
 
-    def __init__(self, dataset, batch_size, shuffle=True, seed=0, device="cuda", drop_last=False,
+    ``seed`` keys the shuffle and the jitter draws; None (the default) takes
+    one from torch's default generator, so two loaders built alike draw
+    independent jitter as the reference's np.random does.  The dataset kind is
+    mixed into the Philox key too: a GT and a no-GT loader given the same
+    seed still draw different fields."""
+
+    _KIND_TAG = {"modelnet_gt": 1, "modelnet_nogt": 2, "shapenet_gt": 3, "shapenet_nogt": 4}
+
+    def __init__(self, dataset, batch_size, shuffle=True, seed=None, device="cuda", drop_last=False,
                  sigma=0.01, clip=0.05):
         self.lib = _lib.load()
         self.ds, self.B, self.shuffle, self.drop_last = dataset, int(batch_size), shuffle, drop_last
@@ -228,7 +236,9 @@ class DeviceCloudLoader:
             raise TypeError(f"unsupported dataset {type(dataset).__name__}")
         self.sigma = float(sigma) if getattr(dataset, "data_augmentation", False) else 0.0
         self.clip = float(clip)
-        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.seed = (int(seed) ^ (self._KIND_TAG[self.kind] << 58)) & 0xFFFFFFFFFFFFFFFF
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed))
         self.step = torch.zeros(1, device=self.device, dtype=torch.int32)
@@ -237,11 +247,18 @@ class DeviceCloudLoader:
     def __len__(self):
         return self.n // self.B if self.drop_last else (self.n + self.B - 1) // self.B
 
-    def gather(self, idx, noise=None, out=None):
-        """One batch for the device index tensor ``idx`` (int64)."""
+    def gather(self, idx, noise=None, out=None, _checked=False):
+        """One batch for the device index tensor ``idx`` (int64, each in
+        [0, len(dataset)): checked here, one host read; the epoch order of
+        __iter__ is in range by construction and skips it)."""
         b = int(idx.numel())
         if idx.dtype != torch.int64 or idx.device != self.device or not idx.is_contiguous():
             raise ValueError("idx: contiguous int64 on the loader's device")
+        if b and not _checked:
+            lo, hi = torch.aminmax(idx)
+            if int(lo) < 0 or int(hi) >= self.n:
+                raise IndexError(f"gather: index out of range [0, {self.n}) "
+                                 f"(min {int(lo)}, max {int(hi)})")
         pts = out if out is not None else torch.empty(b, self.npts, 3, device=self.device)
         lw = 0 if self.labels is None else int(self.labels.shape[1])
         lab = None if self.labels is None else torch.empty(b, lw, device=self.device, dtype=torch.int64)
@@ -276,4 +293,4 @@ class DeviceCloudLoader:
             order = torch.arange(self.n, device=self.device)
         for k in range(len(self)):
             idx = order[k * self.B:(k + 1) * self.B].contiguous()
-            yield self.gather(idx)
+            yield self.gather(idx, _checked=True)

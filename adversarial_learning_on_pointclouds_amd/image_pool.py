@@ -1,5 +1,13 @@
-"""History pool for discriminator inputs (utils/image_pool.py:10-55).
-pool_size=0 (train_classification.py:52 default) is the identity."""
+"""Discriminator-input history (the interface of utils/image_pool.py:10-55).
+
+The hot path runs with pool_size=0 (train_classification.py:52 default), where
+query() hands its input back unchanged.  With pool_size > 0 the history is one
+preallocated device tensor: while it is filling, each queried sample is stored
+and returned; once full, each sample is, with probability 1/2, swapped with a
+uniformly chosen stored one (the stored one is returned), or else returned as
+is.  The draws use Python's `random` module in the same order as the
+reference (one random() per sample, one randrange(pool_size) per swap), so a
+seeded run makes the same choices."""
 from __future__ import annotations
 
 import random
@@ -9,27 +17,27 @@ import torch
 
 class ImagePool:
     def __init__(self, pool_size):
-        self.pool_size = pool_size
-        if self.pool_size > 0:
-            self.num_imgs = 0
-            self.images = []
+        self.pool_size = int(pool_size)
+        self._bank = None  # (pool_size, *sample_shape), allocated on first use
+        self._filled = 0
+
+    @property
+    def num_imgs(self):
+        return self._filled
 
     def query(self, images):
         if self.pool_size == 0:
             return images
-        return_images = []
-        for image in images:
-            image = torch.unsqueeze(image.data, 0)
-            if self.num_imgs < self.pool_size:
-                self.num_imgs = self.num_imgs + 1
-                self.images.append(image)
-                return_images.append(image)
-            else:
-                if random.uniform(0, 1) > 0.5:
-                    random_id = random.randint(0, self.pool_size - 1)
-                    tmp = self.images[random_id].clone()
-                    self.images[random_id] = image
-                    return_images.append(tmp)
-                else:
-                    return_images.append(image)
-        return torch.cat(return_images, 0).requires_grad_(True)
+        batch = images.detach()
+        if self._bank is None:
+            self._bank = batch.new_empty((self.pool_size,) + tuple(batch.shape[1:]))
+        out = batch.clone()
+        for i in range(batch.shape[0]):
+            if self._filled < self.pool_size:
+                self._bank[self._filled].copy_(batch[i])
+                self._filled += 1
+            elif random.random() > 0.5:
+                slot = random.randrange(self.pool_size)
+                out[i].copy_(self._bank[slot])
+                self._bank[slot].copy_(batch[i])
+        return out.requires_grad_(True)

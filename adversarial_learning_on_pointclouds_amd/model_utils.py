@@ -19,32 +19,38 @@ def init_net(net, device, init_type, init_gain=1.0):
     return net
 
 
-def init_weights(net, init_type, init_gain=1.0, verbose=True):
-    """utils/model_utils.py:27-58: Conv/Linear weights by init_type, biases 0."""
-    def init_func(m):
-        classname = m.__class__.__name__
-        if hasattr(m, "weight") and (classname.find("Conv") != -1 or classname.find("Linear") != -1):
-            if init_type == "normal":
-                init.normal_(m.weight.data, 0.0, init_gain)
-            elif init_type == "xavier":
-                init.xavier_normal_(m.weight.data, gain=init_gain)
-            elif init_type == "kaiming":
-                init.kaiming_normal_(m.weight.data, a=0, mode="fan_in")
-            elif init_type == "orthogonal":
-                init.orthogonal_(m.weight.data, gain=init_gain)
-            else:
-                raise NotImplementedError("initialization method [%s] is not implemented" % init_type)
-            if hasattr(m, "bias") and m.bias is not None:
-                init.constant_(m.bias.data, 0.0)
-        elif classname.find("BatchNorm2d") != -1:
-            init.normal_(m.weight.data, 1.0, init_gain)
-            init.constant_(m.bias.data, 0.0)
+# weight initialisers by init_type (utils/model_utils.py:27-58); biases go to 0
+_WEIGHT_INIT = {
+    "normal": lambda w, gain: init.normal_(w, 0.0, gain),
+    "xavier": lambda w, gain: init.xavier_normal_(w, gain=gain),
+    "kaiming": lambda w, gain: init.kaiming_normal_(w, a=0, mode="fan_in"),
+    "orthogonal": lambda w, gain: init.orthogonal_(w, gain=gain),
+}
 
+
+def init_weights(net, init_type, init_gain=1.0, verbose=True):
+    """Initialise every Conv*/Linear weight of `net` by `init_type` and zero its
+    bias; BatchNorm2d weights ~ N(1, init_gain), biases 0 (interface and
+    distributions of utils/model_utils.py:27-58).  Leaf modules are visited in
+    registration order, the order Module.apply reaches them, so a seeded torch
+    RNG gives the reference's weights."""
     if verbose:
         print("initialize network with %s" % init_type)
     if init_type is None:
         return net
-    net.apply(init_func)
+    fill = _WEIGHT_INIT.get(init_type)
+    for mod in net.modules():
+        kind = type(mod).__name__
+        if ("Conv" in kind or "Linear" in kind) and hasattr(mod, "weight"):
+            if fill is None:
+                raise NotImplementedError("initialization method [%s] is not implemented" % init_type)
+            fill(mod.weight.data, init_gain)
+            if getattr(mod, "bias", None) is not None:
+                mod.bias.data.zero_()
+        elif "BatchNorm2d" in kind:
+            init.normal_(mod.weight.data, 1.0, init_gain)
+            mod.bias.data.zero_()
+    return net
 
 
 def load_models(mode, device, args):

@@ -446,19 +446,27 @@ class SegTrainStep:
         self.grad = torch.zeros(n, device=dev)
         self.m = torch.zeros(n, device=dev)
         self.v = torch.zeros(n, device=dev)
-        self.step_count = torch.zeros(1, device=dev, dtype=torch.int32)
         self.grad_views = []
+        t0 = 0
         for (name, p), o in zip(named, offs):
             k = p.numel()
             self.param[o:o + k].copy_(p.detach().reshape(-1))
+            st = optimizer.state.get(p) if optimizer is not None else None
+            if st and "exp_avg" in st:  # Adam state the optimizer already holds carries over
+                self.m[o:o + k].copy_(st["exp_avg"].detach().reshape(-1))
+                self.v[o:o + k].copy_(st["exp_avg_sq"].detach().reshape(-1))
+                t0 = max(t0, int(float(st.get("step", 0))))
             p.data = self.param[o:o + k].view_as(p)
             gv = self.grad[o:o + k].view_as(p)
             p.grad = gv
             self.grad_views.append(gv)
-            if optimizer is not None:
-                optimizer.state[p] = {"step": torch.zeros((), dtype=torch.float32),
+        if optimizer is not None:
+            for (name, p), o in zip(named, offs):
+                k = p.numel()
+                optimizer.state[p] = {"step": torch.tensor(float(t0)),
                                       "exp_avg": self.m[o:o + k].view_as(p),
                                       "exp_avg_sq": self.v[o:o + k].view_as(p)}
+        self.step_count = torch.full((1,), t0, device=dev, dtype=torch.int32)
         self.params = [p for _, p in named]
         # bf16 hi / lo planes of all parameters: one split per step feeds every
         # forward GEMM's weight operand
@@ -480,6 +488,7 @@ class SegTrainStep:
             _engine().split(self.param, self.wph, self.wpl)
             wpl = self.wplanes
         fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params, wplanes=wpl)
+        self.fw = fw  # the last step's activations (logits, x_global, argmax, ...)
         M, ncls = B * N, fw["dims"][2]
         d = torch.empty(M, ncls, device=self.device)
         ws = _ws(self.lib.pcadv_row_ce_workspace_bytes(M), self.device)

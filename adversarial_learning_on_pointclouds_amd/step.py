@@ -47,6 +47,38 @@ def _align(nbytes):
     return (nbytes + 255) // 256 * 256
 
 
+def _adopt_adam_state(optimizer, module, m_flat, v_flat, layout):
+    """Seed flat Adam moments from state an optimizer already holds (a
+    load_state_dict before the first iteration, or the views of a previous
+    step object the trainer rebuilt): exp_avg / exp_avg_sq are copied in and
+    the largest 'step' is returned (0 when there is none)."""
+    if optimizer is None:
+        return 0
+    steps = 0
+    named = dict(module.named_parameters())
+    for name, off in layout.items():
+        st = optimizer.state.get(named[name])
+        if not st or "exp_avg" not in st:
+            continue
+        n = named[name].numel()
+        m_flat[off:off + n].copy_(st["exp_avg"].detach().reshape(-1))
+        v_flat[off:off + n].copy_(st["exp_avg_sq"].detach().reshape(-1))
+        steps = max(steps, int(float(st.get("step", 0))))
+    return steps
+
+
+def _bind_adam_state(optimizer, module, m_flat, v_flat, grad_flat, layout, step_t):
+    """p.grad and the optimizer's exp_avg / exp_avg_sq become views of the flat
+    buffers; 'step' holds the completed-step count."""
+    mv, vv, gv = _views(m_flat, module, layout), _views(v_flat, module, layout), \
+        _views(grad_flat, module, layout)
+    for name, p in module.named_parameters():
+        p.grad = gv[name]
+        if optimizer is not None:
+            optimizer.state[p] = {"step": torch.tensor(float(step_t)),
+                                  "exp_avg": mv[name], "exp_avg_sq": vv[name]}
+
+
 class AdvTrainStep:
     """run_training's iteration body for PointNetCls(k=40) + DeepConvDiscNet(40, 1).
 
@@ -91,16 +123,15 @@ class AdvTrainStep:
         self.g_v = torch.zeros_like(self.g_param)
         self.d_m = torch.zeros_like(self.d_param)
         self.d_v = torch.zeros_like(self.d_param)
-        self.step_count = torch.zeros(1, device=dev, dtype=torch.int32)
-        for opt, mod, layout, m, v, gr in (
-                (optimizer, model, G_LAYOUT, self.g_m, self.g_v, self.g_grad),
-                (optimizer_D, model_D, D_LAYOUT, self.d_m, self.d_v, self.d_grad)):
-            mv, vv, gv = _views(m, mod, layout), _views(v, mod, layout), _views(gr, mod, layout)
-            for name, p in mod.named_parameters():
-                p.grad = gv[name]
-                if opt is not None:
-                    opt.state[p] = {"step": torch.zeros((), dtype=torch.float32),
-                                    "exp_avg": mv[name], "exp_avg_sq": vv[name]}
+        # Adam state the optimizers already hold carries over (one step count
+        # serves both networks: run_training steps them together)
+        t0 = max(_adopt_adam_state(optimizer, model, self.g_m, self.g_v, G_LAYOUT),
+                 _adopt_adam_state(optimizer_D, model_D, self.d_m, self.d_v, D_LAYOUT))
+        self.step_count = torch.full((1,), t0, device=dev, dtype=torch.int32)
+        self._bind = ((optimizer, model, self.g_m, self.g_v, self.g_grad, G_LAYOUT),
+                      (optimizer_D, model_D, self.d_m, self.d_v, self.d_grad, D_LAYOUT))
+        for args_ in self._bind:
+            _bind_adam_state(*args_, t0)
         self.optimizers = (optimizer, optimizer_D)
         self.losses = torch.zeros(6, device=dev)
         self.logits = torch.zeros(2 * self.B, 40, device=dev)
@@ -255,6 +286,20 @@ class AdvTrainStep:
                 for st in opt.state.values():
                     st["step"] = torch.tensor(t)
 
+    def after_torch_step(self):
+        """After an iteration the trainer ran through autograd and the torch
+        optimizers (unequal GT / no-GT batches): the device step counter
+        advances with torch's, and each p.grad (a fresh tensor after
+        zero_grad + backward) is copied back into the flat gradient buffer
+        and rebound as its view."""
+        self.step_count += 1
+        for opt, mod, m, v, gr, layout in self._bind:
+            gv = _views(gr, mod, layout)
+            for name, p in mod.named_parameters():
+                if p.grad is not None and p.grad.data_ptr() != gv[name].data_ptr():
+                    gv[name].copy_(p.grad)
+                p.grad = gv[name]
+
 
 class ClsTrainStep:
     """run_training_pointnet_cls's iteration (utils/trainer.py:222-268) for
@@ -286,14 +331,10 @@ class ClsTrainStep:
         self.g_grad = torch.zeros(G_NUMEL, device=dev)
         self.g_m = torch.zeros_like(self.g_param)
         self.g_v = torch.zeros_like(self.g_param)
-        self.step_count = torch.zeros(1, device=dev, dtype=torch.int32)
-        mv, vv, gv = (_views(self.g_m, model, G_LAYOUT), _views(self.g_v, model, G_LAYOUT),
-                      _views(self.g_grad, model, G_LAYOUT))
-        for name, p in model.named_parameters():
-            p.grad = gv[name]
-            if optimizer is not None:
-                optimizer.state[p] = {"step": torch.zeros((), dtype=torch.float32),
-                                      "exp_avg": mv[name], "exp_avg_sq": vv[name]}
+        t0 = _adopt_adam_state(optimizer, model, self.g_m, self.g_v, G_LAYOUT)
+        self.step_count = torch.full((1,), t0, device=dev, dtype=torch.int32)
+        _bind_adam_state(optimizer, model, self.g_m, self.g_v, self.g_grad, G_LAYOUT, t0)
+        self._bind = ((optimizer, model, self.g_m, self.g_v, self.g_grad, G_LAYOUT),)
         self.optimizer = optimizer
         self.losses = torch.zeros(1, device=dev)
         self.logits = torch.zeros(self.B, 40, device=dev)
@@ -360,3 +401,5 @@ class ClsTrainStep:
             t = float(self.step_count.item())
             for st in self.optimizer.state.values():
                 st["step"] = torch.tensor(t)
+
+    after_torch_step = AdvTrainStep.after_torch_step

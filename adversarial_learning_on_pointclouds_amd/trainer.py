@@ -48,6 +48,11 @@ def run_testing(dataloader, model, criterion, logger, test_iter, writer, args):
     return total_accuracy / denom, total_loss / denom
 
 
+# the fused native steps take at most this many clouds per batch (capi.hip:
+# pcadv_adv_step / pcadv_cls_step); larger batches run the autograd path
+MAX_FUSED_B = 256
+
+
 def _next(loader, it):
     try:
         _, batch = next(it)
@@ -119,7 +124,7 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
         pts_nogt = pts_nogt.float().to(args.device).contiguous()
         semi_on = semi_loss is not None and args.semi_start > 0 and i_iter > args.semi_start
 
-        if fused and pts.shape == pts_nogt.shape:
+        if fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B:
             if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
                 step = AdvTrainStep(model, model_D, pts.shape[0], pts.shape[1],
                                     optimizer=optimizer, optimizer_D=optimizer_D,
@@ -135,6 +140,12 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                 loss_D_value = vals[2] + vals[3]
                 loss_semi_value = vals[4] if semi_on else 0.0
         else:
+            # unequal GT / no-GT batches (a loader's ragged last batch): the
+            # reference's body through autograd over the same kernels; the torch
+            # optimizers continue from the fused step's Adam state (moments are
+            # shared views, the step count is synced in and out)
+            if step is not None:
+                step.sync_optimizer_state()
             optimizer.zero_grad()
             optimizer_D.zero_grad()
             for param in model_D.parameters():
@@ -167,6 +178,8 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             loss_D2.backward()
             optimizer.step()
             optimizer_D.step()
+            if step is not None:
+                step.after_torch_step()
             vals = True
             loss_cls_value, loss_adv_value = l.item(), loss_adv.item()
             loss_D_value = loss_D1.item() + loss_D2.item()
@@ -256,13 +269,15 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
         pts, cls = batch
         pts, cls = pts.float().to(args.device).contiguous(), cls.long().to(args.device).contiguous()
         l_regu = None
-        if fused:
+        if fused and pts.shape[0] <= MAX_FUSED_B:
             if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
                 step = ClsTrainStep(model, pts.shape[0], pts.shape[1], optimizer=optimizer,
                                     lambda_cls=args.lambda_cls,
                                     seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)
             l_value = float(step(pts, cls)[0].item())
         else:
+            if step is not None:
+                step.sync_optimizer_state()
             optimizer.zero_grad()
             pred, global_gt, high_feat = model(pts)
             l = cls_loss(pred, cls)
@@ -272,6 +287,8 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
                 loss = loss + args.lambda_regu * l_regu
             loss.backward()
             optimizer.step()
+            if step is not None:
+                step.after_torch_step()
             l_value = l.item()
         train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
             i_iter, args.total_iterations, l_value, 0.0 if l_regu is None else l_regu.item()))

@@ -9,9 +9,11 @@ B=32 labelled + B=32 unlabelled ModelNet40-shaped clouds of N=1024 points per
 GPU per step, fp32, Adam on both networks.  Synthetic seeded inputs
 (U(-1,1) points, labels in [0,40)), resident in HBM before timing starts.
 metric value = whole-job clouds/s counting 2B clouds per step per rank.
-For --gpus N > 1 run under torch.distributed.run: one process per GPU, each
-rank takes its own shard of the global batch and gradients are averaged with
-an RCCL all-reduce (multi-GPU).
+--gpus N > 1: one process per GPU, each rank takes its own shard of the global
+batch and gradients are averaged with an RCCL all-reduce (see DESIGN.md,
+multi-GPU).  Under torch.distributed.run the ranks come from the environment
+(WORLD_SIZE must equal --gpus); run directly, bench.py spawns the N ranks
+itself before anything touches the GPU.
 """
 from __future__ import annotations
 
@@ -47,7 +49,58 @@ def parse():
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
                          "supervised PointNetCls step of configs[1]")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher self-test: start the --gpus ranks, form the process group, "
+                         "print the JSON world/backend line; no GPU work")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(local_rank, world, port, argv):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = argv
+    main()
+
+
+def spawn_ranks(world):
+    """bench.py --gpus N run without a launcher: start N rank processes (fresh
+    interpreters, spawn start method) with the torch.distributed.run
+    environment.  Called before this process makes any GPU call."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rank_entry, args=(world, _free_port(), list(sys.argv)), nprocs=world, join=True)
+
+
+def _backend():
+    # RCCL; PCADV_BENCH_BACKEND=gloo rehearses the multi-rank path with several
+    # ranks on one GPU (RCCL needs a device per rank) - never for measurements
+    return os.environ.get("PCADV_BENCH_BACKEND", "nccl")
+
+
+def launch_check(args, world, rank):
+    """The launcher's self-test: the process group forms with --gpus ranks."""
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+        t = torch.ones(1)
+        tdist.all_reduce(t)
+        assert int(t.item()) == world
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "world_size": world,
+                          "check_backend": "gloo" if world > 1 else None,
+                          "bench_backend": _backend() if world > 1 else None,
+                          "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+                          else ("bench.py spawn" if world > 1 else "single process")}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
 
 
 def make_models(dev, seed=0):
@@ -282,7 +335,8 @@ def bench_seg(args):
     torch.cuda.synchronize()
     kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
     kflops = 2.0 * Bs * Ns * 512 * 2048
-    kpeak = 2500.0 / 3.0  # three bf16 MFMA products per f32 product (hi/lo splits)
+    kpeak = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
+    kissued = 3 * kflops  # three bf16 MFMA products per f32 product (hi/lo splits)
     # HBM traffic of the same launch pair from the committed PMC passes of
     # `bench.py --config seg` (tools/gpu_round.sh, tools/pmc_traffic.py)
     traffic, traffic_src = None, None
@@ -298,7 +352,9 @@ def bench_seg(args):
         "metric": "point-clouds/sec (seg train step), B=16 N=2048 ShapeNet-part, 1 GPU",
         "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16x3 (fp32-emulated: forward and data-gradient GEMMs as three bf16 hi/lo "
+                 "MFMA products, f32 accumulate; weight gradients six products)",
         "data": "synthetic (seeded U(-1,1) clouds, one-hot classes, part labels in [0,50))",
         "config": {"workload": "PointNetSeg(50) + CrossEntropyLoss + Adam, B=16, N=2048 "
                                "(BASELINE configs[3])", "global_batch": Bs, "points": Ns,
@@ -306,14 +362,17 @@ def bench_seg(args):
         "roofline": {"bound": "mfma",
                      "kernel": kname + " (conv6 512->2048 screened top-2 per 128-point tile) "
                                "+ k_max_combine (exact f32 re-evaluation)",
-                     "achieved": round(kflops / kern_s / 1e12, 2), "peak": round(kpeak, 1),
-                     "unit": "TFLOP/s", "frac": round(kflops / kern_s / 1e12 / kpeak, 4),
+                     "achieved": round(kissued / kern_s / 1e12, 2), "peak": kpeak,
+                     "unit": "TFLOP/s", "frac": round(kissued / kern_s / 1e12 / kpeak, 4),
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
                      "traffic_source": traffic_src, "avg_launch_us": round(kern_s * 1e6, 2),
                      "algorithmic_flops_per_launch": kflops,
                      "algorithmic_bytes_per_launch": Bs * Ns * 512 * 4 + 2048 * 512 * 4 + Bs * 2048 * 8,
-                     "peak_basis": "bf16 2500 TF dense / 3 split products"},
+                     "issued_bf16_flops_per_launch": kissued,
+                     "fp32_equivalent_tflops": round(kflops / kern_s / 1e12, 2),
+                     "peak_basis": "dense bf16 MFMA 2500 TF; achieved = issued bf16 MFMA FLOPs "
+                                   "(3 split products per f32 product) / launch time"},
         "step_flops": {"gflop_per_step": round(gflop, 2),
                        "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
@@ -327,28 +386,38 @@ def main():
     global N
     args = parse()
     N = args.points
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.config != "adv":
+            raise SystemExit(f"--config {args.config} is a single-GPU workload; --gpus applies to adv")
+        return spawn_ranks(args.gpus)  # no GPU call has been made in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks: "
+                         "refusing to report a different n_gpus")
+    if args.launch_check:
+        return launch_check(args, world, rank)
     if args.config == "seg":
         return bench_seg(args)
     if args.config == "cls":
         return bench_cls(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("PCADV_BENCH_BACKEND", "nccl") != "nccl":  # rehearsal: ranks may share a GPU
+    if _backend() != "nccl":  # rehearsal: ranks may share a GPU
         local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        # RCCL; PCADV_BENCH_BACKEND=gloo rehearses the multi-rank path with several
-        # ranks on one GPU (RCCL needs a device per rank) - never for measurements
-        backend = os.environ.get("PCADV_BENCH_BACKEND", "nccl")
+        backend = _backend()
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=dev)
         else:
             tdist.init_process_group(backend)
         dist = tdist
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     from adversarial_learning_on_pointclouds_amd import ops
     from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
@@ -433,17 +502,19 @@ def main():
     # algorithmic f32 FLOPs of conv1..conv4 forward per launch (64 clouds x N points):
     # 2 * N * (3*64 + 64*64 + 64*128 + 128*1024) per cloud
     flops = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64 + 64 * 128 + 128 * 1024)
-    achieved = flops / kern_s / 1e12
-    # Ceiling of this pair on MI355X, by the pipe each layer runs on: conv1 (VALU)
-    # and conv2 (f32 MFMA) at the dense f32 peak (157.3 TF); conv3 as six bf16
-    # products per f32 product at the dense bf16 peak / 6; conv4 as three at the
-    # bf16 peak / 3 (2500 TF dense).  The composite peak is the total FLOPs over
-    # that minimum time (MI355X_MICROARCH.md peaks).
+    f32_equiv = flops / kern_s / 1e12
+    # The pair computes f32-level results on the matrix cores: conv1 (VALU) and
+    # conv2 (f32 MFMA) in f32, conv3 as six bf16 MFMA products of three-way
+    # splits, conv4 as three (hi/lo) plus the exact f32 re-evaluation of each
+    # winner.  Roofline against the named dense bf16 MFMA peak (MI355X_MICROARCH.md:
+    # 2.5 PF): the MFMA work issued, in bf16-MFMA-equivalent FLOPs (conv1-2's f32
+    # work weighted by the f32:bf16 peak ratio 2500/157.3), over the launch time.
+    BF16_PEAK, F32_PEAK = 2500.0, 157.3
     f12 = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64)
     f3 = 2.0 * (2 * B) * N * (64 * 128)
     f4 = flops - f12 - f3
-    t_min = f12 / 157.3e12 + f3 / (2500e12 / 6.0) + f4 / (2500e12 / 3.0)
-    peak = flops / t_min / 1e12
+    issued = f12 * (BF16_PEAK / F32_PEAK) + 6 * f3 + 3 * f4
+    achieved = issued / kern_s / 1e12
     traffic, traffic_src = None, None
     prof = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                      "profiles", "r*_pmc_traffic.json"))
@@ -469,24 +540,35 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32 (f32-level: conv3/conv4 as bf16 split-product MFMAs, f32 accumulate, "
+                 "each max winner re-evaluated in exact f32)",
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
         "config": {"workload": "adversarial cls step: PointNetCls(k=40)+DeepConvDiscNet(40,1), "
                                f"B=32 GT + 32 noGT clouds/GPU, N={N}, Adam x2",
                    "global_batch": 2 * B * world, "points": N,
                    "parallelism": f"dp{world}", "hip_graph": use_graph},
+        "world_size": world,
+        "backend": ((_backend() if _backend() != "nccl" else "nccl (RCCL)") if world > 1 else None),
         "roofline": {"bound": "mfma",
                      "kernel": "k_point_mlp + k_conv4_max (PointNetfeat conv1..4 + max, 2 launches)",
-                     "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "achieved": round(achieved, 2), "peak": BF16_PEAK, "unit": "TFLOP/s",
+                     "frac": round(achieved / BF16_PEAK, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": 2 * B * N * (3 + 128) * 4 + 2 * B * 1024 * 8,
                      "avg_launch_us": round(kern_s * 1e6, 2),
                      "algorithmic_flops_per_launch": flops,
-                     "peak_basis": "f32 157.3 TF for conv1-2, bf16 2500/6 TF for conv3 (6 split products), bf16 2500/3 TF for conv4 (3 split products)"},
-        "step_mfma": {"gflop_per_step": step_gflop, "achieved_tflops": round(step_tf, 2),
-                      "frac_of_f32_peak": round(step_tf / 157.3, 4)},
+                     "issued_bf16_equiv_flops_per_launch": issued,
+                     "peak_basis": "dense bf16 MFMA 2500 TF (MI355X_MICROARCH.md); achieved = issued "
+                                   "MFMA work in bf16-equivalent FLOPs: conv3 x6 and conv4 x3 split "
+                                   "products, conv1-2 f32 FLOPs x 2500/157.3",
+                     "fp32_equivalent": {
+                         "achieved_tflops": round(f32_equiv, 2), "f32_mfma_peak_tflops": F32_PEAK,
+                         "ratio_to_f32_peak": round(f32_equiv / F32_PEAK, 4),
+                         "note": "algorithmic f32 FLOPs / time; the f32 products are emulated on the "
+                                 "bf16 MFMA pipe (split operands, f32 accumulate, winners re-evaluated "
+                                 "in exact f32), so this ratio is not a roofline fraction and can exceed 1"}},
+        "step_flops": {"gflop_per_step": step_gflop, "achieved_tflops": round(step_tf, 2)},
         "losses_last_step": [round(v, 5) for v in losses],
         "finite": finite,
     }

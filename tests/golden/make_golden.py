@@ -275,6 +275,52 @@ def main(ref_root, only=None):
             summarize("paramD." + name, p.detach().numpy(), out)
         np.savez_compressed(os.path.join(HERE, "g9_semi_step3.npz"), **out)
 
+    # ---------------- G10: host helpers (ImagePool history, init_weights) ----
+    # utils/image_pool.py:10-55 with pool_size=3 on seeded Python `random`;
+    # utils/model_utils.py:27-58 xavier init of DeepConvDiscNet on a seeded torch RNG
+    def g10():
+        import random
+        from utils.model_utils import init_weights as ref_init_weights
+        pool = ImagePool(3)
+        random.seed(5)
+        xs = np.random.default_rng(101).standard_normal((6, 2, 40)).astype(np.float32)
+        outs = [pool.query(torch.from_numpy(x)).detach().numpy() for x in xs]
+        out = dict(pool_size=3, random_seed=5, data_seed=101, queries=xs, pool_out=np.stack(outs))
+        torch.manual_seed(3)
+        md = DeepConvDiscNet(40, 1)
+        ref_init_weights(md, "xavier", init_gain=1.0)
+        out["torch_seed"] = 3
+        for name, p in md.named_parameters():
+            summarize("xavier." + name, p.detach().numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g10_host_helpers.npz"), **out)
+
+    # ---------------- G11: configs[1] at full size (B=32, N=1024) ----------
+    # run_training_pointnet_cls's iteration (utils/trainer.py:254-268): forward
+    # with an injected dropout mask, CrossEntropyLoss, backward
+    def g11():
+        G11 = onp.make_params(onp.cls_spec(40), seed=3)
+        rng = np.random.default_rng(2001)
+        B = 32
+        pts11 = rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32)
+        lab11 = rng.integers(0, 40, B)
+        mask11 = make_mask(rng, B)
+        model = load(PointNetCls(k=40, feature_transform=False), G11).train()
+        model.dropout = MaskDropout([mask11.copy()])
+        logits, glob, _ = model(torch.from_numpy(pts11))
+        loss = nn.CrossEntropyLoss()(logits, torch.from_numpy(lab11).long())
+        loss.backward()
+        out = dict(g_seed=3, data_seed=2001, B=B, N=N_PTS, loss=np.float64(loss.item()),
+                   logits=logits.detach().numpy(), gmax=glob.detach().numpy()[:, :, 0])
+        for name, p in model.named_parameters():
+            summarize("grad." + name, p.grad.numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g11_cls_b32.npz"), **out)
+
+    if only == "g10":
+        g10()
+        return
+    if only == "full":
+        g10()
+        g11()
     if only == "g9":
         g9()
         return
@@ -285,44 +331,44 @@ def main(ref_root, only=None):
         g8()
         return
 
-    # ---------------- G1: cls forward (eval) ----------------
-    G = onp.make_params(onp.cls_spec(40), seed=1)
-    model = load(PointNetCls(k=40, feature_transform=False), G).eval()
-    pts = make_pts(11, B_SMALL, N_PTS)
-    am_holder = {}
+    if only != "full":
+        # ---------------- G1: cls forward (eval) ----------------
+        G = onp.make_params(onp.cls_spec(40), seed=1)
+        model = load(PointNetCls(k=40, feature_transform=False), G).eval()
+        pts = make_pts(11, B_SMALL, N_PTS)
+        am_holder = {}
 
-    def hook(mod, inp, out):
-        am_holder["am"] = torch.max(out, 2)[1].detach().numpy().astype(np.int32)
+        def hook(mod, inp, out):
+            am_holder["am"] = torch.max(out, 2)[1].detach().numpy().astype(np.int32)
 
-    h = model.feat.conv4.register_forward_hook(hook)
-    with torch.no_grad():
-        logits, glob, tf = model(torch.from_numpy(pts))
-    h.remove()
-    np.savez_compressed(os.path.join(HERE, "g1_cls_fwd.npz"), g_seed=1, pts_seed=11,
-                        B=B_SMALL, N=N_PTS, logits=logits.numpy(),
-                        gmax=glob.numpy()[:, :, 0], argmax=am_holder["am"])
+        h = model.feat.conv4.register_forward_hook(hook)
+        with torch.no_grad():
+            logits, glob, tf = model(torch.from_numpy(pts))
+        h.remove()
+        np.savez_compressed(os.path.join(HERE, "g1_cls_fwd.npz"), g_seed=1, pts_seed=11,
+                            B=B_SMALL, N=N_PTS, logits=logits.numpy(),
+                            gmax=glob.numpy()[:, :, 0], argmax=am_holder["am"])
 
-    # ---------------- G2: cls forward+backward (train, injected dropout) ----
-    rng = np.random.default_rng(21)
-    mask = make_mask(rng, B_SMALL)
-    labels = rng.integers(0, 40, B_SMALL)
-    model = load(PointNetCls(k=40, feature_transform=False), G).train()
-    model.dropout = MaskDropout([mask.copy()])
-    logits, glob, _ = model(torch.from_numpy(pts))
-    loss = nn.CrossEntropyLoss()(logits, torch.from_numpy(labels).long())
-    loss.backward()
-    out = dict(g_seed=1, pts_seed=11, mask=mask, labels=labels.astype(np.int64),
-               loss=np.float64(loss.item()), logits=logits.detach().numpy())
-    for name, p in model.named_parameters():
-        summarize("grad." + name, p.grad.numpy(), out)
-    np.savez_compressed(os.path.join(HERE, "g2_cls_bwd.npz"), **out)
+        # ---------------- G2: cls forward+backward (train, injected dropout) ----
+        rng = np.random.default_rng(21)
+        mask = make_mask(rng, B_SMALL)
+        labels = rng.integers(0, 40, B_SMALL)
+        model = load(PointNetCls(k=40, feature_transform=False), G).train()
+        model.dropout = MaskDropout([mask.copy()])
+        logits, glob, _ = model(torch.from_numpy(pts))
+        loss = nn.CrossEntropyLoss()(logits, torch.from_numpy(labels).long())
+        loss.backward()
+        out = dict(g_seed=1, pts_seed=11, mask=mask, labels=labels.astype(np.int64),
+                   loss=np.float64(loss.item()), logits=logits.detach().numpy())
+        for name, p in model.named_parameters():
+            summarize("grad." + name, p.grad.numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g2_cls_bwd.npz"), **out)
 
     # ---------------- G3: run_training (adversarial step) ----------------
-    def run_adv(iters, seed):
+    def run_adv(iters, seed, B=B_SMALL):
         Gp = onp.make_params(onp.cls_spec(40), seed=1)
         Dp = onp.make_params(onp.disc_spec(40, 1), seed=2, init="xavier")
         rng = np.random.default_rng(seed)
-        B = B_SMALL
         batches_gt, batches_ng, masks, soft = [], [], [], []
         for _ in range(iters):
             batches_gt.append((rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32),
@@ -385,9 +431,14 @@ def main(ref_root, only=None):
         return dict(batches_gt=batches_gt, batches_ng=batches_ng, masks=masks, soft=soft,
                     rec=rec, model=model, model_D=model_D)
 
-    for iters, fname in ((1, "g3_adv_step1.npz"), (3, "g3_adv_step3.npz")):
-        r = run_adv(iters, seed=31)
-        out = dict(iters=iters, data_seed=31, g_seed=1, d_seed=2, B=B_SMALL, N=N_PTS)
+    # (iters, file, B): the B=32 one is BASELINE configs[2]'s full per-GPU batch
+    g3_cases = ((1, "g3_adv_step1.npz", B_SMALL), (3, "g3_adv_step3.npz", B_SMALL),
+                (1, "g3_adv_step1_b32.npz", 32))
+    if only == "full":
+        g3_cases = g3_cases[2:]
+    for iters, fname, Bc in g3_cases:
+        r = run_adv(iters, seed=31, B=Bc)
+        out = dict(iters=iters, data_seed=31, g_seed=1, d_seed=2, B=Bc, N=N_PTS)
         # cls criterion: index 0 is the train step, index 1 the iter-0 test pass
         cls_train = [r["rec"]["cls"][0]] + r["rec"]["cls"][2:]
         gan = np.array(r["rec"]["gan"]).reshape(iters, 3)
@@ -405,6 +456,8 @@ def main(ref_root, only=None):
         for name, p in r["model_D"].named_parameters():
             summarize("paramD." + name, p.detach().numpy(), out)
         np.savez_compressed(os.path.join(HERE, fname), **out)
+    if only == "full":
+        return
 
     # ---------------- G4: discriminator fwd/bwd ----------------
     Dp = onp.make_params(onp.disc_spec(40, 1), seed=2, init="xavier")
@@ -435,7 +488,6 @@ def main(ref_root, only=None):
 
     g7()
 
-
     # ---------------- G6: segmentation forward ----------------
     Sp = onp.make_params(onp.seg_spec(50), seed=6)
     ms = load(PointNetSeg(50), Sp).eval()
@@ -450,6 +502,8 @@ def main(ref_root, only=None):
     np.savez_compressed(os.path.join(HERE, "g6_seg_fwd.npz"), **out)
     g8()
     g9()
+    g10()
+    g11()
 
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
@@ -459,6 +513,7 @@ def main(ref_root, only=None):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("ref_root", nargs="?", default="/root/reference")
-    ap.add_argument("--only", default=None, help="g7, g8 or g9: regenerate only that fixture")
+    ap.add_argument("--only", default=None, help="g7, g8, g9 or g10: regenerate only that "
+                    "fixture; full: g10, g11 and the B=32 g3")
     a = ap.parse_args()
     main(a.ref_root, a.only)

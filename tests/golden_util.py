@@ -17,6 +17,35 @@ def rel_err(a, ref):
     return float(np.max(np.abs(a - ref)) / max(1.0, float(np.max(np.abs(ref)))))
 
 
+def grad_err(a, ref):
+    """Per-tensor relative errors of a gradient: (max|a-ref| / max|ref|,
+    ||a-ref||_2 / ||ref||_2).  Unlike rel_err there is no max(1, .) floor, so a
+    zeroed or doubled gradient fails however small its entries are (at B=32 the
+    conv gradients are ~1e-4, below rel_err's absolute 1e-3)."""
+    a = np.asarray(a, np.float64).reshape(-1)
+    r = np.asarray(ref, np.float64).reshape(-1)
+    assert a.shape == r.shape, (a.shape, r.shape)
+    d = a - r
+    e_max = float(np.max(np.abs(d))) / max(float(np.max(np.abs(r))), 1e-30)
+    e_l2 = float(np.linalg.norm(d)) / max(float(np.linalg.norm(r)), 1e-30)
+    return e_max, e_l2
+
+
+# Gradient tolerances (fp32 on both sides, different summation orders): the
+# largest elementwise deviation within 1e-3 of the tensor's largest entry, and
+# the relative L2 error within 1e-4.  A zeroed gradient has (1, 1), a doubled
+# one (1, 1): both fail by three orders of magnitude.
+GRAD_TOL_MAX = 1e-3
+GRAD_TOL_L2 = 1e-4
+
+
+def assert_grad_close(a, ref, name, tol_max=GRAD_TOL_MAX, tol_l2=GRAD_TOL_L2):
+    e_max, e_l2 = grad_err(a, ref)
+    assert e_max <= tol_max and e_l2 <= tol_l2, \
+        f"{name}: max-rel {e_max:.3e} (tol {tol_max:g}), L2-rel {e_l2:.3e} (tol {tol_l2:g})"
+    return e_max, e_l2
+
+
 def check_tensor(fx, prefix, arr, tol=1e-3):
     """Compare a tensor against a fixture entry (full, or summary + samples)."""
     arr = np.asarray(arr, np.float32)

@@ -94,3 +94,36 @@ def test_error_message_roundtrip():
     rc = lib.pcadv_linear_fwd(None, None, None, None, 0, 0, 0, 0, None, None, 0, 0.0, 0, None)
     assert rc == -1
     assert b"bad shape" in lib.pcadv_last_error()
+
+
+def test_image_pool_history_vs_reference_g10():
+    """ImagePool(3) over six queries on a seeded Python RNG returns what the
+    reference's utils/image_pool.py:26-55 returned (fixture g10)."""
+    import random
+    from golden_util import load
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    fx = load("g10_host_helpers.npz")
+    pool = ImagePool(int(fx["pool_size"]))
+    random.seed(int(fx["random_seed"]))
+    for q, want in zip(fx["queries"], fx["pool_out"]):
+        got = pool.query(torch.from_numpy(q))
+        assert got.requires_grad
+        assert np.array_equal(got.detach().numpy(), want)
+    assert pool.num_imgs == 3
+
+
+def test_init_weights_xavier_vs_reference_g10():
+    """init_weights(DeepConvDiscNet, 'xavier') on a seeded torch RNG gives the
+    reference's weights (utils/model_utils.py:27-58, fixture g10)."""
+    from golden_util import check_tensor
+    from golden_util import load
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd.model_utils import init_weights
+    fx = load("g10_host_helpers.npz")
+    torch.manual_seed(int(fx["torch_seed"]))
+    md = pc.DeepConvDiscNet(40, 1)
+    init_weights(md, "xavier", init_gain=1.0, verbose=False)
+    for name, p in md.named_parameters():
+        check_tensor(fx, "xavier." + name, p.detach().numpy(), tol=0.0)
+    with pytest.raises(NotImplementedError):
+        init_weights(pc.DeepConvDiscNet(40, 1), "bogus", verbose=False)

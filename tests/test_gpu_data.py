@@ -148,3 +148,86 @@ def test_semi_trainer_end_to_end_on_device_batches(tmp_path):
     assert len(lines) == 5
     for p in list(model.parameters()) + list(model_D.parameters()):
         assert torch.isfinite(p).all()
+
+
+def test_run_training_uneven_batches_keeps_adam_state():
+    """run_training (trainer.py:403-608) with drop_last=False loaders whose
+    GT / no-GT batch sizes differ on some iterations: those run the autograd
+    path with the torch optimizers, the rest the fused step.  The Adam state
+    (moments, bias-correction step count) must carry across both, so the
+    generator's parameter trajectory equals the oracle's five Adam steps.
+    lambda_adv = 0 and dropout p = 0 make G's trajectory independent of the
+    random soft D labels and masks."""
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from oracle import pointnet_np as onp
+    N = 256
+    G = onp.make_params(onp.cls_spec(40), seed=12)
+    Dp = onp.make_params(onp.disc_spec(40, 1), seed=13, init="xavier")
+    rng = np.random.default_rng(14)
+    mk = lambda b: rng.uniform(-1, 1, (b, N, 3)).astype(np.float32)
+    gt = [(mk(4), rng.integers(0, 40, 4)), (mk(3), rng.integers(0, 40, 3))]
+    ng = [mk(4), mk(4), mk(2)]
+    model = pc.PointNetCls(k=40)
+    model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    model.dropout.p = 0.0
+    model_D = pc.DeepConvDiscNet(40, 1)
+    model_D.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in Dp.items()})
+    model.cuda()
+    model_D.cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    tgt = [(torch.from_numpy(p), torch.from_numpy(l)) for p, l in gt]
+    tng = [torch.from_numpy(p) for p in ng]
+    iters = 5
+    args = argparse.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=10 ** 9, exp_dir="/tmp", tensorboard=False,
+                              lambda_cls=1.0, lambda_adv=0.0, batch_size=4)
+    log = _Log()
+    trainer.run_training(tgt, tng, enumerate(tgt), enumerate(tng), [tgt[0]], model, model_D,
+                         torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(), opt, opt_D,
+                         ImagePool(0), ImagePool(0), log, log, None, args)
+    # the oracle over the same batch sequence (GT i % 2, no-GT i % 3)
+    G0 = {k: v.copy() for k, v in G.items()}
+    oG, oD = onp.Adam(G), onp.Adam(Dp)
+    for i in range(iters):
+        pg, lab = gt[i % 2]
+        pn = ng[i % 3]
+        onp.adv_step(G, Dp, oG, oD, pg, lab, pn, np.ones((len(pg), 256), np.float32),
+                     np.ones((len(pn), 256), np.float32), np.full((len(pg), 1), 0.9, np.float32),
+                     np.full((len(pn), 1), 0.1, np.float32), lambda_adv=0.0)
+    for name, p in model.named_parameters():
+        d_gpu = p.detach().cpu().numpy().astype(np.float64) - G0[name]
+        d_ref = G[name].astype(np.float64) - G0[name]
+        e = np.linalg.norm(d_gpu - d_ref) / max(np.linalg.norm(d_ref), 1e-30)
+        assert e < 1e-2, (name, e)   # a stale bias correction moves these by ~0.5
+    for st in opt.state.values():
+        assert float(st["step"]) == iters
+    assert all(p.grad is not None for p in model.parameters())
+
+
+def test_loader_streams_independent_and_index_checked(tmp_path):
+    """GT and no-GT loaders given the same seed draw different jitter fields
+    (the dataset kind is part of the Philox key), default-seeded loaders
+    differ too, and gather() rejects indices outside the split."""
+    lst = _list(tmp_path, ["modelnet_gzip.h5", "modelnet_contig.h5"])
+    rows = np.array([0, 2, 5, 7])
+    gt_ds = D.ModelNetDatasetGT(lst, rows, npoints=32)
+    ng_ds = D.ModelNetDataset_noGT(lst, rows, npoints=32)
+    idx = torch.zeros(1, device="cuda", dtype=torch.int64)
+    jit = []
+    for ld in (D.DeviceCloudLoader(gt_ds, 1, seed=7), D.DeviceCloudLoader(ng_ds, 1, seed=7),
+               D.DeviceCloudLoader(gt_ds, 1), D.DeviceCloudLoader(gt_ds, 1)):
+        out = ld.gather(idx)
+        pts = out[0] if isinstance(out, tuple) else out
+        jit.append((pts.cpu().numpy() - ld.ds.select_data[0]))
+    for a in range(4):
+        for b in range(a + 1, 4):
+            assert not np.allclose(jit[a], jit[b]), (a, b)
+    ld = D.DeviceCloudLoader(gt_ds, 2, seed=1)
+    with pytest.raises(IndexError):
+        ld.gather(torch.tensor([0, len(gt_ds)], device="cuda"))
+    with pytest.raises(IndexError):
+        ld.gather(torch.tensor([-1], device="cuda"))

@@ -144,3 +144,142 @@ def test_bucketed_allreduce_matches_single(tmp_path):
             for ov in (0, 1):
                 got = np.load(tmp_path / f"{name}{rank}_{ov}.npy")
                 assert np.array_equal(got, ref), (name, rank, ov)
+
+
+# ---------------------------------------------------------------------------
+# configs[4]: the data-parallel step on the HIP path vs the single-process
+# oracle on the global batch (models/pointnet.py:109-137, utils/trainer.py:426-559)
+# ---------------------------------------------------------------------------
+
+DP_B, DP_N = 32, 2048  # configs[4]'s per-rank shape (B=256 global over 8 ranks)
+
+
+def _global_batch(world):
+    rng = np.random.default_rng(4242)
+    Bg = DP_B * world
+    pg = rng.uniform(-1, 1, (Bg, DP_N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, Bg)
+    pn = rng.uniform(-1, 1, (Bg, DP_N, 3)).astype(np.float32)
+    m1 = (rng.random((Bg, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((Bg, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (Bg, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (Bg, 1)).astype(np.float32)
+    return pg, lab, pn, m1, m2, y1, y2
+
+
+def _dp_oracle_worker(rank, port, out_dir, world):
+    """One rank: the real AdvTrainStep (HIP) on its slice of the global batch,
+    the bucketed all-reduce (overlap on), the replicated Adam."""
+    import torch.distributed as dist
+    from oracle import pointnet_np as onp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import adversarial_learning_on_pointclouds_amd as pc
+        from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
+        from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        m = pc.PointNetCls(k=40)
+        m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in
+                           onp.make_params(onp.cls_spec(40), seed=5).items()})
+        d = pc.DeepConvDiscNet(40, 1)
+        d.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in
+                           onp.make_params(onp.disc_spec(40, 1), seed=6, init="xavier").items()})
+        m.to(dev)
+        d.to(dev)
+        st = AdvTrainStep(m, d, DP_B, DP_N, device=dev)
+        dp = DataParallelAdvStep(st, overlap=True)
+        sl = slice(rank * DP_B, (rank + 1) * DP_B)
+        t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a[sl])).to(dev, dt)
+        pg, lab, pn, m1, m2, y1, y2 = _global_batch(world)
+        losses = dp(t(pg), t(lab, torch.int64), t(pn), masks=(t(m1), t(m2)), soft=(t(y1), t(y2)))
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), losses=losses.cpu().numpy(),
+                 grad=st.grad_flat.cpu().numpy(), g=st.g_param.cpu().numpy(),
+                 d=st.d_param.cpu().numpy(),
+                 **{"grad." + k: p.grad.cpu().numpy() for k, p in m.named_parameters()},
+                 **{"gradD." + k: p.grad.cpu().numpy() for k, p in d.named_parameters()},
+                 **{"param." + k: p.detach().cpu().numpy() for k, p in m.named_parameters()},
+                 **{"paramD." + k: p.detach().cpu().numpy() for k, p in d.named_parameters()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_hip_step_vs_global_oracle(tmp_path):
+    """Two ranks (gloo, sharing the box's GPU), each the real HIP step at
+    configs[4]'s per-rank shape, all-reduced: both replicas bitwise equal, and
+    the averaged gradients / updated parameters equal the single-process oracle
+    step on the 2B global batch (per-tensor relative gradient tolerance)."""
+    import torch.multiprocessing as mp
+    from oracle import pointnet_np as onp
+    from golden_util import assert_grad_close, rel_err
+    world = 2
+    mp.spawn(_dp_oracle_worker, args=(_free_port(), str(tmp_path), world), nprocs=world, join=True)
+    r0, r1 = (dict(np.load(tmp_path / f"r{r}.npz")) for r in range(world))
+    for k in ("grad", "g", "d"):
+        assert np.array_equal(r0[k], r1[k]), k
+    G = onp.make_params(onp.cls_spec(40), seed=5)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=6, init="xavier")
+    pg, lab, pn, m1, m2, y1, y2 = _global_batch(world)
+    ref, gG, gD, _ = onp.adv_step(G, D, onp.Adam(G), onp.Adam(D), pg, lab, pn, m1, m2, y1, y2)
+    want = [ref["loss_cls"], ref["loss_adv"], ref["loss_D_gt"], ref["loss_D_nogt"]]
+    got = (r0["losses"][:4] + r1["losses"][:4]) / 2  # each rank reports its own shard's means
+    assert np.allclose(got, want, atol=1e-4), (got, want)
+    for k in gG:
+        assert_grad_close(r0["grad." + k], gG[k], k)
+        assert rel_err(r0["param." + k], G[k]) < 1e-5, k
+    for k in gD:
+        assert_grad_close(r0["gradD." + k], gD[k], k)
+        assert rel_err(r0["paramD." + k], D[k]) < 1e-5, k
+
+
+def _rccl_worker(rank, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
+        from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+        res = {}
+        for mode in ("plain", "dp_eager", "dp_graph"):
+            m, d = _models(dev)
+            st = AdvTrainStep(m, d, B, N, seed=7, device=dev)
+            if mode == "plain":
+                for k in range(3):
+                    st(*_batch(dev, 60 + k))
+            else:
+                dp = DataParallelAdvStep(st)  # RCCL: bucketed + overlapped by default
+                assert dp._split()
+                if mode == "dp_eager":
+                    for k in range(3):
+                        dp(*_batch(dev, 60 + k))
+                else:
+                    bufs = _batch(dev, 60)
+                    graph = dp.capture(*bufs)
+                    for k in range(3):
+                        for dst, src in zip(bufs, _batch(dev, 60 + k)):
+                            dst.copy_(src)
+                        graph.replay()
+            torch.cuda.synchronize()
+            res[mode] = np.concatenate([st.g_param.cpu().numpy(), st.d_param.cpu().numpy(),
+                                        st.losses.cpu().numpy()])
+        np.savez(os.path.join(out_dir, "rccl.npz"), **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_bucketed_overlap_path_single_rank(tmp_path):
+    """The RCCL code path of DataParallelAdvStep (ReduceOp.AVG with async_op on
+    RCCL's stream, bucketed around the feature backward, graphs replayed
+    between the collectives) executed on a one-rank RCCL group: with one rank
+    the average is the identity, so three steps must equal the plain step
+    bitwise, eager and captured.  Checks the stream ordering of the overlap
+    (a missed wait shows as a race on the gradient buffer)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rccl_worker, args=(_free_port(), str(tmp_path)), nprocs=1, join=True)
+    r = dict(np.load(tmp_path / "rccl.npz"))
+    assert np.array_equal(r["plain"], r["dp_eager"])
+    assert np.array_equal(r["plain"], r["dp_graph"])

@@ -1,16 +1,19 @@
 """HIP-path parity: libpcadv.so (through its C ABI) vs the numpy oracle and the
 golden vectors captured from the reference.  Runs on an MI355X only.
 
-Tolerance (north_star): max|a - ref| / max(1, max|ref|) <= 1e-3 in fp32; the
-kernels compute in exact f32 (f32 MFMA / FMA) so most checks use 1e-4.
-argmax must match exactly except at near-ties (|v_ours - v_ref| <= 1e-5 * scale).
+Tolerance (north_star): max|a - ref| / max(1, max|ref|) <= 1e-3 in fp32 for
+forward outputs and losses (most checks use 1e-4 or 1e-5).  Gradients are held
+per tensor (golden_util.assert_grad_close): max|a - ref| <= 1e-3 * max|ref| and
+||a - ref|| <= 1e-4 * ||ref||, no max(1, .) floor, so a zeroed or scaled
+gradient fails however small it is.  argmax must match exactly except at
+near-ties (|v_ours - v_ref| <= 1e-5 * scale).
 """
 import numpy as np
 import pytest
 import torch
 
 from oracle import pointnet_np as onp
-from golden_util import check_tensor, load, rel_err
+from golden_util import assert_grad_close, check_tensor, check_tensor_rel, grad_err, load, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -113,8 +116,7 @@ def test_feat_bwd_vs_oracle(C, N):
     ref = [dz1.T @ pts.reshape(-1, 3), dz1.sum(0), dz2.T @ r1.reshape(B_ * N_, -1), dz2.sum(0),
            dz3.T @ r2.reshape(B_ * N_, -1), dz3.sum(0), dW4, db4]
     for i, (g, r) in enumerate(zip(grads, ref)):
-        e = rel_err(g.cpu().numpy().reshape(r.shape), r)
-        assert e < 1e-5, (i, e)
+        assert_grad_close(g.cpu().numpy().reshape(r.shape), r, f"grad {i}", 1e-5, 1e-5)
 
 
 def test_feat_bwd_deterministic():
@@ -149,9 +151,9 @@ def test_linear_vs_torch(M, N, K, act):
     y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), act, mask.to(DEV), 0.3)
     dx, dw, db = ops.linear_bwd(dy.to(DEV), y, act, mask.to(DEV), 0.3, x.to(DEV), w.to(DEV))
     assert rel_err(y.cpu().numpy(), yr.detach().numpy()) < 1e-5
-    assert rel_err(dx.cpu().numpy(), xr.grad.numpy()) < 1e-5
-    assert rel_err(dw.cpu().numpy(), wr.grad.numpy()) < 1e-5
-    assert rel_err(db.cpu().numpy(), br.grad.numpy()) < 1e-5
+    assert_grad_close(dx.cpu().numpy(), xr.grad.numpy(), "dx", 1e-5, 1e-5)
+    assert_grad_close(dw.cpu().numpy(), wr.grad.numpy(), "dw", 1e-5, 1e-5)
+    assert_grad_close(db.cpu().numpy(), br.grad.numpy(), "db", 1e-5, 1e-5)
 
 
 # ---------------------------------------------------------------------------
@@ -175,7 +177,7 @@ def test_cls_module_golden_g1_g2():
     loss.backward()
     assert abs(loss.item() - float(fx2["loss"])) < 1e-4
     for name, p in model.named_parameters():
-        check_tensor(fx2, "grad." + name, p.grad.cpu().numpy(), tol=1e-4)
+        check_tensor_rel(fx2, "grad." + name, p.grad.cpu().numpy(), tol=1e-4)
 
 
 def test_disc_module_golden_g4():
@@ -186,9 +188,9 @@ def test_disc_module_golden_g4():
     out = md(x)
     out.backward(_t(fx["dout"]))
     assert rel_err(out.detach().cpu().numpy(), fx["out"]) < 1e-5
-    assert rel_err(x.grad.cpu().numpy(), fx["dx"]) < 1e-5
+    assert_grad_close(x.grad.cpu().numpy(), fx["dx"], "dx", 1e-5, 1e-5)
     for name, p in md.named_parameters():
-        check_tensor(fx, "grad." + name, p.grad.cpu().numpy(), tol=1e-5)
+        check_tensor_rel(fx, "grad." + name, p.grad.cpu().numpy(), tol=1e-5)
 
 
 # ---------------------------------------------------------------------------
@@ -218,9 +220,15 @@ def _make_step(B, N, g_seed=1, d_seed=2, seed=0):
     return AdvTrainStep(model, model_D, B, N, seed=seed), model, model_D
 
 
-@pytest.mark.parametrize("name", ["g3_adv_step1.npz", "g3_adv_step3.npz"])
+@pytest.mark.parametrize("name", ["g3_adv_step1.npz", "g3_adv_step3.npz", "g3_adv_step1_b32.npz"])
 def test_adv_step_golden_g3(name):
+    """run_training's iteration vs the reference's own capture (B=4, and the
+    full B=32 of configs[2]).  Gradients per tensor relative to each tensor's
+    largest entry: 1e-4 at B=4; 1e-3 at B=32, where a conv3 pre-activation
+    within f32 rounding of 0 can flip one ReLU between two f32 computations
+    (see test_cls_step_full_size_vs_oracle_with_adam)."""
     fx = load(name)
+    gtol = 1e-4 if int(fx["B"]) <= 4 else 1e-3
     step, model, model_D = _make_step(int(fx["B"]), int(fx["N"]))
     for i, (pg, lab, pn, m1, m2, y1, y2) in enumerate(_adv_inputs(fx)):
         losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
@@ -231,9 +239,9 @@ def test_adv_step_golden_g3(name):
         assert abs(losses[3] - fx["loss_D_nogt"][i]) < 1e-4
         if int(fx["iters"]) == 1:
             for nm, p in model.named_parameters():
-                check_tensor(fx, "gradG." + nm, p.grad.cpu().numpy(), tol=1e-4)
+                check_tensor_rel(fx, "gradG." + nm, p.grad.cpu().numpy(), tol=gtol)
             for nm, p in model_D.named_parameters():
-                check_tensor(fx, "gradD." + nm, p.grad.cpu().numpy(), tol=1e-4)
+                check_tensor_rel(fx, "gradD." + nm, p.grad.cpu().numpy(), tol=gtol)
     for nm, p in model.named_parameters():
         check_tensor(fx, "paramG." + nm, p.detach().cpu().numpy(), tol=1e-5)
     for nm, p in model_D.named_parameters():
@@ -293,9 +301,9 @@ def test_semi_step_full_size_vs_oracle(keep):
     assert losses[5] == losses_ref["semi_ratio"]
     assert abs(losses[4] - (losses_ref["loss_semi"] or 0.0)) < 1e-4
     for nm, p in model.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), gG[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), gG[nm], nm)
     for nm, p in model_D.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), gD[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), gD[nm], nm)
 
 
 def test_adv_step_full_size_vs_oracle():
@@ -322,11 +330,17 @@ def test_adv_step_full_size_vs_oracle():
     assert rel_err(gl[:B], aux["logits_gt"]) < 1e-4
     assert rel_err(gl[B:], aux["logits_nogt"]) < 1e-4
     for nm, p in model.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), gG[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), gG[nm], nm)
         assert rel_err(p.detach().cpu().numpy(), G[nm]) < 1e-5, nm
     for nm, p in model_D.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), gD[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), gD[nm], nm)
         assert rel_err(p.detach().cpu().numpy(), D[nm]) < 1e-5, nm
+    # the check is sensitive at these magnitudes (max |g| of conv1.weight is
+    # ~4e-4 at B=32): a zeroed or doubled gradient buffer fails it
+    g1 = model.feat.conv1.weight.grad.cpu().numpy()
+    for broken in (np.zeros_like(g1), 2 * g1):
+        with pytest.raises(AssertionError):
+            assert_grad_close(broken, gG["feat.conv1.weight"], "broken")
 
 
 def test_adv_step_cfg5_shape_vs_oracle():
@@ -351,9 +365,9 @@ def test_adv_step_cfg5_shape_vs_oracle():
     for i, k in enumerate(["loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt"]):
         assert abs(losses[i] - losses_ref[k]) < 1e-4, (k, losses[i], losses_ref[k])
     for nm, p in model.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), gG[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), gG[nm], nm)
     for nm, p in model_D.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), gD[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), gD[nm], nm)
 
 
 def test_adv_step_graph_replay_matches_eager():
@@ -413,10 +427,27 @@ def test_cls_step_golden_g2():
     assert abs(float(loss[0]) - float(fx["loss"])) < 1e-5
     assert rel_err(step.logits.cpu().numpy(), fx["logits"]) < 1e-4
     for nm, p in model.named_parameters():
-        check_tensor(fx, "grad." + nm, p.grad.cpu().numpy(), tol=1e-4)
+        check_tensor_rel(fx, "grad." + nm, p.grad.cpu().numpy(), tol=1e-4)
+
+
+def _relu_flips(x3_gpu, cache):
+    """conv3 outputs whose ReLU the two f32 computations decide differently
+    (pre-activation within rounding of 0) at points that receive gradient."""
+    x3r = cache["x3"]
+    hit = np.zeros(x3r.shape[:2], bool)
+    np.put_along_axis(hit, cache["am"].astype(np.int64), True, axis=1)
+    return int((((x3_gpu > 0) != (x3r > 0)) & hit[:, :, None]).sum())
 
 
 def test_cls_step_full_size_vs_oracle_with_adam():
+    """configs[1] at full size (B=32, N=1024).  Gradients are held two ways:
+    strictly (max-rel 1e-4, L2-rel 1e-5) against the oracle's backward on this
+    forward's own conv3 activations, and end to end against the oracle's own
+    forward.  One conv3 pre-activation within f32 rounding of 0 (3e-8 here) at
+    a point that wins two channels flips its ReLU between the two computations
+    and moves conv1..conv3's gradients by ~5e-4 (L2), so the end-to-end bound
+    is 2e-3 (L2) / 5e-3 (max) when such a flip exists and the default
+    otherwise; a zeroed or doubled gradient still fails both by 1000x."""
     B, N = 32, 1024
     step, model = _cls_step(B, N, g_seed=3)
     rng = np.random.default_rng(2001)
@@ -427,11 +458,20 @@ def test_cls_step_full_size_vs_oracle_with_adam():
     logits, _, cache = onp.cls_forward(G, pts, m)
     l_ref, dlog = onp.cross_entropy(logits, lab)
     grads = onp.cls_backward(G, cache, dlog)
+    _, gidx, x3 = ops.feat_fwd(_t(pts), *_feat_weights(G))  # the step's forward kernels
+    assert (gidx.cpu().numpy() == cache["am"]).all()
+    x3g = x3.cpu().numpy()
+    grads_same = onp.cls_backward(G, dict(cache, x3=x3g), dlog)
+    flips = _relu_flips(x3g, cache)
     onp.Adam(G).step(grads)
     loss = step(_t(pts), _t(lab, torch.int64), mask=_t(m))
     assert abs(float(loss[0]) - l_ref) < 1e-4
     for nm, p in model.named_parameters():
-        assert rel_err(p.grad.cpu().numpy(), grads[nm]) < TOL, nm
+        assert_grad_close(p.grad.cpu().numpy(), grads_same[nm], nm, 1e-4, 1e-5)
+        if flips:
+            assert_grad_close(p.grad.cpu().numpy(), grads[nm], nm, 5e-3, 2e-3)
+        else:
+            assert_grad_close(p.grad.cpu().numpy(), grads[nm], nm)
         # Adam's first step moves each weight by ~lr * g / (|g| + eps): where |g|
         # is within rounding of eps the two f32 gradients give updates up to lr
         # (1e-4) apart, so the parameters are held to lr relative to max |w|
@@ -451,3 +491,21 @@ def test_cls_step_graph_replay_matches_eager():
     torch.cuda.synchronize()
     assert torch.equal(s1.losses, s2.losses)
     assert torch.equal(s1.g_param, s2.g_param)
+
+
+def test_cls_step_golden_g11_full_size():
+    """configs[1] at full size (B=32, N=1024) through pcadv_cls_step against the
+    reference's own capture (g11): loss, logits, and every gradient per tensor
+    relative (1e-3; the ReLU-flip note of the oracle test above applies)."""
+    fx = load("g11_cls_b32.npz")
+    B, N = int(fx["B"]), int(fx["N"])
+    step, model = _cls_step(B, N, g_seed=int(fx["g_seed"]))
+    rng = np.random.default_rng(int(fx["data_seed"]))
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    mask = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    loss = step(_t(pts), _t(lab, torch.int64), mask=_t(mask), apply_adam=False)
+    assert abs(float(loss[0]) - float(fx["loss"])) < 1e-5
+    assert rel_err(step.logits.cpu().numpy(), fx["logits"]) < 1e-4
+    for nm, p in model.named_parameters():
+        check_tensor_rel(fx, "grad." + nm, p.grad.cpu().numpy(), tol=1e-3)

@@ -459,3 +459,55 @@ def test_seg_train_step_matches_autograd_and_graph():
     torch.cuda.synchronize()
     assert torch.equal(st2.param, st3.param)
     assert torch.equal(st2.loss, st3.loss)
+
+
+def test_seg_train_step_full_size_configs3_vs_oracle():
+    """BASELINE configs[3] at full size (B=16, N=2048) through SegTrainStep, the
+    bench's path (models/pointnet.py:261-317, utils/trainer.py:334-349): loss,
+    logits, x_global and argmax vs the numpy oracle; every gradient vs the
+    oracle's backward on this forward's own activations (1e-4 of each tensor's
+    max) and end to end (relative L2, see the module docstring); one Adam step
+    vs the oracle's Adam on the same gradients."""
+    from adversarial_learning_on_pointclouds_amd.seg import SegTrainStep
+    from golden_util import assert_grad_close
+    B, N = 16, 2048
+    S = onp.make_params(onp.seg_spec(50), seed=41)
+    rng = np.random.default_rng(42)
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    cls = np.zeros((B, 1, 16), np.float32)
+    cls[np.arange(B), 0, rng.integers(0, 16, B)] = 1
+    seg = rng.integers(0, 50, (B, N))
+    m = _seg_model(S)
+    step = SegTrainStep(m, device=DEV)
+    loss = step(_t(pts), _t(cls), _t(seg, torch.int64), apply_adam=False).item()
+    fw = step.fw
+    rl, grads, rlog, rg, ram = onp.seg_step(S, pts, cls, seg)
+    assert abs(loss - rl) < 1e-4 * max(1.0, abs(rl)), (loss, rl)
+    logits = fw["logits"].cpu().numpy().reshape(B, N, 50)
+    e = np.abs(logits - rlog).max() / np.abs(rlog).max()
+    assert e < 1e-3, e
+    g = fw["gmax"].cpu().numpy()
+    assert np.abs(g - rg).max() / np.abs(rg).max() < 1e-3
+    gi = fw["gidx"].cpu().numpy()
+    assert ((gi == ram) | (rg <= 0)).mean() > 0.999  # argmax of the positive pooled channels
+    # same-mask backward: the oracle's backward on this forward's activations
+    _, dout = onp.seg_cross_entropy(logits, seg)
+    ref = onp.seg_backward(S, _oracle_cache(fw, pts, cls), dout)
+    for name, p in m.named_parameters():
+        r = ref[name]
+        assert_grad_close(p.grad.cpu().numpy().reshape(r.shape), r, name, 1e-4, 1e-4)
+    # end to end against the oracle's own forward (its own ReLU masks): the
+    # bf16x3 forward (error ~2^-16 of sum|ab|) flips the ReLU of pre-activations
+    # that close to 0, so conv1's gradient lands ~3e-3 off in relative L2 at
+    # this size; held to the module's 1e-2 (the same-mask check above is the
+    # strict one)
+    for name, p in m.named_parameters():
+        r = grads[name]
+        a = p.grad.cpu().numpy().reshape(r.shape)
+        el2 = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
+        assert el2 < 1e-2, (name, el2)
+    gnp = {k: q.grad.cpu().numpy() for k, q in m.named_parameters()}
+    onp.Adam(S).step(gnp)
+    step.adam()
+    for name, p in m.named_parameters():
+        assert np.abs(p.detach().cpu().numpy() - S[name]).max() < 1e-6, name
