@@ -195,8 +195,8 @@ def test_run_training_uneven_batches_keeps_adam_state():
     for i in range(iters):
         pg, lab = gt[i % 2]
         pn = ng[i % 3]
-        onp.adv_step(G, Dp, oG, oD, pg, lab, pn, np.ones((len(pg), 256), np.float32),
-                     np.ones((len(pn), 256), np.float32), np.full((len(pg), 1), 0.9, np.float32),
+        # masks None: no dropout scale (p = 0)
+        onp.adv_step(G, Dp, oG, oD, pg, lab, pn, None, None, np.full((len(pg), 1), 0.9, np.float32),
                      np.full((len(pn), 1), 0.1, np.float32), lambda_adv=0.0)
     for name, p in model.named_parameters():
         d_gpu = p.detach().cpu().numpy().astype(np.float64) - G0[name]
