@@ -138,9 +138,24 @@ def cpu_baseline(seconds):
             break
     dt = time.perf_counter() - t0
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    return {"value": round(2 * B * steps / dt, 2), "unit": "clouds/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N={N}, fp32) in {dt:.1f}s"}
+    out = {"value": round(2 * B * steps / dt, 2), "unit": "clouds/s", "cores": cores,
+           "kind": "port",
+           "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N={N}, fp32) in {dt:.1f}s"}
+    # the port against the reference's own run_training on the same cores, measured
+    # in the build container (the reference never travels to this box):
+    # tools/time_reference_cpu.py -> profiles/rNN_cpu_calibration.json
+    cal = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_cpu_calibration.json")))
+    if cal and N == 1024:
+        c = json.load(open(cal[-1]))
+        ratio = float(c["port_over_reference"])
+        out["calibration"] = {"port_over_reference": ratio, "cores": c["cores"],
+                              "reference_clouds_per_s": c["reference_run_training_clouds_per_s"],
+                              "source": os.path.relpath(cal[-1], REPO),
+                              "note": "the port's sparse max-pool backward skips the reference's "
+                                      "dense MaxBackward + zero-fill, so it runs faster than "
+                                      "run_training on the same cores"}
+        out["reference_equivalent_value"] = round(out["value"] / ratio, 2)
+    return out
 
 
 def cpu_baseline_seg(seconds, Bs, Ns):

@@ -7,7 +7,7 @@ N=1024 on this host's cores, steady state = (T(K2) - T(K1)) / (K2 - K1)
 oracle's adversarial step on the same shapes, so DESIGN.md can state how far
 the port used as bench.py's cpu_baseline is from the reference.
 
-    python tools/time_reference_cpu.py [/root/reference]
+    python tools/time_reference_cpu.py [/root/reference] [--out profiles/rNN_cpu_calibration.json]
 """
 import argparse
 import logging
@@ -62,16 +62,33 @@ def time_reference(ref_root, iters):
 
 
 def main():
-    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
-    k1, k2 = 3, 13
-    t1, t2 = time_reference(ref, k1), time_reference(ref, k2)
-    ref_step = (t2 - t1) / (k2 - k1)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("ref_root", nargs="?", default="/root/reference")
+    ap.add_argument("--rounds", type=int, default=3, help="alternating reference / port timings")
+    ap.add_argument("--out", default=None, help="write the summary JSON here (e.g. profiles/)")
+    a = ap.parse_args()
+    import json
     import bench
-    port = bench.cpu_baseline(15.0)
-    print(f"cores={os.cpu_count()}")
-    print(f"reference run_training: {ref_step * 1e3:.1f} ms/step = {2 * B / ref_step:.1f} clouds/s")
-    print(f"numpy oracle port:      {port['value']:.1f} clouds/s ({port['sample']})")
-    print(f"port / reference = {port['value'] / (2 * B / ref_step):.3f}")
+    k1, k2 = 3, 13
+    refs, ports = [], []
+    for _ in range(a.rounds):  # alternate, so host drift hits both alike
+        t1, t2 = time_reference(a.ref_root, k1), time_reference(a.ref_root, k2)
+        refs.append(2 * B * (k2 - k1) / (t2 - t1))
+        ports.append(bench.cpu_baseline(10.0)["value"])
+    ref_v, port_v = float(np.median(refs)), float(np.median(ports))
+    out = {"cores": os.cpu_count(), "threads": "torch.set_num_threads(cores); numpy/BLAS default",
+           "reference_run_training_clouds_per_s": round(ref_v, 1),
+           "reference_ms_per_step": round(2 * B / ref_v * 1e3, 1),
+           "port_clouds_per_s": round(port_v, 1), "port_over_reference": round(port_v / ref_v, 3),
+           "samples": {"reference": [round(v, 1) for v in refs], "port": [round(v, 1) for v in ports]},
+           "workload": "adversarial step B=32 GT + 32 no-GT, N=1024, fp32 (run_training :426-559)",
+           "method": "reference: (T(13) - T(3)) / 10 iterations of utils/trainer.py:run_training "
+                     "(iteration 0's checkpoint + test pass cancel); port: bench.cpu_baseline(10 s); "
+                     f"median of {a.rounds} alternating rounds"}
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
