@@ -37,9 +37,17 @@ __device__ __forceinline__ f32x4m mfma16(float a, float b, f32x4m c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+constexpr int BW_G = 12;      // hit groups of the dZ3 gather: half-waves of waves 2-7 (4 columns per lane)
+constexpr int BW_RBG = (BW_RB + BW_G - 1) / BW_G;  // batch rows per gather group (mask / combine)
+constexpr int BW_GD = 4;      // W4 rows in flight per gather lane
 struct BwdLds {
-  int key[BW_MAXO];          // o of each hit, grouped by row (arbitrary order in a row)
-  float hg[BW_MAXO];         // g of each hit, same order
+  union {
+    struct {
+      int key[BW_MAXO];      // o of each hit, grouped by row (arbitrary order in a row)
+      float hg[BW_MAXO];     // g of each hit, same order
+    };
+    alignas(16) float bnd[BW_G][128];  // group g's partial dZ3 sums of its cut row (phase b)
+  };
   int so[BW_MAXO];           // o of each hit, sorted by (row, o)
   float sg[BW_MAXO];         // g, same order
   int rcnt[BW_PCH];          // hits per row of the chunk
@@ -48,8 +56,7 @@ struct BwdLds {
   int wsum[2], wact[2];
   int rows_list[BW_PCH];     // compact slot -> row
   int hoff[BW_PCH + 4];      // first sorted hit of each compact slot; hoff[nact] = nhits
-  int bnd_row[4];            // batch row whose hits group g continued (or -1)
-  alignas(16) float bnd[4][128];  // group g's partial dZ3 sums of that row
+  int bnd_row[BW_G];         // batch row whose hits group g continued (or -1)
   alignas(16) float dz3[BW_RB * SZ3];
   alignas(16) float x2[BW_RB * S64];   // recomputed conv2 output (f32, as the forward)
   alignas(16) float x1[BW_RB * S64];   // recomputed conv1 output
@@ -153,11 +160,17 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     }
     if (tid == 0) L.hoff[nact] = nhits;
   }
-  // first batch's points, issued now (used after the sort)
-  float ptv = 0.f;
+  // first batch's points, issued now (used after the sort): waves 0-1 each
+  // hold all 96 coordinates (element lane + 64 u)
+  float ptv[2] = {0.f, 0.f};
   __syncthreads();
-  if (tid < BW_RB * 3 && tid / 3 < nact)
-    ptv = pts[(size_t)(p0 + L.rows_list[tid / 3]) * 3 + tid % 3];
+  if (wave < 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = lane + 64 * u, row = e / 3;
+      if (e < BW_RB * 3 && row < nact) ptv[u] = pts[(size_t)(p0 + L.rows_list[row]) * 3 + e % 3];
+    }
+  }
   BSTAMP(2);
 
   // ---- 3. place each hit in its row's segment, then rank it inside the
@@ -193,28 +206,34 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     const int nb = min(BW_RB, nact - b0);
     const int sb_ = 4 + 5 * (b0 / BW_RB);
     (void)sb_;
-    // ---- a. recompute x1, x2 of the batch rows from their points, with the
-    //      forward's exact operation order (bit-identical activations); the
-    //      conv2 B fragments (waves 0-1) land during conv1 ----------------------
-    f32x4 bf2[8];
-    if (wave < 2) load_bfrag<64>(w2, 32 * wave, lane, bf2);
-    if (tid < BW_RB * 3) {
-      if (b0 > 0 && tid / 3 < nb)
-        ptv = pts[(size_t)(p0 + L.rows_list[b0 + tid / 3]) * 3 + tid % 3];
-      L.pts[(tid / 3) * 4 + tid % 3] = tid / 3 < nb ? ptv : 0.f;
-    }
-    __syncthreads();
-    {
-      const int rg = tid >> 6;  // 8 groups x 4 rows
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int rr = 4 * rg + u;
-        L.x1[rr * S64 + ch1] = conv1_point(w1a, w1b, w1c, b1v, L.pts[rr * 4 + 0],
-                                           L.pts[rr * 4 + 1], L.pts[rr * 4 + 2]);
-      }
-    }
-    __syncthreads();
+    // ---- a | b, side by side: waves 0-1 recompute x1, x2 of the batch rows
+    //      (a); waves 2-7 gather the dZ3 rows meanwhile (b), which needs neither.
     if (wave < 2) {
+      // a. conv1 (VALU) and conv2 (v_mfma_f32_32x32x2_f32) in the forward's
+      //    operation order: bit-identical activations.  Both waves compute all
+      //    of x1 and write the same values to the same LDS words, so each wave
+      //    only has to order its own accesses (no workgroup barrier).
+      f32x4 bf2[8];
+      load_bfrag<64>(w2, 32 * wave, lane, bf2);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // the batch's points: element e = lane + 64 u of 96
+        const int e = lane + 64 * u, row = e / 3;
+        if (e < BW_RB * 3) {
+          if (b0 > 0) ptv[u] = row < nb ? pts[(size_t)(p0 + L.rows_list[b0 + row]) * 3 + e % 3] : 0.f;
+          L.pts[row * 4 + e % 3] = row < nb ? ptv[u] : 0.f;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 8
+      for (int rr = 0; rr < BW_RB; ++rr) {
+        const f32x4 q4 = *reinterpret_cast<const f32x4*>(&L.pts[rr * 4]);
+        L.x1[rr * S64 + lane] = conv1_point(w1a, w1b, w1c, b1v, q4.x, q4.y, q4.z);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       f32x16 acc = {};
       acc = mfma_rows_x_wt<64>(L.x1, S64, bf2, acc, lane);
       const int col = 32 * wave + r32;
@@ -227,27 +246,31 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     }
     BSTAMP(sb_);
 
-    // ---- b. dZ3 rows: thread = (column i, group g); the batch's sorted hits
-    //      are split evenly over the 4 groups whatever their spread over rows.
-    //      A row cut by a group boundary gets the later groups' partial sums
-    //      added in group order (fixed order: bitwise reproducible) ----------
-    {
-      const int i = tid & 127, grp = tid >> 7;
-      uint32_t mask = 0;  // conv3 ReLU mask of rows grp, grp+4, ... (prefetched)
+    // b. dZ3 rows: thread = (column quad cq, group g of 12) on waves 2-7; the
+    //    batch's sorted hits are split evenly over the groups whatever their
+    //    spread over rows, and each hit's W4 row (512 B) is read by the group's
+    //    32 lanes, 16 B each.  A row cut by a group boundary gets the later
+    //    groups' partial sums added in group order (fixed order: bitwise
+    //    reproducible).
+    const int cq = tid & 31, grp = (tid >> 5) - 4;
+    uint32_t mask = 0;  // conv3 ReLU mask of rows grp + 12 u (4 columns each)
+    if (wave >= 2) {
 #pragma unroll
-      for (int u = 0; u < BW_RB / 4; ++u) {
-        const int rr = grp + 4 * u;
+      for (int u = 0; u < BW_RBG; ++u) {
+        const int rr = grp + BW_G * u;
         if (rr < nb) {
           const int p = p0 + L.rows_list[b0 + rr];
-          const float xv =
-              __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(x3r, (p * 128 + i) * 4, 0, 0));
-          mask |= (xv > 0.f ? 1u : 0u) << u;
+          const f32x4 xv = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(x3r, (p * 128 + 4 * cq) * 4, 0, 0));
+          mask |= ((xv.x > 0.f ? 1u : 0u) | (xv.y > 0.f ? 2u : 0u) | (xv.z > 0.f ? 4u : 0u) |
+                   (xv.w > 0.f ? 8u : 0u)) << (4 * u);
         }
       }
       const int jb0 = L.hoff[b0], nh = L.hoff[b0 + nb] - jb0;
-      const int ja = jb0 + (nh * grp) / 4, je = jb0 + (nh * (grp + 1)) / 4;
+      const int ja = jb0 + (nh * grp) / BW_G, je = jb0 + (nh * (grp + 1)) / BW_G;
       auto w4_at = [&](int o) {
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w4r, (o * 128 + i) * 4, 0, 0));
+        return __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(w4r, (o * 128 + 4 * cq) * 4, 0, 0));
       };
       int brow = -1;
       if (ja < je) {
@@ -256,56 +279,83 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
         bool head = L.hoff[s] >= ja;  // row s starts inside my range
         if (!head) brow = s - b0;
         int jnext = L.hoff[s + 1];
-        float acc = 0.f;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         auto flush = [&]() {
-          if (head) L.dz3[(s - b0) * SZ3 + i] = acc;
-          else L.bnd[grp][i] = acc;
-          acc = 0.f;
+          if (head) {  // 8-B aligned rows (SZ3 = 130): two ds_write_b64
+            float* d = &L.dz3[(s - b0) * SZ3 + 4 * cq];
+            *reinterpret_cast<float2*>(d) = make_float2(acc.x, acc.y);
+            *reinterpret_cast<float2*>(d + 2) = make_float2(acc.z, acc.w);
+          } else {
+            *reinterpret_cast<f32x4*>(&L.bnd[grp][4 * cq]) = acc;
+          }
+          acc = f32x4{0.f, 0.f, 0.f, 0.f};
           head = true;
           ++s;
           jnext = L.hoff[s + 1];
         };
+        auto add = [&](float g, const f32x4& w) {
+          acc.x = fmaf(g, w.x, acc.x);
+          acc.y = fmaf(g, w.y, acc.y);
+          acc.z = fmaf(g, w.z, acc.z);
+          acc.w = fmaf(g, w.w, acc.w);
+        };
         int j = ja;
-        for (; j + 8 <= je; j += 8) {
-          float wv[8];
+        for (; j + BW_GD <= je; j += BW_GD) {
+          f32x4 wv[BW_GD];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) wv[u] = w4_at(L.so[j + u]);
+          for (int u = 0; u < BW_GD; ++u) wv[u] = w4_at(L.so[j + u]);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < BW_GD; ++u) {
             while (j + u >= jnext) flush();
-            acc = fmaf(L.sg[j + u], wv[u], acc);
+            add(L.sg[j + u], wv[u]);
           }
         }
         if (j < je) {
-          float wv[8];
+          f32x4 wv[BW_GD];
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
-            wv[u] = j + u < je ? w4_at(L.so[j + u]) : 0.f;
+          for (int u = 0; u < BW_GD; ++u)
+            wv[u] = j + u < je ? w4_at(L.so[j + u]) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < BW_GD; ++u) {
             if (j + u < je) {
               while (j + u >= jnext) flush();
-              acc = fmaf(L.sg[j + u], wv[u], acc);
+              add(L.sg[j + u], wv[u]);
             }
           }
         }
         flush();  // the row holding hit je-1
       }
-      if (i == 0) L.bnd_row[grp] = brow;
-      __syncthreads();
-      // combine the cut rows and apply the conv3 ReLU mask; padding rows -> 0
+      if (cq == 0) L.bnd_row[grp] = brow;
+    }
+    __syncthreads();
+    // combine the cut rows and apply the conv3 ReLU mask; padding rows -> 0
+    if (wave >= 2) {
 #pragma unroll
-      for (int u = 0; u < BW_RB / 4; ++u) {
-        const int rr = grp + 4 * u;
-        float v = 0.f;
+      for (int u = 0; u < BW_RBG; ++u) {
+        const int rr = grp + BW_G * u;
+        if (rr >= BW_RB) continue;
+        float* d = &L.dz3[rr * SZ3 + 4 * cq];
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (rr < nb) {
-          v = L.dz3[rr * SZ3 + i];
-#pragma unroll
-          for (int g = 1; g < 4; ++g)
-            if (L.bnd_row[g] == rr) v += L.bnd[g][i];
-          v = ((mask >> u) & 1u) ? v : 0.f;
+          const float2 v01 = *reinterpret_cast<const float2*>(d);
+          const float2 v23 = *reinterpret_cast<const float2*>(d + 2);
+          v = f32x4{v01.x, v01.y, v23.x, v23.y};
+          for (int g = 1; g < BW_G; ++g)
+            if (L.bnd_row[g] == rr) {
+              const f32x4 t = *reinterpret_cast<const f32x4*>(&L.bnd[g][4 * cq]);
+              v.x += t.x;
+              v.y += t.y;
+              v.z += t.z;
+              v.w += t.w;
+            }
+          const uint32_t mk = mask >> (4 * u);
+          v.x = (mk & 1u) ? v.x : 0.f;
+          v.y = (mk & 2u) ? v.y : 0.f;
+          v.z = (mk & 4u) ? v.z : 0.f;
+          v.w = (mk & 8u) ? v.w : 0.f;
         }
-        L.dz3[rr * SZ3 + i] = v;
+        *reinterpret_cast<float2*>(d) = make_float2(v.x, v.y);
+        *reinterpret_cast<float2*>(d + 2) = make_float2(v.z, v.w);
       }
     }
     __syncthreads();
@@ -364,15 +414,19 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       const float* bp2 = L.x1 + (16 * rh + h) * S64 + 32 * (t2 & 1) + r32;
       const int n2 = max(0, min(nb2 - 16 * rh, 16)) / 2;
       for (int s = 0; s < n2; ++s) a_dw2 = mfma32(ap2[2 * s * SZ2], bp2[2 * s * S64], a_dw2);
+      // rows past nb are zero in dz1 / dz2 / dz3 / pts, so the sums run over all
+      // BW_RB rows unrolled (the LDS reads issue together; adding the zeros leaves
+      // every partial sum bitwise what the nb-row loop gives)
       if (tid < 192) {
         const int o = tid / 3, i = tid % 3;
-        for (int r = 0; r < nb; ++r) acc_w1 = fmaf(L.dz1[r * SZ2 + o], L.pts[r * 4 + i], acc_w1);
-      } else if (tid < 320) {
-        for (int r = 0; r < nb; ++r) acc_b += L.dz3[r * SZ3 + tid - 192];
-      } else if (tid < 384) {
-        for (int r = 0; r < nb; ++r) acc_b += L.dz2[r * SZ2 + tid - 320];
+#pragma unroll 8
+        for (int r = 0; r < BW_RB; ++r) acc_w1 = fmaf(L.dz1[r * SZ2 + o], L.pts[r * 4 + i], acc_w1);
       } else if (tid < 448) {
-        for (int r = 0; r < nb; ++r) acc_b += L.dz1[r * SZ2 + tid - 384];
+        const float* src = tid < 320 ? L.dz3 + (tid - 192) : (tid < 384 ? L.dz2 + (tid - 320)
+                                                                        : L.dz1 + (tid - 384));
+        const int st = tid < 320 ? SZ3 : SZ2;
+#pragma unroll 8
+        for (int r = 0; r < BW_RB; ++r) acc_b += src[r * st];
       }
     }
     __syncthreads();

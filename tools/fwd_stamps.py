@@ -89,10 +89,45 @@ def main():
     for _ in range(5):
         assert fb(*bargs) == 0
     torch.cuda.synchronize()
-    sbn = sb.view(C * T, 16).cpu().numpy()
+    sbn = sb.view(C * T, 16).cpu().numpy().astype(np.int64)
     cols = [c for c in range(1, 15) if (sbn[:, c] > 0).all()]
     summarize("k_feat_bwd_chunk thread 0", sbn, cols)
-    print("  active rows per chunk: median", np.median(sbn[:, 15]))
+    nact = sbn[:, 15]
+    print("  active rows per chunk: median", np.median(nact), "max", nact.max(),
+          "chunks > 32:", int((nact > 32).sum()), "of", len(nact))
+    # stamps: 0 start, 1 hits, 2 compact, 3 sorted; batch k: 4+5k a(x1/x2), 5+5k b(dZ3),
+    # 6+5k c(dX2), 7+5k d(dX1), 8+5k e(wgrad); 14 end
+    t0 = sbn[:, 0].min()
+    tot = (sbn[:, 14] - sbn[:, 0]) * 10 / 1e3
+    end = (sbn[:, 14] - t0) * 10 / 1e3
+    print(f"  workgroup span: median {np.median(tot):.2f} max {tot.max():.2f}; kernel end "
+          f"{end.max():.2f} us after the first start")
+    for lo, hi in ((0, 32), (33, 64), (65, 128)):
+        m = (nact >= lo) & (nact <= hi)
+        if m.any():
+            print(f"  nact {lo:3d}-{hi:3d}: {int(m.sum()):4d} chunks, span median "
+                  f"{np.median(tot[m]):.2f} max {tot[m].max():.2f} us")
+    names = ["setup(hits)", "compact", "sort", "a x1/x2", "b dZ3", "c dX2", "d dX1", "e wgrad"]
+    prev_cols = [0, 1, 2, 3, 4, 5, 6, 7]
+    cur_cols = [1, 2, 3, 4, 5, 6, 7, 8]
+    for nm, a, b in zip(names, prev_cols, cur_cols):
+        d = (sbn[:, b] - sbn[:, a]) * 10 / 1e3
+        print(f"  batch1 {nm:12s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+    two = nact > 32
+    if two.any():
+        for nm, a, b in zip(names[3:], [8, 9, 10, 11, 12], [9, 10, 11, 12, 13]):
+            d = (sbn[two, b] - sbn[two, a]) * 10 / 1e3
+            print(f"  batch2 {nm:12s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+        d = (sbn[two, 14] - sbn[two, 13]) * 10 / 1e3
+        print(f"  slab write (2 batches) median {np.median(d):6.2f}")
+    d = (sbn[~two, 14] - sbn[~two, 8]) * 10 / 1e3
+    print(f"  slab write (1 batch) median {np.median(d):6.2f}")
+    ev0.record()
+    for _ in range(20):
+        fb(*bargs)
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"  feat_bwd (chunk + finish) event time: {ev0.elapsed_time(ev1) / 20 * 1e3:.2f} us")
 
 
 if __name__ == "__main__":
