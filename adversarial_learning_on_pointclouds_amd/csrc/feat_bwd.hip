@@ -39,7 +39,7 @@ __device__ __forceinline__ f32x4m mfma16(float a, float b, f32x4m c) {
 
 constexpr int BW_G = 12;      // hit groups of the dZ3 gather: half-waves of waves 2-7 (4 columns per lane)
 constexpr int BW_RBG = (BW_RB + BW_G - 1) / BW_G;  // batch rows per gather group (mask / combine)
-constexpr int BW_GD = 4;      // W4 rows in flight per gather lane
+constexpr int BW_GD = 8;      // W4 rows in flight per gather lane
 struct BwdLds {
   union {
     struct {
