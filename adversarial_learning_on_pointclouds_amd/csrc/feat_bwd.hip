@@ -56,7 +56,7 @@ struct BwdLds {
   int wsum[2], wact[2];
   int rows_list[BW_PCH];     // compact slot -> row
   int hoff[BW_PCH + 4];      // first sorted hit of each compact slot; hoff[nact] = nhits
-  int bnd_row[BW_G];         // batch row whose hits group g continued (or -1)
+  alignas(16) int bnd_row[BW_G];  // batch row whose hits group g continued (or -1)
   alignas(16) float dz3[BW_RB * SZ3];
   alignas(16) float x2[BW_RB * S64];   // recomputed conv2 output (f32, as the forward)
   alignas(16) float x1[BW_RB * S64];   // recomputed conv1 output
@@ -76,10 +76,16 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
 #ifdef PCADV_STAMPS
   // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
-  uint64_t* st_ = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+  // 32 slots per workgroup: 0-15 by thread 0 (below); 16 + batch by thread 128
+  // (wave 2) when its dZ3 gather loop is done; 24 + k: phase a of batch 1
+  uint64_t* st_ = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 32;
 #define BSTAMP(k) do { if (stamps && threadIdx.x == 0 && (k) < 15) st_[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define GSTAMP(k) do { if (stamps && threadIdx.x == 128 && (k) < 8) st_[16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define ASTAMP(k) do { if (stamps && threadIdx.x == 0 && b0 == 0) st_[24 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define BSTAMP(k) do { } while (0)
+#define GSTAMP(k) do { } while (0)
+#define ASTAMP(k) do { } while (0)
 #endif
   BSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -226,6 +232,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      ASTAMP(0);
 #pragma unroll 8
       for (int rr = 0; rr < BW_RB; ++rr) {
         const f32x4 q4 = *reinterpret_cast<const f32x4*>(&L.pts[rr * 4]);
@@ -234,8 +241,13 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      ASTAMP(1);
       f32x16 acc = {};
       acc = mfma_rows_x_wt<64>(L.x1, S64, bf2, acc, lane);
+#ifdef PCADV_STAMPS
+      asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc[15]));
+#endif
+      ASTAMP(2);
       const int col = 32 * wave + r32;
       const float bias = b2[col];
 #pragma unroll
@@ -326,10 +338,20 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
         flush();  // the row holding hit je-1
       }
       if (cq == 0) L.bnd_row[grp] = brow;
+      GSTAMP(b0 / BW_RB);
     }
     __syncthreads();
     // combine the cut rows and apply the conv3 ReLU mask; padding rows -> 0
     if (wave >= 2) {
+      int br[BW_G];  // the groups' cut rows, read once (three 16-B LDS reads)
+#pragma unroll
+      for (int g = 0; g < BW_G; g += 4) {
+        const int4 t = *reinterpret_cast<const int4*>(&L.bnd_row[g]);
+        br[g] = t.x;
+        br[g + 1] = t.y;
+        br[g + 2] = t.z;
+        br[g + 3] = t.w;
+      }
 #pragma unroll
       for (int u = 0; u < BW_RBG; ++u) {
         const int rr = grp + BW_G * u;
@@ -340,14 +362,18 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
           const float2 v01 = *reinterpret_cast<const float2*>(d);
           const float2 v23 = *reinterpret_cast<const float2*>(d + 2);
           v = f32x4{v01.x, v01.y, v23.x, v23.y};
-          for (int g = 1; g < BW_G; ++g)
-            if (L.bnd_row[g] == rr) {
-              const f32x4 t = *reinterpret_cast<const f32x4*>(&L.bnd[g][4 * cq]);
-              v.x += t.x;
-              v.y += t.y;
-              v.z += t.z;
-              v.w += t.w;
-            }
+          uint32_t gm = 0;  // groups that continued row rr, added in group order
+#pragma unroll
+          for (int g = 1; g < BW_G; ++g) gm |= (br[g] == rr ? 1u : 0u) << g;
+          while (gm) {
+            const int g = __builtin_ctz(gm);
+            gm &= gm - 1;
+            const f32x4 t = *reinterpret_cast<const f32x4*>(&L.bnd[g][4 * cq]);
+            v.x += t.x;
+            v.y += t.y;
+            v.z += t.z;
+            v.w += t.w;
+          }
           const uint32_t mk = mask >> (4 * u);
           v.x = (mk & 1u) ? v.x : 0.f;
           v.y = (mk & 2u) ? v.y : 0.f;
@@ -467,6 +493,8 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   if (stamps && threadIdx.x == 0) { st_[14] = __builtin_amdgcn_s_memrealtime(); st_[15] = nact; }
 #endif
 #undef BSTAMP
+#undef GSTAMP
+#undef ASTAMP
 }
 
 // out[j] = sum over slabs in fixed order: 128 columns per block (lanes hold

@@ -81,7 +81,7 @@ def main():
     grads = [torch.empty_like(t) for t in (w1, b1, w2, b2, w3, b3, w4, b4)]
     nbb = lib.pcadv_feat_bwd_workspace_bytes(C, N)
     wsb = torch.empty(nbb, device=dev, dtype=torch.uint8)
-    sb = torch.zeros(C * T * 16, device=dev, dtype=torch.int64)
+    sb = torch.zeros(C * T * 32, device=dev, dtype=torch.int64)
     fb = lib.pcadv_feat_bwd_stamped
     fb.restype = ctypes.c_int
     bargs = [P(dg), P(gidx), P(pts), C, N, P(w1), P(b1), P(w2), P(b2), P(w3), P(w4), P(x3)] + \
@@ -89,7 +89,8 @@ def main():
     for _ in range(5):
         assert fb(*bargs) == 0
     torch.cuda.synchronize()
-    sbn = sb.view(C * T, 16).cpu().numpy().astype(np.int64)
+    sbw = sb.view(C * T, 32).cpu().numpy().astype(np.int64)
+    sbn = sbw[:, :16]
     cols = [c for c in range(1, 15) if (sbn[:, c] > 0).all()]
     summarize("k_feat_bwd_chunk thread 0", sbn, cols)
     nact = sbn[:, 15]
@@ -113,6 +114,14 @@ def main():
     for nm, a, b in zip(names, prev_cols, cur_cols):
         d = (sbn[:, b] - sbn[:, a]) * 10 / 1e3
         print(f"  batch1 {nm:12s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+    d = (sbw[:, 16] - sbn[:, 3]) * 10 / 1e3
+    print(f"  batch1 gather (wave 2, from the sort) median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+    for nm, a_, b_ in (("a: pts staged", 3, 24), ("a: conv1", 24, 25), ("a: conv2 MFMA", 25, 26),
+                       ("a: x2 written", 26, 4)):
+        ca = sbn[:, a_] if a_ < 16 else sbw[:, a_]
+        cb = sbn[:, b_] if b_ < 16 else sbw[:, b_]
+        d = (cb - ca) * 10 / 1e3
+        print(f"  batch1 {nm:14s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
     two = nact > 32
     if two.any():
         for nm, a, b in zip(names[3:], [8, 9, 10, 11, 12], [9, 10, 11, 12, 13]):
