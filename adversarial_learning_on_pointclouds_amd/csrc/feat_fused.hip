@@ -18,8 +18,8 @@
 //                 x_lo w_hi, f32 accumulate; relative error <= ~1.2e-5 of
 //                 sum|x w|) and the screening epilogue keeps each lane's top-2
 //                 (value, point) over the whole cloud in registers.  The tail
-//                 re-evaluates the winner (and the runner-up on near-ties) as an
-//                 exact f32 dot product, so gmax is f32 and the argmax follows
+//                 re-evaluates the winner and the runner-up as exact f32 dot
+//                 products and ranks them by those, so gmax is f32 and the argmax follows
 //                 the f32 values with the first index on ties (torch.max on
 //                 CPU).  The 128 MB conv4 output never exists.
 #include "common.h"
@@ -236,9 +236,10 @@ union C4Lds {
 // Screening keys: the f32 value mapped to an order-preserving int32 whose low
 // 6 bits are replaced by 63 - (the point's row inside its 64-point step, less
 // the lane-half offset 4 h), so v_max_i32 / v_med3_i32 keep the top-2 (value,
-// row) of a lane with the lower row first on equal truncated values.  The 6 dropped bits (2^-17 relative) sit far
-// inside the near-tie window the exact re-evaluation re-checks; NaN maps above
-// +inf as torch.max ranks it.
+// row) of a lane with the lower row first on equal truncated values.  The 6
+// dropped bits (2^-17 relative) only order the candidates, which the exact
+// re-evaluation then ranks by their f32 values; NaN maps above +inf as
+// torch.max ranks it.
 __device__ __forceinline__ int screen_key(float v, int lowc) {
   const int b = __float_as_int(v);
   const int ord = b ^ ((b >> 31) & 0x7fffffff);  // int order == float order
@@ -576,10 +577,14 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       a2 = na2;
     }
     if (a1 == 0x7fffffff) a1 = 0;
-    // screening error <= ~1.2e-5 sum|x w| (+2^-17 key truncation): anything
-    // within a far wider window of the winner is re-checked in exact f32 (the
-    // second row is the first again when there is no near-tie)
-    const bool near = a2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
+    // The screened top-2 are both re-evaluated as exact f32 dot products and
+    // ranked by those values, whatever their screened gap: the screening error
+    // (<= ~3 2^-16 sum_k |x_k w_k| from the dropped split products, plus the
+    // 2^-17 key truncation) scales with the channel's sum |x w|, which can dwarf
+    // a pooled value near 0, so no window on the screened values is safe.  (A
+    // third point within the screening error of the top two is not re-checked:
+    // DESIGN.md, Numerics.)
+    const bool near = a2 != 0x7fffffff;
     const int b2 = near ? a2 : a1;
     STAMP(4);
     // Exact dot products, eight lanes per row: in pass G lane l takes channel

@@ -611,8 +611,8 @@ k_colsum_fin(const float* __restrict__ part, int nchunk, int N, float* __restric
 
 // ---------------------------------------------------------------------------
 // max over points after a screened GEMM: merge the per-tile top-2 keys of each
-// (cloud, channel), re-evaluate the winner (and the runner-up on near-ties) as
-// an exact f32 dot product of the input row with the weight row, then apply
+// (cloud, channel), re-evaluate the winner and the runner-up as exact f32 dot
+// products of the input row with the weight row, rank them by those, then apply
 // the bias and the ReLU before the max (pointnet.py:301-303: relu(conv6) then
 // torch.max).  Eight lanes per row (octet DPP sums), as k_conv4_max's tail.
 // ---------------------------------------------------------------------------
@@ -690,7 +690,10 @@ k_max_combine(const int2* __restrict__ part, int T, int Npts, int C, int O,
     }
   }
   if (i1 == 0x7fffffff) i1 = 0;
-  const bool near = i2 != 0x7fffffff && !(v1 - v2 > 1e-3f * (fabsf(v1) + fabsf(v2)) + 1e-6f);
+  // both screened candidates are re-evaluated exactly and ranked by the exact
+  // values (the screening error scales with sum |x w|, not with the pooled
+  // value: no window on the screened gap is safe; see k_conv4_max)
+  const bool near = i2 != 0x7fffffff;
   const int j2 = near ? i2 : i1;
   // exact dots: lane part_lane of the octet takes terms part_lane*4 + 32 u
   const float* xr1 = x + (size_t)(c * Npts + i1) * ldx;

@@ -514,3 +514,46 @@ def test_cls_step_golden_g11_full_size():
     for nm, p in model.named_parameters():
         check_tensor_rel(fx, "grad." + nm, p.grad.cpu().numpy(), tol=5e-3)
         check_tensor_l2(fx, "grad." + nm, p.grad.cpu().numpy(), tol=2e-3)
+
+
+@pytest.mark.parametrize("w_scale,twin", [(1.0, 0.0), (64.0, 0.0), (64.0, 3e-6), (8.0, 1e-5)])
+def test_argmax_near_zero_max_heavy_cancellation(w_scale, twin):
+    """models/pointnet.py:129 (torch.max over points) on channels whose pooled
+    max sits at ~0 while sum_k |x_k w_k| is large: the clouds are near-copies
+    of one cloud and conv4's bias is minus the channel's mean max, so every
+    winner is a large cancellation.  The screened bf16 products are off by up
+    to ~1e-5 of sum |x w| there, far more than the pooled values; the exact
+    re-evaluation must still return the f32 argmax, up to true f32 ties
+    (values within 2^-18 sum |x w| of each other, judged in f64).  With twin
+    > 0 every odd point is its even neighbour moved by ~twin, so nearly every
+    channel's winner has a runner-up a few 1e-6 of sum |x w| below it."""
+    C, N = 24, 1024
+    G = onp.make_params(onp.cls_spec(40), seed=41)
+    G["feat.conv4.weight"] = (G["feat.conv4.weight"] * np.float32(w_scale)).astype(np.float32)
+    base = _pts(42, 1, N)
+    if twin:
+        base[:, 1::2] = base[:, 0::2] + np.random.default_rng(44).normal(0, twin, base[:, 0::2].shape)
+    pts = (base + np.random.default_rng(43).normal(0, 1e-4, (C, N, 3))).astype(np.float32)
+    if twin:
+        pts[:, 1::2] = pts[:, 0::2] + (base[:, 1::2] - base[:, 0::2])
+    _, _, x3 = onp.point_mlp_fwd(pts, G)
+    W4 = G["feat.conv4.weight"][:, :, 0].astype(np.float64)
+    m = np.stack([(x3[c].astype(np.float64) @ W4.T).max(0) for c in range(C)])
+    G["feat.conv4.bias"] = (-m.mean(0)).astype(np.float32)
+    b4 = G["feat.conv4.bias"].astype(np.float64)
+    gmax, gidx, x3g = ops.feat_fwd(_t(pts), *_feat_weights(G))
+    gmax, gidx = gmax.cpu().numpy(), gidx.cpu().numpy()
+    assert np.array_equal(x3g.cpu().numpy(), x3) or rel_err(x3g.cpu().numpy(), x3) < 1e-5
+    x3 = x3g.cpu().numpy()  # judge the argmax on the activations the kernel pooled
+    bad = 0
+    for c in range(C):
+        X = x3[c].astype(np.float64)
+        Y = X @ W4.T + b4                      # exact (f64) conv4 outputs, N x O
+        S = np.abs(X) @ np.abs(W4).T            # sum_k |x_k w_k|
+        best = Y.max(0)
+        o = np.arange(Y.shape[1])
+        yg = Y[gidx[c], o]
+        tol = 2.0 ** -18 * S[gidx[c], o]
+        bad += int((yg < best - tol).sum())
+        assert np.all(np.abs(gmax[c] - yg) <= tol + 1e-30)
+    assert bad == 0, f"{bad} channels pooled at a point below the f32 max"
