@@ -18,11 +18,13 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 
-step pytest 900 python -m pytest tests -m gpu -q --timeout 300 -rf
+step pytest 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step trace 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_trace" -o run --output-format csv -- python bench.py --no-cpu --steps 50 --warmup 10
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/${tag}_pmc_fetch" -o run --output-format csv -- python bench.py --no-cpu --steps 3 --warmup 1
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/${tag}_pmc_write" -o run --output-format csv -- python bench.py --no-cpu --steps 3 --warmup 1
+# the adv bench line reads its traffic from the summary of these passes
+python tools/pmc_traffic.py "gpurun_out/${tag}_pmc_fetch" "gpurun_out/${tag}_pmc_write" "profiles/${tag}_pmc_traffic.json" > /dev/null
 step bench 600 python bench.py
 grep '"metric"' "gpurun_out/${tag}_bench.log"
 step trace_seg 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_trace_seg" -o run --output-format csv -- python bench.py --config seg --no-cpu --steps 5 --warmup 1

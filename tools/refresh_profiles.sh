@@ -19,4 +19,6 @@ python tools/kstats.py "$o/${tag}_trace_seg/run_kernel_trace.csv" > "$p/${tag}_s
 python tools/step_timeline.py "$o/${tag}_trace/run_kernel_trace.csv" > "$p/${tag}_step_timeline.txt"
 python tools/pmc_traffic.py "$o/${tag}_pmc_fetch" "$o/${tag}_pmc_write" "$p/${tag}_pmc_traffic.json" > /dev/null
 python tools/pmc_traffic.py "$o/${tag}_pmc_fetch_seg" "$o/${tag}_pmc_write_seg" "$p/${tag}_seg_pmc_traffic.json" > /dev/null
+cp "$o/${tag}_pytest.log" "$p/${tag}_pytest_gpu.log"
+cp "$o/${tag}_smoke.log" "$p/${tag}_smoke.log"
 echo "refreshed $p/${tag}_*"
