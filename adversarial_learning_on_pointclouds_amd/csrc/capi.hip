@@ -32,7 +32,7 @@ size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
                           const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
-                          hipStream_t, uint64_t* stamps = nullptr);
+                          hipStream_t, uint64_t* stamps = nullptr, int precision = 0);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t,
                       int add_identity_k = 0, float* mask_out = nullptr);
@@ -247,7 +247,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
                                G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s));
+                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   // fc2 + dropout: a device-drawn mask is stored for the backward
@@ -357,7 +357,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
                                G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s));
+                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
@@ -408,7 +408,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 4; }
+int pcadv_abi_version(void) { return 5; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -418,6 +418,14 @@ int pcadv_feat_fwd(const float* pts, int C, int N, const float* w1, const float*
                    void* workspace, size_t workspace_bytes, hipStream_t stream) {
   return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
                                nullptr, workspace, workspace_bytes, stream);
+}
+
+int pcadv_feat_fwd_bf16(const float* pts, int C, int N, const float* w1, const float* b1,
+                        const float* w2, const float* b2, const float* w3, const float* b3,
+                        const float* w4, const float* b4, float* x3, float* gmax, int32_t* gidx,
+                        void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
+                               nullptr, workspace, workspace_bytes, stream, nullptr, 1);
 }
 
 #ifdef PCADV_STAMPS

@@ -69,6 +69,9 @@ struct MlpLds {
 // on the bf16 matrix pipe as six products of the three-way splits of x2 and W3
 // (h h, h m, m h, h l, m m, l h; the dropped m l, l m, l l terms are < 2^-23 of
 // |x w|), f32 accumulate: f32-level accuracy at 6/16 of the f32 MFMA cycles.
+// NP3: conv3's bf16 products per f32 product: 6 (f32-level, the default) or 1
+// (bf16 mode: x2 and W3 rounded to bf16, f32 accumulate).
+template <int NP3>
 __global__ void __launch_bounds__(PM_T) __attribute__((amdgpu_waves_per_eu(2)))
 k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split, int N,
             int T, int ntiles, const float* __restrict__ w1, const float* __restrict__ b1,
@@ -171,13 +174,18 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
         for (int pt = 0; pt < 2; ++pt) {
           const int off = (32 * pt + r) * X2S + 16 * kb + 8 * h;
           const bf16x8 xh = *reinterpret_cast<const bf16x8*>(&L.x2[0][off]);
-          const bf16x8 xm = *reinterpret_cast<const bf16x8*>(&L.x2[1][off]);
-          const bf16x8 xl = *reinterpret_cast<const bf16x8*>(&L.x2[2][off]);
-          acc[pt] = mfma_bf16(xl, w3h[kb], acc[pt]);
-          acc[pt] = mfma_bf16(xm, w3m[kb], acc[pt]);
-          acc[pt] = mfma_bf16(xh, w3l[kb], acc[pt]);
-          acc[pt] = mfma_bf16(xm, w3h[kb], acc[pt]);
-          acc[pt] = mfma_bf16(xh, w3m[kb], acc[pt]);
+          bf16x8 xm{}, xl{};
+          if constexpr (NP3 == 6) {
+            xm = *reinterpret_cast<const bf16x8*>(&L.x2[1][off]);
+            xl = *reinterpret_cast<const bf16x8*>(&L.x2[2][off]);
+          }
+          if constexpr (NP3 == 6) {
+            acc[pt] = mfma_bf16(xl, w3h[kb], acc[pt]);
+            acc[pt] = mfma_bf16(xm, w3m[kb], acc[pt]);
+            acc[pt] = mfma_bf16(xh, w3l[kb], acc[pt]);
+            acc[pt] = mfma_bf16(xm, w3h[kb], acc[pt]);
+            acc[pt] = mfma_bf16(xh, w3m[kb], acc[pt]);
+          }
           acc[pt] = mfma_bf16(xh, w3h[kb], acc[pt]);
         }
       }
@@ -328,6 +336,11 @@ __device__ __forceinline__ void pair_merge(int n1, int u1, int n2, int u2, int& 
   t1 = a ? u1 : t1;
 }
 
+// NP4: conv4's bf16 products per f32 product: 3 (f32-level screening + the exact
+// f32 re-evaluation of the top two, the default) or 1 (bf16 mode: x3 and W4
+// rounded to bf16, f32 accumulate; the screened winner is the result, no
+// re-evaluation: gmax carries the 2^-17 key truncation).
+template <int NP4>
 __global__ void __launch_bounds__(C4_T)
 k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
             const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
@@ -377,8 +390,10 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf][1][srow * C4_SB + sk]);
     dh[0] = hi[0];
     dh[1] = hi[1];
-    dl[0] = lo[0];
-    dl[1] = lo[1];
+    if constexpr (NP4 == 3) {
+      dl[0] = lo[0];
+      dl[1] = lo[1];
+    }
   };
   stage_load(0);
   // W4 rows of this wave's 32 channels: coalesced 1 KB loads into the wave's
@@ -455,7 +470,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     bf16x8 fa[3][2];  // A fragments, a 3-deep register ring: [k-block % 3][hi, lo]
     auto frag = [&](int kb) {
       fa[kb % 3][0] = *reinterpret_cast<const bf16x8*>(xh + 16 * kb);
-      fa[kb % 3][1] = *reinterpret_cast<const bf16x8*>(xl + 16 * kb);
+      if constexpr (NP4 == 3) fa[kb % 3][1] = *reinterpret_cast<const bf16x8*>(xl + 16 * kb);
     };
     frag(0);
     frag(1);
@@ -465,9 +480,12 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     for (int kb = 0; kb < 8; ++kb) {
       __builtin_amdgcn_sched_barrier(0);
       if (kb + 2 < 8) frag(kb + 2);  // two k-blocks (six MFMAs) ahead of its use
-      const bf16x8 ah = fa[kb % 3][0], al = fa[kb % 3][1];
-      cur = mfma_bf16(al, bh[kb], cur);
-      cur = mfma_bf16(ah, bl[kb], cur);
+      const bf16x8 ah = fa[kb % 3][0];
+      const bf16x8 al = NP4 == 3 ? fa[kb % 3][1] : bf16x8{};
+      if constexpr (NP4 == 3) {
+        cur = mfma_bf16(al, bh[kb], cur);
+        cur = mfma_bf16(ah, bl[kb], cur);
+      }
       cur = mfma_bf16(ah, bh[kb], cur);
       if constexpr (decltype(SCREEN)::value && decltype(MASKED)::value) {
         screen_unit(prev, uprev, MASKED, kb, kb + 1, k1, k2);
@@ -493,17 +511,20 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
           const float v = stg[j >> 2][j & 3];
           const __bf16 hb = (__bf16)v;
           shi[j >> 3][j & 7] = hb;
-          slo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
+          if constexpr (NP4 == 3) slo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
         }
-        asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
+        if constexpr (NP4 == 3) asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
+        else asm volatile("" ::"v"(shi[kb >> 1]));
       }
       if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb == 4) {  // the next step's tile (buffer free since the barrier)
         bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][srow * C4_SB + sk]);
         bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][srow * C4_SB + sk]);
         dh[0] = shi[0];
         dh[1] = shi[1];
-        dl[0] = slo[0];
-        dl[1] = slo[1];
+        if constexpr (NP4 == 3) {
+          dl[0] = slo[0];
+          dl[1] = slo[1];
+        }
       }
       // tile s + 2 into the staging registers just freed (clamped: past the
       // end it re-reads the last row): 1.5 units ahead of its conversion
@@ -530,11 +551,13 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   const int oc = lane >> 3, part = lane & 7;
   const float* wbase = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128 + 16 * part;
   f32x4 wv[4][4];
+  if constexpr (NP4 == 3) {
 #pragma unroll
-  for (int G = 0; G < 4; ++G)
+    for (int G = 0; G < 4; ++G)
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)(8 * G + oc) * 128 + 4 * u);
+      for (int u = 0; u < 4; ++u)
+        wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)(8 * G + oc) * 128 + 4 * u);
+  }
   {  // the last unit
     int k1 = KEY_NONE, k2 = KEY_NONE;
     screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2);
@@ -584,6 +607,13 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     // a pooled value near 0, so no window on the screened values is safe.  (A
     // third point within the screening error of the top two is not re-checked:
     // DESIGN.md, Numerics.)
+    if constexpr (NP4 == 1) {  // bf16 mode: the screened winner and its value
+      if (h == 0) {
+        gmax[(size_t)c * C4_O + o] = v1 + b4[o];
+        gidx[(size_t)c * C4_O + o] = a1;
+      }
+      return;
+    }
     const bool near = a2 != 0x7fffffff;
     const int b2 = near ? a2 : a1;
     STAMP(4);
@@ -646,21 +676,18 @@ size_t feat_fwd_workspace_bytes(int C, int N) {
   return 256;  // no scratch: kept so callers can size a shared workspace
 }
 
-int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int C, int N,
-                          const float* w1, const float* b1, const float* w2, const float* b2,
-                          const float* w3, const float* b3, const float* w4, const float* b4,
-                          float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
-                          size_t ws_bytes, hipStream_t s, uint64_t* stamps) {
-  (void)ws;
-  (void)ws_bytes;
-  PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
-  PC_REQUIRE((size_t)C * 4 <= 0x7fffffff / 1, "feat_fwd: too many clouds (%d)", C);
+template <int NP3, int NP4>
+static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split, int C, int N,
+                              const float* w1, const float* b1, const float* w2, const float* b2,
+                              const float* w3, const float* b3, const float* w4, const float* b4,
+                              float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter,
+                              hipStream_t s, uint64_t* stamps) {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(C4Lds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(MlpLds)) != hipSuccess) {
       set_error("feat_fwd: cannot reserve LDS (%zu / %zu bytes)", sizeof(C4Lds), sizeof(MlpLds));
@@ -670,14 +697,33 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
   }
   const int T = (N + PM_P - 1) / PM_P;
   const int ntiles = C * T;
-  hipLaunchKernelGGL(k_point_mlp, dim3((ntiles + PM_TPW - 1) / PM_TPW), dim3(PM_T), sizeof(MlpLds),
-                     s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3, inc_counter,
-                     stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr);
+  hipLaunchKernelGGL(k_point_mlp<NP3>, dim3((ntiles + PM_TPW - 1) / PM_TPW), dim3(PM_T),
+                     sizeof(MlpLds), s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3,
+                     x3, inc_counter, stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
-  hipLaunchKernelGGL(k_conv4_max, dim3(C * (C4_O / C4_CB)), dim3(C4_T), sizeof(C4Lds), s, x3, C,
-                     N, w4, b4, gmax, gidx, stamps);
+  hipLaunchKernelGGL(k_conv4_max<NP4>, dim3(C * (C4_O / C4_CB)), dim3(C4_T), sizeof(C4Lds), s, x3,
+                     C, N, w4, b4, gmax, gidx, stamps);
   PC_HIP_CHECK_LAUNCH("k_conv4_max");
   return PCADV_OK;
+}
+
+// precision 0: f32-level (conv3 six bf16 products, conv4 three + the exact
+// re-evaluation); 1: bf16 (one product each, the screened winner as is)
+int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int C, int N,
+                          const float* w1, const float* b1, const float* w2, const float* b2,
+                          const float* w3, const float* b3, const float* w4, const float* b4,
+                          float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
+                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int precision) {
+  (void)ws;
+  (void)ws_bytes;
+  PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
+  PC_REQUIRE((size_t)C * 4 <= 0x7fffffff / 1, "feat_fwd: too many clouds (%d)", C);
+  PC_REQUIRE(precision == 0 || precision == 1, "feat_fwd: precision %d (0 fp32, 1 bf16)", precision);
+  if (precision == 1)
+    return launch_feat_fwd_np<1, 1>(pts_a, pts_b, split, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3,
+                                    gmax, gidx, inc_counter, s, stamps);
+  return launch_feat_fwd_np<6, 3>(pts_a, pts_b, split, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3,
+                                  gmax, gidx, inc_counter, s, stamps);
 }
 
 }  // namespace pcadv

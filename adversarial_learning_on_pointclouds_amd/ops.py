@@ -41,8 +41,14 @@ def _mat(w):
 # PointNetfeat (feature_transform=False)
 # ---------------------------------------------------------------------------
 
-def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4):
-    """pts (C, N, 3) -> gmax (C, 1024), gidx (C, 1024) int32, x3 (C, N, 128)."""
+PRECISIONS = {"fp32": 0, "bf16": 1}
+
+
+def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4, precision="fp32"):
+    """pts (C, N, 3) -> gmax (C, 1024), gidx (C, 1024) int32, x3 (C, N, 128).
+    precision "bf16": conv3 / conv4 on bf16-rounded operands (pcadv_feat_fwd_bf16)."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}")
     lib = _lib.load()
     _req(pts, "pts")
     if pts.dim() != 3 or pts.shape[2] != 3:
@@ -58,8 +64,9 @@ def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4):
     gidx = torch.empty(C, 1024, device=dev, dtype=torch.int32)
     nbytes = lib.pcadv_feat_fwd_workspace_bytes(C, N)
     work = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-    check(lib.pcadv_feat_fwd(ptr(pts), C, N, *[ptr(t) for t in ws], ptr(x3), ptr(gmax), ptr(gidx),
-                             ptr(work), nbytes, stream_ptr()), "pcadv_feat_fwd")
+    fn = lib.pcadv_feat_fwd_bf16 if precision == "bf16" else lib.pcadv_feat_fwd
+    check(fn(ptr(pts), C, N, *[ptr(t) for t in ws], ptr(x3), ptr(gmax), ptr(gidx),
+             ptr(work), nbytes, stream_ptr()), "pcadv_feat_fwd")
     return gmax, gidx, x3
 
 

@@ -43,6 +43,14 @@ def _views(flat, module, layout):
             for name, off in layout.items()}
 
 
+def _precision(name):
+    """Feature-forward precision code of pcadv_adv_args.precision."""
+    codes = {"fp32": 0, "bf16": 1}
+    if name not in codes:
+        raise ValueError(f"precision {name!r}: one of {sorted(codes)}")
+    return codes[name]
+
+
 def _align(nbytes):
     return (nbytes + 255) // 256 * 256
 
@@ -95,9 +103,10 @@ class AdvTrainStep:
 
     def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
                  lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
-                 seed=0, device="cuda", lambda_semi=1.0, semi_th=0.8):
+                 seed=0, device="cuda", lambda_semi=1.0, semi_th=0.8, precision="fp32"):
         self.lib = _lib.load()
         self.model, self.model_D = model, model_D
+        self.precision = _precision(precision)
         self.B, self.N = int(B), int(N)
         dev = torch.device(device)
         if dev.type != "cuda":
@@ -184,6 +193,7 @@ class AdvTrainStep:
         a.semi = int(bool(semi))
         a.lambda_semi, a.semi_th = hp["lambda_semi"], hp["semi_th"]
         a.part = int(part)
+        a.precision = self.precision
         return a
 
     # gradients that are final before the feature backward: g_grad[G_FC1_W:] and
@@ -306,12 +316,15 @@ class ClsTrainStep:
     PointNetCls(k=40, feature_transform=False): forward on B labelled clouds,
     lambda_cls * CrossEntropyLoss, backward, Adam - one pcadv_cls_step call
     (BASELINE configs[1]).  Parameters, gradients and Adam moments are flat
-    buffers as in AdvTrainStep; returns the device tensor [loss_cls]."""
+    buffers as in AdvTrainStep; returns the device tensor [loss_cls].
+    precision="bf16": the feature forward's conv3 / conv4 on bf16-rounded
+    operands (configs[1] is quoted in bf16); everything else f32."""
 
     def __init__(self, model, B, N, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 lambda_cls=1.0, seed=0, device="cuda"):
+                 lambda_cls=1.0, seed=0, device="cuda", precision="fp32"):
         self.lib = _lib.load()
         self.model = model
+        self.precision = _precision(precision)
         self.B, self.N = int(B), int(N)
         dev = torch.device(device)
         if dev.type != "cuda":
@@ -371,6 +384,7 @@ class ClsTrainStep:
         a.logits = self.logits.data_ptr()
         a.workspace = self.workspace.data_ptr()
         a.workspace_bytes = self.workspace.numel()
+        a.precision = self.precision
         return a
 
     def __call__(self, pts, labels, mask=None, apply_adam=True):

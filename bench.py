@@ -49,6 +49,9 @@ def parse():
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
                          "supervised PointNetCls step of configs[1]")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
+                    help="feature-forward precision (default: bf16 for --config cls, the dtype "
+                         "BASELINE configs[1] names; fp32 for adv and seg)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: start the --gpus ranks, form the process group, "
                          "print the JSON world/backend line; no GPU work")
@@ -230,7 +233,8 @@ def bench_cls(args):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = pc.PointNetCls(k=40).to(dev)
-    step = ClsTrainStep(model, B, N, seed=7, device=dev)
+    prec = args.precision or "bf16"
+    step = ClsTrainStep(model, B, N, seed=7, device=dev, precision=prec)
     pool = []
     for k in range(POOL):
         rng = np.random.default_rng(3000 + k)
@@ -252,11 +256,14 @@ def bench_cls(args):
         "value": round(B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32 (conv4 as three bf16 MFMA products, f32-level; configs[1] allows bf16)",
+        "dtype": ("bf16 (conv3 / conv4 MFMAs on bf16-rounded operands, f32 accumulate; conv1-2, "
+                  "head, losses, backward and Adam f32)" if prec == "bf16" else
+                  "fp32 (f32-level: conv3 / conv4 as bf16 split-product MFMAs, exact-f32 max "
+                  "winners)"),
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
         "config": {"workload": "run_training_pointnet_cls: PointNetCls(k=40), CE, Adam, B=32, "
                                "N=1024 (BASELINE configs[1])", "global_batch": B, "points": N,
-                   "parallelism": "dp1", "hip_graph": True},
+                   "parallelism": "dp1", "hip_graph": True, "precision": prec},
         "step_flops": {"gflop_per_step": gflop,
                        "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
@@ -439,7 +446,8 @@ def main():
     from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
 
     model, model_D = make_models(dev, seed=0)
-    step = AdvTrainStep(model, model_D, B, N, seed=1234 + rank, device=dev)
+    adv_prec = args.precision or "fp32"
+    step = AdvTrainStep(model, model_D, B, N, seed=1234 + rank, device=dev, precision=adv_prec)
     # PCADV_BENCH_OVERLAP=1 forces the bucketed all-reduce (the RCCL default) in a gloo rehearsal
     overlap = {"1": True, "0": False}.get(os.environ.get("PCADV_BENCH_OVERLAP", ""))
     runner = DataParallelAdvStep(step, overlap=overlap) if dist is not None else None
@@ -500,13 +508,13 @@ def main():
           model.feat.conv4.weight, model.feat.conv4.bias]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
-        ops.feat_fwd(pts_all, *fw)
+        ops.feat_fwd(pts_all, *fw, precision=adv_prec)
     torch.cuda.synchronize()
     reps = 50
     pair_graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(pair_graph):
         for _ in range(reps):
-            ops.feat_fwd(pts_all, *fw)
+            ops.feat_fwd(pts_all, *fw, precision=adv_prec)
     pair_graph.replay()  # warm
     torch.cuda.synchronize()
     ev0.record()
@@ -528,7 +536,8 @@ def main():
     f12 = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64)
     f3 = 2.0 * (2 * B) * N * (64 * 128)
     f4 = flops - f12 - f3
-    issued = f12 * (BF16_PEAK / F32_PEAK) + 6 * f3 + 3 * f4
+    np3, np4 = (6, 3) if adv_prec == "fp32" else (1, 1)  # bf16 products per f32 product
+    issued = f12 * (BF16_PEAK / F32_PEAK) + np3 * f3 + np4 * f4
     achieved = issued / kern_s / 1e12
     traffic, traffic_src = None, None
     prof = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
@@ -555,8 +564,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32 (f32-level: conv3/conv4 as bf16 split-product MFMAs, f32 accumulate, "
-                 "each max winner re-evaluated in exact f32)",
+        "dtype": ("fp32 (f32-level: conv3/conv4 as bf16 split-product MFMAs, f32 accumulate, "
+                  "each max winner re-evaluated in exact f32)" if adv_prec == "fp32" else
+                  "bf16 (conv3 / conv4 MFMAs on bf16-rounded operands, f32 accumulate; the rest f32)"),
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
         "config": {"workload": "adversarial cls step: PointNetCls(k=40)+DeepConvDiscNet(40,1), "
                                f"B=32 GT + 32 noGT clouds/GPU, N={N}, Adam x2",

@@ -94,15 +94,27 @@ int pcadv_abi_version(void);
  * One fused pass (conv1..conv4 + max): writes x3 [C][N][128] (post-ReLU conv3
  * output, read by the backward), gmax [C][1024] (x_global, pointnet.py:129-130,
  * an exact f32 dot product) and gidx [C][1024] (argmax over points, first index
- * on ties as torch.max on CPU).  conv1..conv3 are computed in f32; conv4 screens
- * the points with three bf16 MFMAs per product (|err| <= ~1.2e-5 sum|x w|) and
- * re-evaluates the winning point (and the runner-up on near-ties) in f32. */
+ * on ties as torch.max on CPU).  conv1/conv2 are computed in f32, conv3 as six
+ * bf16 split products (f32-level); conv4 screens the points with three bf16
+ * MFMAs per product (|err| <= ~3 2^-16 sum|x w|) and re-evaluates the top two
+ * points of every channel in exact f32, ranked by those values. */
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N);
 int pcadv_feat_fwd(const float* pts, int C, int N,
                    const float* w1, const float* b1, const float* w2, const float* b2,
                    const float* w3, const float* b3, const float* w4, const float* b4,
                    float* x3, float* gmax, int32_t* gidx,
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* pcadv_feat_fwd in bf16 mode (BASELINE configs[1]'s "bf16"): conv3 and conv4
+ * multiply bf16-rounded operands with f32 accumulation (one MFMA product each);
+ * gmax is the winner's bf16-product value (low 6 bits of its screening key
+ * dropped), gidx its point (first index on equal keys).  conv1/conv2 stay f32
+ * (the backward's recompute of x1/x2 is bitwise). */
+int pcadv_feat_fwd_bf16(const float* pts, int C, int N,
+                        const float* w1, const float* b1, const float* w2, const float* b2,
+                        const float* w3, const float* b3, const float* w4, const float* b4,
+                        float* x3, float* gmax, int32_t* gidx,
+                        void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Bytes of workspace pcadv_feat_bwd needs for C clouds of N points. */
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N);
@@ -361,6 +373,10 @@ typedef struct pcadv_adv_args {
    * 2 = the feature backward (those conv1..conv4 gradients; and both Adam
    *     updates when apply_adam) on the state part 1 left in the workspace. */
   int part;
+  /* feature forward precision: 0 = f32-level (default), 1 = bf16 (as
+   * pcadv_feat_fwd_bf16; the head, the discriminator and every backward stay
+   * f32).  ABI version 5. */
+  int precision;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

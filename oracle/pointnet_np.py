@@ -131,11 +131,25 @@ def relu(x):
 # generator: PointNetCls
 # --------------------------------------------------------------------------
 
-def point_mlp_fwd(pts, p, prefix="feat."):
+def bf16_round(a):
+    """Round an f32 array to bfloat16 (nearest, ties to even), returned as f32:
+    the operand rounding of the build's bf16 mode (a bf16 MFMA input)."""
+    u = np.ascontiguousarray(a, F32).view(np.uint32)
+    r = (u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) & np.uint32(0xFFFF0000)
+    return r.view(F32)
+
+
+def point_mlp_fwd(pts, p, prefix="feat.", precision="fp32"):
     """relu(conv1), relu(conv2), relu(conv3) as per-point matvecs
-    (models/pointnet.py:115-116,127).  pts: (B, N, 3)."""
+    (models/pointnet.py:115-116,127).  pts: (B, N, 3).  precision "bf16" (the
+    build's bf16 mode, not a reference behaviour): conv3's inputs and weights
+    rounded to bf16, the products summed exactly (f64) and rounded to f32."""
     def layer(x, i):
-        y = x @ _w(p, f"{prefix}conv{i}.weight").T
+        w = _w(p, f"{prefix}conv{i}.weight")
+        if precision == "bf16" and i == 3:
+            y = (bf16_round(x).astype(np.float64) @ bf16_round(w).astype(np.float64).T).astype(F32)
+        else:
+            y = x @ w.T
         y += p[f"{prefix}conv{i}.bias"]
         return np.maximum(y, F32(0), out=y)
     x1 = layer(pts, 1)
@@ -144,15 +158,20 @@ def point_mlp_fwd(pts, p, prefix="feat."):
     return x1, x2, x3
 
 
-def conv_max_fwd(x, w, b, relu_before_max=False):
+def conv_max_fwd(x, w, b, relu_before_max=False, precision="fp32"):
     """conv (1x1) then max over points, first index on ties
     (models/pointnet.py:128-130; torch.max(dim) returns the first maximal index
-    on CPU).  x: (B, N, K), w: (O, K).  Returns (gmax (B, O), argmax (B, O))."""
+    on CPU).  x: (B, N, K), w: (O, K).  Returns (gmax (B, O), argmax (B, O)).
+    precision "bf16": the conv on bf16-rounded x and w, products summed in f64."""
     B = x.shape[0]
     O = w.shape[0]
     N, K = x.shape[1], x.shape[2]
     # channel-major (O, B, N) from one GEMM, so the argmax runs along contiguous memory
-    y = w @ x.reshape(B * N, K).T
+    if precision == "bf16":
+        y = (bf16_round(w).astype(np.float64) @ bf16_round(x.reshape(B * N, K)).astype(np.float64).T
+             ).astype(F32)
+    else:
+        y = w @ x.reshape(B * N, K).T
     y += b[:, None]
     if relu_before_max:
         np.maximum(y, F32(0), out=y)
@@ -177,12 +196,15 @@ def head_fwd(g, p, mask=None, p_drop=0.3):
     return logits, (h1, h2, scale)
 
 
-def cls_forward(p, pts, mask=None):
+def cls_forward(p, pts, mask=None, precision="fp32"):
     """PointNetCls.forward (models/pointnet.py:197-203), feature_transform=False.
-    Returns logits (B, k), global (B, 1024) and a cache for cls_backward."""
+    Returns logits (B, k), global (B, 1024) and a cache for cls_backward.
+    precision "bf16": conv3 / conv4 as in point_mlp_fwd / conv_max_fwd (the
+    backward stays f32 on those activations)."""
     pts = np.ascontiguousarray(pts, F32)
-    x1, x2, x3 = point_mlp_fwd(pts, p)
-    gmax, am = conv_max_fwd(x3, _w(p, "feat.conv4.weight"), p["feat.conv4.bias"])
+    x1, x2, x3 = point_mlp_fwd(pts, p, precision=precision)
+    gmax, am = conv_max_fwd(x3, _w(p, "feat.conv4.weight"), p["feat.conv4.bias"],
+                            precision=precision)
     logits, hc = head_fwd(gmax, p, mask)
     cache = dict(pts=pts, x1=x1, x2=x2, x3=x3, gmax=gmax, am=am, head=hc)
     return logits, gmax, cache

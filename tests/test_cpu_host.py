@@ -24,7 +24,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
-    assert lib.pcadv_abi_version() == 4
+    assert lib.pcadv_abi_version() == 5
 
 
 def test_layout_matches_header_enums():

@@ -190,3 +190,23 @@ def test_g11_cls_full_size():
     grads = onp.cls_backward(G, cache, dlog)
     for k in G:
         check_tensor_rel(fx, "grad." + k, grads[k], tol=1e-4)
+
+
+def test_bf16_mode_oracle_close_to_reference_g11():
+    """The oracle's bf16 mode (conv3 / conv4 on bf16-rounded operands: the
+    build's configs[1] variant, not a reference behaviour) stays close to the
+    reference's fp32 outputs (g11): logits within 2e-2 of their scale, loss
+    within 1e-2."""
+    fx = load("g11_cls_b32.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    rng = np.random.default_rng(int(fx["data_seed"]))
+    B = int(fx["B"])
+    pts = rng.uniform(-1, 1, (B, int(fx["N"]), 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    mask = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    logits, gmax, _ = onp.cls_forward(G, pts, mask, precision="bf16")
+    scale = np.abs(fx["logits"]).max()
+    assert np.abs(logits - fx["logits"]).max() <= 2e-2 * scale
+    loss, _ = onp.cross_entropy(logits, lab)
+    assert abs(loss - float(fx["loss"])) < 1e-2
+    assert not np.array_equal(logits, fx["logits"])  # the mode does change the arithmetic
