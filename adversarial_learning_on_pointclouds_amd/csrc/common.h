@@ -25,6 +25,20 @@ __device__ __forceinline__ int acc_row(int r, int lane) {
   return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
 }
 
+// Kernel arguments are read by scalar loads at their first use, and a use that
+// sits behind a branch on another argument costs a further dependent round trip
+// to the kernarg segment (0.6-0.8 us each at the start of a launch, measured by
+// tools/lin_stamps.py).  Naming every argument a kernel reads at its entry lets
+// the compiler issue all of those loads together: one round trip.
+template <typename T>
+__device__ __forceinline__ void kernarg_pin(const T& v) {
+  asm volatile("" ::"s"(v));
+}
+template <typename... T>
+__device__ __forceinline__ void kernarg_prefetch(const T&... v) {
+  (kernarg_pin(v), ...);
+}
+
 // activation codes shared with the C ABI (include/pcadv.h)
 enum Act { ACT_NONE = PCADV_ACT_NONE, ACT_RELU = PCADV_ACT_RELU, ACT_LRELU = PCADV_ACT_LRELU };
 

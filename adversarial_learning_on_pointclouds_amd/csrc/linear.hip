@@ -12,6 +12,7 @@
 // tile instead.  Dropout masks and activation derivatives are applied where
 // the operands are loaded.
 #include "common.h"
+#include "wgrad.h"
 
 namespace pcadv {
 
@@ -57,7 +58,30 @@ struct GemmArgs {
   int ox_act;
   const float* ox_mask;
   float ox_keep;
+  int stamp_slot;  // diagnostic build: row of g_lin_stamps (-1: none)
 };
+
+#ifdef PCADV_STAMPS
+// diagnostic build only: wave 0's timestamps per block (s_memrealtime):
+// [launch][block][start, tile summed, partials met, end, operands landed, loads issued]
+__device__ uint64_t g_lin_stamps[16][256][6];
+#define LSTAMP(g, k)                                                            \
+  do {                                                                          \
+    if (threadIdx.x == 0 && (g).stamp_slot >= 0 && blockIdx.x < 256)            \
+      g_lin_stamps[(g).stamp_slot][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+static int g_lin_seq = 0;
+static int next_stamp_slot() { return g_lin_seq < 16 ? g_lin_seq++ : -1; }
+int lin_stamps_read(uint64_t* host, int reset) {
+  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lin_stamps), sizeof(g_lin_stamps)) != hipSuccess)
+    return PCADV_EHIP;
+  if (reset) g_lin_seq = 0;
+  return PCADV_OK;
+}
+#else
+#define LSTAMP(g, k) do { } while (0)
+static int next_stamp_slot() { return -1; }
+#endif
 
 // dropout scale s at (m, n) of an [M][N] output
 template <int DM>
@@ -152,6 +176,14 @@ __device__ __forceinline__ f32x4v wave_tile(const GemmArgs& g, int r0, int c0, i
 #pragma unroll
   for (int c = 0; c < NC; ++c)
     load_ab<OP, ACT, DM>(g, r0, c0, r, k0 + 16 * c + 4 * q, c < nch, step, a[c], b[c]);
+#ifdef PCADV_STAMPS
+  if (OP != OP_BWD_WEIGHT) {
+    asm volatile("" ::: "memory");
+    LSTAMP(g, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LSTAMP(g, 4);
+  }
+#endif
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -165,11 +197,67 @@ __device__ __forceinline__ f32x4v wave_tile(const GemmArgs& g, int r0, int c0, i
   return acc;
 }
 
+// Backward-data tile with dz stored as is (ACT_NONE, DM_NONE, N % 4 == 0):
+// the B operand W[n][c0 + r] is a column walk of W, which as one 4-byte load
+// per MFMA costs a vector-memory instruction per 256 bytes (issue-bound at the
+// start of a launch: tools/lin_stamps.py).  The wave instead fetches its
+// 16*NC x 16 block of W as 16-byte row pieces, parks it in its own LDS
+// region and reads the fragments from there.  Same operands, same MFMA order:
+// bitwise the result of wave_tile<OP_BWD_DATA>.
+constexpr int BT_S = 20;                // LDS row stride (floats): conflict-free fragment reads
+constexpr int BT_WAVE = 16 * SPLITC * BT_S;
+constexpr int BT_MAXS = 8;              // waves per block with an LDS region
+template <int NC>
+__device__ __forceinline__ f32x4v wave_tile_bdt(const GemmArgs& g, int r0, int c0, int k0, int nch,
+                                                int lane, float* bt, f32x4v acc) {
+  const int r = lane & 15, q = lane >> 4;
+  const int m = r0 + r;
+  float a[NC][4];
+  f32x4v wv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int kk = k0 + 16 * c + 4 * q;
+    const bool va = c < nch && m < g.M && kk < g.N;
+    const f32x4v av = *reinterpret_cast<const f32x4v*>(g.dy + (size_t)(va ? m : 0) * g.N +
+                                                       (va ? kk : 0));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[c][j] = va ? av[j] : 0.f;
+    // W rows n = k0 + 16c + lane/4, columns c0 + 4 (lane & 3) .. + 3
+    const int n = k0 + 16 * c + (lane >> 2), kc = c0 + 4 * (lane & 3);
+    const bool vb = c < nch && n < g.N && kc < g.K;
+    const f32x4v w = *reinterpret_cast<const f32x4v*>(g.w + (size_t)(vb ? n : 0) * g.K +
+                                                      (vb ? kc : 0));
+    wv[c] = vb ? w : f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+#ifdef PCADV_STAMPS
+  asm volatile("" ::: "memory");
+  LSTAMP(g, 5);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  LSTAMP(g, 4);
+#endif
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    *reinterpret_cast<f32x4v*>(bt + (16 * c + (lane >> 2)) * BT_S + 4 * (lane & 3)) = wv[c];
+  // the wave's own lanes read what the others wrote
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma16(a[c][j], bt[(16 * c + 4 * q + j) * BT_S + r], acc);
+  }
+  // the region is rewritten by the next round of the same wave
+  __builtin_amdgcn_wave_barrier();
+  return acc;
+}
+
 // Split-reduction job (forward, backward-data): block = one 16x16 tile, wave w
 // takes reduction slice w.  Tiles are numbered row-major over (rows, cols).
+// bt: LDS regions for wave_tile_bdt (backward data, dz as is), or nullptr.
 template <int OP, int ACT, int DM>
 __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R, int S, int L,
-                          float* red) {
+                          float* red, float* bt = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t step = DM == DM_RNG ? (uint32_t)*g.drop.step : 0u;
   const int ctiles = (cols + 15) / 16;
@@ -182,13 +270,18 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
     int nch = 0;
     if (kb < R) nch = min(min(L - base, 16 * SPLITC), R - kb + 15) / 16;
     float s;
-    acc = wave_tile<OP, SPLITC, ACT, DM>(g, r0, c0, kb, nch, lane, step, &s, acc);
+    if (OP == OP_BWD_DATA && ACT == ACT_NONE && DM == DM_NONE && bt)
+      acc = wave_tile_bdt<SPLITC>(g, r0, c0, kb, nch, lane, bt + wave * BT_WAVE, acc);
+    else
+      acc = wave_tile<OP, SPLITC, ACT, DM>(g, r0, c0, kb, nch, lane, step, &s, acc);
   }
+  LSTAMP(g, 1);
   const int col = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[wave * 256 + (4 * q + j) * 16 + col] = acc[j];
   __syncthreads();
-  for (int e = tid; e < 256; e += blockDim.x) {
+  LSTAMP(g, 2);
+  for (int e = tid; e < 256; e += 64 * S) {
     const int row = e >> 4, cc = e & 15;
     float v = 0.f;
     for (int w = 0; w < S; ++w) v += red[w * 256 + e];
@@ -223,6 +316,13 @@ template <int ACT, int DM>
 __device__ void weight_job(const GemmArgs& g, int tile, int ntiles_total) {
   const int lane = threadIdx.x & 63;
   if (tile >= ntiles_total) return;
+  if constexpr (ACT == ACT_NONE && DM == DM_NONE) {
+    // dz stored as is: the shared job code (wgrad.h), bitwise the same as the
+    // deferred jobs that ride along the feature backward
+    const WgradJob j{g.dy, g.x, g.dw, g.db, g.N, g.K, g.m_w, 0};
+    wgrad_wave(j, tile, lane);
+    return;
+  }
   const uint32_t step = DM == DM_RNG ? (uint32_t)*g.drop.step : 0u;
   const int ctiles = (g.K + 15) / 16;
   const int r0 = (tile / ctiles) * 16, c0 = (tile % ctiles) * 16;
@@ -250,7 +350,11 @@ template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
 k_linear_fwd(GemmArgs g, int S, int L) {
   __shared__ float red[16 * 256];
+  kernarg_prefetch(g.x, g.w, g.b, g.y, g.M, g.N, g.K, g.diag, S, L);
+  if (DM != DM_NONE) kernarg_prefetch(g.drop.mask, g.drop.step, g.drop.seed, g.drop.p, g.mask_out);
+  LSTAMP(g, 0);
   split_job<OP_FWD, ACT, DM>(g, blockIdx.x, g.M, g.N, g.K, S, L, red);
+  LSTAMP(g, 3);
 }
 
 // Independent work that rides along a backward launch (saves a dependent
@@ -264,27 +368,62 @@ struct BwdExtra {
   int red_n, red_cnt;
 };
 
-// blocks [0, nbx): dx tiles (split over S waves); then dw tiles (S per block);
-// then the extra weight tiles; then the slab reduction
+// The weight-gradient blocks of a launch: the block-level LDS-staged form
+// (wgrad.h) where the layer allows it, else one tile per wave.
+static bool wgrad_block_mode(int act, int dm, int N, int K, int S) {
+  return act == ACT_NONE && dm == DM_NONE && (N & 3) == 0 && (K & 3) == 0 && S >= WGB_MIN_WAVES;
+}
+
+// LDS of the <ACT_NONE, DM_NONE> instance: the backward-data blocks' W regions
+// + partials, or a weight-gradient block's staged operands
+constexpr int LB_RED = 16 * 256;
+constexpr int LB_LDS = BT_MAXS * BT_WAVE + LB_RED > WGB_LDS_FLOATS ? BT_MAXS * BT_WAVE + LB_RED
+                                                                   : WGB_LDS_FLOATS;
+
+// blocks [0, nbx): dx tiles (split over S waves); then dw tiles (S per block,
+// or one 64x32 region per block in block mode, wmode bit 0); then the extra
+// weight tiles (block mode: wmode bit 1); then the slab reduction
 template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
-k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0) {
-  __shared__ float red[16 * 256];
-  const int b = blockIdx.x + blk0, nbw = (nwt + S - 1) / S, nbw2 = (ex.nwt2 + S - 1) / S;
+k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, int wmode) {
+  kernarg_prefetch(g.x, g.w, g.dy, g.dx, g.dw, g.db, g.M, g.N, g.K, g.m_w, g.ox_act, g.ox_mask,
+                   g.ox_keep, S, L, nbx, nwt, blk0, ex.nwt2, ex.g2.x, ex.g2.dy, ex.g2.dw, ex.g2.db,
+                   ex.g2.M, ex.g2.N, ex.g2.K, ex.g2.m_w, ex.red_src, ex.red_dst, ex.red_n,
+                   ex.red_cnt, wmode);
+  if (ACT != ACT_NONE) kernarg_prefetch(g.yact);
+  if (DM != DM_NONE) kernarg_prefetch(g.drop.mask, g.drop.step, g.drop.seed, g.drop.p);
+  constexpr bool FAST = ACT == ACT_NONE && DM == DM_NONE;
+  __shared__ __attribute__((aligned(16))) float lds[FAST ? LB_LDS : LB_RED];
+  float* red = FAST ? lds + BT_MAXS * BT_WAVE : lds;
+  const int nbw = (wmode & 1) ? wgrad_regions(g.N, g.K) : (nwt + S - 1) / S;
+  const int nbw2 = (wmode & 2) ? wgrad_regions(ex.g2.N, ex.g2.K) : (ex.nwt2 + S - 1) / S;
+  const int b = blockIdx.x + blk0;
+  LSTAMP(g, 0);
   if (b < nbx) {
-    split_job<OP_BWD_DATA, ACT, DM>(g, b, g.M, g.K, g.N, S, L, red);
+    const bool use_bt = FAST && S <= BT_MAXS && (g.N & 3) == 0;
+    split_job<OP_BWD_DATA, ACT, DM>(g, b, g.M, g.K, g.N, S, L, red, use_bt ? lds : nullptr);
   } else if (b < nbx + nbw) {
-    weight_job<ACT, DM>(g, (b - nbx) * S + (threadIdx.x >> 6), nwt);
+    if (FAST && (wmode & 1)) {
+      if (nwt > 0) wgrad_region(WgradJob{g.dy, g.x, g.dw, g.db, g.N, g.K, g.m_w, 0}, b - nbx, lds, S);
+    } else {
+      weight_job<ACT, DM>(g, (b - nbx) * S + (threadIdx.x >> 6), nwt);
+    }
   } else if (b < nbx + nbw + nbw2) {
-    weight_job<ACT_NONE, DM_NONE>(ex.g2, (b - nbx - nbw) * S + (threadIdx.x >> 6), ex.nwt2);
+    if (FAST && (wmode & 2)) {
+      wgrad_region(WgradJob{ex.g2.dy, ex.g2.x, ex.g2.dw, ex.g2.db, ex.g2.N, ex.g2.K, ex.g2.m_w, 0},
+                   b - nbx - nbw, lds, S);
+    } else {
+      weight_job<ACT_NONE, DM_NONE>(ex.g2, (b - nbx - nbw) * S + (threadIdx.x >> 6), ex.nwt2);
+    }
   } else {
-    const int j = (b - nbx - nbw - nbw2) * blockDim.x + threadIdx.x;
+    const int j = (b - nbx - nbw - nbw2) * 64 * S + threadIdx.x;
     if (j < ex.red_n) {
       float acc = 0.f;
       for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_n + j];
       ex.red_dst[j] = acc;
     }
   }
+  LSTAMP(g, 3);
 }
 
 // host-side dispatch over the (activation, dropout-source) instantiations
@@ -336,6 +475,7 @@ int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, 
   split_cfg(K, &S, &L);
   PC_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU, "linear_fwd: bad act %d", act);
   const int tiles = ((M + 15) / 16) * ((N + 15) / 16);
+  g.stamp_slot = next_stamp_slot();
   launch_variant<FwdK>(act, drop_mode(g.drop), dim3(tiles), dim3(64 * S), s, g, S, L);
   PC_HIP_CHECK_LAUNCH("k_linear_fwd");
   return PCADV_OK;
@@ -366,7 +506,10 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   split_cfg(N, &S, &L);
   const int nbx = dx ? ((M + 15) / 16) * ((K + 15) / 16) : 0;
   const int nwt = dw ? ((N + 15) / 16) * ((K + 15) / 16) : 0;
-  const int nbw = (nwt + S - 1) / S;
+  const int dm = drop_mode(g.drop);
+  int wmode = 0;
+  if (nwt > 0 && wgrad_block_mode(act, dm, N, K, S)) wmode |= 1;
+  const int nbw = nwt == 0 ? 0 : (wmode & 1) ? wgrad_regions(N, K) : (nwt + S - 1) / S;
   BwdExtra ex{};
   int nbe = 0;
   if (extra) {
@@ -380,7 +523,12 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
       g2.dw = e.dw; g2.db = e.db;
       g2.M = e.M; g2.N = e.N; g2.K = e.K; g2.m_w = e.m_w;
       ex.nwt2 = ((e.N + 15) / 16) * ((e.K + 15) / 16);
-      nbe += (ex.nwt2 + S - 1) / S;
+      if (act == ACT_NONE && dm == DM_NONE && wgrad_block_mode(ACT_NONE, DM_NONE, e.N, e.K, S)) {
+        wmode |= 2;
+        nbe += wgrad_regions(e.N, e.K);
+      } else {
+        nbe += (ex.nwt2 + S - 1) / S;
+      }
     }
     if (extra->red_src) {
       PC_REQUIRE(extra->red_dst && extra->red_n > 0 && extra->red_cnt > 0,
@@ -394,17 +542,9 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   }
   if (nbx + nbw + nbe == 0) return PCADV_OK;
   PC_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU, "linear_bwd: bad act %d", act);
-#ifdef PCADV_STAMPS
-  // diagnostic build: data-gradient tiles and the rest as separate launches
-  if (nbx > 0)
-    launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx), dim3(64 * S), s, g, S, L, nbx, nwt, ex, 0);
-  if (nbw + nbe > 0)
-    launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbw + nbe), dim3(64 * S), s, g, S, L, nbx, nwt,
-                         ex, nbx);
-#else
-  launch_variant<BwdK>(act, drop_mode(g.drop), dim3(nbx + nbw + nbe), dim3(64 * S), s, g, S, L,
-                       nbx, nwt, ex, 0);
-#endif
+  g.stamp_slot = next_stamp_slot();
+  launch_variant<BwdK>(act, dm, dim3(nbx + nbw + nbe), dim3(64 * S), s, g, S, L, nbx, nwt, ex, 0,
+                       wmode);
   PC_HIP_CHECK_LAUNCH("k_linear_bwd");
   return PCADV_OK;
 }

@@ -157,6 +157,29 @@ def test_linear_vs_torch(M, N, K, act):
     assert_grad_close(db.cpu().numpy(), br.grad.numpy(), "db", 1e-5, 1e-5)
 
 
+# dz stored as is (no activation, no dropout): the backward-data tiles take W
+# through LDS (csrc/linear.hip wave_tile_bdt) when N % 4 == 0 and the block has
+# <= 8 waves (N <= 512); the other shapes take the direct loads.  Edge tiles
+# (M, K not multiples of 16), multi-round slices (N > 1024) and both routes.
+@pytest.mark.parametrize("M,N,K", [(64, 512, 1024), (96, 256, 512), (96, 256, 256), (64, 40, 256),
+                                   (33, 76, 12), (20, 1100, 36), (17, 30, 20), (64, 2048, 64)])
+def test_linear_bwd_dz_as_is_vs_torch(M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    dy = torch.randn(M, N, generator=g)
+    dx_ref = dy @ w
+    y = torch.zeros(M, N)
+    dx, dw, db = ops.linear_bwd(dy.to(DEV), y.to(DEV), 0, None, 0.0, x.to(DEV), w.to(DEV))
+    assert_grad_close(dx.cpu().numpy(), dx_ref.numpy(), "dx", 1e-5, 1e-5)
+    assert_grad_close(dw.cpu().numpy(), (dy.T @ x).numpy(), "dw", 1e-5, 1e-5)
+    assert_grad_close(db.cpu().numpy(), dy.sum(0).numpy(), "db", 1e-5, 1e-5)
+    # data gradient alone (the launch the step's chain runs) is bitwise the same
+    dx2, _, _ = ops.linear_bwd(dy.to(DEV), y.to(DEV), 0, None, 0.0, x.to(DEV), w.to(DEV),
+                               need_dw=False)
+    assert torch.equal(dx, dx2)
+
+
 # ---------------------------------------------------------------------------
 # drop-in modules vs the reference's golden vectors
 # ---------------------------------------------------------------------------
