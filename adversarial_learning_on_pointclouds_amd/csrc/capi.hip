@@ -27,7 +27,7 @@ int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, in
                     const float*, const float*, const float*, const float*, const float*,
                     const float*, const float*, float*, float*, float*, float*, float*, float*,
                     float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr,
-                    const FinAdam* adam = nullptr);
+                    const FinAdam* adam = nullptr, const int* sortrec = nullptr);
 size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
@@ -51,13 +51,16 @@ int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, c
                  hipStream_t);
 int launch_inc(int32_t*, hipStream_t);
 size_t disc_tail_slab_floats();
+int disc_tail_slab_n();
 int head_rowblocks(int B);
 int disc_rowblocks(int B);
 int launch_head_fwd(const float*, const float*, const float*, const int64_t*, int, float, float*,
                     float*, float*, const float*, const float*, float*, float*, hipStream_t);
 int launch_disc_tail(const float*, int, const float*, const float*, const float*, const float*,
                      const float*, const float*, const float*, const float*, const int32_t*,
-                     uint64_t, float, float*, float*, float*, float*, hipStream_t);
+                     uint64_t, float, float*, float*, float*, float*, hipStream_t,
+                     const int32_t* gidx = nullptr, int C = 0, int N = 0, int* sortrec = nullptr);
+size_t feat_sort_record_ints(int C, int N);
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
 int lin_stamps_read(uint64_t* host, int reset);
@@ -102,6 +105,7 @@ struct StepWs {
   float *mask;
   float *lpart, *lpart3, *dslabs, *dout;
   int32_t* gidx;
+  int* sortrec;  // the feature backward's hit sort, done early (feat_sort.h)
   void* feat_ws;
   size_t feat_ws_bytes;
   size_t total;
@@ -140,6 +144,7 @@ static StepWs carve(int B, int N, char* base) {
   w.lpart3 = take(3 * (size_t)disc_rowblocks(B));
   w.dslabs = take((size_t)disc_rowblocks(B) * disc_tail_slab_floats());
   w.dout = take(R);
+  w.sortrec = reinterpret_cast<int*>(take(feat_sort_record_ints((int)C, N)));
   w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
   if (feat_fwd_workspace_bytes((int)C, N) > w.feat_ws_bytes)
     w.feat_ws_bytes = feat_fwd_workspace_bytes((int)C, N);
@@ -216,7 +221,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr);
+                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec);
 }
 
 // Part 1 of adv_step: everything before the feature backward.
@@ -270,7 +275,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   PC_TRY(launch_disc_tail(w.d3, B, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, D + PCADV_D_CONV5_W,
                           D + PCADV_D_CONV5_B, D + PCADV_D_FC_W, D + PCADV_D_FC_B, a->soft_gt,
                           a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
-                          w.dout, s));
+                          w.dout, s, w.gidx, C, N, w.sortrec));
   // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
   //      input grads of all rows (rows [2B,3B) feed the generator, D frozen).
   //      Every data gradient is stored as the layer below's dz (its activation
@@ -282,7 +287,8 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
     LinBwdExtra ex{};  // + sum of the conv4/conv5/fc partial-gradient slabs
     ex.red_src = w.dslabs;
     ex.red_dst = gD + PCADV_D_CONV4_W;
-    ex.red_n = (int)disc_tail_slab_floats();
+    ex.red_n = disc_tail_slab_n();
+    ex.red_ld = (int)disc_tail_slab_floats();
     ex.red_cnt = disc_rowblocks(B);
     ex.dx_act = PCADV_ACT_LRELU;  // x = conv2 output
     PC_TRY(launch_linear_bwd(w.dd3, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.d2,

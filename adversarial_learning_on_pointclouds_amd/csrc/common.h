@@ -197,6 +197,7 @@ struct LinBwdExtra {
   const float* red_src;
   float* red_dst;
   int red_n, red_cnt;
+  int red_ld;  // floats between slabs (0: red_n)
   // data-gradient output mask: dx *= act'(x) (* dx_mask * dx_keep), dx then
   // being the layer below's dz (its backward runs with act NONE, no dropout)
   int dx_act;

@@ -20,6 +20,7 @@
 // Each workgroup writes its weight-gradient partials to its own slab;
 // k_feat_bwd_finish sums the slabs in a fixed order (no atomics) and gathers dW4.
 #include "common.h"
+#include "feat_sort.h"
 
 namespace pcadv {
 
@@ -65,13 +66,19 @@ struct BwdLds {
   alignas(16) float pts[BW_RB * 4];
 };
 
+static_assert(FS_PCH == BW_PCH && FS_MAXO == BW_MAXO && FS_T == BW_T, "feat_sort.h geometry");
+
+// PRE: phases 1-3 (the hit sort) were done ahead of this launch (feat_sort.h,
+// records at sortrec): load them and gather the hits' gradients instead.
+template <bool PRE>
 __global__ void __launch_bounds__(BW_T, 4)
 k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx, int O,
                  const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
                  int N, const float* __restrict__ w1, const float* __restrict__ b1,
                  const float* __restrict__ w2, const float* __restrict__ b2,
                  const float* __restrict__ w3, const float* __restrict__ w4,
-                 const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps) {
+                 const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps,
+                 const int* __restrict__ sortrec) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
 #ifdef PCADV_STAMPS
@@ -111,6 +118,47 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   // conv1 weights, fetched up front so they land during the hit sort
   const int ch1 = tid & 63;
   const float w1a = w1[ch1 * 3 + 0], w1b = w1[ch1 * 3 + 1], w1c = w1[ch1 * 3 + 2], b1v = b1[ch1];
+  int nact;
+  float ptv[2] = {0.f, 0.f};
+  if constexpr (PRE) {
+    // ---- 1-3 done ahead (feat_sort.h): one round of loads, the fixed-size
+    //      record and this cloud's pooled gradients, then g of each sorted hit
+    const int* rec = sortrec + ((size_t)c * gridDim.x + chunk) * FS_REC;
+    int so_v[2];
+    float dg_v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      so_v[u] = rec[FSR_SO + u * BW_T + tid];
+      dg_v[u] = dg[(size_t)c * O + u * BW_T + tid];
+    }
+    int rl_v = 0, ho_v = 0;
+    if (tid < BW_PCH) rl_v = rec[FSR_ROWS + tid];
+    if (tid <= BW_PCH) ho_v = rec[FSR_HOFF + tid];
+    nact = rec[0];
+    if (tid < BW_PCH) L.rows_list[tid] = rl_v;
+    if (tid <= BW_PCH) L.hoff[tid] = ho_v;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      L.so[u * BW_T + tid] = so_v[u];
+      L.hg[u * BW_T + tid] = dg_v[u];  // the cloud's gradient row, indexed by o
+    }
+    __syncthreads();
+    const int nhits = L.hoff[nact];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = u * BW_T + tid;
+      if (j < nhits) L.sg[j] = L.hg[L.so[j]];
+    }
+    if (wave < 2) {  // first batch's points (waves 0-1 hold all 96 coordinates)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = lane + 64 * u, row = e / 3;
+        if (e < BW_RB * 3 && row < nact) ptv[u] = pts[(size_t)(p0 + L.rows_list[row]) * 3 + e % 3];
+      }
+    }
+    __syncthreads();
+    BSTAMP(3);
+  } else {
   if (tid < BW_PCH) {
     L.rcnt[tid] = 0;
     L.fill[tid] = 0;
@@ -152,7 +200,8 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     L.roff[row] = v - cnt;  // wave-local for now
   }
   __syncthreads();
-  const int nact = L.wact[0] + L.wact[1], nhits = L.wsum[0] + L.wsum[1];
+  nact = L.wact[0] + L.wact[1];
+  const int nhits = L.wsum[0] + L.wsum[1];
   if (wave < 2) {
     const int row = tid;
     const bool f = L.rcnt[row] > 0;
@@ -168,7 +217,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   }
   // first batch's points, issued now (used after the sort): waves 0-1 each
   // hold all 96 coordinates (element lane + 64 u)
-  float ptv[2] = {0.f, 0.f};
   __syncthreads();
   if (wave < 2) {
 #pragma unroll
@@ -203,6 +251,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   }
   __syncthreads();
   BSTAMP(3);
+  }  // !PRE
 
   // register accumulators that live across batches
   f32x16 a_dw3 = {}, a_dw2 = {};
@@ -743,14 +792,17 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                     const float* b2, const float* w3, const float* w4, const float* x3,
                     float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
                     float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s,
-                    uint64_t* stamps, const FinAdam* adam) {
+                    uint64_t* stamps, const FinAdam* adam, const int* sortrec) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
   float* slabs = static_cast<float*>(ws);
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(BwdLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(BwdLds)) != hipSuccess) {
       set_error("feat_bwd: cannot reserve %zu bytes of LDS", sizeof(BwdLds));
@@ -758,8 +810,14 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
     }
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_feat_bwd_chunk, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg, gidx, O,
-                     pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps);
+  if (sortrec)
+    hipLaunchKernelGGL(k_feat_bwd_chunk<true>, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg,
+                       gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps,
+                       sortrec);
+  else
+    hipLaunchKernelGGL(k_feat_bwd_chunk<false>, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg,
+                       gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps,
+                       sortrec);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   PC_REQUIRE(dw4 && db4, "feat_bwd: dw4/db4 required");
   FinAdam fa{};

@@ -365,7 +365,7 @@ struct BwdExtra {
   int nwt2;
   const float* red_src;
   float* red_dst;
-  int red_n, red_cnt;
+  int red_n, red_cnt, red_ld;
 };
 
 // The weight-gradient blocks of a launch: the block-level LDS-staged form
@@ -389,7 +389,7 @@ k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, 
   kernarg_prefetch(g.x, g.w, g.dy, g.dx, g.dw, g.db, g.M, g.N, g.K, g.m_w, g.ox_act, g.ox_mask,
                    g.ox_keep, S, L, nbx, nwt, blk0, ex.nwt2, ex.g2.x, ex.g2.dy, ex.g2.dw, ex.g2.db,
                    ex.g2.M, ex.g2.N, ex.g2.K, ex.g2.m_w, ex.red_src, ex.red_dst, ex.red_n,
-                   ex.red_cnt, wmode);
+                   ex.red_cnt, ex.red_ld, wmode);
   if (ACT != ACT_NONE) kernarg_prefetch(g.yact);
   if (DM != DM_NONE) kernarg_prefetch(g.drop.mask, g.drop.step, g.drop.seed, g.drop.p);
   constexpr bool FAST = ACT == ACT_NONE && DM == DM_NONE;
@@ -419,7 +419,7 @@ k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, 
     const int j = (b - nbx - nbw - nbw2) * 64 * S + threadIdx.x;
     if (j < ex.red_n) {
       float acc = 0.f;
-      for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_n + j];
+      for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_ld + j];
       ex.red_dst[j] = acc;
     }
   }
@@ -531,12 +531,14 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
       }
     }
     if (extra->red_src) {
-      PC_REQUIRE(extra->red_dst && extra->red_n > 0 && extra->red_cnt > 0,
+      PC_REQUIRE(extra->red_dst && extra->red_n > 0 && extra->red_cnt > 0 &&
+                     (extra->red_ld == 0 || extra->red_ld >= extra->red_n),
                  "linear_bwd: bad extra reduction");
       ex.red_src = extra->red_src;
       ex.red_dst = extra->red_dst;
       ex.red_n = extra->red_n;
       ex.red_cnt = extra->red_cnt;
+      ex.red_ld = extra->red_ld ? extra->red_ld : extra->red_n;
       nbe += (ex.red_n + 64 * S - 1) / (64 * S);
     }
   }

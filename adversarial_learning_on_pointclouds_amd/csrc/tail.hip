@@ -21,6 +21,7 @@
 // f32), one reduction chunk of <= 128 per work item; items are spread over the
 // 16 waves and their partial tiles summed in a fixed order.
 #include "common.h"
+#include "feat_sort.h"
 
 namespace pcadv {
 
@@ -208,16 +209,21 @@ __device__ void rows_wgrad(const float* Z, int zs, const float* X, int xs, float
 // ---------------------------------------------------------------------------
 // k_head_fwd: rows m of the 2B generator outputs
 // ---------------------------------------------------------------------------
+// The discriminator conv1 outputs (512 columns) are split over HF_SPLIT
+// workgroups per row block; each recomputes fc3 and log_softmax of its 16 rows
+// (a fifth of the conv1 work), and split 0 alone writes the head's outputs.
+constexpr int HF_SPLIT = 4;
+constexpr int HF_COLS = 512 / HF_SPLIT;
 struct HeadFwdLds {
-  float w1[512 * 44];          // discriminator conv1 weight [512][40], padded rows
+  float w1[HF_COLS * 44];      // this split's rows of the D conv1 weight [512][40], padded
   float w3[40 * 260];          // fc3 weight [40][256], padded rows
-  float b1[512];
+  float b1[HF_COLS];
   float b3[40];
   alignas(16) float h2[TR * 260];
   float lg[TR * 44];
   float lsm[TR * 44];
   float rl[TR];
-  alignas(16) float scratch[6 * 256];
+  alignas(16) float scratch[12 * 256];
 };
 
 __global__ void __launch_bounds__(TT)
@@ -229,17 +235,20 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
   HeadFwdLds& L = *reinterpret_cast<HeadFwdLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   TSTAMP(0, 0);
-  const int C = 2 * B, r0 = blockIdx.x * TR, nrows = min(TR, C - r0);
+  const int rb = blockIdx.x / HF_SPLIT, sp = blockIdx.x % HF_SPLIT, j0 = sp * HF_COLS;
+  const int C = 2 * B, r0 = rb * TR, nrows = min(TR, C - r0);
   const int label = wave < nrows && r0 + wave < B ? (int)labels[r0 + wave] : 0;
   {
-    const Fill f[5] = {{L.w1, 44, dw1, 512, 40, 512}, {L.h2, 260, h2 + (size_t)r0 * 256, TR, 256, nrows},
-                       {L.b1, 512, db1, 1, 512, 1}, {L.b3, 40, b3, 1, 40, 1},
+    const Fill f[5] = {{L.w1, 44, dw1 + (size_t)j0 * 40, HF_COLS, 40, HF_COLS},
+                       {L.h2, 260, h2 + (size_t)r0 * 256, TR, 256, nrows},
+                       {L.b1, HF_COLS, db1 + j0, 1, HF_COLS, 1}, {L.b3, 40, b3, 1, 40, 1},
                        {L.w3, 260, w3, 40, 256, 40}};
-    lds_fill<5, 9>(f);  // 8842 float4: <= 9 per thread
+    lds_fill<5, 5>(f);  // 4362 float4: <= 5 per thread
   }
   __syncthreads();
   TSTAMP(0, 1);
-  rows_layer<256, 40, B_OK, ACT_NONE>(L.h2, 260, L.w3, 260, L.b3, L.lg, 44, L.scratch);
+  // reduction chunks of 64: twelve 16-MFMA chains instead of six of 32
+  rows_layer<256, 40, B_OK, ACT_NONE, 64>(L.h2, 260, L.w3, 260, L.b3, L.lg, 44, L.scratch);
   TSTAMP(0, 2);
   // log_softmax, CrossEntropy (GT rows), discriminator input rows: one wave per row
   {
@@ -255,12 +264,12 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
     const float lsm = (v - mx) - logf(se);
     if (lane < 40) L.lsm[row * 44 + lane] = lsm;
     float rloss = 0.f;
-    if (m < C && lane < 40) {
+    if (sp == 0 && m < C && lane < 40) {
       logits[(size_t)m * 40 + lane] = v;
       din[(size_t)m * 40 + lane] = lsm;
       if (m >= B) din[(size_t)(m + B) * 40 + lane] = lsm;
     }
-    if (m < B) {
+    if (sp == 0 && m < B) {
       const int y = label;
       const float sm = expf(lsm);
       if (lane < 40)
@@ -270,16 +279,17 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
     if (lane == 0) L.rl[row] = rloss;
   }
   __syncthreads();
-  if (tid == 0) {
+  if (sp == 0 && tid == 0) {
     float s = 0.f;
     for (int row = 0; row < TR; ++row) s += L.rl[row];
-    lpart[blockIdx.x] = s;
+    lpart[rb] = s;
   }
   // D conv1 on the GT rows (D rows [0,B)) and noGT rows (D rows [B,2B) and,
   // identical, [2B,3B)): rows r0.. of d1, copied to r0+B.. for noGT blocks
   TSTAMP(0, 3);
-  rows_layer<40, 512, B_OK, ACT_LRELU>(L.lsm, 44, L.w1, 44, L.b1, d1 + (size_t)r0 * 512, 512,
-                                       nullptr, nrows, max(0, B - r0), (long)B * 512);
+  rows_layer<40, HF_COLS, B_OK, ACT_LRELU>(L.lsm, 44, L.w1, 44, L.b1,
+                                           d1 + (size_t)r0 * 512 + j0, 512, nullptr, nrows,
+                                           max(0, B - r0), (long)B * 512);
   TSTAMP(0, 4);
 }
 
@@ -287,6 +297,7 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
 // k_disc_tail: rows m of the 3B discriminator rows
 // ---------------------------------------------------------------------------
 constexpr int DT_SLAB = 64 * 256 + 64 + 64 * 64 + 64 + 64 + 1;  // = gD[conv4.w .. fc.b]
+constexpr int DT_SLAB_LD = (DT_SLAB + 3) & ~3;  // slab stride: 16-byte aligned slabs
 
 struct DiscTailLds {
   float w4[64 * 260];          // conv4 weight [64][256], padded rows
@@ -310,12 +321,26 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
             const float* __restrict__ bf, const float* __restrict__ soft_gt,
             const float* __restrict__ soft_nogt, const int32_t* __restrict__ step, uint64_t seed,
             float lambda_adv, float* __restrict__ dd3, float* __restrict__ slabs,
-            float* __restrict__ lpart3, float* __restrict__ dout) {
+            float* __restrict__ lpart3, float* __restrict__ dout, const int32_t* __restrict__ gidx,
+            int C, int N, int* __restrict__ sortrec) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DiscTailLds& L = *reinterpret_cast<DiscTailLds*>(smem);
   const int tid = threadIdx.x;
+  const int R = 3 * B, nrb = (R + TR - 1) / TR;
+  if ((int)blockIdx.x >= nrb) {
+    // the feature backward's hit sort (feat_sort.h) on the CUs this launch
+    // leaves idle: two (cloud, chunk) records per workgroup, one per half
+    static_assert(TT == 2 * FS_T && sizeof(DiscTailLds) >= 2 * sizeof(SortLds), "sort geometry");
+    const int nch = (N + FS_PCH - 1) / FS_PCH, half = tid / FS_T;
+    const int id = 2 * ((int)blockIdx.x - nrb) + half, cc = id / nch, ch = id % nch;
+    SortLds& S = reinterpret_cast<SortLds*>(smem)[half];
+    const bool valid = cc < C;
+    chunk_sort(gidx + (size_t)(valid ? cc : 0) * FS_MAXO, FS_MAXO, ch * FS_PCH, tid % FS_T, valid,
+               S, sortrec + (size_t)id * FS_REC);
+    return;
+  }
   TSTAMP(1, 0);
-  const int R = 3 * B, r0 = blockIdx.x * TR, nrows = min(TR, R - r0);
+  const int r0 = blockIdx.x * TR, nrows = min(TR, R - r0);
   // per-row label inputs, fetched with the weights (thread t < 16: row r0 + t)
   float ysoft = 0.f;
   uint32_t stepv = 0;
@@ -409,7 +434,7 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
   }
   if (tid < TR && r0 + tid >= 2 * B) L.out[tid * 4 + 1] = 0.f;
   __syncthreads();
-  float* slab = slabs + (size_t)blockIdx.x * DT_SLAB;
+  float* slab = slabs + (size_t)blockIdx.x * DT_SLAB_LD;
   TSTAMP(1, 9);
   rows_wgrad<64, 256>(L.z4, 68, L.x3, 260, slab, slab + 64 * 256);
   rows_wgrad<64, 64>(L.z5, 68, L.a4, 68, slab + 64 * 256 + 64, slab + 64 * 256 + 64 + 4096);
@@ -648,7 +673,8 @@ static int set_lds(K kern, size_t bytes, const char* what) {
   return PCADV_OK;
 }
 
-size_t disc_tail_slab_floats() { return DT_SLAB; }
+size_t disc_tail_slab_floats() { return DT_SLAB_LD; }  // per row block (stride)
+int disc_tail_slab_n() { return DT_SLAB; }             // floats reduced into gD
 int head_rowblocks(int B) { return (2 * B + TR - 1) / TR; }
 int disc_rowblocks(int B) { return (3 * B + TR - 1) / TR; }
 
@@ -660,24 +686,31 @@ int launch_head_fwd(const float* h2, const float* w3, const float* b3, const int
     if (set_lds(k_head_fwd, sizeof(HeadFwdLds), "head_fwd") != PCADV_OK) return PCADV_EHIP;
     once = true;
   }
-  hipLaunchKernelGGL(k_head_fwd, dim3(head_rowblocks(B)), dim3(TT), sizeof(HeadFwdLds), s, h2, w3,
+  hipLaunchKernelGGL(k_head_fwd, dim3(head_rowblocks(B) * HF_SPLIT), dim3(TT), sizeof(HeadFwdLds), s, h2, w3,
                      b3, labels, B, lambda_cls, logits, dlogits, din, dw1, db1, d1, lpart);
   PC_HIP_CHECK_LAUNCH("k_head_fwd");
   return PCADV_OK;
 }
 
+size_t feat_sort_record_ints(int C, int N) { return (size_t)C * ((N + FS_PCH - 1) / FS_PCH) * FS_REC; }
+
+// sortrec (optional): also run the feature backward's hit sort over the C
+// clouds' argmax gidx [C][1024] into sortrec (feat_sort_record_ints(C, N))
 int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, const float* w5,
                      const float* b5, const float* wf, const float* bf, const float* soft_gt,
                      const float* soft_nogt, const int32_t* step, uint64_t seed, float lambda_adv,
-                     float* dd3, float* slabs, float* lpart3, float* dout, hipStream_t s) {
+                     float* dd3, float* slabs, float* lpart3, float* dout, hipStream_t s,
+                     const int32_t* gidx, int C, int N, int* sortrec) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_disc_tail, sizeof(DiscTailLds), "disc_tail") != PCADV_OK) return PCADV_EHIP;
     once = true;
   }
-  hipLaunchKernelGGL(k_disc_tail, dim3(disc_rowblocks(B)), dim3(TT), sizeof(DiscTailLds), s, d3, B,
-                     w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3, slabs,
-                     lpart3, dout);
+  PC_REQUIRE(!sortrec || (gidx && C > 0 && N > 0), "disc_tail: the hit sort needs gidx, C and N");
+  const int nsort = sortrec ? (C * ((N + FS_PCH - 1) / FS_PCH) + 1) / 2 : 0;
+  hipLaunchKernelGGL(k_disc_tail, dim3(disc_rowblocks(B) + nsort), dim3(TT), sizeof(DiscTailLds), s,
+                     d3, B, w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3,
+                     slabs, lpart3, dout, gidx, C, N, sortrec);
   PC_HIP_CHECK_LAUNCH("k_disc_tail");
   return PCADV_OK;
 }
