@@ -96,7 +96,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #endif
   BSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5, r16 = lane & 15, q = lane >> 4;
   const int c = blockIdx.y, chunk = blockIdx.x, p0 = chunk * BW_PCH;
   const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
 
@@ -109,7 +108,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       __builtin_amdgcn_make_buffer_rsrc((void*)w3, (short)0, 128 * 64 * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t w2r =
       __builtin_amdgcn_make_buffer_rsrc((void*)w2, (short)0, 64 * 64 * 4, 0x00020000);
-  const int boff = (q * 64 + 16 * ct + r16) * 4;
   const __amdgpu_buffer_rsrc_t w4r =
       __builtin_amdgcn_make_buffer_rsrc((void*)w4, (short)0, BW_MAXO * 128 * 4, 0x00020000);
   // this cloud's x3 rows (C x N x 128 f32 < 4 GB: 32-bit offsets from the cloud base)
@@ -258,6 +256,14 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   float acc_w1 = 0.f, acc_b = 0.f;
 
   for (int b0 = 0; b0 < nact; b0 += BW_RB) {
+    // the lane-dependent indices are re-derived in every batch: otherwise each
+    // LDS / buffer offset built from them is hoisted out of the batch loop and
+    // kept live (or spilled) across it
+    int lane_l = lane;
+    asm volatile("" : "+v"(lane_l));
+    const int lane = lane_l, tid = wave * 64 + lane;
+    const int r32 = lane & 31, h = lane >> 5, r16 = lane & 15, q = lane >> 4;
+    const int boff = (q * 64 + 16 * ct + r16) * 4;  // this lane's W3 / W2 fragment offset
     const int nb = min(BW_RB, nact - b0);
     const int sb_ = 4 + 5 * (b0 / BW_RB);
     (void)sb_;
@@ -509,6 +515,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   }
 
   // ---- 4. write this workgroup's slab ----------------------------------------
+  const int r32 = lane & 31;
   float* slab = slabs + ((size_t)c * gridDim.x + chunk) * SLAB;
   {
     const int ot = wave >> 1, it = wave & 1;
