@@ -543,9 +543,9 @@ def main():
     prof = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                      "profiles", "r*_pmc_traffic.json"))
                   if "_seg_" not in os.path.basename(p))
-    if prof and N == 1024:  # the committed PMC passes ran the default N=1024 workload
+    if prof and N == 1024 and adv_prec == "fp32":  # the committed PMC passes ran the default workload
         kern = json.load(open(prof[-1]))["kernels"]
-        names = ("pcadv::k_point_mlp", "pcadv::k_conv4_max")
+        names = ("pcadv::k_point_mlp<6>", "pcadv::k_conv4_max<3>")  # the fp32-mode instances
         if all(n in kern for n in names):
             traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
             traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))
