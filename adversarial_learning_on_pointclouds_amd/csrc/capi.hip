@@ -59,7 +59,8 @@ int launch_head_fwd(const float*, const float*, const float*, const int64_t*, in
 int launch_disc_tail(const float*, int, const float*, const float*, const float*, const float*,
                      const float*, const float*, const float*, const float*, const int32_t*,
                      uint64_t, float, float*, float*, float*, float*, hipStream_t,
-                     const int32_t* gidx = nullptr, int C = 0, int N = 0, int* sortrec = nullptr);
+                     const int32_t* gidx, int C, int N, int* sortrec, float* z4g, float* z5g,
+                     float* a4g);
 size_t feat_sort_record_ints(int C, int N);
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
@@ -102,6 +103,7 @@ struct StepWs {
   float *x3, *gmax, *h1, *h2, *logits, *dlogits, *dh2, *dh1, *dgmax;
   float *din, *d1, *d2, *d3;
   float *dd3, *dd2, *dd1;
+  float *z4, *z5, *a4;  // D conv4 / conv5 dz rows and conv4 output rows (k_disc_tail)
   float *mask;
   float *lpart, *lpart3, *dslabs, *dout;
   int32_t* gidx;
@@ -139,6 +141,9 @@ static StepWs carve(int B, int N, char* base) {
   w.dd3 = take(R * 256);
   w.dd2 = take(R * 256);
   w.dd1 = take(R * 512);
+  w.z4 = take(R * 64);
+  w.z5 = take(R * 64);
+  w.a4 = take(R * 64);
   w.mask = take(C * 256);
   w.lpart = take(head_rowblocks(B));
   w.lpart3 = take(3 * (size_t)disc_rowblocks(B));
@@ -275,7 +280,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   PC_TRY(launch_disc_tail(w.d3, B, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, D + PCADV_D_CONV5_W,
                           D + PCADV_D_CONV5_B, D + PCADV_D_FC_W, D + PCADV_D_FC_B, a->soft_gt,
                           a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
-                          w.dout, s, w.gidx, C, N, w.sortrec));
+                          w.dout, s, w.gidx, C, N, w.sortrec, w.z4, w.z5, w.a4));
   // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
   //      input grads of all rows (rows [2B,3B) feed the generator, D frozen).
   //      Every data gradient is stored as the layer below's dz (its activation
@@ -284,9 +289,14 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   //      (k_head_bwd) dh2 -> dh1 -> dgmax (raw: the max-pool has no activation)
   const int MW = 2 * B;
   {
-    LinBwdExtra ex{};  // + sum of the conv4/conv5/fc partial-gradient slabs
+    // + conv4's and conv5's weight gradients (block jobs over k_disc_tail's
+    // z4 / z5 / a4 rows and the conv3 output) and the fc slabs' sum
+    LinBwdExtra ex{};
+    ex.job[0] = LinBwdJob{w.z4, w.d3, gD + PCADV_D_CONV4_W, gD + PCADV_D_CONV4_B, MW, 64, 256};
+    ex.job[1] = LinBwdJob{w.z5, w.a4, gD + PCADV_D_CONV5_W, gD + PCADV_D_CONV5_B, MW, 64, 64};
+    ex.njobs = 2;
     ex.red_src = w.dslabs;
-    ex.red_dst = gD + PCADV_D_CONV4_W;
+    ex.red_dst = gD + PCADV_D_FC_W;
     ex.red_n = disc_tail_slab_n();
     ex.red_ld = (int)disc_tail_slab_floats();
     ex.red_cnt = disc_rowblocks(B);
@@ -311,15 +321,8 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   // ---- generator head backward (:520); fc3's weight grad rides along -------
   {
     LinBwdExtra ex{};
-    ex.dy = w.dlogits;
-    ex.act = PCADV_ACT_NONE;
-    ex.x = w.h2;
-    ex.dw = gG + PCADV_G_FC3_W;
-    ex.db = gG + PCADV_G_FC3_B;
-    ex.M = C;
-    ex.m_w = C;
-    ex.N = 40;
-    ex.K = 256;
+    ex.job[0] = LinBwdJob{w.dlogits, w.h2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, 40, 256};
+    ex.njobs = 1;
     ex.dx_act = PCADV_ACT_RELU;  // x = fc1 output
     PC_TRY(launch_linear_bwd(w.dh2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h1,
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,

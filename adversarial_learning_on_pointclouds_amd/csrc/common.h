@@ -184,16 +184,19 @@ struct FinAdam {
   int step_offset;
 };
 
-struct LinBwdExtra {
-  const float* dy;
-  const float* y;
-  int act;
-  const float* mask;
-  const int32_t* step;
+// extra weight-gradient job: dw[N][K] (+ db) = sum over rows m < m_w of
+// dz[m][N]^T x[m][K] (dz stored as is: no activation, no dropout)
+struct LinBwdJob {
+  const float* dz;
   const float* x;
   float* dw;
   float* db;
-  int M, m_w, N, K;
+  int m_w, N, K;
+};
+constexpr int LB_MAXJOBS = 3;
+struct LinBwdExtra {
+  LinBwdJob job[LB_MAXJOBS];
+  int njobs;
   const float* red_src;
   float* red_dst;
   int red_n, red_cnt;

@@ -361,8 +361,8 @@ k_linear_fwd(GemmArgs g, int S, int L) {
 // launch): a second weight-gradient job (no activation / dropout), and a
 // fixed-order sum of partial slabs: red_dst[j] = sum_s red_src[s * red_n + j].
 struct BwdExtra {
-  GemmArgs g2;
-  int nwt2;
+  WgradJob job[LB_MAXJOBS];  // .tiles = this job's blocks (block mode) or wave tiles
+  int njobs;
   const float* red_src;
   float* red_dst;
   int red_n, red_cnt, red_ld;
@@ -387,8 +387,7 @@ template <int ACT, int DM>
 __global__ void __launch_bounds__(1024)
 k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, int wmode) {
   kernarg_prefetch(g.x, g.w, g.dy, g.dx, g.dw, g.db, g.M, g.N, g.K, g.m_w, g.ox_act, g.ox_mask,
-                   g.ox_keep, S, L, nbx, nwt, blk0, ex.nwt2, ex.g2.x, ex.g2.dy, ex.g2.dw, ex.g2.db,
-                   ex.g2.M, ex.g2.N, ex.g2.K, ex.g2.m_w, ex.red_src, ex.red_dst, ex.red_n,
+                   g.ox_keep, S, L, nbx, nwt, blk0, ex.njobs, ex.red_src, ex.red_dst, ex.red_n,
                    ex.red_cnt, ex.red_ld, wmode);
   if (ACT != ACT_NONE) kernarg_prefetch(g.yact);
   if (DM != DM_NONE) kernarg_prefetch(g.drop.mask, g.drop.step, g.drop.seed, g.drop.p);
@@ -396,32 +395,43 @@ k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, 
   __shared__ __attribute__((aligned(16))) float lds[FAST ? LB_LDS : LB_RED];
   float* red = FAST ? lds + BT_MAXS * BT_WAVE : lds;
   const int nbw = (wmode & 1) ? wgrad_regions(g.N, g.K) : (nwt + S - 1) / S;
-  const int nbw2 = (wmode & 2) ? wgrad_regions(ex.g2.N, ex.g2.K) : (ex.nwt2 + S - 1) / S;
-  const int b = blockIdx.x + blk0;
+  int b = blockIdx.x + blk0;
   LSTAMP(g, 0);
   if (b < nbx) {
     const bool use_bt = FAST && S <= BT_MAXS && (g.N & 3) == 0;
     split_job<OP_BWD_DATA, ACT, DM>(g, b, g.M, g.K, g.N, S, L, red, use_bt ? lds : nullptr);
-  } else if (b < nbx + nbw) {
+    LSTAMP(g, 3);
+    return;
+  }
+  b -= nbx;
+  if (b < nbw) {
     if (FAST && (wmode & 1)) {
-      if (nwt > 0) wgrad_region(WgradJob{g.dy, g.x, g.dw, g.db, g.N, g.K, g.m_w, 0}, b - nbx, lds, S);
+      if (nwt > 0) wgrad_region(WgradJob{g.dy, g.x, g.dw, g.db, g.N, g.K, g.m_w, 0}, b, lds, S);
     } else {
-      weight_job<ACT, DM>(g, (b - nbx) * S + (threadIdx.x >> 6), nwt);
+      weight_job<ACT, DM>(g, b * S + (threadIdx.x >> 6), nwt);
     }
-  } else if (b < nbx + nbw + nbw2) {
-    if (FAST && (wmode & 2)) {
-      wgrad_region(WgradJob{ex.g2.dy, ex.g2.x, ex.g2.dw, ex.g2.db, ex.g2.N, ex.g2.K, ex.g2.m_w, 0},
-                   b - nbx - nbw, lds, S);
-    } else {
-      weight_job<ACT_NONE, DM_NONE>(ex.g2, (b - nbx - nbw) * S + (threadIdx.x >> 6), ex.nwt2);
+    LSTAMP(g, 3);
+    return;
+  }
+  b -= nbw;
+  // the extra jobs (block mode: one region per block, wmode bit 1; else one
+  // tile per wave)
+  for (int i = 0; i < LB_MAXJOBS; ++i) {
+    if (i >= ex.njobs) break;
+    if (b < ex.job[i].tiles) {
+      if (FAST && (wmode & 2)) wgrad_region(ex.job[i], b, lds, S);
+      else if (b * S + (int)(threadIdx.x >> 6) < ((ex.job[i].N + 15) / 16) * ((ex.job[i].K + 15) / 16))
+        wgrad_wave(ex.job[i], b * S + (threadIdx.x >> 6), (int)threadIdx.x & 63);
+      LSTAMP(g, 3);
+      return;
     }
-  } else {
-    const int j = (b - nbx - nbw - nbw2) * 64 * S + threadIdx.x;
-    if (j < ex.red_n) {
-      float acc = 0.f;
-      for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_ld + j];
-      ex.red_dst[j] = acc;
-    }
+    b -= ex.job[i].tiles;
+  }
+  const int j = b * 64 * S + threadIdx.x;
+  if (j < ex.red_n) {
+    float acc = 0.f;
+    for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_ld + j];
+    ex.red_dst[j] = acc;
   }
   LSTAMP(g, 3);
 }
@@ -513,22 +523,27 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
   BwdExtra ex{};
   int nbe = 0;
   if (extra) {
-    if (extra->dw) {
-      const LinBwdExtra& e = *extra;
-      PC_REQUIRE(e.M > 0 && e.N > 0 && e.K > 0 && e.m_w > 0 && e.m_w <= e.M &&
-                     e.m_w <= 16 * MAXC && e.act == ACT_NONE && !e.mask && !e.step,
-                 "linear_bwd: bad extra weight job (M=%d m_w=%d N=%d K=%d)", e.M, e.m_w, e.N, e.K);
-      GemmArgs& g2 = ex.g2;
-      g2.x = e.x; g2.dy = e.dy; g2.yact = e.y; g2.act = ACT_NONE;
-      g2.dw = e.dw; g2.db = e.db;
-      g2.M = e.M; g2.N = e.N; g2.K = e.K; g2.m_w = e.m_w;
-      ex.nwt2 = ((e.N + 15) / 16) * ((e.K + 15) / 16);
-      if (act == ACT_NONE && dm == DM_NONE && wgrad_block_mode(ACT_NONE, DM_NONE, e.N, e.K, S)) {
-        wmode |= 2;
-        nbe += wgrad_regions(e.N, e.K);
-      } else {
-        nbe += (ex.nwt2 + S - 1) / S;
-      }
+    PC_REQUIRE(extra->njobs >= 0 && extra->njobs <= LB_MAXJOBS, "linear_bwd: %d extra jobs",
+               extra->njobs);
+    // extra jobs in block mode when this launch's blocks allow it (all of them or none)
+    bool blk = S >= WGB_MIN_WAVES;
+    for (int i = 0; i < extra->njobs; ++i) {
+      const LinBwdJob& e = extra->job[i];
+      PC_REQUIRE(e.dz && e.x && e.dw && e.N > 0 && e.K > 0 && e.m_w > 0 &&
+                     e.m_w <= 16 * WG_MAXC && e.K % 4 == 0,
+                 "linear_bwd: bad extra weight job %d (m_w=%d N=%d K=%d)", i, e.m_w, e.N, e.K);
+      blk = blk && (e.N & 3) == 0;
+    }
+    if (blk && extra->njobs > 0) wmode |= 2;
+    ex.njobs = extra->njobs;
+    for (int i = 0; i < extra->njobs; ++i) {
+      const LinBwdJob& e = extra->job[i];
+      WgradJob& j = ex.job[i];
+      j.dz = e.dz; j.x = e.x; j.dw = e.dw; j.db = e.db;
+      j.N = e.N; j.K = e.K; j.m_w = e.m_w;
+      const int tiles = ((e.N + 15) / 16) * ((e.K + 15) / 16);
+      j.tiles = blk ? wgrad_regions(e.N, e.K) : (tiles + S - 1) / S;  // blocks of this job
+      nbe += j.tiles;
     }
     if (extra->red_src) {
       PC_REQUIRE(extra->red_dst && extra->red_n > 0 && extra->red_cnt > 0 &&

@@ -181,31 +181,6 @@ __device__ __forceinline__ void lds_fill(const Fill (&f)[NF]) {
   }
 }
 
-// dst[o][k] = sum_r Z[r][o] X[r][k] over the 16 rows (Z rows that must not
-// contribute are zero), db[o] = sum_r Z[r][o]; O, K multiples of 16.
-template <int O, int K>
-__device__ void rows_wgrad(const float* Z, int zs, const float* X, int xs, float* __restrict__ dst,
-                           float* __restrict__ db) {
-  constexpr int TO = O / 16, TK = K / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, q = lane >> 4;
-  for (int t = wave; t < TO * TK; t += TW) {
-    const int o0 = 16 * (t / TK), k0 = 16 * (t % TK);
-    f32x4t acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int row = 4 * s + q;
-      acc = mfma16t(Z[row * zs + o0 + r], X[row * xs + k0 + r], acc);
-    }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) dst[(size_t)(o0 + 4 * q + v) * K + k0 + r] = acc[v];
-  }
-  for (int o = tid; o < O; o += TT) {
-    float s = 0.f;
-    for (int row = 0; row < TR; ++row) s += Z[row * zs + o];
-    db[o] = s;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k_head_fwd: rows m of the 2B generator outputs
 // ---------------------------------------------------------------------------
@@ -296,7 +271,10 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
 // ---------------------------------------------------------------------------
 // k_disc_tail: rows m of the 3B discriminator rows
 // ---------------------------------------------------------------------------
-constexpr int DT_SLAB = 64 * 256 + 64 + 64 * 64 + 64 + 64 + 1;  // = gD[conv4.w .. fc.b]
+// per row block: the partial fc weight and bias gradients (= gD[fc.w .. fc.b]);
+// conv4's and conv5's weight gradients are block jobs of the next launch, over
+// the z4 / z5 / a4 rows this kernel stores (DtOut)
+constexpr int DT_SLAB = 64 + 1;
 constexpr int DT_SLAB_LD = (DT_SLAB + 3) & ~3;  // slab stride: 16-byte aligned slabs
 
 struct DiscTailLds {
@@ -305,11 +283,11 @@ struct DiscTailLds {
   float wf[64];                // fc weight [1][64]
   float b4[64], b5[64], bf[4];
   alignas(16) float x3[TR * 260];   // conv3 output rows (conv4 input)
-  float a4[TR * 68];
+  alignas(16) float a4[TR * 68];
   float a5[TR * 68];
   float out[TR * 4];
-  float z5[TR * 68];
-  float z4[TR * 68];
+  alignas(16) float z5[TR * 68];
+  alignas(16) float z4[TR * 68];
   float lt[3][TR];
   alignas(16) float scratch[16 * 256];
 };
@@ -322,7 +300,8 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
             const float* __restrict__ soft_nogt, const int32_t* __restrict__ step, uint64_t seed,
             float lambda_adv, float* __restrict__ dd3, float* __restrict__ slabs,
             float* __restrict__ lpart3, float* __restrict__ dout, const int32_t* __restrict__ gidx,
-            int C, int N, int* __restrict__ sortrec) {
+            int C, int N, int* __restrict__ sortrec, float* __restrict__ z4g,
+            float* __restrict__ z5g, float* __restrict__ a4g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DiscTailLds& L = *reinterpret_cast<DiscTailLds*>(smem);
   const int tid = threadIdx.x;
@@ -423,29 +402,31 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
                                                       dd3 + (size_t)r0 * 256, 256, L.scratch,
                                                       nrows, TR, 0, OutMask{L.x3, 260, nullptr, 1.f});
   TSTAMP(1, 8);
-  // partial weight gradients over this block's D-loss rows (m < 2B; the
-  // adversarial rows train only the generator)
-  for (int e = tid; e < TR * 64; e += TT) {
-    const int row = e >> 6, col = e & 63;
-    if (r0 + row >= 2 * B) {
-      L.z4[row * 68 + col] = 0.f;
-      L.z5[row * 68 + col] = 0.f;
+  // weight gradients over the D-loss rows (m < 2B; the adversarial rows train
+  // only the generator): conv4's and conv5's run as block jobs of the next
+  // launch over the z4 / z5 / a4 rows stored here (one 16-B store per thread
+  // and row array); fc's (64 + 1 values) as this block's partial slab
+  if (tid < 3 * 256) {
+    const int arr = tid >> 8, e = tid & 255, row = e >> 4, c4 = e & 15, m = r0 + row;
+    if (m < 2 * B) {
+      const float* src = arr == 0 ? L.z4 : (arr == 1 ? L.z5 : L.a4);
+      float* dst = arr == 0 ? z4g : (arr == 1 ? z5g : a4g);
+      *reinterpret_cast<f32x4t*>(dst + (size_t)m * 64 + 4 * c4) =
+          *reinterpret_cast<const f32x4t*>(src + row * 68 + 4 * c4);
     }
   }
-  if (tid < TR && r0 + tid >= 2 * B) L.out[tid * 4 + 1] = 0.f;
-  __syncthreads();
   float* slab = slabs + (size_t)blockIdx.x * DT_SLAB_LD;
   TSTAMP(1, 9);
-  rows_wgrad<64, 256>(L.z4, 68, L.x3, 260, slab, slab + 64 * 256);
-  rows_wgrad<64, 64>(L.z5, 68, L.a4, 68, slab + 64 * 256 + 64, slab + 64 * 256 + 64 + 4096);
   TSTAMP(1, 10);
   if (tid < 64) {
     float s = 0.f;
-    for (int row = 0; row < TR; ++row) s = fmaf(L.out[row * 4 + 1], L.a5[row * 68 + tid], s);
-    slab[64 * 256 + 64 + 4096 + 64 + tid] = s;
+    for (int row = 0; row < TR; ++row)
+      if (r0 + row < 2 * B) s = fmaf(L.out[row * 4 + 1], L.a5[row * 68 + tid], s);
+    slab[tid] = s;
   } else if (tid == 64) {
     float s = 0.f;
-    for (int row = 0; row < TR; ++row) s += L.out[row * 4 + 1];
+    for (int row = 0; row < TR; ++row)
+      if (r0 + row < 2 * B) s += L.out[row * 4 + 1];
     slab[DT_SLAB - 1] = s;
   }
 }
@@ -700,7 +681,8 @@ int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, c
                      const float* b5, const float* wf, const float* bf, const float* soft_gt,
                      const float* soft_nogt, const int32_t* step, uint64_t seed, float lambda_adv,
                      float* dd3, float* slabs, float* lpart3, float* dout, hipStream_t s,
-                     const int32_t* gidx, int C, int N, int* sortrec) {
+                     const int32_t* gidx, int C, int N, int* sortrec, float* z4g, float* z5g,
+                     float* a4g) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_disc_tail, sizeof(DiscTailLds), "disc_tail") != PCADV_OK) return PCADV_EHIP;
@@ -710,7 +692,7 @@ int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, c
   const int nsort = sortrec ? (C * ((N + FS_PCH - 1) / FS_PCH) + 1) / 2 : 0;
   hipLaunchKernelGGL(k_disc_tail, dim3(disc_rowblocks(B) + nsort), dim3(TT), sizeof(DiscTailLds), s,
                      d3, B, w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3,
-                     slabs, lpart3, dout, gidx, C, N, sortrec);
+                     slabs, lpart3, dout, gidx, C, N, sortrec, z4g, z5g, a4g);
   PC_HIP_CHECK_LAUNCH("k_disc_tail");
   return PCADV_OK;
 }
