@@ -254,10 +254,11 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
     if (lane == 0) L.rl[row] = rloss;
   }
   __syncthreads();
-  if (sp == 0 && tid == 0) {
-    float s = 0.f;
-    for (int row = 0; row < TR; ++row) s += L.rl[row];
-    lpart[rb] = s;
+  if (sp == 0 && wave == 0) {  // the block's CE sum: a fixed butterfly over wave 0
+    float s = lane < TR ? L.rl[lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) lpart[rb] = s;
   }
   // D conv1 on the GT rows (D rows [0,B)) and noGT rows (D rows [B,2B) and,
   // identical, [2B,3B)): rows r0.. of d1, copied to r0+B.. for noGT blocks
@@ -288,7 +289,6 @@ struct DiscTailLds {
   float out[TR * 4];
   alignas(16) float z5[TR * 68];
   alignas(16) float z4[TR * 68];
-  float lt[3][TR];
   alignas(16) float scratch[16 * 256];
 };
 
@@ -346,9 +346,10 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
   TSTAMP(1, 4);
   // BCEWithLogits terms (train_classification.py:200): rows [0,B) D(lsm_gt) vs U(0.7,1.05),
   // [B,2B) D(lsm_nogt) vs U(0,0.305), [2B,3B) adversarial vs 1
+  float l0 = 0.f, l1 = 0.f, l2 = 0.f;
   if (tid < TR) {
     const int m = r0 + tid;
-    float g = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
+    float g = 0.f;
     if (m < R) {
       const float x = L.out[tid * 4];
       if (dout) dout[m] = x;  // the D logits (run_training_semi's confidence, trainer.py:717)
@@ -371,16 +372,21 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
       else l0 = bce;
     }
     L.out[tid * 4 + 1] = g;
-    L.lt[0][tid] = l0;
-    L.lt[1][tid] = l1;
-    L.lt[2][tid] = l2;
+  }
+  if (tid < 64) {  // the block's three loss sums: a fixed butterfly over wave 0 (lanes >= TR add 0)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      l0 += __shfl_xor(l0, o);
+      l1 += __shfl_xor(l1, o);
+      l2 += __shfl_xor(l2, o);
+    }
+    if (tid == 0) {
+      lpart3[blockIdx.x * 3 + 0] = l0;
+      lpart3[blockIdx.x * 3 + 1] = l1;
+      lpart3[blockIdx.x * 3 + 2] = l2;
+    }
   }
   __syncthreads();
-  if (tid < 3) {
-    float s = 0.f;
-    for (int row = 0; row < TR; ++row) s += L.lt[tid][row];
-    lpart3[blockIdx.x * 3 + tid] = s;
-  }
   // backward: fc (dz = dL/dout, no activation), conv5, conv4
   TSTAMP(1, 5);
   rows_layer<1, 64, B_KO, ACT_NONE>(L.out + 1, 4, L.wf, 64, nullptr, L.z5, 68, L.scratch);
