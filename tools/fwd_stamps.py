@@ -66,9 +66,17 @@ def main():
     summarize("k_conv4_max", st, [1, 2, 4, 5, 3])
     n1 = (C * ((N + 63) // 64) + 1) // 2
     st1 = stamps[nwg * 16:nwg * 16 + n1 * 16].view(n1, 16).cpu().numpy()
-    # k_point_mlp thread 0: 1 weights loaded; per tile t: 3+5t pts staged, 4+5t conv1,
-    # 5+5t conv2 (+split), 6+5t conv3 MFMAs, 7+5t x3 stores issued; 2 both tiles done
-    summarize("k_point_mlp", st1, [1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 2])
+    st1 = st1[st1[:, 0] > 0]
+    ntiles = C * ((N + 63) // 64)
+    if st1.shape[0] < n1:
+        # k_point_mlp_ws (one workgroup per CU): 1 weights split; 3 + it after the
+        # barrier of pipeline step it (A: tile it, B: tile it - 1); 2 end
+        tpw = (ntiles + 255) // 256
+        summarize("k_point_mlp_ws", st1, [1] + [3 + i for i in range(min(tpw + 1, 13))] + [2])
+    else:
+        # k_point_mlp thread 0: 1 weights loaded; per tile t: 3+5t pts staged, 4+5t conv1,
+        # 5+5t conv2 (+split), 6+5t conv3 MFMAs, 7+5t x3 stores issued; 2 both tiles done
+        summarize("k_point_mlp", st1, [1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 2])
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(20):
