@@ -279,9 +279,16 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #pragma unroll
       for (int u = 0; u < 2; ++u) {  // the batch's points: element e = lane + 64 u of 96
         const int e = lane + 64 * u, row = e / 3;
-        if (e < BW_RB * 3) {
-          if (b0 > 0) ptv[u] = row < nb ? pts[(size_t)(p0 + L.rows_list[b0 + row]) * 3 + e % 3] : 0.f;
-          L.pts[row * 4 + e % 3] = row < nb ? ptv[u] : 0.f;
+        if (e < BW_RB * 3) L.pts[row * 4 + e % 3] = row < nb ? ptv[u] : 0.f;
+      }
+      // the next batch's points, in flight until its phase a
+      if (b0 + BW_RB < nact) {
+        const int nb2 = min(BW_RB, nact - b0 - BW_RB);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int e = lane + 64 * u, row = e / 3;
+          if (e < BW_RB * 3)
+            ptv[u] = row < nb2 ? pts[(size_t)(p0 + L.rows_list[b0 + BW_RB + row]) * 3 + e % 3] : 0.f;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
