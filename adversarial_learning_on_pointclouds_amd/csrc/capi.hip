@@ -315,14 +315,17 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   // ---- D conv1 input grad of the adversarial rows -> log_softmax backward ->
   //      fc3 input grad (stored as fc2's dz); D conv1 weight grad; the losses -
   PC_TRY(launch_head_bwd(w.dd1, w.h2, bmask, a->drop_p, w.din, B, D + PCADV_D_CONV1_W,
-                         G + PCADV_G_FC3_W, w.dlogits, w.dh2, gD + PCADV_D_CONV1_W,
-                         gD + PCADV_D_CONV1_B, w.lpart, w.lpart3, a->losses, a->semi,
-                         a->lambda_semi, a->semi_th, logits, w.dout, s));
+                         G + PCADV_G_FC3_W, w.dlogits, w.dh2, nullptr, nullptr, w.lpart,
+                         w.lpart3, a->losses, a->semi, a->lambda_semi, a->semi_th, logits,
+                         w.dout, s));
   // ---- generator head backward (:520); fc3's weight grad rides along -------
   {
     LinBwdExtra ex{};
     ex.job[0] = LinBwdJob{w.dlogits, w.h2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, 40, 256};
-    ex.njobs = 1;
+    // D conv1's weight gradient over the D-loss rows: dz = conv1's dz (D conv2's
+    // backward output), x = the D input rows
+    ex.job[1] = LinBwdJob{w.dd1, w.din, gD + PCADV_D_CONV1_W, gD + PCADV_D_CONV1_B, 2 * B, 512, 40};
+    ex.njobs = 2;
     ex.dx_act = PCADV_ACT_RELU;  // x = fc1 output
     PC_TRY(launch_linear_bwd(w.dh2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h1,
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,

@@ -495,8 +495,11 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
                       const int32_t* step, uint64_t seed, float p, const float* x, const float* w,
                       float* dx, float* dw, float* db, int M, int m_w, int N, int K,
                       hipStream_t s, const LinBwdExtra* extra) {
+  // the weight-gradient rows: any number with dz as is (wgrad.h forms), at
+  // most 16 MAXC when an activation or dropout applies on the fly
+  const bool dz_as_is = act == ACT_NONE && !mask && !step;
   PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0 && m_w >= 0 && m_w <= M &&
-                 m_w <= 16 * MAXC,
+                 (dz_as_is || !dw || m_w <= 16 * MAXC),
              "linear_bwd: bad shape M=%d m_w=%d N=%d K=%d", M, m_w, N, K);
   GemmArgs g{};
   g.x = x; g.w = w; g.dy = dy; g.yact = y; g.act = act;
@@ -529,8 +532,7 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
     bool blk = S >= WGB_MIN_WAVES;
     for (int i = 0; i < extra->njobs; ++i) {
       const LinBwdJob& e = extra->job[i];
-      PC_REQUIRE(e.dz && e.x && e.dw && e.N > 0 && e.K > 0 && e.m_w > 0 &&
-                     e.m_w <= 16 * WG_MAXC && e.K % 4 == 0,
+      PC_REQUIRE(e.dz && e.x && e.dw && e.N > 0 && e.K > 0 && e.m_w > 0 && e.K % 4 == 0,
                  "linear_bwd: bad extra weight job %d (m_w=%d N=%d K=%d)", i, e.m_w, e.N, e.K);
       blk = blk && (e.N & 3) == 0;
     }

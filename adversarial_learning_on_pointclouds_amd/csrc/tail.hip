@@ -714,7 +714,9 @@ int launch_head_bwd(const float* dz1, const float* h2, const float* drop_mask, f
     if (set_lds(k_head_bwd, sizeof(HeadBwdLds), "head_bwd") != PCADV_OK) return PCADV_EHIP;
     once = true;
   }
-  const int nrb = head_rowblocks(B), nwb = (32 * 3 + TW - 1) / TW;
+  // gw1 = nullptr: D conv1's weight gradient is computed elsewhere (the
+  // adversarial step runs it as a block job of the fc2 backward launch)
+  const int nrb = head_rowblocks(B), nwb = gw1 ? (32 * 3 + TW - 1) / TW : 0;
   const SemiArgs sa{semi, lambda_semi, semi_th, logits, dout};
   PC_REQUIRE(!semi || (logits && dout), "head_bwd: the semi term needs the logits and D outputs");
   const float keep = 1.0f / (1.0f - drop_p);  // as the linear kernels' dropout scale

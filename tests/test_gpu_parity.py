@@ -160,9 +160,11 @@ def test_linear_vs_torch(M, N, K, act):
 # dz stored as is (no activation, no dropout): the backward-data tiles take W
 # through LDS (csrc/linear.hip wave_tile_bdt) when N % 4 == 0 and the block has
 # <= 8 waves (N <= 512); the other shapes take the direct loads.  Edge tiles
-# (M, K not multiples of 16), multi-round slices (N > 1024) and both routes.
+# (M, K not multiples of 16), multi-round slices (N > 1024) and both routes;
+# weight gradients over more than one 128-row slab (M = 300, 200).
 @pytest.mark.parametrize("M,N,K", [(64, 512, 1024), (96, 256, 512), (96, 256, 256), (64, 40, 256),
-                                   (33, 76, 12), (20, 1100, 36), (17, 30, 20), (64, 2048, 64)])
+                                   (33, 76, 12), (20, 1100, 36), (17, 30, 20), (64, 2048, 64),
+                                   (300, 256, 512), (200, 40, 36), (150, 30, 20)])
 def test_linear_bwd_dz_as_is_vs_torch(M, N, K):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
     x = torch.randn(M, K, generator=g)
@@ -365,6 +367,60 @@ def test_adv_step_full_size_vs_oracle():
     for broken in (np.zeros_like(g1), 2 * g1):
         with pytest.raises(AssertionError):
             assert_grad_close(broken, gG["feat.conv1.weight"], "broken")
+
+
+def test_adv_step_large_batch_vs_oracle():
+    """B=80 (the trainer fuses batches up to 256 clouds): the head's and the
+    discriminator's weight gradients then reduce over 160 rows, more than one
+    128-row slab of the weight-gradient jobs (csrc/wgrad.h).  Head and D
+    gradients at the default per-tensor tolerance; the feature layers at the
+    ReLU-flip bound of test_cls_step_full_size_vs_oracle_with_adam."""
+    B, N = 80, 128
+    step, model, model_D = _make_step(B, N, g_seed=7, d_seed=8)
+    rng = np.random.default_rng(808)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+    G = onp.make_params(onp.cls_spec(40), seed=7)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=8, init="xavier")
+    losses_ref, gG, gD, _ = onp.adv_step(G, D, None, None, pg, lab, pn, m1, m2, y1, y2,
+                                         apply_adam=False)
+    losses = step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                  soft=(_t(y1), _t(y2)), apply_adam=False).cpu().numpy()
+    for i, k in enumerate(["loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt"]):
+        assert abs(losses[i] - losses_ref[k]) < 1e-4, (k, losses[i], losses_ref[k])
+    for nm, p in model.named_parameters():
+        if nm.startswith("feat."):
+            assert_grad_close(p.grad.cpu().numpy(), gG[nm], nm, 5e-3, 2e-3)
+        else:
+            assert_grad_close(p.grad.cpu().numpy(), gG[nm], nm)
+    for nm, p in model_D.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), gD[nm], nm)
+
+
+def test_cls_step_large_batch_vs_oracle():
+    """configs[1]'s step at B=160: fc1..fc3's weight gradients over 160 rows."""
+    B, N = 160, 64
+    step, model = _cls_step(B, N, g_seed=9)
+    rng = np.random.default_rng(909)
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    m = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    G = onp.make_params(onp.cls_spec(40), seed=9)
+    logits, _, cache = onp.cls_forward(G, pts, m)
+    l_ref, dlog = onp.cross_entropy(logits, lab)
+    grads = onp.cls_backward(G, cache, dlog)
+    loss = step(_t(pts), _t(lab, torch.int64), mask=_t(m), apply_adam=False)
+    assert abs(float(loss[0]) - l_ref) < 1e-4
+    for nm, p in model.named_parameters():
+        if nm.startswith("feat."):
+            assert_grad_close(p.grad.cpu().numpy(), grads[nm], nm, 5e-3, 2e-3)
+        else:
+            assert_grad_close(p.grad.cpu().numpy(), grads[nm], nm)
 
 
 def test_adv_step_cfg5_shape_vs_oracle():
