@@ -170,13 +170,14 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = __fmaf_rn(-h.step, __fdiv_rn(m, denom), p);
 }
 
-// Adam riding along the launch that finishes the gradients (k_feat_bwd_finish):
-// the generator's conv1..conv4 parameters as their gradients are formed, plus
-// the parameters whose gradients are already final (G from fc1 on, all of D).
+// Adam riding along the feature backward: the generator's conv1..conv4
+// parameters in k_feat_bwd_finish as their gradients are formed, the
+// parameters whose gradients are already final (G from fc1 on, all of D) in
+// trailing workgroups of k_feat_bwd_chunk.
 struct FinAdam {
   int on;
   float* gp; float* gm; float* gv; const float* gg;  // generator flat buffers
-  int64_t g_rest0, g_n;                             // G [g_rest0, g_n) in the extra blocks
+  int64_t g_rest0, g_n;                             // G [g_rest0, g_n) in the extra workgroups
   float* dp; float* dm; float* dv; const float* dg;  // discriminator (d_n = 0: none)
   int64_t d_n;
   float lr_g, lr_d, b1, b2, eps;

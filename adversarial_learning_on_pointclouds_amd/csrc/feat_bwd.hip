@@ -68,6 +68,61 @@ struct BwdLds {
 
 static_assert(FS_PCH == BW_PCH && FS_MAXO == BW_MAXO && FS_T == BW_T, "feat_sort.h geometry");
 
+// Adam over the parameters whose gradients are final before the feature
+// backward: the generator from fc1 on (segment 0) and the discriminator
+// (segment 1), in trailing workgroups of k_feat_bwd_chunk (NT = BW_T threads);
+// V4 float4 per thread and pass, blocks [0, nb0) on segment 0.
+constexpr int FIN_ADAM_V4 = 4;  // float4 per thread in the chunk launch's Adam workgroups
+template <int NT, int V4>
+__device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
+  const bool first = blk < nb0;
+  float* p = first ? fa.gp + fa.g_rest0 : fa.dp;
+  float* m = first ? fa.gm + fa.g_rest0 : fa.dm;
+  float* v = first ? fa.gv + fa.g_rest0 : fa.dv;
+  const float* g = first ? fa.gg + fa.g_rest0 : fa.dg;
+  const int64_t n = first ? fa.g_n - fa.g_rest0 : fa.d_n;
+  const int b = first ? blk : blk - nb0, nb = first ? nb0 : nb1;
+  const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps,
+                           first ? fa.lr_g : fa.lr_d);
+  const int64_t n4 = n / 4;
+  // V4 float4 per thread, all loads issued before any update: one
+  // memory round trip per pass
+  const int64_t stride = (int64_t)nb * NT;
+  for (int64_t i0 = (int64_t)b * NT + threadIdx.x; i0 < n4; i0 += stride * V4) {
+    f32x4 p4[V4], g4[V4], m4[V4], v4[V4];
+#pragma unroll
+    for (int u = 0; u < V4; ++u) {
+      const int64_t i = i0 + u * stride < n4 ? i0 + u * stride : i0;  // clamped, not stored
+      p4[u] = reinterpret_cast<f32x4*>(p)[i];
+      g4[u] = reinterpret_cast<const f32x4*>(g)[i];
+      m4[u] = reinterpret_cast<f32x4*>(m)[i];
+      v4[u] = reinterpret_cast<f32x4*>(v)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < V4; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n4) continue;
+      float pp[4] = {p4[u].x, p4[u].y, p4[u].z, p4[u].w};
+      float mm[4] = {m4[u].x, m4[u].y, m4[u].z, m4[u].w};
+      float vv[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
+      const float gg[4] = {g4[u].x, g4[u].y, g4[u].z, g4[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], h);
+      reinterpret_cast<f32x4*>(p)[i] = f32x4{pp[0], pp[1], pp[2], pp[3]};
+      reinterpret_cast<f32x4*>(m)[i] = f32x4{mm[0], mm[1], mm[2], mm[3]};
+      reinterpret_cast<f32x4*>(v)[i] = f32x4{vv[0], vv[1], vv[2], vv[3]};
+    }
+  }
+  if (b == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    adam_elem(p[i], g[i], m[i], v[i], h);
+  }
+}
+static int fin_adam_blocks(int64_t n, int nt, int v4) {
+  int64_t b = (n / 4 + (int64_t)nt * v4 - 1) / ((int64_t)nt * v4);
+  return (int)(b < 1 ? 1 : b);
+}
+
 // PRE: phases 1-3 (the hit sort) were done ahead of this launch (feat_sort.h,
 // records at sortrec): load them and gather the hits' gradients instead.
 template <bool PRE>
@@ -78,7 +133,17 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
                  const float* __restrict__ w2, const float* __restrict__ b2,
                  const float* __restrict__ w3, const float* __restrict__ w4,
                  const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps,
-                 const int* __restrict__ sortrec) {
+                 const int* __restrict__ sortrec, int nclouds, FinAdam fa, int nb_adam0,
+                 int nb_adam1) {
+  // Workgroup rows past the clouds: the Adam update of the parameters whose
+  // gradients are final before this launch (G from fc1 on, D).  They are
+  // dispatched last, so they take the CU slots of the chunks that finish first
+  // while the two-batch chunks run on.
+  if ((int)blockIdx.y >= nclouds) {
+    const int b = ((int)blockIdx.y - nclouds) * (int)gridDim.x + (int)blockIdx.x;
+    if (b < nb_adam0 + nb_adam1) adam_block<BW_T, FIN_ADAM_V4>(b, nb_adam0, nb_adam1, fa);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
 #ifdef PCADV_STAMPS
@@ -633,21 +698,23 @@ __device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __r
 }
 
 // dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :];  db4[o] = sum_c g[c,o].
-// Four channels per 1024-thread block (256 blocks: every CU takes a share of
-// the 33.5 MB of gathered rows); four waves per channel, each summing a quarter
-// of the clouds in cloud order, the quarters then added in order (fixed).
+// DW4_CPB channels per 1024-thread block (with the slab reduction, one block
+// per CU in a single dispatch round); DW4_WPC = 16 / DW4_CPB waves per channel,
+// each summing a contiguous share of the clouds in cloud order, the shares then
+// added in order (fixed).
 // Lanes hold two of the 128 columns.  Per group of 64 clouds, lane c fetches
 // (g, gidx) of cloud c once and the row addresses are broadcast with
 // v_readlane (scalar base + lane offset), so the row loads are all in flight
 // together: two memory round trips per wave.
-constexpr int DW4_CPB = 4;  // channels per block
+constexpr int DW4_CPB = 8;              // channels per block
+constexpr int DW4_WPC = 16 / DW4_CPB;  // waves per channel
 __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__ dg,
                           const int32_t* __restrict__ gidx, int C, int N, int O,
                           const float* __restrict__ x3, float* __restrict__ dw4,
                           float* __restrict__ db4, const FinAdam& fa) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int o = blk * DW4_CPB + (wave >> 2), qq = wave & 3;
-  const int ca = C * qq / 4, cb = C * (qq + 1) / 4;
+  const int o = blk * DW4_CPB + wave / DW4_WPC, qq = wave % DW4_WPC;
+  const int ca = C * qq / DW4_WPC, cb = C * (qq + 1) / DW4_WPC;
   // Adam state of the row (and bias) this wave finishes, in flight during the gather
   const bool adam = fa.on && qq == 0 && o < O;
   const size_t jw = PCADV_G_CONV4_W + (size_t)(o < O ? o : 0) * 128 + 2 * lane;
@@ -698,7 +765,7 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
   if (qq == 0 && o < O) {
     float4 t = part[wave][lane];
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < DW4_WPC; ++k) {
       const float4 p = part[wave + k][lane];
       t.x += p.x;
       t.y += p.y;
@@ -722,69 +789,18 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
   }
 }
 
-// Adam over the parameters whose gradients are final before this launch: the
-// generator from fc1 on (segment 0) and the discriminator (segment 1); one
-// float4 per thread and pass, blocks [0, nb0) on segment 0.
-constexpr int FIN_ADAM_V4 = 2;  // float4 per thread
-__device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
-  const bool first = blk < nb0;
-  float* p = first ? fa.gp + fa.g_rest0 : fa.dp;
-  float* m = first ? fa.gm + fa.g_rest0 : fa.dm;
-  float* v = first ? fa.gv + fa.g_rest0 : fa.dv;
-  const float* g = first ? fa.gg + fa.g_rest0 : fa.dg;
-  const int64_t n = first ? fa.g_n - fa.g_rest0 : fa.d_n;
-  const int b = first ? blk : blk - nb0, nb = first ? nb0 : nb1;
-  const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps,
-                           first ? fa.lr_g : fa.lr_d);
-  const int64_t n4 = n / 4;
-  // FIN_ADAM_V4 float4 per thread, all loads issued before any update: one
-  // memory round trip per pass
-  const int64_t stride = (int64_t)nb * 1024;
-  for (int64_t i0 = (int64_t)b * 1024 + threadIdx.x; i0 < n4; i0 += stride * FIN_ADAM_V4) {
-    f32x4 p4[FIN_ADAM_V4], g4[FIN_ADAM_V4], m4[FIN_ADAM_V4], v4[FIN_ADAM_V4];
-#pragma unroll
-    for (int u = 0; u < FIN_ADAM_V4; ++u) {
-      const int64_t i = i0 + u * stride < n4 ? i0 + u * stride : i0;  // clamped, not stored
-      p4[u] = reinterpret_cast<f32x4*>(p)[i];
-      g4[u] = reinterpret_cast<const f32x4*>(g)[i];
-      m4[u] = reinterpret_cast<f32x4*>(m)[i];
-      v4[u] = reinterpret_cast<f32x4*>(v)[i];
-    }
-#pragma unroll
-    for (int u = 0; u < FIN_ADAM_V4; ++u) {
-      const int64_t i = i0 + u * stride;
-      if (i >= n4) continue;
-      float pp[4] = {p4[u].x, p4[u].y, p4[u].z, p4[u].w};
-      float mm[4] = {m4[u].x, m4[u].y, m4[u].z, m4[u].w};
-      float vv[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
-      const float gg[4] = {g4[u].x, g4[u].y, g4[u].z, g4[u].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], h);
-      reinterpret_cast<f32x4*>(p)[i] = f32x4{pp[0], pp[1], pp[2], pp[3]};
-      reinterpret_cast<f32x4*>(m)[i] = f32x4{mm[0], mm[1], mm[2], mm[3]};
-      reinterpret_cast<f32x4*>(v)[i] = f32x4{vv[0], vv[1], vv[2], vv[3]};
-    }
-  }
-  if (b == 0 && threadIdx.x < (n & 3)) {
-    const int64_t i = n4 * 4 + threadIdx.x;
-    adam_elem(p[i], g[i], m[i], v[i], h);
-  }
-}
-static int fin_adam_blocks(int64_t n) {
-  int64_t b = (n / 4 + 1024 * FIN_ADAM_V4 - 1) / (1024 * FIN_ADAM_V4);
-  return (int)(b < 1 ? 1 : b);
-}
 
 // One launch after k_feat_bwd_chunk: blocks [0, nred) reduce the slabs
-// (dW1..db3), the rest gather dW4/db4 (16 channels per block; independent of
-// the chunk kernel, they simply share its launch).
+// (dW1..db3), the rest gather dW4/db4 (DW4_CPB channels per block): 228
+// blocks, one dispatch round.  With the fused Adam each block also updates the
+// parameters it finished (the other Adam work rode along k_feat_bwd_chunk).
 constexpr int FIN_NRED = (SLAB + 127) / 128;
 __global__ void __launch_bounds__(1024)
 k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
                   float* db2, float* dw3, float* db3, const float* __restrict__ dg,
                   const int32_t* __restrict__ gidx, int C, int N, int O,
                   const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4,
-                  int blk0, FinAdam fa, int nb_adam0, int nb_adam1) {
+                  int blk0, FinAdam fa) {
   __shared__ float4 part[16][64];
   const int blk = (int)blockIdx.x + blk0, ndw4 = (O + DW4_CPB - 1) / DW4_CPB;
   if (blk < FIN_NRED)
@@ -792,8 +808,6 @@ k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float
                        db2, dw3, db3, fa);
   else if (blk < FIN_NRED + ndw4)
     dw4_block(blk - FIN_NRED, part, dg, gidx, C, N, O, x3, dw4, db4, fa);
-  else
-    adam_block(blk - FIN_NRED - ndw4, nb_adam0, nb_adam1, fa);
 }
 
 size_t feat_bwd_workspace_bytes(int C, int N) {
@@ -824,18 +838,9 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
     }
     attr_set = true;
   }
-  if (sortrec)
-    hipLaunchKernelGGL(k_feat_bwd_chunk<true>, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg,
-                       gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps,
-                       sortrec);
-  else
-    hipLaunchKernelGGL(k_feat_bwd_chunk<false>, dim3(nchunk, C), dim3(BW_T), sizeof(BwdLds), s, dg,
-                       gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps,
-                       sortrec);
-  PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   PC_REQUIRE(dw4 && db4, "feat_bwd: dw4/db4 required");
   FinAdam fa{};
-  int nba0 = 0, nba1 = 0;
+  int nba0 = 0, nba1 = 0;  // Adam workgroups (BW_T threads) of the chunk launch
   if (adam && adam->on) {
     fa = *adam;
     PC_REQUIRE(fa.gp && fa.gm && fa.gv && fa.gg && fa.step_count && fa.g_n > fa.g_rest0 &&
@@ -843,25 +848,31 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                    dw1 == fa.gg + PCADV_G_CONV1_W && dw4 == fa.gg + PCADV_G_CONV4_W &&
                    db4 == fa.gg + PCADV_G_CONV4_B,
                "feat_bwd: the fused Adam needs the generator's flat buffers");
-    nba0 = fin_adam_blocks(fa.g_n - fa.g_rest0);
-    nba1 = fa.d_n > 0 ? fin_adam_blocks(fa.d_n) : 0;
+    nba0 = fin_adam_blocks(fa.g_n - fa.g_rest0, BW_T, FIN_ADAM_V4);
+    nba1 = fa.d_n > 0 ? fin_adam_blocks(fa.d_n, BW_T, FIN_ADAM_V4) : 0;
   }
+  const int arows = (nba0 + nba1 + nchunk - 1) / nchunk;
+  if (sortrec)
+    hipLaunchKernelGGL(k_feat_bwd_chunk<true>, dim3(nchunk, C + arows), dim3(BW_T), sizeof(BwdLds),
+                       s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs,
+                       stamps, sortrec, C, fa, nba0, nba1);
+  else
+    hipLaunchKernelGGL(k_feat_bwd_chunk<false>, dim3(nchunk, C + arows), dim3(BW_T),
+                       sizeof(BwdLds), s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3,
+                       w4, x3, slabs, stamps, sortrec, C, fa, nba0, nba1);
+  PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   const int ndw4 = (O + DW4_CPB - 1) / DW4_CPB;
 #ifdef PCADV_STAMPS
-  // diagnostic build: the slab reduction, the dW4 gather and the Adam blocks as
-  // separate launches so a kernel trace times each part
+  // diagnostic build: the slab reduction and the dW4 gather as separate
+  // launches so a kernel trace times each part
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED), dim3(1024), 0, s, slabs, C * nchunk, dw1,
-                     db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0, fa, nba0, nba1);
+                     db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0, fa);
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(ndw4), dim3(1024), 0, s, slabs, C * nchunk, dw1, db1,
-                     dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, FIN_NRED, fa, nba0, nba1);
-  if (nba0 + nba1 > 0)
-    hipLaunchKernelGGL(k_feat_bwd_finish, dim3(nba0 + nba1), dim3(1024), 0, s, slabs, C * nchunk,
-                       dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4,
-                       FIN_NRED + ndw4, fa, nba0, nba1);
+                     dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, FIN_NRED, fa);
 #else
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + ndw4 + nba0 + nba1), dim3(1024), 0, s,
-                     slabs, C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4,
-                     db4, 0, fa, nba0, nba1);
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + ndw4), dim3(1024), 0, s, slabs,
+                     C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0,
+                     fa);
 #endif
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
   return PCADV_OK;
