@@ -2,7 +2,7 @@
 //
 // The max-pool has no ReLU before it (pointnet.py:128-129), so channel o of
 // cloud c sends its whole gradient to the single point gidx[c][o]:
-//   dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :]            (k_feat_bwd_finish)
+//   dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :]            (k_feat_bwd_chunk, trailing workgroups)
 //   dX3[c,n,:] = sum_{o: gidx[c,o]=n} g[c,o] W4[o,:]         (k_feat_bwd_chunk)
 // Only points that are the argmax of some channel ("active" points, ~1/4 of a
 // cloud) carry gradient into conv3..conv1, so k_feat_bwd_chunk compacts them
@@ -18,7 +18,7 @@
 //      dX2 = dZ3 W3 and dX1 = dZ2 W2 on v_mfma_f32_16x16x4_f32 (one 16x16 tile
 //      per wave), weight gradients on v_mfma_f32_32x32x2_f32.
 // Each workgroup writes its weight-gradient partials to its own slab;
-// k_feat_bwd_finish sums the slabs in a fixed order (no atomics) and gathers dW4.
+// k_feat_bwd_finish sums the slabs in a fixed order (no atomics).
 #include "common.h"
 #include "feat_sort.h"
 
@@ -74,16 +74,9 @@ static_assert(FS_PCH == BW_PCH && FS_MAXO == BW_MAXO && FS_T == BW_T, "feat_sort
 // V4 float4 per thread and pass, blocks [0, nb0) on segment 0.
 constexpr int FIN_ADAM_V4 = 4;  // float4 per thread in the chunk launch's Adam workgroups
 template <int NT, int V4>
-__device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
-  const bool first = blk < nb0;
-  float* p = first ? fa.gp + fa.g_rest0 : fa.dp;
-  float* m = first ? fa.gm + fa.g_rest0 : fa.dm;
-  float* v = first ? fa.gv + fa.g_rest0 : fa.dv;
-  const float* g = first ? fa.gg + fa.g_rest0 : fa.dg;
-  const int64_t n = first ? fa.g_n - fa.g_rest0 : fa.d_n;
-  const int b = first ? blk : blk - nb0, nb = first ? nb0 : nb1;
-  const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps,
-                           first ? fa.lr_g : fa.lr_d);
+__device__ void adam_range(int b, int nb, float* p, float* m, float* v, const float* g, int64_t n,
+                           float lr, const FinAdam& fa) {
+  const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, lr);
   const int64_t n4 = n / 4;
   // V4 float4 per thread, all loads issued before any update: one
   // memory round trip per pass
@@ -118,10 +111,82 @@ __device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
     adam_elem(p[i], g[i], m[i], v[i], h);
   }
 }
+template <int NT, int V4>
+__device__ void adam_block(int blk, int nb0, int nb1, const FinAdam& fa) {
+  if (blk < nb0)
+    adam_range<NT, V4>(blk, nb0, fa.gp + fa.g_rest0, fa.gm + fa.g_rest0, fa.gv + fa.g_rest0,
+                       fa.gg + fa.g_rest0, fa.g_n - fa.g_rest0, fa.lr_g, fa);
+  else
+    adam_range<NT, V4>(blk - nb0, nb1, fa.dp, fa.dm, fa.dv, fa.dg, fa.d_n, fa.lr_d, fa);
+}
 static int fin_adam_blocks(int64_t n, int nt, int v4) {
   int64_t b = (n / 4 + (int64_t)nt * v4 - 1) / ((int64_t)nt * v4);
   return (int)(b < 1 ? 1 : b);
 }
+
+// dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :];  db4[o] = sum_c g[c,o].
+// In trailing workgroups of k_feat_bwd_chunk (it needs only dg, gidx and x3,
+// all final before that launch): NW waves per workgroup, DW4_WPC waves per
+// channel, each summing a contiguous share of the clouds in cloud order, the
+// shares then added in order (fixed).
+// Lanes hold two of the 128 columns.  Per group of 64 clouds, lane c fetches
+// (g, gidx) of cloud c once and the row addresses are broadcast with
+// v_readlane (scalar base + lane offset), so the row loads are all in flight
+// together: two memory round trips per wave.
+constexpr int DW4_WPC = 2;  // waves per channel
+template <int NW>
+__device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__ dg,
+                          const int32_t* __restrict__ gidx, int C, int N, int O,
+                          const float* __restrict__ x3, float* __restrict__ dw4,
+                          float* __restrict__ db4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int o = blk * (NW / DW4_WPC) + wave / DW4_WPC, qq = wave % DW4_WPC;
+  const int ca = C * qq / DW4_WPC, cb = C * (qq + 1) / DW4_WPC;
+  float ax = 0.f, ay = 0.f, ab = 0.f;
+  if (o < O) {
+    for (int c0 = ca; c0 < cb; c0 += 64) {
+      const int cl = c0 + lane, cnt = min(64, cb - c0);
+      const bool vl = lane < cnt;
+      const float gl = vl ? dg[(size_t)cl * O + o] : 0.f;
+      const int nl = vl ? gidx[(size_t)cl * O + o] : 0;
+      constexpr int U = 16;
+      for (int u0 = 0; u0 < cnt; u0 += U) {
+        float2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int cu = min(u0 + u, cnt - 1);  // clamped: loads past cnt are discarded
+          const int n = __builtin_amdgcn_readlane(nl, cu);
+          v[u] = *reinterpret_cast<const float2*>(x3 + ((size_t)(c0 + cu) * N + n) * 128 + 2 * lane);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u0 + u < cnt) {
+            const float g = __builtin_bit_cast(
+                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gl), u0 + u));
+            ax = fmaf(g, v[u].x, ax);
+            ay = fmaf(g, v[u].y, ay);
+            ab += g;
+          }
+        }
+      }
+    }
+  }
+  part[wave][lane] = make_float4(ax, ay, ab, 0.f);
+  __syncthreads();
+  if (qq == 0 && o < O) {
+    float4 t = part[wave][lane];
+#pragma unroll
+    for (int k = 1; k < DW4_WPC; ++k) {
+      const float4 p = part[wave + k][lane];
+      t.x += p.x;
+      t.y += p.y;
+      t.z += p.z;
+    }
+    *reinterpret_cast<float2*>(dw4 + (size_t)o * 128 + 2 * lane) = make_float2(t.x, t.y);
+    if (lane == 0) db4[o] = t.z;
+  }
+}
+
 
 // PRE: phases 1-3 (the hit sort) were done ahead of this launch (feat_sort.h,
 // records at sortrec): load them and gather the hits' gradients instead.
@@ -133,18 +198,24 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
                  const float* __restrict__ w2, const float* __restrict__ b2,
                  const float* __restrict__ w3, const float* __restrict__ w4,
                  const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps,
-                 const int* __restrict__ sortrec, int nclouds, FinAdam fa, int nb_adam0,
-                 int nb_adam1) {
-  // Workgroup rows past the clouds: the Adam update of the parameters whose
-  // gradients are final before this launch (G from fc1 on, D).  They are
+                 const int* __restrict__ sortrec, int nclouds, float* __restrict__ dw4,
+                 float* __restrict__ db4, FinAdam fa, int nb_adam0, int nb_adam1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // Workgroup rows past the clouds: work that needs nothing from this launch,
+  // the dW4 / db4 gather and the Adam update of the parameters whose gradients
+  // are final before it (G from fc1 on, D; not W4, which the chunks read).  They are
   // dispatched last, so they take the CU slots of the chunks that finish first
   // while the two-batch chunks run on.
   if ((int)blockIdx.y >= nclouds) {
     const int b = ((int)blockIdx.y - nclouds) * (int)gridDim.x + (int)blockIdx.x;
-    if (b < nb_adam0 + nb_adam1) adam_block<BW_T, FIN_ADAM_V4>(b, nb_adam0, nb_adam1, fa);
+    constexpr int NDW4 = BW_MAXO / (BW_T / 64 / DW4_WPC);
+    if (b < NDW4)
+      dw4_block<BW_T / 64>(b, reinterpret_cast<float4(*)[64]>(smem), dg, gidx, nclouds, N, O, x3,
+                           dw4, db4);
+    else if (b - NDW4 < nb_adam0 + nb_adam1)
+      adam_block<BW_T, FIN_ADAM_V4>(b - NDW4, nb_adam0, nb_adam1, fa);
     return;
   }
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
 #ifdef PCADV_STAMPS
   // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
@@ -625,189 +696,86 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #undef ASTAMP
 }
 
-// out[j] = sum over slabs in fixed order: 128 columns per block (lanes hold
-// float2), 16 waves split the slabs into contiguous ranges, combined in wave
-// order through LDS.
-__device__ void reduce_slabs_block(int blk, float2 (*part)[64], const float* __restrict__ slabs,
+// out[j] = sum over slabs in fixed order: 64 columns per block (one per lane;
+// 199 blocks, so with conv4's Adam blocks the launch spreads over most CUs), 16
+// waves split the slabs into contiguous ranges, combined in wave order.
+constexpr int FIN_COLS = 64;
+__device__ void reduce_slabs_block(int blk, float (*part)[64], const float* __restrict__ slabs,
                                    int nslabs, float* dw1, float* db1, float* dw2, float* db2,
                                    float* dw3, float* db3, const FinAdam& fa) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = blk * 128 + 2 * lane;  // SLAB is even: j, j+1 both valid or both not
+  const int j = blk * FIN_COLS + lane;
   const int s0 = wave * nslabs / 16, s1 = (wave + 1) * nslabs / 16;
-  // Adam state of this lane's two parameters, in flight during the reduction
+  // Adam state of this lane's parameter, in flight during the reduction
   const bool adam = fa.on && wave == 0 && j < SLAB;
-  float2 ap = make_float2(0.f, 0.f), am = ap, av = ap;
+  float ap = 0.f, am = 0.f, av = 0.f;
   if (adam) {
-    ap = *reinterpret_cast<const float2*>(fa.gp + j);
-    am = *reinterpret_cast<const float2*>(fa.gm + j);
-    av = *reinterpret_cast<const float2*>(fa.gv + j);
+    ap = fa.gp[j];
+    am = fa.gm[j];
+    av = fa.gv[j];
   }
   // bias corrections (f64 pow) computed while the loads are in flight
   const AdamHp h = adam ? adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g)
                         : AdamHp{};
-  float2 acc = make_float2(0.f, 0.f);
+  float acc = 0.f;
   if (j < SLAB) {
-    // 32 slabs in flight per lane (a block is alone on its CU at this kernel's
-    // register use, so the registers are free): one round trip per 32 slabs
+    // 32 slabs in flight per lane: one round trip per 32 slabs
     int s = s0;
     constexpr int RD = 32;
     for (; s + RD <= s1; s += RD) {
-      float2 v[RD];
+      float v[RD];
 #pragma unroll
-      for (int u = 0; u < RD; ++u) v[u] = *reinterpret_cast<const float2*>(slabs + (size_t)(s + u) * SLAB + j);
+      for (int u = 0; u < RD; ++u) v[u] = slabs[(size_t)(s + u) * SLAB + j];
 #pragma unroll
-      for (int u = 0; u < RD; ++u) { acc.x += v[u].x; acc.y += v[u].y; }
+      for (int u = 0; u < RD; ++u) acc += v[u];
     }
     for (; s + 8 <= s1; s += 8) {
-      float2 v[8];
+      float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(slabs + (size_t)(s + u) * SLAB + j);
+      for (int u = 0; u < 8; ++u) v[u] = slabs[(size_t)(s + u) * SLAB + j];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; }
+      for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    for (; s < s1; ++s) {
-      const float2 v = *reinterpret_cast<const float2*>(slabs + (size_t)s * SLAB + j);
-      acc.x += v.x;
-      acc.y += v.y;
-    }
+    for (; s < s1; ++s) acc += slabs[(size_t)s * SLAB + j];
   }
   part[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && j < SLAB) {
-    float2 v = part[0][lane];
-    for (int w = 1; w < 16; ++w) { v.x += part[w][lane].x; v.y += part[w][lane].y; }
-    const float vv[2] = {v.x, v.y};
-    for (int e = 0; e < 2; ++e) {
-      const int jj = j + e;
-      const float x = vv[e];
-      if (jj < SL_DB1) dw1[jj] = x;
-      else if (jj < SL_DW2) db1[jj - SL_DB1] = x;
-      else if (jj < SL_DB2) dw2[jj - SL_DW2] = x;
-      else if (jj < SL_DW3) db2[jj - SL_DB2] = x;
-      else if (jj < SL_DB3) dw3[jj - SL_DW3] = x;
-      else db3[jj - SL_DB3] = x;
-    }
+    float x = part[0][lane];
+    for (int w = 1; w < 16; ++w) x += part[w][lane];
+    if (j < SL_DB1) dw1[j] = x;
+    else if (j < SL_DW2) db1[j - SL_DB1] = x;
+    else if (j < SL_DB2) dw2[j - SL_DW2] = x;
+    else if (j < SL_DW3) db2[j - SL_DB2] = x;
+    else if (j < SL_DB3) dw3[j - SL_DW3] = x;
+    else db3[j - SL_DB3] = x;
     if (adam) {  // the slab order is the generator's flat order (PCADV_G_CONV1_W = 0 ..)
-      adam_elem(ap.x, v.x, am.x, av.x, h);
-      adam_elem(ap.y, v.y, am.y, av.y, h);
-      *reinterpret_cast<float2*>(fa.gp + j) = ap;
-      *reinterpret_cast<float2*>(fa.gm + j) = am;
-      *reinterpret_cast<float2*>(fa.gv + j) = av;
+      adam_elem(ap, x, am, av, h);
+      fa.gp[j] = ap;
+      fa.gm[j] = am;
+      fa.gv[j] = av;
     }
   }
 }
 
-// dW4[o,:] = sum_c g[c,o] x3[c, gidx[c,o], :];  db4[o] = sum_c g[c,o].
-// DW4_CPB channels per 1024-thread block (with the slab reduction, one block
-// per CU in a single dispatch round); DW4_WPC = 16 / DW4_CPB waves per channel,
-// each summing a contiguous share of the clouds in cloud order, the shares then
-// added in order (fixed).
-// Lanes hold two of the 128 columns.  Per group of 64 clouds, lane c fetches
-// (g, gidx) of cloud c once and the row addresses are broadcast with
-// v_readlane (scalar base + lane offset), so the row loads are all in flight
-// together: two memory round trips per wave.
-constexpr int DW4_CPB = 8;              // channels per block
-constexpr int DW4_WPC = 16 / DW4_CPB;  // waves per channel
-__device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__ dg,
-                          const int32_t* __restrict__ gidx, int C, int N, int O,
-                          const float* __restrict__ x3, float* __restrict__ dw4,
-                          float* __restrict__ db4, const FinAdam& fa) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int o = blk * DW4_CPB + wave / DW4_WPC, qq = wave % DW4_WPC;
-  const int ca = C * qq / DW4_WPC, cb = C * (qq + 1) / DW4_WPC;
-  // Adam state of the row (and bias) this wave finishes, in flight during the gather
-  const bool adam = fa.on && qq == 0 && o < O;
-  const size_t jw = PCADV_G_CONV4_W + (size_t)(o < O ? o : 0) * 128 + 2 * lane;
-  const size_t jb = PCADV_G_CONV4_B + (o < O ? o : 0);
-  float2 ap = make_float2(0.f, 0.f), am = ap, av = ap;
-  float bp = 0.f, bm = 0.f, bv = 0.f;
-  if (adam) {
-    ap = *reinterpret_cast<const float2*>(fa.gp + jw);
-    am = *reinterpret_cast<const float2*>(fa.gm + jw);
-    av = *reinterpret_cast<const float2*>(fa.gv + jw);
-    bp = fa.gp[jb];
-    bm = fa.gm[jb];
-    bv = fa.gv[jb];
-  }
-  const AdamHp h = adam ? adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g)
-                        : AdamHp{};
-  float ax = 0.f, ay = 0.f, ab = 0.f;
-  if (o < O) {
-    for (int c0 = ca; c0 < cb; c0 += 64) {
-      const int cl = c0 + lane, cnt = min(64, cb - c0);
-      const bool vl = lane < cnt;
-      const float gl = vl ? dg[(size_t)cl * O + o] : 0.f;
-      const int nl = vl ? gidx[(size_t)cl * O + o] : 0;
-      constexpr int U = 16;
-      for (int u0 = 0; u0 < cnt; u0 += U) {
-        float2 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int cu = min(u0 + u, cnt - 1);  // clamped: loads past cnt are discarded
-          const int n = __builtin_amdgcn_readlane(nl, cu);
-          v[u] = *reinterpret_cast<const float2*>(x3 + ((size_t)(c0 + cu) * N + n) * 128 + 2 * lane);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u0 + u < cnt) {
-            const float g = __builtin_bit_cast(
-                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gl), u0 + u));
-            ax = fmaf(g, v[u].x, ax);
-            ay = fmaf(g, v[u].y, ay);
-            ab += g;
-          }
-        }
-      }
-    }
-  }
-  part[wave][lane] = make_float4(ax, ay, ab, 0.f);
-  __syncthreads();
-  if (qq == 0 && o < O) {
-    float4 t = part[wave][lane];
-#pragma unroll
-    for (int k = 1; k < DW4_WPC; ++k) {
-      const float4 p = part[wave + k][lane];
-      t.x += p.x;
-      t.y += p.y;
-      t.z += p.z;
-    }
-    *reinterpret_cast<float2*>(dw4 + (size_t)o * 128 + 2 * lane) = make_float2(t.x, t.y);
-    if (lane == 0) db4[o] = t.z;
-    if (adam) {
-      adam_elem(ap.x, t.x, am.x, av.x, h);
-      adam_elem(ap.y, t.y, am.y, av.y, h);
-      *reinterpret_cast<float2*>(fa.gp + jw) = ap;
-      *reinterpret_cast<float2*>(fa.gm + jw) = am;
-      *reinterpret_cast<float2*>(fa.gv + jw) = av;
-      if (lane == 0) {
-        adam_elem(bp, t.z, bm, bv, h);
-        fa.gp[jb] = bp;
-        fa.gm[jb] = bm;
-        fa.gv[jb] = bv;
-      }
-    }
-  }
-}
-
-
-// One launch after k_feat_bwd_chunk: blocks [0, nred) reduce the slabs
-// (dW1..db3), the rest gather dW4/db4 (DW4_CPB channels per block): 228
-// blocks, one dispatch round.  With the fused Adam each block also updates the
-// parameters it finished (the other Adam work rode along k_feat_bwd_chunk).
-constexpr int FIN_NRED = (SLAB + 127) / 128;
+// One launch after k_feat_bwd_chunk: FIN_NRED blocks reduce the slabs
+// (dW1..db3) and, with the fused Adam, update those parameters; nb4 more
+// blocks update conv4's (its gradient came from the chunk launch, whose
+// chunks read W4 until they end).  The dW4 gather and the other Adam work rode
+// along k_feat_bwd_chunk.
+constexpr int FIN_NRED = (SLAB + FIN_COLS - 1) / FIN_COLS;
 __global__ void __launch_bounds__(1024)
 k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
-                  float* db2, float* dw3, float* db3, const float* __restrict__ dg,
-                  const int32_t* __restrict__ gidx, int C, int N, int O,
-                  const float* __restrict__ x3, float* __restrict__ dw4, float* __restrict__ db4,
-                  int blk0, FinAdam fa) {
-  __shared__ float4 part[16][64];
-  const int blk = (int)blockIdx.x + blk0, ndw4 = (O + DW4_CPB - 1) / DW4_CPB;
-  if (blk < FIN_NRED)
-    reduce_slabs_block(blk, reinterpret_cast<float2(*)[64]>(part), slabs, nslabs, dw1, db1, dw2,
-                       db2, dw3, db3, fa);
-  else if (blk < FIN_NRED + ndw4)
-    dw4_block(blk - FIN_NRED, part, dg, gidx, C, N, O, x3, dw4, db4, fa);
+                  float* db2, float* dw3, float* db3, FinAdam fa, int nb4) {
+  __shared__ float part[16][64];
+  const int blk = (int)blockIdx.x;
+  if (blk < FIN_NRED) {
+    reduce_slabs_block(blk, part, slabs, nslabs, dw1, db1, dw2, db2, dw3, db3, fa);
+  } else {
+    constexpr int64_t W4 = PCADV_G_CONV4_W, N4 = PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W;
+    adam_range<1024, 2>(blk - FIN_NRED, nb4, fa.gp + W4, fa.gm + W4, fa.gv + W4, fa.gg + W4, N4,
+                        fa.lr_g, fa);
+  }
 }
 
 size_t feat_bwd_workspace_bytes(int C, int N) {
@@ -851,29 +819,22 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
     nba0 = fin_adam_blocks(fa.g_n - fa.g_rest0, BW_T, FIN_ADAM_V4);
     nba1 = fa.d_n > 0 ? fin_adam_blocks(fa.d_n, BW_T, FIN_ADAM_V4) : 0;
   }
-  const int arows = (nba0 + nba1 + nchunk - 1) / nchunk;
+  // trailing workgroup rows: the dW4 gather (NDW4), then the Adam workgroups
+  PC_REQUIRE(O == BW_MAXO, "feat_bwd: %d pooled channels (expects %d)", O, BW_MAXO);
+  constexpr int NDW4 = BW_MAXO / (BW_T / 64 / DW4_WPC);
+  const int arows = (NDW4 + nba0 + nba1 + nchunk - 1) / nchunk;
   if (sortrec)
     hipLaunchKernelGGL(k_feat_bwd_chunk<true>, dim3(nchunk, C + arows), dim3(BW_T), sizeof(BwdLds),
                        s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs,
-                       stamps, sortrec, C, fa, nba0, nba1);
+                       stamps, sortrec, C, dw4, db4, fa, nba0, nba1);
   else
     hipLaunchKernelGGL(k_feat_bwd_chunk<false>, dim3(nchunk, C + arows), dim3(BW_T),
                        sizeof(BwdLds), s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3,
-                       w4, x3, slabs, stamps, sortrec, C, fa, nba0, nba1);
+                       w4, x3, slabs, stamps, sortrec, C, dw4, db4, fa, nba0, nba1);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
-  const int ndw4 = (O + DW4_CPB - 1) / DW4_CPB;
-#ifdef PCADV_STAMPS
-  // diagnostic build: the slab reduction and the dW4 gather as separate
-  // launches so a kernel trace times each part
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED), dim3(1024), 0, s, slabs, C * nchunk, dw1,
-                     db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0, fa);
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(ndw4), dim3(1024), 0, s, slabs, C * nchunk, dw1, db1,
-                     dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, FIN_NRED, fa);
-#else
-  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + ndw4), dim3(1024), 0, s, slabs,
-                     C * nchunk, dw1, db1, dw2, db2, dw3, db3, dg, gidx, C, N, O, x3, dw4, db4, 0,
-                     fa);
-#endif
+  const int nb4 = fa.on ? fin_adam_blocks(PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W, 1024, 2) : 0;
+  hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + nb4), dim3(1024), 0, s, slabs, C * nchunk,
+                     dw1, db1, dw2, db2, dw3, db3, fa, nb4);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
   return PCADV_OK;
 }
