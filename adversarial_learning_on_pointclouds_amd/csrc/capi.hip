@@ -69,7 +69,7 @@ int lin_stamps_read(uint64_t* host, int reset);
 int launch_head_bwd(const float*, const float*, const float*, float, const float*, int,
                     const float*, const float*, float*, float*, float*, float*, const float*,
                     const float*, float*, int, float, float, const float*, const float*,
-                    hipStream_t);
+                    hipStream_t, const float*);
 int launch_gemm(const float*, long long, int, const float*, long long, int, float*, long long,
                 int, int, int, const float*, const float*, int, int, int, const float*, long long,
                 int, void*, void*, long long, hipStream_t);
@@ -104,6 +104,7 @@ struct StepWs {
   float *din, *d1, *d2, *d3;
   float *dd3, *dd2, *dd1;
   float *z4, *z5, *a4;  // D conv4 / conv5 dz rows and conv4 output rows (k_disc_tail)
+  float* ddp;           // D conv1 input-gradient partials [512 / 16][B][40] (chained)
   float *mask;
   float *lpart, *lpart3, *dslabs, *dout;
   int32_t* gidx;
@@ -144,6 +145,7 @@ static StepWs carve(int B, int N, char* base) {
   w.z4 = take(R * 64);
   w.z5 = take(R * 64);
   w.a4 = take(R * 64);
+  w.ddp = take(32 * (size_t)B * 40);
   w.mask = take(C * 256);
   w.lpart = take(head_rowblocks(B));
   w.lpart3 = take(3 * (size_t)disc_rowblocks(B));
@@ -305,9 +307,19 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
                              D + PCADV_D_CONV3_W, w.dd2, gD + PCADV_D_CONV3_W,
                              gD + PCADV_D_CONV3_B, R, MW, 256, 256, s, &ex));
   }
+  // the adversarial rows' dd1 tiles also multiply into D conv1's weight: the
+  // partials of its input gradient (summed by k_head_bwd), when the rows [2B, 3B)
+  // start a row tile
+  const bool chain = (2 * B) % 16 == 0;
   {
     LinBwdExtra ex{};
     ex.dx_act = PCADV_ACT_LRELU;  // x = conv1 output
+    if (chain) {
+      ex.chain_w = D + PCADV_D_CONV1_W;  // [512][40]
+      ex.chain_out = w.ddp;
+      ex.chain_row0 = 2 * B;
+      ex.chain_n = 40;
+    }
     PC_TRY(launch_linear_bwd(w.dd2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.d1,
                              D + PCADV_D_CONV2_W, w.dd1, gD + PCADV_D_CONV2_W,
                              gD + PCADV_D_CONV2_B, R, MW, 256, 512, s, &ex));
@@ -317,7 +329,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   PC_TRY(launch_head_bwd(w.dd1, w.h2, bmask, a->drop_p, w.din, B, D + PCADV_D_CONV1_W,
                          G + PCADV_G_FC3_W, w.dlogits, w.dh2, nullptr, nullptr, w.lpart,
                          w.lpart3, a->losses, a->semi, a->lambda_semi, a->semi_th, logits,
-                         w.dout, s));
+                         w.dout, s, chain ? w.ddp : nullptr));
   // ---- generator head backward (:520); fc3's weight grad rides along -------
   {
     LinBwdExtra ex{};

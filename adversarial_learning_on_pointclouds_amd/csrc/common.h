@@ -207,6 +207,14 @@ struct LinBwdExtra {
   int dx_act;
   const float* dx_mask;
   float dx_keep;
+  // chained product of the data gradient's rows >= chain_row0 with the next
+  // layer down's weight W' [K][chain_n] (row-major): per 16-column tile ct of
+  // dx, chain_out[ct][m - chain_row0][j] = sum_{c in tile} dx[m][c] W'[c][j].
+  // The consumer sums the K / 16 tile partials (the discriminator conv1 input
+  // gradient of the adversarial rows, k_head_bwd).
+  const float* chain_w;
+  float* chain_out;
+  int chain_row0, chain_n;
 };
 int launch_linear_bwd(const float* dy, const float* y, int act, const float* mask,
                       const int32_t* step, uint64_t seed, float p, const float* x, const float* w,

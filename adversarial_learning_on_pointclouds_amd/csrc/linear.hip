@@ -59,6 +59,10 @@ struct GemmArgs {
   const float* ox_mask;
   float ox_keep;
   int stamp_slot;  // diagnostic build: row of g_lin_stamps (-1: none)
+  // backward data: chained tile product (LinBwdExtra.chain_*), chain_n <= 48
+  const float* chain_w;
+  float* chain_out;
+  int chain_row0, chain_n;
 };
 
 #ifdef PCADV_STAMPS
@@ -305,6 +309,36 @@ __device__ void split_job(const GemmArgs& g, int tile, int rows, int cols, int R
         if (g.ox_act != ACT_NONE) v *= act_bwd(g.x[i], g.ox_act);
         if (g.ox_mask) v *= g.ox_mask[i] * g.ox_keep;
         g.dx[i] = v;
+        if (OP == OP_BWD_DATA && g.chain_out) bt[e] = v;
+      }
+    }
+  }
+  if (OP == OP_BWD_DATA && g.chain_out && r0 >= g.chain_row0) {
+    // this tile's share of dx[rows] W'[c0 .. c0 + 16][:]: 16 x chain_n on
+    // 16x16x4 MFMAs (exact f32), k = the tile's 16 columns in order; the tile
+    // sits in bt[] (rows or columns past the matrix are zero)
+    for (int e = tid; e < 256; e += 64 * S) {
+      const int row = e >> 4, cc = e & 15;
+      if (!(r0 + row < rows && c0 + cc < cols)) bt[e] = 0.f;
+    }
+    __syncthreads();
+    const int nt = (g.chain_n + 15) / 16, r = lane & 15;
+    if (wave < nt) {
+      const int j = 16 * wave + r;
+      f32x4v acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int k = 4 * s4 + q;
+        const bool vb = j < g.chain_n && c0 + k < cols;
+        const float wv = g.chain_w[(size_t)(vb ? c0 + k : 0) * g.chain_n + (vb ? j : 0)];
+        acc2 = mfma16(bt[r * 16 + k], vb ? wv : 0.f, acc2);
+      }
+      const int nrc = g.M - g.chain_row0;
+      float* out = g.chain_out + ((size_t)(c0 / 16) * nrc + (r0 - g.chain_row0)) * g.chain_n;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = 4 * q + v;
+        if (r0 + row < rows && j < g.chain_n) out[(size_t)row * g.chain_n + j] = acc2[v];
       }
     }
   }
@@ -388,7 +422,7 @@ __global__ void __launch_bounds__(1024)
 k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, int wmode) {
   kernarg_prefetch(g.x, g.w, g.dy, g.dx, g.dw, g.db, g.M, g.N, g.K, g.m_w, g.ox_act, g.ox_mask,
                    g.ox_keep, S, L, nbx, nwt, blk0, ex.njobs, ex.red_src, ex.red_dst, ex.red_n,
-                   ex.red_cnt, ex.red_ld, wmode);
+                   ex.red_cnt, ex.red_ld, wmode, g.chain_out, g.chain_w, g.chain_row0, g.chain_n);
   if (ACT != ACT_NONE) kernarg_prefetch(g.yact);
   if (DM != DM_NONE) kernarg_prefetch(g.drop.mask, g.drop.step, g.drop.seed, g.drop.p);
   constexpr bool FAST = ACT == ACT_NONE && DM == DM_NONE;
@@ -514,9 +548,21 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
     g.ox_act = extra->dx_act;
     g.ox_mask = extra->dx_mask;
     g.ox_keep = extra->dx_keep;
+    g.chain_w = extra->chain_w;
+    g.chain_out = extra->chain_out;
+    g.chain_row0 = extra->chain_row0;
+    g.chain_n = extra->chain_n;
   }
   int S, L;
   split_cfg(N, &S, &L);
+  if (g.chain_out) {
+    // the tile product runs in the backward-data blocks' LDS regions, one
+    // 16-column output tile per wave, on row tiles that start at chain_row0
+    PC_REQUIRE(dx && g.chain_w && dz_as_is && (N & 3) == 0 && S <= BT_MAXS && g.chain_n > 0 &&
+                   g.chain_n <= 16 * S && g.chain_row0 >= 0 && g.chain_row0 < M &&
+                   g.chain_row0 % 16 == 0,
+               "linear_bwd: bad chained product (n=%d row0=%d S=%d)", g.chain_n, g.chain_row0, S);
+  }
   const int nbx = dx ? ((M + 15) / 16) * ((K + 15) / 16) : 0;
   const int nwt = dw ? ((N + 15) / 16) * ((K + 15) / 16) : 0;
   const int dm = drop_mode(g.drop);

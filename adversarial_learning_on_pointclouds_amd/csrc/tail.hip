@@ -485,7 +485,7 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
            const float* __restrict__ w3, float* __restrict__ dlogits, float* __restrict__ dh2,
            float* __restrict__ gw1, float* __restrict__ gb1, const float* __restrict__ lpart,
            int nlp, const float* __restrict__ lpart3, int nlp3, float* __restrict__ losses,
-           SemiArgs semi) {
+           SemiArgs semi, const float* __restrict__ ddp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   HeadBwdLds& L = *reinterpret_cast<HeadBwdLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -537,41 +537,79 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
     const int m = r0 + wave;
     if (m < C && lane < 40) lsm_or_dl = m >= B ? din[(size_t)m * 40 + lane] : dlogits[(size_t)m * 40 + lane];
   }
-  // dz of the adversarial D rows m + B (m in [B, 2B)); zero for GT rows.  The
-  // row loads are issued together with the conv1 weight staging.
-  f32x4 zd[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
-    const bool v = m >= B && m < C;
-    const size_t i = v ? (size_t)(m + B) * 512 + 4 * c4 : 0;
-    zd[u] = *reinterpret_cast<const f32x4*>(dz1 + i);
-  }
   // this block's h2 and dropout-mask rows (the output mask of the last layer),
   // fetched now and parked in LDS once z1 is consumed: one float4 each
   f32x4 hv, mv = {1.f, 1.f, 1.f, 1.f};
-  {
+  auto load_h2_mask = [&]() {
     const int row = tid >> 6, c4 = tid & 63, m = r0 + row;
     const size_t i = (size_t)(m < C ? m : 0) * 256 + 4 * c4;
     hv = *reinterpret_cast<const f32x4*>(h2 + i);
     if (drop_mask) mv = *reinterpret_cast<const f32x4*>(drop_mask + i);
-  }
-  {
-    const Fill f[1] = {{L.w1, 48, dw1, 512, 40, 512}};
-    lds_fill(f);  // 5120 float4: 5 per thread
-  }
+  };
+  if (ddp) {
+    // D conv1's input gradient of the adversarial rows from the 32 column-tile
+    // partials the D conv2 backward chained onto its data gradient
+    // (ddp[ct][m - B][40], LinBwdExtra.chain_*): 640 threads = (row, 4
+    // columns) x 4 groups of 8 tiles, summed in tile order, the groups in order
+    constexpr int NCT = 512 / 16, G4 = 4, PER = NCT / G4, NIT = TR * 10;
+    const bool any = r0 + TR > B;  // block-uniform: GT-only blocks need no ddin
+    f32x4 pv[PER];
+    const int item = tid % NIT, grp = tid / NIT, row = item / 10, j4 = item % 10, m = r0 + row;
+    const bool vr = any && grp < G4 && m >= B && m < C;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
-    const bool v = m >= B && m < C;
+    for (int u = 0; u < PER; ++u) {
+      const size_t i = vr ? ((size_t)(grp * PER + u) * B + (m - B)) * 40 + 4 * j4 : 0;
+      pv[u] = *reinterpret_cast<const f32x4*>(ddp + i);
+    }
+    load_h2_mask();
+    f32x4* gs = reinterpret_cast<f32x4*>(L.scratch);  // [G4][NIT]
+    if (grp < G4) {
+      f32x4 t = vr ? pv[0] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      L.z1[row * 516 + 4 * c4 + i] = v ? zd[u][i] : 0.f;
+      for (int u = 1; u < PER; ++u)
+        if (vr) t += pv[u];
+      gs[grp * NIT + item] = t;
+    }
+    __syncthreads();
+    TSTAMP(2, 1);
+    if (tid < NIT) {
+      f32x4 t = gs[item];
+#pragma unroll
+      for (int g = 1; g < G4; ++g) t += gs[g * NIT + item];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) L.ddin[row * 44 + 4 * j4 + i] = t[i];
+    }
+    __syncthreads();
+    TSTAMP(2, 2);
+  } else {
+    // dz of the adversarial D rows m + B (m in [B, 2B)); zero for GT rows.  The
+    // row loads are issued together with the conv1 weight staging.
+    f32x4 zd[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
+      const bool v = m >= B && m < C;
+      const size_t i = v ? (size_t)(m + B) * 512 + 4 * c4 : 0;
+      zd[u] = *reinterpret_cast<const f32x4*>(dz1 + i);
+    }
+    load_h2_mask();
+    {
+      const Fill f[1] = {{L.w1, 48, dw1, 512, 40, 512}};
+      lds_fill(f);  // 5120 float4: 5 per thread
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * TT, row = e >> 7, c4 = e & 127, m = r0 + row;
+      const bool v = m >= B && m < C;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        L.z1[row * 516 + 4 * c4 + i] = v ? zd[u][i] : 0.f;
+    }
+    __syncthreads();
+    TSTAMP(2, 1);
+    rows_layer<512, 40, B_KO, ACT_NONE>(L.z1, 516, L.w1, 48, nullptr, L.ddin, 44, L.scratch);
+    TSTAMP(2, 2);
   }
-  __syncthreads();
-  TSTAMP(2, 1);
-  rows_layer<512, 40, B_KO, ACT_NONE>(L.z1, 516, L.w1, 48, nullptr, L.ddin, 44, L.scratch);
-  TSTAMP(2, 2);
   float* h2s = L.z1;             // [16][256], z1 is free now
   float* ms = L.z1 + TR * 256;   // [16][256]
   *reinterpret_cast<f32x4*>(h2s + 4 * tid) = hv;
@@ -708,7 +746,7 @@ int launch_head_bwd(const float* dz1, const float* h2, const float* drop_mask, f
                     const float* w3, float* dlogits, float* dh2, float* gw1, float* gb1,
                     const float* lpart, const float* lpart3, float* losses, int semi,
                     float lambda_semi, float semi_th, const float* logits, const float* dout,
-                    hipStream_t s) {
+                    hipStream_t s, const float* ddp) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_head_bwd, sizeof(HeadBwdLds), "head_bwd") != PCADV_OK) return PCADV_EHIP;
@@ -722,7 +760,7 @@ int launch_head_bwd(const float* dz1, const float* h2, const float* drop_mask, f
   const float keep = 1.0f / (1.0f - drop_p);  // as the linear kernels' dropout scale
   hipLaunchKernelGGL(k_head_bwd, dim3(nrb + nwb), dim3(TT), sizeof(HeadBwdLds), s, dz1, h2,
                      drop_mask, keep, din, B, dw1, w3, dlogits, dh2, gw1, gb1, lpart, nrb, lpart3, disc_rowblocks(B),
-                     losses, sa);
+                     losses, sa, ddp);
   PC_HIP_CHECK_LAUNCH("k_head_bwd");
   return PCADV_OK;
 }
