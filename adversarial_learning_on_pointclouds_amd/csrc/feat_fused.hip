@@ -195,7 +195,10 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       STAMP(6 + 5 * it);
       // stage the 64 x 128 tile through LDS (over x1 / x2: every wave is past
       // conv3's reads after the barrier), then write it as the contiguous 32 KB
-      // it is in HBM with 16-B stores: a quarter of the store instructions
+      // it is in HBM with 16-B stores: a quarter of the store instructions.
+      // Nontemporal: a cloud's tiles are written from all eight XCDs and read by
+      // k_conv4_max on one, so lines left dirty in this XCD's L2 would only be
+      // written back at the launch boundary (step -1.2 us in A/B)
       __syncthreads();
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt)
@@ -210,8 +213,8 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       for (int u = 0; u < PM_P * 32 / PM_T; ++u) {
         const int e = tid + PM_T * u, row = e >> 5, c4 = e & 31;
         if (p0 + row < N)
-          *reinterpret_cast<f32x4*>(xg + (size_t)row * 128 + 4 * c4) =
-              *reinterpret_cast<const f32x4*>(&L.x3[row * X3S + 4 * c4]);
+          __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&L.x3[row * X3S + 4 * c4]),
+                                      reinterpret_cast<f32x4*>(xg + (size_t)row * 128 + 4 * c4));
       }
       STAMP(7 + 5 * it);
     }
