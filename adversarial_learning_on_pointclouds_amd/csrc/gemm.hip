@@ -106,7 +106,9 @@ constexpr int GKEY_NONE = (int)0x80000000;
 // on the way into LDS.  Transposed operands (TA / TB = 1: the reduction axis is
 // the slow one) are read as 4 (k) x 4 (m) blocks per thread and written as
 // 4-k runs (ds_write_b64) of each plane.
-template <int TA, int TB, int MODE, int NP>
+// VEC bit 0 / bit 1: A / B staged by 16-byte loads (vector-aligned, no
+// vector straddles an edge), else by dword loads
+template <int TA, int TB, int MODE, int NP, int VEC>
 __global__ void __launch_bounds__(GM_T)
 k_gemm_x3(GemmP p) {
   constexpr int NPL = NP == 6 ? 3 : 2;
@@ -157,40 +159,69 @@ k_gemm_x3(GemmP p) {
   // one operand tile (128 x 32 f32 = 4096 values, 16 per thread)
   //   [m][k] layout: thread = (row tid >> 1, 16 k at 16 (tid & 1))
   //   [k][m] layout: thread = (4 k at 4 (tid & 7), 4 m at 4 (tid >> 3))
-  auto load_rows = [&](f32x4 (&v)[4], const float* base, long long ld, int row0, int rlim, int k0,
-                       bool vec) {
+  // Buffer loads with no data-dependent selects or branches: a masked vector
+  // or element gets an offset past the buffer's end and reads zeros (the old
+  // `if (in range) load` form made the compiler wait out each load before the
+  // next one).  Vector loads only where no vector straddles the edge (vec and
+  // the edge a multiple of 4, a launch constant), else four dword loads.
+  constexpr uint32_t OOB = 0x80000000u;
+  // an opaque copy of a masked offset: the compiler otherwise turns the mask
+  // into branches around duplicated loads (divergent control flow that drains
+  // the loads in flight)
+  auto opq = [](uint32_t o) {
+    asm("" : "+v"(o));
+    return o;
+  };
+  auto rsrc = [](const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+  };
+  // (planes: hi and lo resources, A's at this cloud's rows in mode 2)
+  const __amdgpu_buffer_rsrc_t ars = rsrc(TA == 2 ? (const void*)(p.ap[0] + aoff2) : (const void*)Ab);
+  const __amdgpu_buffer_rsrc_t arsl = rsrc(TA == 2 ? (const void*)(p.ap[1] + aoff2) : (const void*)Ab);
+  const __amdgpu_buffer_rsrc_t brs = rsrc(TB == 2 ? (const void*)p.bp[0] : (const void*)p.b);
+  const __amdgpu_buffer_rsrc_t brsl = rsrc(TB == 2 ? (const void*)p.bp[1] : (const void*)p.b);
+  constexpr bool vecA = (VEC & 1) != 0, vecB = (VEC & 2) != 0;
+  auto load_rows = [&](f32x4 (&v)[4], const __amdgpu_buffer_rsrc_t& rs, long long ld, int row0,
+                       int rlim, int k0, auto VECT) {
+    constexpr bool vec = decltype(VECT)::value;
     const int row = row0 + (tid >> 1), kk = k0 + 16 * (tid & 1);
+    const bool rok = row < rlim;
+    const uint32_t rb = rok ? (uint32_t)((long long)row * ld) : 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = kk + 4 * j;
-      f32x4 x = {0.f, 0.f, 0.f, 0.f};
-      if (row < rlim && k >= kz0 && k < kz1) {
-        const float* src = base + (size_t)row * ld + k;
-        if (vec && k + 3 < kz1) {
-          x = *reinterpret_cast<const f32x4*>(src);
-        } else {
-          for (int t = 0; t < 4 && k + t < kz1; ++t) x[t] = src[t];
+      if constexpr (vec) {
+        const uint32_t off = opq(rok && k >= kz0 && k < kz1 ? (rb + (uint32_t)k) * 4u : OOB);
+        v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int kt = k + t;
+          const uint32_t off = opq(rok && kt >= kz0 && kt < kz1 ? (rb + (uint32_t)kt) * 4u : OOB);
+          v[j][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
         }
       }
-      v[j] = x;
     }
   };
-  auto load_cols = [&](f32x4 (&v)[4], const float* base, long long ld, int col0, int clim, int k0,
-                       bool vec) {
+  auto load_cols = [&](f32x4 (&v)[4], const __amdgpu_buffer_rsrc_t& rs, long long ld, int col0,
+                       int clim, int k0, auto VECT) {
+    constexpr bool vec = decltype(VECT)::value;
     const int col = col0 + 4 * (tid >> 3), kk = k0 + 4 * (tid & 7);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = kk + j;
-      f32x4 x = {0.f, 0.f, 0.f, 0.f};
-      if (k >= kz0 && k < kz1 && col < clim) {
-        const float* src = base + (size_t)k * ld + col;
-        if (vec && col + 3 < clim) {
-          x = *reinterpret_cast<const f32x4*>(src);
-        } else {
-          for (int t = 0; t < 4 && col + t < clim; ++t) x[t] = src[t];
+      const bool kok = k >= kz0 && k < kz1;
+      const uint32_t kb = kok ? (uint32_t)((long long)k * ld) : 0u;
+      if constexpr (vec) {
+        const uint32_t off = opq(kok && col < clim ? (kb + (uint32_t)col) * 4u : OOB);
+        v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t off = opq(kok && col + t < clim ? (kb + (uint32_t)(col + t)) * 4u : OOB);
+          v[j][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
         }
       }
-      v[j] = x;
     }
   };
   auto store_rows = [&](const f32x4 (&v)[4], __bf16 (*planes)[GM_BM * GM_S]) {
@@ -228,16 +259,15 @@ k_gemm_x3(GemmP p) {
   };
   // planes: thread = (row tid >> 1, 16 k at 16 (tid & 1)); v[0..1] = hi, v[2..3]
   // = lo, each 8 bf16 carried as 16 raw bytes (K % 16 == 0, ld % 8 == 0)
-  auto load_planes = [&](f32x4 (&v)[4], const __bf16* const (&pl)[2], size_t off, long long ld,
-                         int row0, int rlim, int k0) {
+  auto load_planes = [&](f32x4 (&v)[4], const __amdgpu_buffer_rsrc_t& rh,
+                         const __amdgpu_buffer_rsrc_t& rl, long long ld, int row0, int rlim, int k0) {
     const int row = row0 + (tid >> 1), k = k0 + 16 * (tid & 1);
     const bool ok = row < rlim && k >= kz0 && k < kz1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const __bf16* src = pl[q] + off + (size_t)row * ld + k;
-      v[2 * q] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
-      v[2 * q + 1] = ok ? *reinterpret_cast<const f32x4*>(src + 8) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    const uint32_t o = opq(ok ? (uint32_t)((long long)row * ld + k) * 2u : OOB);
+    v[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, o, 0, 0));
+    v[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, o + 16u, 0, 0));
+    v[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, o, 0, 0));
+    v[3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, o + 16u, 0, 0));
   };
   auto store_planes = [&](const f32x4 (&v)[4], __bf16 (*planes)[GM_BM * GM_S]) {
     const int row = tid >> 1, kk = 16 * (tid & 1);
@@ -249,12 +279,12 @@ k_gemm_x3(GemmP p) {
   };
   float cs[4] = {0.f, 0.f, 0.f, 0.f};  // TA = 1: this thread's column sums of A
   auto load_tile = [&](f32x4 (&ra)[4], f32x4 (&rb)[4], int k0) {
-    if (TA == 2) load_planes(ra, p.ap, aoff2, p.ldap, m0, Mlim, k0);
-    else if (TA == 0) load_rows(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
-    else load_cols(ra, Ab, p.lda, m0, Mlim, k0, p.avec);
-    if (TB == 2) load_planes(rb, p.bp, 0, p.ldbp, n0, p.N, k0);
-    else if (TB == 0) load_rows(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
-    else load_cols(rb, p.b, p.ldb, n0, p.N, k0, p.bvec);
+    if (TA == 2) load_planes(ra, ars, arsl, p.ldap, m0, Mlim, k0);
+    else if (TA == 0) load_rows(ra, ars, p.lda, m0, Mlim, k0, std::integral_constant<bool, vecA>{});
+    else load_cols(ra, ars, p.lda, m0, Mlim, k0, std::integral_constant<bool, vecA>{});
+    if (TB == 2) load_planes(rb, brs, brsl, p.ldbp, n0, p.N, k0);
+    else if (TB == 0) load_rows(rb, brs, p.ldb, n0, p.N, k0, std::integral_constant<bool, vecB>{});
+    else load_cols(rb, brs, p.ldb, n0, p.N, k0, std::integral_constant<bool, vecB>{});
   };
   auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
     if (TA == 2) store_planes(ra, L.a);
@@ -311,25 +341,17 @@ k_gemm_x3(GemmP p) {
     }
   };
 
-  // two register sets: tile t+2 is loaded while tile t is multiplied.  The
-  // loop is unrolled by two with straight-line phases (so each store waits
-  // only for its own set's loads); an odd tile count starts one empty tile
-  // early (its loads are all masked to zero).
-  f32x4 ra0[4], rb0[4], ra1[4], rb1[4];
-  const int ntile = (kz1 - kz0 + GM_BK - 1) / GM_BK;
-  const int kb0 = kz0 - (ntile & 1) * GM_BK;  // first (possibly empty) tile
-  load_tile(ra0, rb0, kb0);
-  load_tile(ra1, rb1, kb0 + GM_BK);
-  for (int k0 = kb0; k0 < kz1; k0 += 2 * GM_BK) {
+  // one register set: tile t + 1 is loaded right after tile t is stored; the
+  // sched_barrier keeps those loads ahead of tile t's MFMAs (as
+  // k_gemm_bf2_big), so one tile's MFMAs cover the next tile's loads
+  f32x4 ra[4], rb[4];
+  load_tile(ra, rb, kz0);
+  for (int k0 = kz0; k0 < kz1; k0 += GM_BK) {
     __syncthreads();  // every wave is done reading the previous tile
-    store_tile(ra0, rb0);
+    store_tile(ra, rb);
     __syncthreads();
-    load_tile(ra0, rb0, k0 + 2 * GM_BK);
-    mfma_tile();
-    __syncthreads();
-    store_tile(ra1, rb1);
-    __syncthreads();
-    load_tile(ra1, rb1, k0 + 3 * GM_BK);
+    load_tile(ra, rb, k0 + GM_BK);
+    __builtin_amdgcn_sched_barrier(0);
     mfma_tile();
   }
 
@@ -451,6 +473,282 @@ k_gemm_x3(GemmP p) {
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// 256 x 256 tiles for the wide plane-operand GEMMs (conv5 -> 2048 with the
+// max screening, conv4 -> 512): both operands given as bf16 hi / lo planes
+// (TA = TB = 2), three products.  At 128 x 128 a workgroup streams 1 KB of
+// planes per k for 16 K MACs; at 256 x 256 the same bytes feed 4x the MACs,
+// which halves the L2 -> LDS bytes per FLOP (the 128-tile conv6 pulls ~2 GB
+// per launch through L2).  Eight waves (2 x 4), each a 128 x 64 block of C
+// as 4 x 2 accumulators of 32 x 32; one workgroup per CU.  Every output sums
+// the same MFMAs in the same order as k_gemm_x3<2, 2, MODE, 3> (k-blocks in
+// order, lo.hi + hi.lo + hi.hi), so the results are bitwise the same; the
+// screening epilogue writes one top-2 record per 128-row half, the format
+// k_max_combine reads from the 128-row kernel.
+// ---------------------------------------------------------------------------
+constexpr int GB_BM = 256, GB_BN = 256;
+constexpr int GB_T = 512;
+constexpr int GB_ES = 132;  // row stride (floats) of the staged 256 x 128 epilogue half
+struct GemmBigLds {
+  union {
+    struct {
+      alignas(16) __bf16 a[2][GB_BM * GM_S];  // [hi, lo][m][k]
+      alignas(16) __bf16 b[2][GB_BN * GM_S];  // [hi, lo][n][k]
+    } op;
+    alignas(16) float stage[GB_BM * GB_ES];
+  };
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(GB_T)
+k_gemm_bf2_big(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  GemmBigLds& L = *reinterpret_cast<GemmBigLds*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 2, wn = wave & 3;
+  // XCD-aware order (as k_gemm_x3): the workgroups of one XCD take consecutive
+  // tiles, column tile fastest, so the column tiles of a row tile share its A
+  int tx, ty;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy;
+    const int lin = blockIdx.x + gx * blockIdx.y;
+    const int xcd = lin & 7, q = n >> 3, rr = n & 7;
+    const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (lin >> 3);
+    tx = t / gy;
+    ty = t % gy;
+  }
+  const int n0 = ty * GB_BN;
+  // mode 2: tx = (cloud, 256-row tile of that cloud); rows never straddle clouds
+  const int T2 = MODE == 2 ? p.rows_per_group / GB_BM : 1;
+  const int cl = MODE == 2 ? tx / T2 : 0;
+  const int m0 = MODE == 2 ? (tx % T2) * GB_BM : tx * GB_BM;
+  const int Mlim = MODE == 2 ? p.rows_per_group : p.M;
+  const size_t aoff = MODE == 2 ? (size_t)cl * p.rows_per_group * p.ldap : 0;
+  const int K = p.K;
+
+  // planes of one 256 x 32 tile: thread = (row tid >> 1, 16 k at 16 (tid & 1));
+  // v[0..1] = hi, v[2..3] = lo, 8 bf16 each carried as 16 raw bytes.  Buffer
+  // loads: a masked element (row past the matrix, k outside [0, K)) gets an
+  // offset past the buffer's end and reads zeros, so no select waits on the
+  // data (a select after the load made the compiler drain every load of the
+  // prefetch right after issuing it); 32-bit offsets, no 64-bit addresses.
+  const int lrow = tid >> 1, lk = 16 * (tid & 1);
+  const __amdgpu_buffer_rsrc_t arsc[2] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.ap[0] + aoff), (short)0, 0x7fffffff, 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.ap[1] + aoff), (short)0, 0x7fffffff, 0x00020000)};
+  const __amdgpu_buffer_rsrc_t brsc[2] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.bp[0], (short)0, 0x7fffffff, 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.bp[1], (short)0, 0x7fffffff, 0x00020000)};
+  constexpr uint32_t OOB = 0x80000000u;  // >= num_records: the load returns zeros
+  const bool arow_ok = m0 + lrow < Mlim, brow_ok = n0 + lrow < p.N;
+  const uint32_t abase = (uint32_t)((m0 + lrow) * p.ldap + lk) * 2u;
+  const uint32_t bbase = (uint32_t)((n0 + lrow) * p.ldbp + lk) * 2u;
+  auto load_planes = [&](f32x4 (&v)[4], const __amdgpu_buffer_rsrc_t (&rs)[2], uint32_t base,
+                         bool row_ok, int k0) {
+    const int k = k0 + lk;
+    const uint32_t off = row_ok && k >= 0 && k < K ? base + (uint32_t)k0 * 2u : OOB;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      v[2 * q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs[q], off, 0, 0));
+      v[2 * q + 1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs[q], off + 16u, 0, 0));
+    }
+  };
+  auto store_planes = [&](const f32x4 (&v)[4], __bf16 (*planes)[GB_BM * GM_S]) {
+    const int row = tid >> 1, kk = 16 * (tid & 1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk]) = v[2 * q];
+      *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk + 8]) = v[2 * q + 1];
+    }
+  };
+  auto load_tile = [&](f32x4 (&ra)[4], f32x4 (&rb)[4], int k0) {
+    load_planes(ra, arsc, abase, arow_ok, k0);
+    load_planes(rb, brsc, bbase, brow_ok, k0);
+  };
+  auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
+    store_planes(ra, L.op.a);
+    store_planes(rb, L.op.b);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  auto mfma_tile = [&]() {
+#pragma unroll
+    for (int kb = 0; kb < GM_BK / 16; ++kb) {
+      bf16x8g fb[2][2];  // [plane][j]
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int br = (64 * wn + 32 * j + r) * GM_S + 16 * kb + 8 * h;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) fb[q][j] = *reinterpret_cast<const bf16x8g*>(&L.op.b[q][br]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ar = (128 * wm + 32 * i + r) * GM_S + 16 * kb + 8 * h;
+        const bf16x8g ah = *reinterpret_cast<const bf16x8g*>(&L.op.a[0][ar]);
+        const bf16x8g al = *reinterpret_cast<const bf16x8g*>(&L.op.a[1][ar]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma_bf16g(al, fb[0][j], acc[i][j]);
+          acc[i][j] = mfma_bf16g(ah, fb[1][j], acc[i][j]);
+          acc[i][j] = mfma_bf16g(ah, fb[0][j], acc[i][j]);
+        }
+      }
+    }
+  };
+
+  // one register set: tile t + 1 is loaded right after tile t is stored, and
+  // the sched_barrier keeps those loads ahead of tile t's MFMAs (at 256 VGPRs
+  // the scheduler otherwise sinks them below the MFMAs, where their registers
+  // free up, and every store then waits out a full L2 round trip)
+  f32x4 ra[4], rb[4];
+  load_tile(ra, rb, 0);
+  for (int k0 = 0; k0 < K; k0 += GM_BK) {
+    __syncthreads();
+    store_tile(ra, rb);
+    __syncthreads();
+    load_tile(ra, rb, k0 + GM_BK);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_tile();
+  }
+
+  if constexpr (MODE == 2) {
+    // per column, the top-2 (value, row) of this wave's 128 rows: the wave's
+    // half of the tile is one 128-row tile of k_max_combine's record
+    const int T = 2 * T2;
+    const int t128 = 2 * (tx % T2) + wm;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int k1 = GKEY_NONE, k2 = GKEY_NONE;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = 32 * i + acc_row(e, lane);
+          if (m0 + 128 * wm + row < Mlim) {
+            const int key = gkey(acc[i][j][e], row);
+            k2 = max(min(key, k1), k2);
+            k1 = max(k1, key);
+          }
+        }
+      const int o1 = __shfl_xor(k1, 32), o2 = __shfl_xor(k2, 32);
+      k2 = max(min(k1, o1), max(k2, o2));
+      k1 = max(k1, o1);
+      const int n = n0 + 64 * wn + 32 * j + r;
+      if (h == 0 && n < p.N) p.part[((size_t)cl * T + t128) * p.N + n] = make_int2(k1, k2);
+    }
+  } else {
+    // epilogue through LDS, one 256 x 128 half of the tile at a time (each
+    // wave's 32-column block j), rows written by 32 lanes x 4 columns
+    float* stage = L.stage;
+    const bool vec = p.cvec;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      __syncthreads();  // the MFMA operands / the previous half are no longer read
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          stage[(128 * wm + 32 * i + acc_row(e, lane)) * GB_ES + 32 * wn + r] = acc[i][j][e];
+      __syncthreads();
+      const int c4 = 4 * (tid & 31);                 // staged column (0..124)
+      const int n = n0 + 64 * (c4 >> 5) + 32 * j + (c4 & 31);
+#pragma unroll 2
+      for (int it = 0; it < 16; ++it) {
+        const int row = (tid >> 5) + 16 * it;
+        const int m = m0 + row;
+        if (m >= p.M) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(&stage[row * GB_ES + c4]);
+        float* dst = p.c + (size_t)m * p.ldc + n;
+        const float* br = p.bias_rows ? p.bias_rows + (size_t)(m / p.rows_per_group) * p.N + n : nullptr;
+        const float* mk = p.cmask ? p.cmask + (size_t)m * p.ldm + n : nullptr;
+        if (vec && n + 3 < p.N) {
+          if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+          if (br) v += *reinterpret_cast<const f32x4*>(br);
+          if (MODE == 1) v += *reinterpret_cast<const f32x4*>(dst);
+          const f32x4 mv = mk ? *reinterpret_cast<const f32x4*>(mk) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (p.relu) v[t] = v[t] > 0.f ? v[t] : 0.f;
+            if (!(mv[t] > 0.f)) v[t] = 0.f;
+          }
+          *reinterpret_cast<f32x4*>(dst) = v;
+          if (p.cp[0]) {
+            bf16x4g hv, lv;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              hv[t] = (__bf16)v[t];
+              lv[t] = (__bf16)(v[t] - (float)hv[t]);
+            }
+            const size_t pofs = (size_t)m * p.ldcp + n;
+            *reinterpret_cast<bf16x4g*>(p.cp[0] + pofs) = hv;
+            *reinterpret_cast<bf16x4g*>(p.cp[1] + pofs) = lv;
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (n + t >= p.N) break;
+            float x = v[t];
+            if (p.bias) x += p.bias[n + t];
+            if (br) x += br[t];
+            if (MODE == 1) x += dst[t];
+            if (p.relu) x = x > 0.f ? x : 0.f;
+            if (mk && !(mk[t] > 0.f)) x = 0.f;
+            dst[t] = x;
+            if (p.cp[0]) {
+              const __bf16 hx = (__bf16)x;
+              p.cp[0][(size_t)m * p.ldcp + n + t] = hx;
+              p.cp[1][(size_t)m * p.ldcp + n + t] = (__bf16)(x - (float)hx);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// the 256-tile kernel takes a plane-operand GEMM when its columns come in
+// whole 256-blocks and the grid still gives every CU work (>= 256 tiles);
+// PCADV_GEMM_BIG=0 keeps the 128-tile kernel (A/B and bitwise checks)
+static bool gemm_big_enabled() {
+  const char* e = getenv("PCADV_GEMM_BIG");
+  return !(e && e[0] == '0');
+}
+static bool use_gemm_big(int M, int N, int rows_per_group, int mode, long long lda, long long ldb) {
+  if (!gemm_big_enabled() || N % GB_BN != 0) return false;
+  // 32-bit buffer offsets (bytes) below 2^31 over the A rows one launch (or
+  // one cloud, mode 2) addresses and over B
+  if ((long long)(mode == 2 ? rows_per_group : M) * lda * 2 >= 0x7fffffffLL ||
+      (long long)N * ldb * 2 >= 0x7fffffffLL)
+    return false;
+  if (mode == 2 && rows_per_group % GB_BM != 0) return false;
+  const long long tiles = (long long)((M + GB_BM - 1) / GB_BM) * (N / GB_BN);
+  return tiles >= 256;
+}
+template <int MODE>
+static int gemm_big_launch(const GemmP& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_bf2_big<MODE>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(GemmBigLds)) != hipSuccess) {
+      set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(GemmBigLds));
+      return PCADV_EHIP;
+    }
+    attr = true;
+  }
+  const dim3 grid((p.M + GB_BM - 1) / GB_BM, p.N / GB_BN, 1);
+  hipLaunchKernelGGL((k_gemm_bf2_big<MODE>), grid, dim3(GB_T), sizeof(GemmBigLds), s, p);
+  PC_HIP_CHECK_LAUNCH("k_gemm_bf2_big");
+  return PCADV_OK;
 }
 
 // Skinny GEMM (M <= 16 rows per workgroup: one row per cloud, e.g. fc1's
@@ -729,11 +1027,17 @@ k_max_combine(const int2* __restrict__ part, int T, int Npts, int C, int O,
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <int TA, int TB, int MODE, int NP>
-static int gemm_launch(const GemmP& p, int nz, hipStream_t s) {
+// the engine's loads are buffer loads with 32-bit byte offsets from the
+// operand base (a masked element reads at 2^31): every operand must span < 2^31 B
+static bool fits31(long long rows, long long ld, int esz) {
+  return rows >= 0 && ld >= 0 && (rows * ld + 16) * esz < 0x7fffffffLL;
+}
+
+template <int TA, int TB, int MODE, int NP, int VEC>
+static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<TA, TB, MODE, NP>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<TA, TB, MODE, NP, VEC>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(GemmLds)) != hipSuccess) {
       set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(GemmLds));
@@ -741,10 +1045,35 @@ static int gemm_launch(const GemmP& p, int nz, hipStream_t s) {
     }
     attr = true;
   }
-  dim3 grid((p.M + GM_BM - 1) / GM_BM, (p.N + GM_BN - 1) / GM_BN, nz);
-  hipLaunchKernelGGL((k_gemm_x3<TA, TB, MODE, NP>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
+  hipLaunchKernelGGL((k_gemm_x3<TA, TB, MODE, NP, VEC>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
   PC_HIP_CHECK_LAUNCH("k_gemm_x3");
   return PCADV_OK;
+}
+
+// the staging form of each operand: 16-byte loads where the operand allows
+// them (aligned, row stride % 4) and no vector straddles an edge (rows: the
+// reduction range [kz0, kz1) in multiples of 4; columns: M or N % 4), else dwords
+template <int TA, int TB>
+static int gemm_vec_flags(const GemmP& p) {
+  const bool kq = p.K % 4 == 0 && p.grp % 4 == 0 && (p.zpg == 1 || p.ksplit_len % 4 == 0);
+  const bool va = TA == 2 || (p.avec && (TA == 0 ? kq : p.M % 4 == 0 && p.rows_per_group % 4 == 0));
+  const bool vb = TB == 2 || (p.bvec && (TB == 0 ? kq : p.N % 4 == 0));
+  return (va ? 1 : 0) | (vb ? 2 : 0);
+}
+
+template <int TA, int TB, int MODE, int NP>
+static int gemm_launch_grid(const GemmP& p, dim3 grid, hipStream_t s) {
+  switch (gemm_vec_flags<TA, TB>(p)) {
+    case 3: return gemm_launch_v<TA, TB, MODE, NP, 3>(p, grid, s);
+    case 2: return gemm_launch_v<TA, TB, MODE, NP, 2>(p, grid, s);
+    case 1: return gemm_launch_v<TA, TB, MODE, NP, 1>(p, grid, s);
+    default: return gemm_launch_v<TA, TB, MODE, NP, 0>(p, grid, s);
+  }
+}
+template <int TA, int TB, int MODE, int NP>
+static int gemm_launch(const GemmP& p, int nz, hipStream_t s) {
+  return gemm_launch_grid<TA, TB, MODE, NP>(
+      p, dim3((p.M + GM_BM - 1) / GM_BM, (p.N + GM_BN - 1) / GM_BN, nz), s);
 }
 
 // C[M][N] (+)= op(A) op(B)^T: see the header comment for ta / tb.
@@ -762,6 +1091,8 @@ int launch_gemm(const float* a, long long lda, int ta, const float* b, long long
   PC_REQUIRE(!cmask || ldm >= N, "gemm: bad ldm %lld", ldm);
   PC_REQUIRE(!bias_rows || rows_per_group > 0, "gemm: bias_rows needs rows_per_group");
   PC_REQUIRE(ta == 0 || tb == 1, "gemm: A^T needs B^T (the weight-gradient form)");
+  PC_REQUIRE(fits31(ta ? K : M, lda, 4) && fits31(tb ? K : N, ldb, 4),
+             "gemm: operands must span < 2 GB (M=%d N=%d K=%d)", M, N, K);
   GemmP p{};
   p.a = a; p.lda = lda; p.b = b; p.ldb = ldb; p.c = c; p.ldc = ldc;
   p.cmask = cmask; p.ldm = ldm;
@@ -811,6 +1142,7 @@ int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const voi
              "gemm_bf2: planes must be 16-B aligned");
   PC_REQUIRE(ldc >= N && (!cmask || ldm >= N) && (!bias_rows || rows_per_group > 0),
              "gemm_bf2: bad ldc / ldm / bias_rows");
+  PC_REQUIRE(fits31(M, lda, 2) && fits31(N, ldb, 2), "gemm_bf2: planes must span < 2 GB");
   GemmP p{};
   p.ap[0] = static_cast<const __bf16*>(a_hi); p.ap[1] = static_cast<const __bf16*>(a_lo);
   p.ldap = lda;
@@ -826,6 +1158,7 @@ int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const voi
              "gemm_bf2: output planes need N %% 4, ldcp %% 4 and 16-B aligned C");
   p.cp[0] = static_cast<__bf16*>(c_hi); p.cp[1] = static_cast<__bf16*>(c_lo); p.ldcp = ldcp;
   p.grp = K; p.zpg = 1; p.ksplit_len = K;
+  if (use_gemm_big(M, N, 0, 0, lda, ldb)) return accumulate ? gemm_big_launch<1>(p, s) : gemm_big_launch<0>(p, s);
   return accumulate ? gemm_launch<2, 2, 1, 3>(p, 1, s) : gemm_launch<2, 2, 0, 3>(p, 1, s);
 }
 
@@ -887,6 +1220,7 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
              "gemm_wgrad: bad shape rows=%d O=%d Kin=%d", rows, O, Kin);
   PC_REQUIRE(!gsum || (rows_per_group > 0 && rows % rows_per_group == 0),
              "gemm_wgrad: per-group sums need rows %% rows_per_group == 0");
+  PC_REQUIRE(fits31(rows, ldz, 4) && fits31(rows, ldx, 4), "gemm_wgrad: operands must span < 2 GB");
   PC_REQUIRE(rows_per_group <= 0 || rows % rows_per_group == 0, "gemm_wgrad: rows %% rows_per_group");
   const WgradPlan w = wgrad_plan(rows, O, Kin, rows_per_group);
   PC_REQUIRE(ws && ws_bytes >= gemm_wgrad_workspace_bytes(rows, O, Kin, rows_per_group),
@@ -977,6 +1311,8 @@ int launch_conv_max_x3(const float* x, long long ldx, int C, int Npts, int K, co
              "conv_max_x3: bad shape");
   PC_REQUIRE(K % 32 == 0 && ldx % 4 == 0, "conv_max_x3: K %% 32 and ldx %% 4 required");
   PC_REQUIRE(ws && ws_bytes >= conv_max_x3_workspace_bytes(C, Npts, O), "conv_max_x3: workspace");
+  PC_REQUIRE(fits31(Npts, ldx, 4) && fits31(Npts, ldxp, 2) && fits31(O, K, 4),
+             "conv_max_x3: a cloud's rows and the weights must span < 2 GB");
   const bool planes = x_hi != nullptr;
   PC_REQUIRE(!planes || (x_lo && w_hi && w_lo && ldxp % 8 == 0 && ldxp >= K &&
                          ((((uintptr_t)x_hi | (uintptr_t)x_lo | (uintptr_t)w_hi | (uintptr_t)w_lo) & 15) == 0)),
@@ -999,32 +1335,13 @@ int launch_conv_max_x3(const float* x, long long ldx, int C, int Npts, int K, co
     p.M = C * Npts; p.N = O; p.K = K; p.grp = K; p.zpg = 1; p.ksplit_len = K;
     p.part = part;
     const dim3 grid(C * T, (O + GM_BN - 1) / GM_BN, 1);
-    if (planes) {
-      static bool attr2 = false;
-      if (!attr2) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<2, 2, 2, 3>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(GemmLds)) != hipSuccess) {
-          set_error("conv_max_x3: cannot reserve LDS");
-          return PCADV_EHIP;
-        }
-        attr2 = true;
-      }
-      hipLaunchKernelGGL((k_gemm_x3<2, 2, 2, 3>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
+    if (planes && use_gemm_big(C * Npts, O, Npts, 2, ldxp, K)) {
+      PC_TRY_GEMM(gemm_big_launch<2>(p, s));
+    } else if (planes) {
+      PC_TRY_GEMM((gemm_launch_grid<2, 2, 2, 3>(p, grid, s)));
     } else {
-      static bool attr = false;
-      if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<0, 0, 2, 3>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(GemmLds)) != hipSuccess) {
-          set_error("conv_max_x3: cannot reserve LDS");
-          return PCADV_EHIP;
-        }
-        attr = true;
-      }
-      hipLaunchKernelGGL((k_gemm_x3<0, 0, 2, 3>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
+      PC_TRY_GEMM((gemm_launch_grid<0, 0, 2, 3>(p, grid, s)));
     }
-    PC_HIP_CHECK_LAUNCH("k_gemm_x3 (max)");
   }
   const int pairs = C * O;
   hipLaunchKernelGGL(k_max_combine, dim3((pairs + 31) / 32), dim3(256), 0, s, part, T, Npts, C, O,

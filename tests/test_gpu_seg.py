@@ -14,6 +14,7 @@ of a ReLU net route a whole gradient element differently where a
 pre-activation lies within rounding of 0 (the oracle and the fp64 reference
 agree to 1e-6 only because numpy's f32 rounding flips almost none of them)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -117,6 +118,112 @@ def test_gemm_bf2_is_bitwise_the_f32_staged_gemm(M, N, K):
     assert torch.equal(C, ref)
     assert torch.equal(ch, C.to(torch.bfloat16))
     assert torch.equal(cl, (C - ch.float()).to(torch.bfloat16))
+
+
+def _with_gemm_big(enabled, fn):
+    saved = os.environ.get("PCADV_GEMM_BIG")
+    os.environ["PCADV_GEMM_BIG"] = "1" if enabled else "0"
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out
+    finally:
+        if saved is None:
+            del os.environ["PCADV_GEMM_BIG"]
+        else:
+            os.environ["PCADV_GEMM_BIG"] = saved
+
+
+def _planes(x):
+    lib = _lib.load()
+    R, K = x.shape
+    hi = torch.empty(R, K, device=DEV, dtype=torch.bfloat16)
+    lo = torch.empty(R, K, device=DEV, dtype=torch.bfloat16)
+    check(lib.pcadv_split_bf2(_p(x), K, R, K, _pb(hi), _pb(lo), K, stream_ptr()), "split")
+    return hi, lo
+
+
+@pytest.mark.parametrize("M,N,K,acc", [(33000, 512, 80, 0), (32768, 512, 128, 1),
+                                       (8192, 2048, 512, 0)])
+def test_gemm_bf2_256_tiles_bitwise(M, N, K, acc):
+    """The 256 x 256-tile kernel (wide plane GEMMs: >= 256 tiles, N % 256 == 0)
+    sums the same MFMAs in the same order as the 128-tile kernel: C, its
+    output planes, the bias / per-group bias / mask / accumulate epilogue all
+    bitwise equal.  Shapes: ragged last row tile + odd k-tile count, the
+    accumulate form with a mask, conv6's 2048 columns."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g)
+    b = torch.randn(N, device=DEV, generator=g)
+    rpg = 4096
+    br = torch.randn((M + rpg - 1) // rpg, N, device=DEV, generator=g)
+    Y = torch.randn(M, N, device=DEV, generator=g)
+    base = torch.randn(M, N, device=DEV, generator=g)
+    ah, al = _planes(A)
+    wh, wl = _planes(W)
+
+    def run():
+        C = base.clone()
+        ch = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        cl = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        check(lib.pcadv_gemm_bf2(_pb(ah), _pb(al), K, _pb(wh), _pb(wl), K, _p(C), N,
+                                 _pb(ch), _pb(cl), N, M, N, K, _p(b), _p(br), rpg, 1, acc,
+                                 _p(Y) if acc else None, N if acc else 0, stream_ptr()), "gemm_bf2")
+        return C, ch, cl
+
+    big = _with_gemm_big(True, run)
+    small = _with_gemm_big(False, run)
+    for x, y in zip(big, small):
+        assert torch.equal(x, y)
+    # and the values themselves: within the three-product bound of fp64
+    A64, W64 = A.double(), W.double()
+    ref = A64 @ W64.T + b.double() + br.double()[torch.arange(M, device=DEV) // rpg]
+    if acc:
+        ref = ref + base.double()
+    ref = ref.clamp_min(0)
+    if acc:
+        ref = ref * (Y > 0)
+    bound = 2e-5 * (A64.abs() @ W64.abs().T) + 2e-6 * (1 + base.double().abs())
+    assert ((big[0].double() - ref).abs() <= bound).all()
+
+
+def test_conv_max_bf2_256_tiles_bitwise():
+    """conv6's screened max on the 256-tile kernel (one top-2 record per
+    128-row half) gives gmax / gidx bitwise equal to the 128-tile kernel,
+    and the argmax agrees with the fp64 one except at near-ties."""
+    lib = _lib.load()
+    C, Np, K, O = 4, 2048, 512, 2048
+    rng = np.random.default_rng(11)
+    x = np.maximum(rng.standard_normal((C * Np, K)), 0).astype(np.float32)
+    x[5] = x[700]  # a twin pair inside one cloud: equal values, first index wins
+    w = (rng.standard_normal((O, K)) / 22.6).astype(np.float32)
+    bias = (rng.standard_normal(O) * 0.05).astype(np.float32)
+    tx, tw, tb = _t(x), _t(w), _t(bias)
+    xh, xl = _planes(tx)
+    whh, wll = _planes(tw)
+    nb = lib.pcadv_conv_max_x3_workspace_bytes(C, Np, O)
+    ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+
+    def run():
+        gmax = torch.empty(C, O, device=DEV)
+        gidx = torch.empty(C, O, device=DEV, dtype=torch.int32)
+        check(lib.pcadv_conv_max_bf2(_p(tx), K, _pb(xh), _pb(xl), K, C, Np, K, _p(tw), _pb(whh),
+                                     _pb(wll), _p(tb), O, 1, _p(gmax), _p(gidx), _p(ws), nb,
+                                     stream_ptr()), "conv_max_bf2")
+        return gmax, gidx
+
+    gb, ib = _with_gemm_big(True, run)
+    gs, is_ = _with_gemm_big(False, run)
+    assert torch.equal(gb, gs) and torch.equal(ib, is_)
+    z = x.astype(np.float64).reshape(C, Np, K) @ w.T.astype(np.float64) + bias
+    ref = np.maximum(z.max(1), 0)
+    assert np.abs(gb.cpu().numpy() - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+    gi = ib.cpu().numpy()
+    bad = (gi != z.argmax(1)) & (ref > 0)
+    for c, o in np.argwhere(bad):  # only at near-ties of the f64 values
+        top = np.sort(z[c, :, o])[-2:]
+        assert top[1] - top[0] <= 1e-5 * np.abs(x[c * Np:(c + 1) * Np] @ w[o]).max()
 
 
 def test_seg_forward_planes_path_is_bitwise_the_f32_path():

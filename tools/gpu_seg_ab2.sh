@@ -1,0 +1,20 @@
+#!/bin/bash
+# Seg A/B against build/ab/libA.so (A = a previous tree's library, B = this
+# tree's), after the GPU suite on this tree.  Each GPU step has its own time
+# limit; the first failure ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/ab2_pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/ab2_pytest.log
+[ $rc -eq 0 ] || exit $rc
+for i in 1 2 3; do
+  for v in A B; do
+    if [ $v = A ]; then lib=build/ab/libA.so; else lib=adversarial_learning_on_pointclouds_amd/lib/libpcadv.so; fi
+    PCADV_LIB=$lib timeout -k 10 200 python bench.py --config seg --steps 20 --warmup 3 --no-cpu > gpurun_out/ab2_$v$i.log 2>&1 || { echo "bench $v failed"; exit 1; }
+    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if '\"metric\"' in l][-1]); print('$v', d['ms_per_step'], d['roofline']['avg_launch_us'])" gpurun_out/ab2_$v$i.log
+  done
+done
+rm -rf gpurun_out/ab2_trace
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab2_trace -o run --output-format csv -- python bench.py --config seg --no-cpu --steps 5 --warmup 1 > gpurun_out/ab2_trace.log 2>&1 || exit 1
+python tools/kstats.py gpurun_out/ab2_trace/run_kernel_trace.csv > gpurun_out/ab2_kstats.txt; head -16 gpurun_out/ab2_kstats.txt
