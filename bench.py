@@ -313,7 +313,7 @@ def bench_seg(args):
     gflop = 2.0 * Bs * Ns * (per_pt_fwd + dense_bwd) / 1e9
     loss = float(step.loss.item())
     # dominant kernel: conv6 + ReLU + max over points as the step runs it
-    # (pcadv_conv_max_bf2: the screened GEMM k_gemm_x3<2,2,2,3> on the bf16 planes
+    # (pcadv_conv_max_bf2: the screened GEMM k_gemm_bf2_big<2> (256x256 tiles) on the bf16 planes
     # conv5's epilogue wrote + the exact re-evaluation k_max_combine), timed with
     # HIP events on the current stream over the last batch's x5
     from adversarial_learning_on_pointclouds_amd import seg as segmod
@@ -331,7 +331,9 @@ def bench_seg(args):
     x5 = ctypes.c_void_p(fw["xloc"].data_ptr() + 4 * segmod._OFF[4])
 
     xp, w6p = fw["xp"], fw["W6p"]
-    kname = "pcadv_conv_max_bf2: k_gemm_x3<2,2,2,3>" if xp is not None else "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3>"
+    big = os.environ.get("PCADV_GEMM_BIG", "1") != "0"
+    gname = "k_gemm_bf2_big<2>" if big else "k_gemm_x3<2,2,2,3>"
+    kname = f"pcadv_conv_max_bf2: {gname}" if xp is not None else "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3>"
 
     def cmx():
         if xp is not None:
@@ -366,7 +368,8 @@ def bench_seg(args):
     prof = sorted(glob.glob(os.path.join(here, "profiles", "r*_seg_pmc_traffic.json")))
     if prof:
         kern = json.load(open(prof[-1]))["kernels"]
-        names = ("pcadv::k_gemm_x3<2, 2, 2, 3>", "pcadv::k_max_combine")
+        names = ("pcadv::k_gemm_bf2_big<2>" if big else "pcadv::k_gemm_x3<2, 2, 2, 3>",
+                 "pcadv::k_max_combine")
         if all(n in kern for n in names):
             traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
             traffic_src = os.path.relpath(prof[-1], here)
