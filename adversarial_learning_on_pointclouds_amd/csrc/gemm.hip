@@ -491,12 +491,16 @@ k_gemm_x3(GemmP p) {
 constexpr int GB_BM = 256, GB_BN = 256;
 constexpr int GB_T = 512;
 constexpr int GB_ES = 132;  // row stride (floats) of the staged 256 x 128 epilogue half
+#ifndef PCADV_GEMM_BIG_DB
+#define PCADV_GEMM_BIG_DB 1
+#endif
+constexpr int GB_NBUF = PCADV_GEMM_BIG_DB ? 2 : 1;  // LDS operand buffers (2: 160 KB, the whole LDS)
 struct GemmBigLds {
   union {
     struct {
       alignas(16) __bf16 a[2][GB_BM * GM_S];  // [hi, lo][m][k]
       alignas(16) __bf16 b[2][GB_BN * GM_S];  // [hi, lo][n][k]
-    } op;
+    } op[GB_NBUF];
     alignas(16) float stage[GB_BM * GB_ES];
   };
 };
@@ -569,9 +573,9 @@ k_gemm_bf2_big(GemmP p) {
     load_planes(ra, arsc, abase, arow_ok, k0);
     load_planes(rb, brsc, bbase, brow_ok, k0);
   };
-  auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
-    store_planes(ra, L.op.a);
-    store_planes(rb, L.op.b);
+  auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4], int buf) {
+    store_planes(ra, L.op[buf].a);
+    store_planes(rb, L.op[buf].b);
   };
 
   f32x16 acc[4][2];
@@ -580,7 +584,7 @@ k_gemm_bf2_big(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
-  auto mfma_tile = [&]() {
+  auto mfma_tile = [&](int buf) {
 #pragma unroll
     for (int kb = 0; kb < GM_BK / 16; ++kb) {
       bf16x8g fb[2][2];  // [plane][j]
@@ -588,13 +592,13 @@ k_gemm_bf2_big(GemmP p) {
       for (int j = 0; j < 2; ++j) {
         const int br = (64 * wn + 32 * j + r) * GM_S + 16 * kb + 8 * h;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) fb[q][j] = *reinterpret_cast<const bf16x8g*>(&L.op.b[q][br]);
+        for (int q = 0; q < 2; ++q) fb[q][j] = *reinterpret_cast<const bf16x8g*>(&L.op[buf].b[q][br]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ar = (128 * wm + 32 * i + r) * GM_S + 16 * kb + 8 * h;
-        const bf16x8g ah = *reinterpret_cast<const bf16x8g*>(&L.op.a[0][ar]);
-        const bf16x8g al = *reinterpret_cast<const bf16x8g*>(&L.op.a[1][ar]);
+        const bf16x8g ah = *reinterpret_cast<const bf16x8g*>(&L.op[buf].a[0][ar]);
+        const bf16x8g al = *reinterpret_cast<const bf16x8g*>(&L.op[buf].a[1][ar]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           acc[i][j] = mfma_bf16g(al, fb[0][j], acc[i][j]);
@@ -610,15 +614,35 @@ k_gemm_bf2_big(GemmP p) {
   // the scheduler otherwise sinks them below the MFMAs, where their registers
   // free up, and every store then waits out a full L2 round trip)
   f32x4 ra[4], rb[4];
+#if PCADV_GEMM_BIG_DB
+  // two LDS buffers, one barrier per tile: tile t + 1 is stored into the
+  // other buffer while tile t's MFMAs run (its loads were issued one tile
+  // earlier), and tile t + 2's loads go out right after that store
+  load_tile(ra, rb, 0);
+  store_tile(ra, rb, 0);
+  load_tile(ra, rb, GM_BK);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += GM_BK) {
+    mfma_tile(buf);
+    if (k0 + GM_BK < K) {
+      store_tile(ra, rb, buf ^ 1);  // buffer buf ^ 1 was last read before the previous barrier
+      load_tile(ra, rb, k0 + 2 * GM_BK);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+#else
   load_tile(ra, rb, 0);
   for (int k0 = 0; k0 < K; k0 += GM_BK) {
     __syncthreads();
-    store_tile(ra, rb);
+    store_tile(ra, rb, 0);
     __syncthreads();
     load_tile(ra, rb, k0 + GM_BK);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_tile();
+    mfma_tile(0);
   }
+#endif
 
   if constexpr (MODE == 2) {
     // per column, the top-2 (value, row) of this wave's 128 rows: the wave's
