@@ -106,6 +106,162 @@ constexpr int GKEY_NONE = (int)0x80000000;
 // on the way into LDS.  Transposed operands (TA / TB = 1: the reduction axis is
 // the slow one) are read as 4 (k) x 4 (m) blocks per thread and written as
 // 4-k runs (ds_write_b64) of each plane.
+// The same rows without a mask or an accumulate target (the forward layers:
+// bias, per-group bias, ReLU, planes): loads at their use, which measured
+// faster there than the batched form below.
+template <int MODE>
+__device__ __forceinline__ void epilogue_rows_plain(const GemmP& p, float* C, const float* stage,
+                                                    int es, int c4, int row0, int rstep, int nit,
+                                                    int m0, int n) {
+#pragma unroll 2
+  for (int it = 0; it < nit; ++it) {
+    const int row = row0 + rstep * it;
+    const int m = m0 + row;
+    if (m >= p.M) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(&stage[row * es + c4]);
+    float* dst = C + (size_t)m * p.ldc + n;
+    const float* br = p.bias_rows ? p.bias_rows + (size_t)(m / p.rows_per_group) * p.N + n : nullptr;
+    if (p.cvec && n + 3 < p.N) {
+      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+      if (br) v += *reinterpret_cast<const f32x4*>(br);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (p.relu) v[t] = v[t] > 0.f ? v[t] : 0.f;
+      *reinterpret_cast<f32x4*>(dst) = v;
+      if (p.cp[0]) {  // the hi / lo planes the next layer stages (ldcp % 4 == 0)
+        bf16x4g hv, lv;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          hv[t] = (__bf16)v[t];
+          lv[t] = (__bf16)(v[t] - (float)hv[t]);
+        }
+        const size_t pofs = (size_t)m * p.ldcp + n;
+        *reinterpret_cast<bf16x4g*>(p.cp[0] + pofs) = hv;
+        *reinterpret_cast<bf16x4g*>(p.cp[1] + pofs) = lv;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (n + t >= p.N) break;
+        float x = v[t];
+        if (p.bias) x += p.bias[n + t];
+        if (br) x += br[t];
+        if (p.relu) x = x > 0.f ? x : 0.f;
+        dst[t] = x;
+        if (p.cp[0]) {
+          const __bf16 hx = (__bf16)x;
+          p.cp[0][(size_t)m * p.ldcp + n + t] = hx;
+          p.cp[1][(size_t)m * p.ldcp + n + t] = (__bf16)(x - (float)hx);
+        }
+      }
+    }
+  }
+}
+
+// Epilogue rows of a staged half tile: this thread's 4 columns n.. of rows
+// row0 + rstep * it (it < NIT), C (+)= staged + bias + per-group bias, ReLU,
+// output mask, optional bf16 hi / lo planes.  Every load of the NIT rows (the
+// per-group bias, the accumulate target, the mask) is a buffer load issued
+// before the first use (masked rows read zeros past the buffer's end); the
+// per-row `if (present) load` form drained each load before the next (three
+// L2 / HBM round trips per row: the masked data gradients and the accumulating
+// GEMMs use this form).  Same additions in the same order as before.
+template <int MODE, int NIT>
+__device__ __forceinline__ void epilogue_rows(const GemmP& p, float* C, const float* stage, int es,
+                                              int c4, int row0, int rstep, int m0, int n) {
+  constexpr uint32_t OOB = 0x80000000u;
+  auto opq = [](uint32_t o) {
+    asm("" : "+v"(o));
+    return o;
+  };
+  auto ld4 = [](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  };
+  auto rs = [](const void* b) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(b), (short)0, 0x7fffffff, 0x00020000);
+  };
+  const bool nv = p.cvec && n + 3 < p.N;  // this thread's columns as one 16-B vector
+  // (each operand's loads under one launch-uniform branch: none are issued
+  // for an absent operand)
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias) bv = ld4(rs(p.bias), opq(nv ? (uint32_t)n * 4u : OOB));
+  f32x4 brv[NIT], dv[NIT], mv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) brv[it] = dv[it] = mv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (p.bias_rows) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + row0 + rstep * it;
+      brv[it] = ld4(rs(p.bias_rows),
+                    opq(nv && m < p.M ? (uint32_t)((m / p.rows_per_group) * p.N + n) * 4u : OOB));
+    }
+  }
+  if (MODE == 1) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + row0 + rstep * it;
+      dv[it] = ld4(rs(C), opq(nv && m < p.M ? (uint32_t)((long long)m * p.ldc + n) * 4u : OOB));
+    }
+  }
+  if (p.cmask) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + row0 + rstep * it;
+      mv[it] = ld4(rs(p.cmask), opq(nv && m < p.M ? (uint32_t)((long long)m * p.ldm + n) * 4u : OOB));
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = row0 + rstep * it;
+    const int m = m0 + row;
+    if (m >= p.M) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(&stage[row * es + c4]);
+    float* dst = C + (size_t)m * p.ldc + n;
+    if (nv) {
+      if (p.bias) v += bv;
+      if (p.bias_rows) v += brv[it];
+      if (MODE == 1) v += dv[it];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (p.relu) v[t] = v[t] > 0.f ? v[t] : 0.f;
+        if (p.cmask && !(mv[it][t] > 0.f)) v[t] = 0.f;
+      }
+      *reinterpret_cast<f32x4*>(dst) = v;
+      if (p.cp[0]) {  // the hi / lo planes the next layer stages (ldcp % 4 == 0)
+        bf16x4g hv, lv;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          hv[t] = (__bf16)v[t];
+          lv[t] = (__bf16)(v[t] - (float)hv[t]);
+        }
+        const size_t pofs = (size_t)m * p.ldcp + n;
+        *reinterpret_cast<bf16x4g*>(p.cp[0] + pofs) = hv;
+        *reinterpret_cast<bf16x4g*>(p.cp[1] + pofs) = lv;
+      }
+    } else {  // ragged right edge or unaligned output: element by element
+      const float* br = p.bias_rows ? p.bias_rows + (size_t)(m / p.rows_per_group) * p.N + n : nullptr;
+      const float* mk = p.cmask ? p.cmask + (size_t)m * p.ldm + n : nullptr;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (n + t >= p.N) break;
+        float x = v[t];
+        if (p.bias) x += p.bias[n + t];
+        if (br) x += br[t];
+        if (MODE == 1) x += dst[t];
+        if (p.relu) x = x > 0.f ? x : 0.f;
+        if (mk && !(mk[t] > 0.f)) x = 0.f;
+        dst[t] = x;
+        if (p.cp[0]) {
+          const __bf16 hx = (__bf16)x;
+          p.cp[0][(size_t)m * p.ldcp + n + t] = hx;
+          p.cp[1][(size_t)m * p.ldcp + n + t] = (__bf16)(x - (float)hx);
+        }
+      }
+    }
+  }
+}
+
 // VEC bit 0 / bit 1: A / B staged by 16-byte loads (vector-aligned, no
 // vector straddles an edge), else by dword loads
 template <int TA, int TB, int MODE, int NP, int VEC>
@@ -409,7 +565,6 @@ k_gemm_x3(GemmP p) {
     // coalesced 16-B accesses with one address per row
     float* stage = reinterpret_cast<float*>(smem);
     constexpr int ES = 68;  // row stride (floats) of the staged half tile
-    const bool vec = p.cvec;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       __syncthreads();  // the MFMA operands / the previous half are no longer read
@@ -421,56 +576,8 @@ k_gemm_x3(GemmP p) {
       __syncthreads();
       const int c4 = 4 * (tid & 15);                 // staged column (0..60)
       const int n = n0 + 64 * (c4 >> 5) + 32 * j + (c4 & 31);
-#pragma unroll 2
-      for (int it = 0; it < 8; ++it) {
-        const int row = (tid >> 4) + 16 * it;
-        const int m = m0 + row;
-        if (m >= p.M) continue;
-        f32x4 v = *reinterpret_cast<const f32x4*>(&stage[row * ES + c4]);
-        float* dst = C + (size_t)m * p.ldc + n;
-        const float* br = p.bias_rows ? p.bias_rows + (size_t)(m / p.rows_per_group) * p.N + n : nullptr;
-        const float* mk = p.cmask ? p.cmask + (size_t)m * p.ldm + n : nullptr;
-        if (vec && n + 3 < p.N) {
-          if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
-          if (br) v += *reinterpret_cast<const f32x4*>(br);
-          if (MODE == 1) v += *reinterpret_cast<const f32x4*>(dst);
-          const f32x4 mv = mk ? *reinterpret_cast<const f32x4*>(mk) : f32x4{1.f, 1.f, 1.f, 1.f};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (p.relu) v[t] = v[t] > 0.f ? v[t] : 0.f;
-            if (!(mv[t] > 0.f)) v[t] = 0.f;
-          }
-          *reinterpret_cast<f32x4*>(dst) = v;
-          if (p.cp[0]) {  // the hi / lo planes the next layer stages (ldcp % 4 == 0)
-            bf16x4g hv, lv;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              hv[t] = (__bf16)v[t];
-              lv[t] = (__bf16)(v[t] - (float)hv[t]);
-            }
-            const size_t pofs = (size_t)m * p.ldcp + n;
-            *reinterpret_cast<bf16x4g*>(p.cp[0] + pofs) = hv;
-            *reinterpret_cast<bf16x4g*>(p.cp[1] + pofs) = lv;
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (n + t >= p.N) break;
-            float x = v[t];
-            if (p.bias) x += p.bias[n + t];
-            if (br) x += br[t];
-            if (MODE == 1) x += dst[t];
-            if (p.relu) x = x > 0.f ? x : 0.f;
-            if (mk && !(mk[t] > 0.f)) x = 0.f;
-            dst[t] = x;
-            if (p.cp[0]) {
-              const __bf16 hx = (__bf16)x;
-              p.cp[0][(size_t)m * p.ldcp + n + t] = hx;
-              p.cp[1][(size_t)m * p.ldcp + n + t] = (__bf16)(x - (float)hx);
-            }
-          }
-        }
-      }
+      if (MODE == 1 || p.cmask) epilogue_rows<MODE, 8>(p, C, stage, ES, c4, tid >> 4, 16, m0, n);
+      else epilogue_rows_plain<MODE>(p, C, stage, ES, c4, tid >> 4, 16, 8, m0, n);
     }
   }
 }
@@ -673,7 +780,6 @@ k_gemm_bf2_big(GemmP p) {
     // epilogue through LDS, one 256 x 128 half of the tile at a time (each
     // wave's 32-column block j), rows written by 32 lanes x 4 columns
     float* stage = L.stage;
-    const bool vec = p.cvec;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       __syncthreads();  // the MFMA operands / the previous half are no longer read
@@ -685,55 +791,15 @@ k_gemm_bf2_big(GemmP p) {
       __syncthreads();
       const int c4 = 4 * (tid & 31);                 // staged column (0..124)
       const int n = n0 + 64 * (c4 >> 5) + 32 * j + (c4 & 31);
-#pragma unroll 2
-      for (int it = 0; it < 16; ++it) {
-        const int row = (tid >> 5) + 16 * it;
-        const int m = m0 + row;
-        if (m >= p.M) continue;
-        f32x4 v = *reinterpret_cast<const f32x4*>(&stage[row * GB_ES + c4]);
-        float* dst = p.c + (size_t)m * p.ldc + n;
-        const float* br = p.bias_rows ? p.bias_rows + (size_t)(m / p.rows_per_group) * p.N + n : nullptr;
-        const float* mk = p.cmask ? p.cmask + (size_t)m * p.ldm + n : nullptr;
-        if (vec && n + 3 < p.N) {
-          if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
-          if (br) v += *reinterpret_cast<const f32x4*>(br);
-          if (MODE == 1) v += *reinterpret_cast<const f32x4*>(dst);
-          const f32x4 mv = mk ? *reinterpret_cast<const f32x4*>(mk) : f32x4{1.f, 1.f, 1.f, 1.f};
+      // 16 rows per thread in batches (the loads of a batch in flight
+      // together; the other half's accumulators are still live)
+      constexpr int NIT = MODE == 1 ? 2 : 4;  // accumulate: the targets' loads too
+      if (MODE == 1 || p.cmask) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (p.relu) v[t] = v[t] > 0.f ? v[t] : 0.f;
-            if (!(mv[t] > 0.f)) v[t] = 0.f;
-          }
-          *reinterpret_cast<f32x4*>(dst) = v;
-          if (p.cp[0]) {
-            bf16x4g hv, lv;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              hv[t] = (__bf16)v[t];
-              lv[t] = (__bf16)(v[t] - (float)hv[t]);
-            }
-            const size_t pofs = (size_t)m * p.ldcp + n;
-            *reinterpret_cast<bf16x4g*>(p.cp[0] + pofs) = hv;
-            *reinterpret_cast<bf16x4g*>(p.cp[1] + pofs) = lv;
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (n + t >= p.N) break;
-            float x = v[t];
-            if (p.bias) x += p.bias[n + t];
-            if (br) x += br[t];
-            if (MODE == 1) x += dst[t];
-            if (p.relu) x = x > 0.f ? x : 0.f;
-            if (mk && !(mk[t] > 0.f)) x = 0.f;
-            dst[t] = x;
-            if (p.cp[0]) {
-              const __bf16 hx = (__bf16)x;
-              p.cp[0][(size_t)m * p.ldcp + n + t] = hx;
-              p.cp[1][(size_t)m * p.ldcp + n + t] = (__bf16)(x - (float)hx);
-            }
-          }
-        }
+        for (int q4 = 0; q4 < 16 / NIT; ++q4)
+          epilogue_rows<MODE, NIT>(p, p.c, stage, GB_ES, c4, (tid >> 5) + 16 * NIT * q4, 16, m0, n);
+      } else {
+        epilogue_rows_plain<MODE>(p, p.c, stage, GB_ES, c4, tid >> 5, 16, 16, m0, n);
       }
     }
   }
@@ -1115,7 +1181,8 @@ int launch_gemm(const float* a, long long lda, int ta, const float* b, long long
   PC_REQUIRE(!cmask || ldm >= N, "gemm: bad ldm %lld", ldm);
   PC_REQUIRE(!bias_rows || rows_per_group > 0, "gemm: bias_rows needs rows_per_group");
   PC_REQUIRE(ta == 0 || tb == 1, "gemm: A^T needs B^T (the weight-gradient form)");
-  PC_REQUIRE(fits31(ta ? K : M, lda, 4) && fits31(tb ? K : N, ldb, 4),
+  PC_REQUIRE(fits31(ta ? K : M, lda, 4) && fits31(tb ? K : N, ldb, 4) && fits31(M, ldc, 4) &&
+                 (!cmask || fits31(M, ldm, 4)),
              "gemm: operands must span < 2 GB (M=%d N=%d K=%d)", M, N, K);
   GemmP p{};
   p.a = a; p.lda = lda; p.b = b; p.ldb = ldb; p.c = c; p.ldc = ldc;
@@ -1166,7 +1233,9 @@ int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const voi
              "gemm_bf2: planes must be 16-B aligned");
   PC_REQUIRE(ldc >= N && (!cmask || ldm >= N) && (!bias_rows || rows_per_group > 0),
              "gemm_bf2: bad ldc / ldm / bias_rows");
-  PC_REQUIRE(fits31(M, lda, 2) && fits31(N, ldb, 2), "gemm_bf2: planes must span < 2 GB");
+  PC_REQUIRE(fits31(M, lda, 2) && fits31(N, ldb, 2) && fits31(M, ldc, 4) &&
+                 (!cmask || fits31(M, ldm, 4)),
+             "gemm_bf2: operands must span < 2 GB");
   GemmP p{};
   p.ap[0] = static_cast<const __bf16*>(a_hi); p.ap[1] = static_cast<const __bf16*>(a_lo);
   p.ldap = lda;
