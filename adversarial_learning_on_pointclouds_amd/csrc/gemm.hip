@@ -1479,6 +1479,85 @@ k_row_ce(const float* __restrict__ logits, long long ld, const int64_t* __restri
   if (threadIdx.x == 0) part[blockIdx.x] = sm[0];
 }
 
+// The same per row, with the block's rows staged through LDS: the logits come
+// in and the gradients go out as coalesced rows (a lane per row walking its
+// own row touched a new cache line per load: 64 lines per wave instruction).
+// Each row's max, exp sum and gradient follow the lane-per-row order above,
+// so the results are the same.  LDS rows padded to an odd stride.
+constexpr int CE_MAXC = 63;  // the staged rows stay within the default 64 KB of LDS
+__global__ void __launch_bounds__(256)
+k_row_ce_lds(const float* __restrict__ logits, long long ld, const int64_t* __restrict__ labels,
+             int M, int Ccls, float scale, float* __restrict__ dlogits, float* __restrict__ part) {
+  extern __shared__ float xs[];  // [256][Ccls | 1]
+  const int S = Ccls | 1, tid = threadIdx.x, r0 = blockIdx.x * 256;
+  const int nrows = min(256, M - r0), ne = nrows * Ccls;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(logits), (short)0, 0x7fffffff, 0x00020000);
+  // element e = tid + 256 i of the block's rows: (row, col) stepped without divisions
+  const int q256 = 256 / Ccls, r256 = 256 % Ccls;
+  {
+    int row = tid / Ccls, col = tid % Ccls;
+    for (int e0 = 0; e0 < ne; e0 += 256 * 8) {
+      float v[8];
+      int rw[8], cl[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bool ok = e0 + tid + 256 * i < ne;
+        uint32_t off = ok ? (uint32_t)(((long long)(r0 + row) * ld + col) * 4) : 0x80000000u;
+        asm("" : "+v"(off));
+        v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+        rw[i] = row;
+        cl[i] = col;
+        row += q256;
+        col += r256;
+        if (col >= Ccls) {
+          col -= Ccls;
+          ++row;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (e0 + tid + 256 * i < ne) xs[rw[i] * S + cl[i]] = v[i];
+    }
+  }
+  const int m = r0 + tid;
+  const int64_t y = m < M ? labels[m] : 0;
+  __syncthreads();
+  float l = 0.f;
+  if (tid < nrows) {
+    float* x = xs + tid * S;
+    float mx = -INFINITY;
+    for (int c = 0; c < Ccls; ++c) mx = fmaxf(mx, x[c]);
+    float se = 0.f;
+    for (int c = 0; c < Ccls; ++c) se += expf(x[c] - mx);
+    const float lse = mx + logf(se);
+    l = lse - x[y];
+    const float inv = scale / (float)M;
+    for (int c = 0; c < Ccls; ++c) x[c] = (expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * inv;
+  }
+  __syncthreads();
+  {
+    int row = tid / Ccls, col = tid % Ccls;
+    for (int e = tid; e < ne; e += 256) {
+      dlogits[(size_t)(r0 + row) * ld + col] = xs[row * S + col];
+      row += q256;
+      col += r256;
+      if (col >= Ccls) {
+        col -= Ccls;
+        ++row;
+      }
+    }
+  }
+  __shared__ float sm[256];
+  sm[tid] = l;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) sm[tid] += sm[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) part[blockIdx.x] = sm[0];
+}
+
 __global__ void k_row_ce_fin(const float* __restrict__ part, int nb, int M, float* __restrict__ loss) {
   if (threadIdx.x != 0) return;
   double s = 0.0;
@@ -1494,10 +1573,15 @@ int launch_row_ce(const float* logits, long long ld, const int64_t* labels, int 
   PC_REQUIRE(logits && labels && loss && dlogits && M > 0 && Ccls > 0 && ld >= Ccls,
              "row_ce: bad shape");
   PC_REQUIRE(ws && ws_bytes >= row_ce_workspace_bytes(M), "row_ce: workspace");
+  PC_REQUIRE((long long)M * ld * 4 < 0x7fffffffLL, "row_ce: logits must span < 2 GB");
   const int nb = (M + 255) / 256;
   float* part = static_cast<float*>(ws);
-  hipLaunchKernelGGL(k_row_ce, dim3(nb), dim3(256), 0, s, logits, ld, labels, M, Ccls, scale,
-                     dlogits, part);
+  if (Ccls <= CE_MAXC)
+    hipLaunchKernelGGL(k_row_ce_lds, dim3(nb), dim3(256), 256 * (Ccls | 1) * sizeof(float), s,
+                       logits, ld, labels, M, Ccls, scale, dlogits, part);
+  else
+    hipLaunchKernelGGL(k_row_ce, dim3(nb), dim3(256), 0, s, logits, ld, labels, M, Ccls, scale,
+                       dlogits, part);
   PC_HIP_CHECK_LAUNCH("k_row_ce");
   hipLaunchKernelGGL(k_row_ce_fin, dim3(1), dim3(64), 0, s, part, nb, M, loss);
   PC_HIP_CHECK_LAUNCH("k_row_ce_fin");
