@@ -1487,7 +1487,8 @@ k_row_ce(const float* __restrict__ logits, long long ld, const int64_t* __restri
 constexpr int CE_MAXC = 63;  // the staged rows stay within the default 64 KB of LDS
 __global__ void __launch_bounds__(256)
 k_row_ce_lds(const float* __restrict__ logits, long long ld, const int64_t* __restrict__ labels,
-             int M, int Ccls, float scale, float* __restrict__ dlogits, float* __restrict__ part) {
+             int M, int Ccls, float scale, float* __restrict__ dlogits, float* __restrict__ part,
+             float* __restrict__ loss) {
   extern __shared__ float xs[];  // [256][Ccls | 1]
   const int S = Ccls | 1, tid = threadIdx.x, r0 = blockIdx.x * 256;
   const int nrows = min(256, M - r0), ne = nrows * Ccls;
@@ -1555,7 +1556,46 @@ k_row_ce_lds(const float* __restrict__ logits, long long ld, const int64_t* __re
     if (tid < w) sm[tid] += sm[tid + w];
     __syncthreads();
   }
-  if (tid == 0) part[blockIdx.x] = sm[0];
+  if (tid == 0) {
+    part[blockIdx.x] = sm[0];
+    // one block (M <= 256, the classification heads): the mean here, as
+    // k_row_ce_fin forms it, and no finishing launch
+    if (gridDim.x == 1) *loss = (float)((double)sm[0] / (double)M);
+  }
+}
+
+// Few rows (M <= 256, Ccls <= 64: the classification heads' CE over a batch):
+// one wave per row, the lanes across the classes, wave butterflies for the max
+// and the exp sum (a lane walking its row serially left 32 active lanes in a
+// 40-step dependent chain, three times); the batch mean in row order.
+__global__ void __launch_bounds__(1024)
+k_row_ce_wave(const float* __restrict__ logits, long long ld, const int64_t* __restrict__ labels,
+              int M, int Ccls, float scale, float* __restrict__ dlogits, float* __restrict__ loss) {
+  __shared__ float rl[256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const float inv = scale / (float)M;
+  for (int m = wave; m < M; m += nw) {
+    const float* x = logits + (size_t)m * ld;
+    const int y = (int)labels[m];
+    const float v = lane < Ccls ? x[lane] : -INFINITY;
+    float mx = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float e = lane < Ccls ? expf(v - mx) : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o);
+    const float lse = mx + logf(e);
+    if (lane < Ccls)
+      dlogits[(size_t)m * ld + lane] = (expf(v - lse) - (lane == y ? 1.f : 0.f)) * inv;
+    const float xy = __shfl(v, y);
+    if (lane == 0) rl[m] = lse - xy;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int m = 0; m < M; ++m) s += rl[m];
+    *loss = (float)(s / (double)M);
+  }
 }
 
 __global__ void k_row_ce_fin(const float* __restrict__ part, int nb, int M, float* __restrict__ loss) {
@@ -1576,13 +1616,22 @@ int launch_row_ce(const float* logits, long long ld, const int64_t* labels, int 
   PC_REQUIRE((long long)M * ld * 4 < 0x7fffffffLL, "row_ce: logits must span < 2 GB");
   const int nb = (M + 255) / 256;
   float* part = static_cast<float*>(ws);
-  if (Ccls <= CE_MAXC)
+  if (M <= 256 && Ccls <= 64) {
+    hipLaunchKernelGGL(k_row_ce_wave, dim3(1), dim3(1024), 0, s, logits, ld, labels, M, Ccls,
+                       scale, dlogits, loss);
+    PC_HIP_CHECK_LAUNCH("k_row_ce_wave");
+    return PCADV_OK;
+  }
+  if (Ccls <= CE_MAXC) {
     hipLaunchKernelGGL(k_row_ce_lds, dim3(nb), dim3(256), 256 * (Ccls | 1) * sizeof(float), s,
-                       logits, ld, labels, M, Ccls, scale, dlogits, part);
-  else
+                       logits, ld, labels, M, Ccls, scale, dlogits, part, loss);
+    PC_HIP_CHECK_LAUNCH("k_row_ce");
+    if (nb == 1) return PCADV_OK;  // the block wrote the mean
+  } else {
     hipLaunchKernelGGL(k_row_ce, dim3(nb), dim3(256), 0, s, logits, ld, labels, M, Ccls, scale,
                        dlogits, part);
-  PC_HIP_CHECK_LAUNCH("k_row_ce");
+    PC_HIP_CHECK_LAUNCH("k_row_ce");
+  }
   hipLaunchKernelGGL(k_row_ce_fin, dim3(1), dim3(64), 0, s, part, nb, M, loss);
   PC_HIP_CHECK_LAUNCH("k_row_ce_fin");
   return PCADV_OK;

@@ -413,6 +413,37 @@ def test_row_ce_vs_oracle():
     assert np.abs(t.grad.cpu().numpy() - rg).max() <= 1e-6
 
 
+@pytest.mark.parametrize("M,C,ld", [(32, 40, 40), (200, 64, 64), (1000, 50, 50), (300, 100, 100),
+                                    (777, 50, 52)])
+def test_row_ce_kernel_forms(M, C, ld):
+    """pcadv_row_ce's three kernels against fp64: one wave per row (M <= 256,
+    C <= 64, the cls heads), rows staged through LDS (C <= 63), a lane per row
+    (wider rows); a strided logits matrix too.  Loss = mean CE * 1, gradient
+    (softmax - onehot) * scale / M."""
+    lib = _lib.load()
+    rng = np.random.default_rng(M + C)
+    lg = (rng.standard_normal((M, ld)) * 3).astype(np.float32)
+    y = rng.integers(0, C, M)
+    tl, ty = _t(lg), _t(y, torch.int64)
+    loss = torch.empty(1, device=DEV)
+    dl = torch.zeros(M, ld, device=DEV)
+    nb = lib.pcadv_row_ce_workspace_bytes(M)
+    ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+    scale = 0.7
+    check(lib.pcadv_row_ce(_p(tl), ld, _p(ty), M, C, ctypes.c_float(scale), _p(loss), _p(dl),
+                           _p(ws), nb, stream_ptr()), "row_ce")
+    x = lg[:, :C].astype(np.float64)
+    lse = np.log(np.exp(x - x.max(1, keepdims=True)).sum(1)) + x.max(1)
+    ref_loss = (lse - x[np.arange(M), y]).mean()
+    p = np.exp(x - lse[:, None])
+    p[np.arange(M), y] -= 1
+    ref_g = p * scale / M
+    assert abs(loss.item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+    g = dl.cpu().numpy()
+    assert np.abs(g[:, :C] - ref_g).max() <= 1e-6 * max(1.0, np.abs(ref_g).max())
+    assert (g[:, C:] == 0).all()  # the padding columns are not written
+
+
 def _seg_model(S):
     m = PointNetSeg(50)
     m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in S.items()})
