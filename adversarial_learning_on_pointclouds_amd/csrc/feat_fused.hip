@@ -343,7 +343,13 @@ __device__ __forceinline__ void pair_merge(int n1, int u1, int n2, int u2, int& 
 // f32 re-evaluation of the top two, the default) or 1 (bf16 mode: x3 and W4
 // rounded to bf16, f32 accumulate; the screened winner is the result, no
 // re-evaluation: gmax carries the 2^-17 key truncation).
-template <int NP4>
+// G2: fewer than 64 clouds leave CUs idle with 256-channel workgroups, so a
+// workgroup takes 128 channels (8 per cloud) and its two wave groups (waves
+// 0-3, 4-7: the same 32-channel blocks) screen alternate 32-point units of the
+// same staged tiles; group 1 hands its top-2 to group 0 through LDS before the
+// exact re-evaluation.  Still two waves per SIMD (a lone wave gets half the
+// throughput: 4-wave workgroups measured slower).
+template <int NP4, bool G2>
 __global__ void __launch_bounds__(C4_T)
 k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
             const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
@@ -356,7 +362,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   int bid = blockIdx.x;
   const int nwg = gridDim.x;
   if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);
-  const int c = bid >> 2, cb = bid & 3;
+  const int c = G2 ? bid >> 3 : bid >> 2, cb = G2 ? bid & 7 : bid & 3;
 #ifdef PCADV_STAMPS
   uint64_t* st = stamps + (size_t)blockIdx.x * 16;
 #define STAMP(k) do { if (stamps && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -366,7 +372,10 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int o = cb * C4_CB + 32 * wave + r;  // this lane's output channel
+  const int wblk = G2 ? wave & 3 : wave;  // 32-channel block of this wave
+  const int grp = G2 ? wave >> 2 : 0;     // G2: wave group = unit of each step
+  constexpr int CB = G2 ? C4_CB / 2 : C4_CB;
+  const int o = cb * CB + 32 * wblk + r;  // this lane's output channel
   const float* xc = x3g + (size_t)c * N * 128;
   const int S = (N + C4_P - 1) / C4_P;
 
@@ -404,7 +413,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   // each lane takes k = 16 kb + 8 h .. + 8 of its channel, split to bf16 hi / lo
   bf16x8 bh[8], bl[8];
   {
-    const float* wsrc = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128;
+    const float* wsrc = w4 + (size_t)(cb * CB + 32 * wblk) * 128;
     float* wl = L.w[wave];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -468,7 +477,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     const int buf = s & 1;
     const __bf16* xh = &L.x[buf][0][(32 * pt + r) * C4_SB + 8 * h];
     const __bf16* xl = &L.x[buf][1][(32 * pt + r) * C4_SB + 8 * h];
-    const int uprev = 2 * s + pt - 1;
+    const int uprev = G2 ? 2 * s + pt - 2 : 2 * s + pt - 1;
     int k1 = KEY_NONE, k2 = KEY_NONE;
     bf16x8 fa[3][2];  // A fragments, a 3-deep register ring: [k-block % 3][hi, lo]
     auto frag = [&](int kb) {
@@ -508,7 +517,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         // screening below the MFMAs, next to its only use)
         asm volatile("" ::"v"(k1), "v"(k2));
       }
-      if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
+      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
 #pragma unroll
         for (int j = 4 * kb; j < 4 * kb + 4; ++j) {
           const float v = stg[j >> 2][j & 3];
@@ -519,7 +528,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         if constexpr (NP4 == 3) asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
         else asm volatile("" ::"v"(shi[kb >> 1]));
       }
-      if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb == 4) {  // the next step's tile (buffer free since the barrier)
+      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) {  // the next step's tile (buffer free since the barrier)
         bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][srow * C4_SB + sk]);
         bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][srow * C4_SB + sk]);
         dh[0] = shi[0];
@@ -531,37 +540,55 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       }
       // tile s + 2 into the staging registers just freed (clamped: past the
       // end it re-reads the last row): 1.5 units ahead of its conversion
-      if ((PCADV_C4_DIAG & 2) == 0 && pt == 0 && kb == 4) stage_load(s + 2);
+      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) stage_load(s + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (decltype(SCREEN)::value) pair_merge(k1, uprev, k2, uprev, r1, t1, r2, t2);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  unit(0, 0, accA, accB, F_{}, F_{});
-  if (S > 1) unit(0, 1, accB, accA, T_{}, F_{});
-  else unit(0, 1, accB, accA, T_{}, T_{});
-  __syncthreads();
-  for (int s = 1; s < S; ++s) {
-    unit(s, 0, accA, accB, T_{}, F_{});
-    if (s + 1 < S) unit(s, 1, accB, accA, T_{}, F_{});
-    else unit(s, 1, accB, accA, T_{}, T_{});
+  if constexpr (G2) {
+    // one unit per step (unit 2 s + grp), the previous step's unit screened
+    // during it; steps before the last are full, so only the last is masked
+    unit(0, grp, accA, accB, F_{}, F_{});
     __syncthreads();
+    for (int s = 1; s < S; ++s) {
+      if (s & 1) unit(s, grp, accB, accA, T_{}, F_{});
+      else unit(s, grp, accA, accB, T_{}, F_{});
+      __syncthreads();
+    }
+  } else {
+    unit(0, 0, accA, accB, F_{}, F_{});
+    if (S > 1) unit(0, 1, accB, accA, T_{}, F_{});
+    else unit(0, 1, accB, accA, T_{}, T_{});
+    __syncthreads();
+    for (int s = 1; s < S; ++s) {
+      unit(s, 0, accA, accB, T_{}, F_{});
+      if (s + 1 < S) unit(s, 1, accB, accA, T_{}, F_{});
+      else unit(s, 1, accB, accA, T_{}, T_{});
+      __syncthreads();
+    }
   }
   // W4 rows of the exact re-evaluation (eight lanes per row, see below): they
   // do not depend on the winners, so they are fetched while the last unit is
   // screened and merged (the W4 fragments' registers are free by now)
   const int oc = lane >> 3, part = lane & 7;
-  const float* wbase = w4 + (size_t)(cb * C4_CB + 32 * wave) * 128 + 16 * part;
+  const float* wbase = w4 + (size_t)(cb * CB + 32 * wblk) * 128 + 16 * part;
   f32x4 wv[4][4];
-  if constexpr (NP4 == 3) {
+  if (NP4 == 3 && grp == 0) {
 #pragma unroll
     for (int G = 0; G < 4; ++G)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)(8 * G + oc) * 128 + 4 * u);
   }
-  {  // the last unit
+  if constexpr (G2) {  // this wave's last unit
+    int k1 = KEY_NONE, k2 = KEY_NONE;
+    const int ul = 2 * (S - 1) + grp;
+    if ((S - 1) & 1) screen_unit(accB, ul, T_{}, 0, 8, k1, k2);
+    else screen_unit(accA, ul, T_{}, 0, 8, k1, k2);
+    pair_merge(k1, ul, k2, ul, r1, t1, r2, t2);
+  } else {  // the last unit
     int k1 = KEY_NONE, k2 = KEY_NONE;
     screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2);
     pair_merge(k1, 2 * S - 1, k2, 2 * S - 1, r1, t1, r2, t2);
@@ -601,6 +628,32 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       a1 = a ? p : a1;
       v2 = nv2;
       a2 = na2;
+    }
+    if constexpr (G2) {  // group 1's top-2 of each channel into group 0's
+      float* xv = L.w[0];  // free: the point loop's last barrier has passed
+      int* xi = reinterpret_cast<int*>(L.w[1]);
+      const int slot = 32 * wblk + r;  // lanes r and r + 32 hold the same pair
+      if (grp == 1 && h == 0) {
+        xv[2 * slot] = v1;
+        xv[2 * slot + 1] = v2;
+        xi[2 * slot] = a1;
+        xi[2 * slot + 1] = a2;
+      }
+      __syncthreads();
+      if (grp == 1) return;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float v = xv[2 * slot + q];
+        const int p = xi[2 * slot + q];
+        const bool a = ranks_before(v, p, v1, a1);
+        const bool b = !a && ranks_before(v, p, v2, a2);
+        const float nv2 = a ? v1 : (b ? v : v2);
+        const int na2 = a ? a1 : (b ? p : a2);
+        v1 = a ? v : v1;
+        a1 = a ? p : a1;
+        v2 = nv2;
+        a2 = na2;
+      }
     }
     if (a1 == 0x7fffffff) a1 = 0;
     // The screened top-2 are both re-evaluated as exact f32 dot products and
@@ -687,7 +740,10 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
                               hipStream_t s, uint64_t* stamps) {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(C4Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(C4Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3>),
@@ -704,8 +760,14 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
                      sizeof(MlpLds), s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3,
                      x3, inc_counter, stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
-  hipLaunchKernelGGL(k_conv4_max<NP4>, dim3(C * (C4_O / C4_CB)), dim3(C4_T), sizeof(C4Lds), s, x3,
-                     C, N, w4, b4, gmax, gidx, stamps);
+  // two wave groups per 128-channel workgroup when 256-channel workgroups would
+  // leave CUs idle (the diagnostic stamps layout assumes the plain form)
+  if (4 * C < 256 && !stamps)
+    hipLaunchKernelGGL((k_conv4_max<NP4, true>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
+  else
+    hipLaunchKernelGGL((k_conv4_max<NP4, false>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
   PC_HIP_CHECK_LAUNCH("k_conv4_max");
   return PCADV_OK;
 }

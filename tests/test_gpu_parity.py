@@ -95,6 +95,30 @@ def test_argmax_ties_first_index():
     assert (gidx.cpu().numpy() == ra).all()
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("N", [1024, 1000, 40])
+def test_conv4_max_workgroup_forms_bitwise(precision, N):
+    """k_conv4_max runs 256-channel workgroups from 64 clouds up and, below
+    that, 128-channel workgroups whose two wave groups split each step's
+    units: both forms compute every screened value with the same MFMA
+    sequence and re-evaluate the same candidates, so clouds 0..31 of a
+    64-cloud launch equal a 32-cloud launch bitwise (ragged N too)."""
+    G = onp.make_params(onp.cls_spec(40), seed=21)
+    pts = _pts(321, 64, N)
+    pts[5, N // 2:] = pts[5, 0]  # ties across both wave groups' units
+    w = _feat_weights(G)
+    g64, i64, x64 = ops.feat_fwd(_t(pts), *w, precision=precision)
+    g32, i32, x32 = ops.feat_fwd(_t(pts[:32]), *w, precision=precision)
+    assert torch.equal(x64[:32], x32)
+    assert torch.equal(i64[:32], i32)
+    assert torch.equal(g64[:32], g32)
+    if precision == "fp32":
+        r3 = onp.point_mlp_fwd(pts[:32], G)[2]
+        W4 = G["feat.conv4.weight"][:, :, 0]
+        _, ra = onp.conv_max_fwd(r3, W4, G["feat.conv4.bias"])
+        assert _argmax_ok(i32.cpu().numpy(), ra, r3, W4, G["feat.conv4.bias"]) == 0
+
+
 @pytest.mark.parametrize("C,N", [(4, 1024), (64, 1024), (3, 1000), (2, 300)])
 def test_feat_bwd_vs_oracle(C, N):
     G = onp.make_params(onp.cls_spec(40), seed=9)
