@@ -49,7 +49,8 @@ __device__ __forceinline__ void split3(float v, __bf16& hi, __bf16& mid, __bf16&
 // ============================================================================
 constexpr int PM_P = 64;    // points per tile
 constexpr int PM_T = 256;   // 4 waves; 2 workgroups per CU (register-bound)
-constexpr int PM_TPW = 2;   // tiles per workgroup (the next tile's points are prefetched)
+// TPW: tiles per workgroup (the next tile's points are prefetched): 2, or 1 when
+// two would leave fewer than two workgroups per CU (fewer than 64 clouds at N = 1024)
 constexpr int X2S = 72;     // bf16 row stride of the x2 planes (144 B: conflict-free b128 reads)
 
 constexpr int X3S = 136;     // f32 row stride of the x3 store staging (the two half-waves' rows 32 banks apart)
@@ -71,7 +72,7 @@ struct MlpLds {
 // |x w|), f32 accumulate: f32-level accuracy at 6/16 of the f32 MFMA cycles.
 // NP3: conv3's bf16 products per f32 product: 6 (f32-level, the default) or 1
 // (bf16 mode: x2 and W3 rounded to bf16, f32 accumulate).
-template <int NP3>
+template <int NP3, int TPW>
 __global__ void __launch_bounds__(PM_T) __attribute__((amdgpu_waves_per_eu(2)))
 k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split, int N,
             int T, int ntiles, const float* __restrict__ w1, const float* __restrict__ b1,
@@ -98,7 +99,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     const int p = tid / 3;
     return (tid < PM_P * 3 && p0 + p < N) ? pts[(size_t)p0 * 3 + tid] : 0.f;
   };
-  int tile = blockIdx.x * PM_TPW;
+  int tile = blockIdx.x * TPW;
   // loads in the order they are consumed (the memory counter waits in issue
   // order): the first tile's points and conv1's weights, then conv2's B
   // fragments, then W3 (split three ways only after conv1 of the first tile)
@@ -137,12 +138,12 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
   };
   STAMP(1);
 
-  for (int it = 0; it < PM_TPW && tile < ntiles; ++it, ++tile) {
+  for (int it = 0; it < TPW && tile < ntiles; ++it, ++tile) {
     const int c = tile / T, p0 = (tile % T) * PM_P;
     if (tid < PM_P * 3) L.pts[(tid / 3) * 4 + tid % 3] = pv;
     __syncthreads();  // (also: every wave is past the previous tile's conv3 reads)
     STAMP(3 + 5 * it);
-    if (it + 1 < PM_TPW && tile + 1 < ntiles) pv = pts_load(tile + 1);  // in flight during this tile
+    if (it + 1 < TPW && tile + 1 < ntiles) pv = pts_load(tile + 1);  // in flight during this tile
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int p = pg * 16 + i;
@@ -746,7 +747,10 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(C4Lds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(MlpLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 1>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(MlpLds)) != hipSuccess) {
       set_error("feat_fwd: cannot reserve LDS (%zu / %zu bytes)", sizeof(C4Lds), sizeof(MlpLds));
@@ -756,9 +760,17 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
   }
   const int T = (N + PM_P - 1) / PM_P;
   const int ntiles = C * T;
-  hipLaunchKernelGGL(k_point_mlp<NP3>, dim3((ntiles + PM_TPW - 1) / PM_TPW), dim3(PM_T),
-                     sizeof(MlpLds), s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3,
-                     x3, inc_counter, stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr);
+  uint64_t* mlp_stamps = stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr;
+  // one tile per workgroup when two would give fewer than two workgroups per
+  // CU (512); the diagnostic stamps layout assumes two
+  if (ntiles < 1024 && !stamps)
+    hipLaunchKernelGGL((k_point_mlp<NP3, 1>), dim3(ntiles), dim3(PM_T), sizeof(MlpLds), s, pts_a,
+                       pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3, inc_counter,
+                       mlp_stamps);
+  else
+    hipLaunchKernelGGL((k_point_mlp<NP3, 2>), dim3((ntiles + 1) / 2), dim3(PM_T), sizeof(MlpLds),
+                       s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3,
+                       inc_counter, mlp_stamps);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
   // two wave groups per 128-channel workgroup when 256-channel workgroups would
   // leave CUs idle (the diagnostic stamps layout assumes the plain form)

@@ -548,9 +548,9 @@ def main():
                   if "_seg_" not in os.path.basename(p))
     if prof and N == 1024 and adv_prec == "fp32":  # the committed PMC passes ran the default workload
         kern = json.load(open(prof[-1]))["kernels"]
-        # the fp32-mode instances (k_conv4_max<3, false>: the one-group form B = 32 runs)
+        # the fp32-mode instances (<6, 2> and <3, false>: the forms B = 32 runs)
         names = [next((k for k in kern if k.startswith(p)), None)
-                 for p in ("pcadv::k_point_mlp<6>", "pcadv::k_conv4_max<3")]
+                 for p in ("pcadv::k_point_mlp<6", "pcadv::k_conv4_max<3")]
         if all(names):
             traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
             traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))

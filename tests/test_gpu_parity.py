@@ -102,7 +102,9 @@ def test_conv4_max_workgroup_forms_bitwise(precision, N):
     that, 128-channel workgroups whose two wave groups split each step's
     units: both forms compute every screened value with the same MFMA
     sequence and re-evaluate the same candidates, so clouds 0..31 of a
-    64-cloud launch equal a 32-cloud launch bitwise (ragged N too)."""
+    64-cloud launch equal a 32-cloud launch bitwise (ragged N too).  The same
+    holds for k_point_mlp's x3 (two tiles per workgroup at 64 clouds, one at
+    32)."""
     G = onp.make_params(onp.cls_spec(40), seed=21)
     pts = _pts(321, 64, N)
     pts[5, N // 2:] = pts[5, 0]  # ties across both wave groups' units
