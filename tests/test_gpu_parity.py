@@ -96,7 +96,7 @@ def test_argmax_ties_first_index():
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-@pytest.mark.parametrize("N", [1024, 1000, 40])
+@pytest.mark.parametrize("N", [1024, 1000, 40, 20])
 def test_conv4_max_workgroup_forms_bitwise(precision, N):
     """k_conv4_max runs 256-channel workgroups from 64 clouds up and, below
     that, 128-channel workgroups whose two wave groups split each step's
@@ -114,6 +114,8 @@ def test_conv4_max_workgroup_forms_bitwise(precision, N):
     assert torch.equal(x64[:32], x32)
     assert torch.equal(i64[:32], i32)
     assert torch.equal(g64[:32], g32)
+    g1, i1, _ = ops.feat_fwd(_t(pts[5:6]), *w, precision=precision)  # one cloud: 8 workgroups
+    assert torch.equal(i64[5:6], i1) and torch.equal(g64[5:6], g1)
     if precision == "fp32":
         r3 = onp.point_mlp_fwd(pts[:32], G)[2]
         W4 = G["feat.conv4.weight"][:, :, 0]
