@@ -162,6 +162,44 @@ k_pw_bwd_data(const float* __restrict__ dy, const float* __restrict__ yv, int M,
   }
 }
 
+// K = 3 (the points' gradient through a T-Net's conv1, STN3d models/pointnet.py:
+// 28): thread = row, its three sums over o in ascending order (fma), W staged
+// in LDS.  One weight matrix for all rows.
+template <int R, int ACT>
+__global__ void __launch_bounds__(PW_T)
+k_pw_bwd_data3(const float* __restrict__ dy, const float* __restrict__ yv, int M, WView wv,
+               float* __restrict__ dx, int accumulate) {
+  __shared__ __attribute__((aligned(16))) float ws[R * 4];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < R * 3; e += PW_T) ws[(e / 3) * 4 + e % 3] = wv.get(wv.w, e / 3, e % 3);
+  __syncthreads();
+  const int m = blockIdx.x * PW_T + tid;
+  if (m >= M) return;
+  const float* dyr = dy + (size_t)m * R;
+  const float* yr = yv + (size_t)m * R;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll 4
+  for (int o4 = 0; o4 < R / 4; ++o4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(dyr + 4 * o4);
+    if (ACT != ACT_NONE) {
+      const f32x4 yy = *reinterpret_cast<const f32x4*>(yr + 4 * o4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] *= act_bwd(yy[j], ACT);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(ws + (4 * o4 + j) * 4);
+      a0 = fmaf(v[j], w[0], a0);
+      a1 = fmaf(v[j], w[1], a1);
+      a2 = fmaf(v[j], w[2], a2);
+    }
+  }
+  float* p = dx + (size_t)m * 3;
+  p[0] = accumulate ? p[0] + a0 : a0;
+  p[1] = accumulate ? p[1] + a1 : a1;
+  p[2] = accumulate ? p[2] + a2 : a2;
+}
+
 // ---------------------------------------------------------------------------
 // backward, weight gradient: per PWW_ROWS rows a slab of dW (O x K, layout
 // [o][k] or [k][o]) and db (O)
@@ -468,13 +506,24 @@ int launch_pw_fwd(const float* x, int M, int K, const float* w, const float* b, 
 int launch_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,
                        int K, int w_kmajor, int rows_per_w, float* dx, int accumulate,
                        hipStream_t s) {
-  PC_REQUIRE(M > 0 && (O == 64 || O == 128) && K > 0 && K % 32 == 0,
+  PC_REQUIRE(M > 0 && (O == 64 || O == 128) && K > 0 && (K % 32 == 0 || K == 3),
              "pw_bwd_data: unsupported shape M=%d O=%d K=%d", M, O, K);
   PC_REQUIRE(act == ACT_NONE || act == ACT_RELU, "pw_bwd_data: act %d", act);
   PC_REQUIRE(rows_per_w == 0 || rows_per_w % PW_ROWS == 0, "pw_bwd_data: rows per weight %d",
              rows_per_w);
+  PC_REQUIRE(K != 3 || rows_per_w == 0, "pw_bwd_data: K=3 takes one weight matrix");
   PC_REQUIRE(act == ACT_NONE || y, "pw_bwd_data: the layer output is needed for act'");
   const WView wv = make_view(w, O, K, w_kmajor, rows_per_w);
+  if (K == 3) {
+    const dim3 g3((M + PW_T - 1) / PW_T);
+#define PW_CASE3(R, A)                                                                     \
+  if (O == R && act == A)                                                                  \
+    hipLaunchKernelGGL((k_pw_bwd_data3<R, A>), g3, dim3(PW_T), 0, s, dy, y, M, wv, dx, accumulate);
+    PW_CASE3(64, ACT_NONE) PW_CASE3(64, ACT_RELU) PW_CASE3(128, ACT_NONE) PW_CASE3(128, ACT_RELU)
+#undef PW_CASE3
+    PC_HIP_CHECK_LAUNCH("k_pw_bwd_data3");
+    return PCADV_OK;
+  }
   const dim3 grid((M + PW_ROWS - 1) / PW_ROWS, (K + 127) / 128);
 #define PW_CASE(R, A)                                                                      \
   if (O == R && act == A)                                                                  \

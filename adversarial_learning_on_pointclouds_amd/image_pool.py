@@ -29,8 +29,17 @@ class ImagePool:
         if self.pool_size == 0:
             return images
         batch = images.detach()
-        if self._bank is None:
-            self._bank = batch.new_empty((self.pool_size,) + tuple(batch.shape[1:]))
+        shape = (self.pool_size,) + tuple(batch.shape[1:])
+        if self._bank is None or (self._filled == 0 and (
+                tuple(self._bank.shape) != shape or self._bank.dtype != batch.dtype
+                or self._bank.device != batch.device)):
+            self._bank = batch.new_empty(shape)  # (re)allocated while the history is empty
+        elif (tuple(self._bank.shape) != shape or self._bank.dtype != batch.dtype
+              or self._bank.device != batch.device):
+            raise ValueError(f"ImagePool: samples of shape {tuple(batch.shape[1:])} {batch.dtype} "
+                             f"on {batch.device}, but the history holds "
+                             f"{tuple(self._bank.shape[1:])} {self._bank.dtype} on "
+                             f"{self._bank.device}")
         out = batch.clone()
         for i in range(batch.shape[0]):
             if self._filled < self.pool_size:

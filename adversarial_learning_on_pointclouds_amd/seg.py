@@ -424,8 +424,13 @@ class SegTrainStep:
     launch over the whole network."""
 
     def __init__(self, model, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 lambda_seg=1.0, device="cuda"):
+                 lambda_seg=1.0, device="cuda", keep_activations=False):
         self.lib = _lib.load()
+        # keep_activations: hold the last step's forward tensors in self.fw (for
+        # inspection / tests); off by default, so a step's per-point activations
+        # (hundreds of MB at B=16, N=2048) are released when it returns
+        self.keep_activations = bool(keep_activations)
+        self.fw = None
         dev = torch.device(device)
         if dev.type != "cuda":
             raise ValueError("SegTrainStep runs on the HIP device only")
@@ -488,7 +493,8 @@ class SegTrainStep:
             _engine().split(self.param, self.wph, self.wpl)
             wpl = self.wplanes
         fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params, wplanes=wpl)
-        self.fw = fw  # the last step's activations (logits, x_global, argmax, ...)
+        if self.keep_activations:
+            self.fw = fw  # the last step's activations (logits, x_global, argmax, ...)
         M, ncls = B * N, fw["dims"][2]
         d = torch.empty(M, ncls, device=self.device)
         ws = _ws(self.lib.pcadv_row_ce_workspace_bytes(M), self.device)

@@ -306,7 +306,9 @@ class AdvTrainStep:
         for opt, mod, m, v, gr, layout in self._bind:
             gv = _views(gr, mod, layout)
             for name, p in mod.named_parameters():
-                if p.grad is not None and p.grad.data_ptr() != gv[name].data_ptr():
+                if p.grad is None:
+                    gv[name].zero_()  # no gradient this iteration: not the last fused one's
+                elif p.grad.data_ptr() != gv[name].data_ptr():
                     gv[name].copy_(p.grad)
                 p.grad = gv[name]
 

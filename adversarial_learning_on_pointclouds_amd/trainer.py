@@ -126,6 +126,8 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
 
         if fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B:
             if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
+                if step is not None:  # the replacement adopts the Adam state: count included
+                    step.sync_optimizer_state()
                 step = AdvTrainStep(model, model_D, pts.shape[0], pts.shape[1],
                                     optimizer=optimizer, optimizer_D=optimizer_D,
                                     lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
@@ -271,6 +273,8 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
         l_regu = None
         if fused and pts.shape[0] <= MAX_FUSED_B:
             if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
+                if step is not None:
+                    step.sync_optimizer_state()
                 step = ClsTrainStep(model, pts.shape[0], pts.shape[1], optimizer=optimizer,
                                     lambda_cls=args.lambda_cls,
                                     seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)

@@ -116,9 +116,8 @@ def make_models(dev, seed=0):
     return model, model_D
 
 
-def cpu_baseline(seconds):
-    """The numpy oracle's adversarial step on a bounded sample of the same
-    workload (B=32, N=1024), timed on this host's cores."""
+def _time_adv_oracle(seconds, dense):
+    """Steps of the numpy oracle's adversarial step (B=32+32, N) for `seconds`."""
     from oracle import pointnet_np as onp
     G = onp.make_params(onp.cls_spec(40), seed=3)
     D = onp.make_params(onp.disc_spec(40, 1), seed=4, init="xavier")
@@ -131,33 +130,51 @@ def cpu_baseline(seconds):
     m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
     y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
     y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
-    onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2)  # warm-up
+
+    def one():
+        onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2, dense_max_bwd=dense)
+
+    one()  # warm-up
     t0 = time.perf_counter()
     steps = 0
     while True:
-        onp.adv_step(G, D, oG, oD, pg, lab, pn, m1, m2, y1, y2)
+        one()
         steps += 1
         if time.perf_counter() - t0 >= seconds and steps >= 2:
             break
-    dt = time.perf_counter() - t0
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds):
+    """The reference's algorithm on the host cores: the numpy oracle's
+    adversarial step with the conv4 + max backward in the reference autograd's
+    dense form (MaxBackward zero-fill + scatter, dense Conv1d dX / dW GEMMs over
+    all points: oracle.conv_max_bwd_dense), on a bounded sample of the same
+    workload (B=32+32, N).  The sparse-backward port (what the GPU path
+    computes) is timed beside it on a shorter sample as a secondary figure."""
+    steps, dt = _time_adv_oracle(seconds, dense=True)
+    s_steps, s_dt = _time_adv_oracle(max(2.0, seconds / 3), dense=False)
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     out = {"value": round(2 * B * steps / dt, 2), "unit": "clouds/s", "cores": cores,
            "kind": "port",
-           "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N={N}, fp32) in {dt:.1f}s"}
-    # the port against the reference's own run_training on the same cores, measured
-    # in the build container (the reference never travels to this box):
+           "algorithm": "reference (dense MaxBackward + dense conv4 backward, as autograd runs "
+                        "models/pointnet.py:128-129)",
+           "sample": f"{steps} numpy-oracle adversarial steps (B=32+32, N={N}, fp32, dense max-pool "
+                     f"backward) in {dt:.1f}s",
+           "sparse_port_value": round(2 * B * s_steps / s_dt, 2),
+           "sparse_port_sample": f"{s_steps} steps with the sparse max-pool backward in {s_dt:.1f}s"}
+    # the dense port against the reference's own run_training on the same cores,
+    # measured in the build container (the reference never travels to this box):
     # tools/time_reference_cpu.py -> profiles/rNN_cpu_calibration.json
     cal = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_cpu_calibration.json")))
     if cal and N == 1024:
         c = json.load(open(cal[-1]))
-        ratio = float(c["port_over_reference"])
-        out["calibration"] = {"port_over_reference": ratio, "cores": c["cores"],
-                              "reference_clouds_per_s": c["reference_run_training_clouds_per_s"],
-                              "source": os.path.relpath(cal[-1], REPO),
-                              "note": "the port's sparse max-pool backward skips the reference's "
-                                      "dense MaxBackward + zero-fill, so it runs faster than "
-                                      "run_training on the same cores"}
-        out["reference_equivalent_value"] = round(out["value"] / ratio, 2)
+        if "dense_port_over_reference" in c:
+            out["calibration"] = {"port_over_reference": c["dense_port_over_reference"],
+                                  "sparse_port_over_reference": c["port_over_reference"],
+                                  "cores": c["cores"],
+                                  "reference_clouds_per_s": c["reference_run_training_clouds_per_s"],
+                                  "source": os.path.relpath(cal[-1], REPO)}
     return out
 
 

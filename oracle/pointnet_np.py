@@ -226,9 +226,29 @@ def conv_max_bwd(dg, am, x, w):
     return dW.astype(F32), dg.sum(0).astype(F32), dX
 
 
-def cls_backward(p, cache, dlogits):
+def conv_max_bwd_dense(dg, am, x, w):
+    """conv_max_bwd as the reference's autograd computes it (models/pointnet.py:
+    128-129 under loss.backward(), utils/trainer.py:520): MaxBackward zero-fills
+    the whole (B, N, O) conv4 output gradient and scatters dg at the argmax
+    points, then the Conv1d backward runs its two dense GEMMs over all B*N
+    points (dX = dY W, dW = dY^T X).  Same values as the sparse form (up to
+    summation order); used only to time the reference's algorithm (bench.py's
+    cpu_baseline), never as a checker."""
+    B, N, K = x.shape
+    O = w.shape[0]
+    dY = np.zeros((B, N, O), F32)
+    dY[np.arange(B)[:, None], am, np.arange(O)[None, :]] = dg
+    dY2 = dY.reshape(B * N, O)
+    dX = np.matmul(dY, w)  # per cloud, as the Conv1d backward batches it
+    dW = dY2.T @ x.reshape(B * N, K)
+    return dW.astype(F32), dY2.sum(0).astype(F32), dX.astype(F32)
+
+
+def cls_backward(p, cache, dlogits, dense_max_bwd=False):
     """Autograd of cls_forward given dL/dlogits; returns grads keyed like the
-    reference state_dict (conv weights shaped [out, in, 1])."""
+    reference state_dict (conv weights shaped [out, in, 1]).  dense_max_bwd:
+    conv4 + max backward in the reference's dense form (conv_max_bwd_dense:
+    timing of the reference algorithm only)."""
     pts, x1, x2, x3 = cache["pts"], cache["x1"], cache["x2"], cache["x3"]
     gmax, am = cache["gmax"], cache["am"]
     h1, h2, scale = cache["head"]
@@ -246,7 +266,7 @@ def cls_backward(p, cache, dlogits):
     g["fc1.bias"] = dz1.sum(0)
     dgl = (dz1 @ p["fc1.weight"]).astype(F32)
     W4 = _w(p, "feat.conv4.weight")
-    dW4, db4, dX3 = conv_max_bwd(dgl, am, x3, W4)
+    dW4, db4, dX3 = (conv_max_bwd_dense if dense_max_bwd else conv_max_bwd)(dgl, am, x3, W4)
     B, N, _ = x3.shape
     dz3 = (dX3 * (x3 > 0)).reshape(B * N, -1)
     dz2p = (dz3 @ _w(p, "feat.conv3.weight")) * (x2.reshape(B * N, -1) > 0)
@@ -405,13 +425,14 @@ def semi_ce(logits_ng, d_ng, semi_th):
 
 def adv_step(G, D, optG, optD, pts_gt, labels, pts_nogt, mask_gt, mask_nogt,
              y_gt, y_nogt, lambda_cls=1.0, lambda_adv=0.001, apply_adam=True,
-             semi=False, semi_th=0.8, lambda_semi=1.0):
+             semi=False, semi_th=0.8, lambda_semi=1.0, dense_max_bwd=False):
     """One run_training iteration (semi=True: one run_training_semi iteration
     past semi_start, utils/trainer.py:611-847).  The stochastic parts are
     inputs: dropout masks (B, 256) for the two G passes and the U(0.7,1.05) /
     U(0,0.305) soft D labels drawn by make_D_label(random=True)
     (utils/utils.py:22-31).  ImagePool(0).query is the identity
-    (utils/image_pool.py:35-36)."""
+    (utils/image_pool.py:35-36).  dense_max_bwd: the conv4 + max backward in
+    the reference autograd's dense form (the CPU baseline's timing mode)."""
     logits_gt, _, c_gt = cls_forward(G, pts_gt, mask_gt)             # :468
     l, dce = cross_entropy(logits_gt, labels)                          # :469
     lsm_gt = log_softmax(logits_gt)                                    # :472
@@ -426,8 +447,8 @@ def adv_step(G, D, optG, optD, pts_gt, labels, pts_nogt, mask_gt, mask_nogt,
     if semi:                                                           # :716-743
         loss_semi, dsemi, semi_ratio = semi_ce(logits_ng, d_ng, semi_th)
         dlog_ng = (dlog_ng + F32(lambda_semi) * dsemi).astype(F32)
-    ga = cls_backward(G, c_gt, F32(lambda_cls) * dce)
-    gb = cls_backward(G, c_ng, dlog_ng)
+    ga = cls_backward(G, c_gt, F32(lambda_cls) * dce, dense_max_bwd)
+    gb = cls_backward(G, c_ng, dlog_ng, dense_max_bwd)
     gG = OrderedDict((k, (ga[k] + gb[k]).astype(F32)) for k in G)
     # D backward (:526-556)
     d_gt, acts_gt = disc_forward(D, lsm_gt)

@@ -315,6 +315,30 @@ def main(ref_root, only=None):
             summarize("grad." + name, p.grad.numpy(), out)
         np.savez_compressed(os.path.join(HERE, "g11_cls_b32.npz"), **out)
 
+    # ---------------- G12: STN3d forward + backward (models/pointnet.py:14-43) ----
+    # The 3x3 input transform regressor on the reference layout B x 3 x N, then
+    # T.backward(dT) with a seeded dT: the transform, every parameter gradient
+    # and the input gradient (returned point-major, B x N x 3).
+    def g12():
+        from models.pointnet import STN3d
+        Sp = onp.make_params(onp.stnkd_spec("", 3), seed=12)
+        m = load(STN3d(), Sp)
+        rng = np.random.default_rng(121)
+        B12 = 4
+        pts12 = rng.uniform(-1, 1, (B12, N_PTS, 3)).astype(np.float32)
+        dT = rng.normal(0, 1, (B12, 3, 3)).astype(np.float32)
+        x = torch.from_numpy(np.ascontiguousarray(pts12.transpose(0, 2, 1))).requires_grad_(True)
+        T = m(x)
+        T.backward(torch.from_numpy(dT))
+        out = dict(s_seed=12, data_seed=121, B=B12, N=N_PTS, trans=T.detach().numpy(),
+                   dx=np.ascontiguousarray(x.grad.numpy().transpose(0, 2, 1)))
+        for name, p in m.named_parameters():
+            summarize("grad." + name, p.grad.numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g12_stn3d.npz"), **out)
+
+    if only == "g12":
+        g12()
+        return
     if only == "g10":
         g10()
         return
@@ -504,6 +528,7 @@ def main(ref_root, only=None):
     g9()
     g10()
     g11()
+    g12()
 
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
@@ -513,7 +538,7 @@ def main(ref_root, only=None):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("ref_root", nargs="?", default="/root/reference")
-    ap.add_argument("--only", default=None, help="g7, g8, g9 or g10: regenerate only that "
+    ap.add_argument("--only", default=None, help="g7, g8, g9, g10 or g12: regenerate only that "
                     "fixture; full: g10, g11 and the B=32 g3")
     a = ap.parse_args()
     main(a.ref_root, a.only)

@@ -46,6 +46,34 @@ def assert_grad_close(a, ref, name, tol_max=GRAD_TOL_MAX, tol_l2=GRAD_TOL_L2):
     return e_max, e_l2
 
 
+def adam_update_err(p_new, p_old, ref_new, ref_old, g_ref, g_floor=1e-5, rel_floor=1e-2):
+    """Relative error of an Adam update: (p_new - p_old) against the oracle's
+    (ref_new - ref_old), max over the elements whose reference gradient is
+    above g_floor (1e3 x Adam's eps) and above rel_floor x the tensor's largest
+    gradient (the gradient checks allow 1e-3 of that, so no selected element can
+    change sign within them), relative to the largest reference update,
+    each element's difference less one f32 spacing of its parameter (both sides
+    round p_new to f32).  On those elements the first update is lr g / (|g| +
+    eps) ~ lr sign(g): a wrong lr, bias correction or eps placement moves it by
+    a large fraction, the rounding of the gradient does not."""
+    p_old = np.asarray(p_old, np.float32).reshape(-1)
+    du = np.asarray(p_new, np.float64).reshape(-1) - p_old.astype(np.float64)
+    dr = np.asarray(ref_new, np.float64).reshape(-1) - np.asarray(ref_old, np.float64).reshape(-1)
+    ga = np.abs(np.asarray(g_ref, np.float64).reshape(-1))
+    sel = ga > max(g_floor, rel_floor * float(ga.max()))
+    if not sel.any():
+        return 0.0, 0
+    d = np.maximum(np.abs(du - dr)[sel] - np.spacing(np.abs(p_old[sel])).astype(np.float64), 0.0)
+    return float(d.max()) / max(float(np.abs(dr[sel]).max()), 1e-30), int(sel.sum())
+
+
+def assert_adam_update_close(p_new, p_old, ref_new, ref_old, g_ref, name, tol=1e-3):
+    e, n = adam_update_err(p_new, p_old, ref_new, ref_old, g_ref)
+    assert n > 0, f"{name}: no gradient element above the floor: the check would be vacuous"
+    assert e <= tol, f"{name}: Adam update rel err {e:.3e} over {n} elements (tol {tol:g})"
+    return e
+
+
 def check_tensor(fx, prefix, arr, tol=1e-3):
     """Compare a tensor against a fixture entry (full, or summary + samples)."""
     arr = np.asarray(arr, np.float32)

@@ -616,7 +616,7 @@ def test_seg_train_step_full_size_configs3_vs_oracle():
     cls[np.arange(B), 0, rng.integers(0, 16, B)] = 1
     seg = rng.integers(0, 50, (B, N))
     m = _seg_model(S)
-    step = SegTrainStep(m, device=DEV)
+    step = SegTrainStep(m, device=DEV, keep_activations=True)
     loss = step(_t(pts), _t(cls), _t(seg, torch.int64), apply_adam=False).item()
     fw = step.fw
     rl, grads, rlog, rg, ram = onp.seg_step(S, pts, cls, seg)

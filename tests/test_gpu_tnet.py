@@ -64,7 +64,7 @@ def test_pw_bwd_vs_oracle(K, O):
     w = rng.normal(size=(O, K, 1)).astype(np.float32) / np.sqrt(K)
     b = rng.normal(size=O).astype(np.float32)
     dy = rng.normal(size=(M, O)).astype(np.float32)
-    xt = _t(x).requires_grad_(K != 3)
+    xt = _t(x).requires_grad_(True)  # K = 3: the points' gradient (k_pw_bwd_data3)
     wt, bt = _t(w).requires_grad_(True), _t(b).requires_grad_(True)
     y = ops.PointwiseFunction.apply(xt, wt, bt, ops.ACT_RELU)
     y.backward(_t(dy))
@@ -72,8 +72,7 @@ def test_pw_bwd_vs_oracle(K, O):
     dW, db, dx = onp._layer_bwd(dy, x, yr, w[:, :, 0])
     assert rel_err(_np(wt.grad)[:, :, 0], dW) < 1e-5
     assert rel_err(_np(bt.grad), db) < 1e-5
-    if K != 3:
-        assert rel_err(_np(xt.grad), dx) < 1e-5
+    assert rel_err(_np(xt.grad), dx) < 1e-5
 
 
 @pytest.mark.parametrize("relu", [False, True])
@@ -196,3 +195,51 @@ def test_cls_ft_full_size_vs_oracle():
     assert abs(l.item() - lr) < 1e-4 and abs(reg.item() - rr) < 1e-3
     for name, p in m.named_parameters():
         assert_grad_close(_np(p.grad), grads[name], name)
+
+
+def _stn3d(seed):
+    from adversarial_learning_on_pointclouds_amd.pointnet import STN3d
+    S = onp.make_params(onp.stnkd_spec("", 3), seed=seed)
+    m = STN3d()
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in S.items()})
+    return m.to(DEV), S
+
+
+def test_stn3d_golden_g12():
+    """STN3d (models/pointnet.py:14-43, the 3x3 T-Net north_star names) on the
+    reference layout B x 3 x N: forward and backward against the reference's own
+    capture (g12): the transform, every parameter gradient per tensor and the
+    input gradient."""
+    fx = load("g12_stn3d.npz")
+    m, _ = _stn3d(int(fx["s_seed"]))
+    rng = np.random.default_rng(int(fx["data_seed"]))
+    B, N = int(fx["B"]), int(fx["N"])
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    dT = rng.normal(0, 1, (B, 3, 3)).astype(np.float32)
+    x = _t(pts.transpose(0, 2, 1)).requires_grad_(True)
+    T = m(x)
+    assert T.shape == (B, 3, 3)
+    T.backward(_t(dT))
+    assert rel_err(_np(T), fx["trans"]) < 1e-5
+    for name, p in m.named_parameters():
+        check_tensor_rel(fx, "grad." + name, _np(p.grad), tol=1e-4)
+    check_tensor_rel(fx, "dx", _np(x.grad).transpose(0, 2, 1), tol=1e-4)
+
+
+def test_stn3d_full_size_vs_oracle():
+    """STN3d at B=32, N=1024 against the oracle's forward / backward: every
+    gradient per tensor (default tolerance) and the input gradient."""
+    m, S = _stn3d(33)
+    rng = np.random.default_rng(331)
+    B, N = 32, 1024
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    dT = rng.normal(0, 1, (B, 3, 3)).astype(np.float32)
+    x = _t(pts.transpose(0, 2, 1)).requires_grad_(True)
+    T = m(x)
+    T.backward(_t(dT))
+    Tr, cache = onp.stn_forward_train(S, pts, "", 3)
+    grads, dx = onp.stn_backward(S, cache, dT, "")
+    assert rel_err(_np(T), Tr) < 1e-5
+    for name, p in m.named_parameters():
+        assert_grad_close(_np(p.grad), grads[name], name)
+    assert_grad_close(_np(x.grad).transpose(0, 2, 1), dx, "dx")

@@ -210,3 +210,58 @@ def test_bf16_mode_oracle_close_to_reference_g11():
     loss, _ = onp.cross_entropy(logits, lab)
     assert abs(loss - float(fx["loss"])) < 1e-2
     assert not np.array_equal(logits, fx["logits"])  # the mode does change the arithmetic
+
+
+def test_g12_stn3d():
+    """STN3d (models/pointnet.py:14-43, the 3x3 T-Net of north_star) forward and
+    backward against the reference's capture: the transform, every parameter
+    gradient (strict per-tensor form) and the input gradient."""
+    fx = load("g12_stn3d.npz")
+    S = onp.make_params(onp.stnkd_spec("", 3), seed=int(fx["s_seed"]))
+    rng = np.random.default_rng(int(fx["data_seed"]))
+    B, N = int(fx["B"]), int(fx["N"])
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    dT = rng.normal(0, 1, (B, 3, 3)).astype(np.float32)
+    T, cache = onp.stn_forward_train(S, pts, "", 3)
+    assert rel_err(T, fx["trans"]) < 1e-5
+    assert rel_err(onp.stn_forward(S, pts, "", 3), fx["trans"]) < 1e-5
+    grads, dx = onp.stn_backward(S, cache, dT, "")
+    for k in S:
+        check_tensor_rel(fx, "grad." + k, grads[k], tol=1e-4)
+    check_tensor_rel(fx, "dx", dx, tol=1e-4)
+
+
+def test_adam_update_check_is_sensitive():
+    """The update check of the fused-Adam GPU tests (golden_util.adam_update_err):
+    an Adam at the right lr passes with a gradient perturbed at the GPU tests'
+    tolerance (1e-3 of each tensor's max), one at half the lr fails every
+    tensor, and so does one with eps inside the square root."""
+    from golden_util import adam_update_err
+    fx = load("g3_adv_step1.npz")
+    G = onp.make_params(onp.cls_spec(40), seed=int(fx["g_seed"]))
+    D = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
+    pg, lab, pn, m1, m2, y1, y2 = _adv_inputs(fx)[0]
+    _, gG, _, _ = onp.adv_step(G, D, None, None, pg, lab, pn, m1, m2, y1, y2, apply_adam=False)
+    old = {k: v.copy() for k, v in G.items()}
+    rng = np.random.default_rng(0)
+
+    def run(lr=1e-4, eps=1e-8, noise=0.0):
+        P = {k: v.copy() for k, v in old.items()}
+        g = {k: (v + noise * np.abs(v).max() * rng.uniform(-1, 1, v.shape)).astype(np.float32)
+             for k, v in gG.items()}
+        onp.Adam(P, lr=lr, eps=eps).step(g)
+        return P
+
+    ref = run()
+    ok, half = run(noise=1e-3), run(lr=0.5e-4)
+    # eps misplaced: sqrt(v + eps) instead of sqrt(v) + eps (v = g^2 after step 1)
+    bad_eps = {k: (old[k] - np.float32(1e-4) * gG[k] / (np.sqrt(gG[k].astype(np.float64) ** 2 + 1e-8)
+                                                       )).astype(np.float32) for k in old}
+    for k in G:
+        e, n = adam_update_err(ok[k], old[k], ref[k], old[k], gG[k])
+        assert n > 0 and e < 1e-3, (k, e)
+        assert adam_update_err(half[k], old[k], ref[k], old[k], gG[k])[0] > 0.4, k
+        # eps moves the update only where |g| is within a few decades of it: the
+        # feature layers' small gradients
+        if k.startswith("feat.") and k.endswith("weight"):
+            assert adam_update_err(bad_eps[k], old[k], ref[k], old[k], gG[k])[0] > 2e-3, k

@@ -70,20 +70,28 @@ def main():
     import json
     import bench
     k1, k2 = 3, 13
-    refs, ports = [], []
-    for _ in range(a.rounds):  # alternate, so host drift hits both alike
+    refs, ports, dense = [], [], []
+    for _ in range(a.rounds):  # alternate, so host drift hits all alike
         t1, t2 = time_reference(a.ref_root, k1), time_reference(a.ref_root, k2)
         refs.append(2 * B * (k2 - k1) / (t2 - t1))
-        ports.append(bench.cpu_baseline(10.0)["value"])
-    ref_v, port_v = float(np.median(refs)), float(np.median(ports))
+        st, dt = bench._time_adv_oracle(10.0, dense=False)
+        ports.append(2 * B * st / dt)
+        st, dt = bench._time_adv_oracle(10.0, dense=True)
+        dense.append(2 * B * st / dt)
+    ref_v, port_v, dense_v = float(np.median(refs)), float(np.median(ports)), float(np.median(dense))
     out = {"cores": os.cpu_count(), "threads": "torch.set_num_threads(cores); numpy/BLAS default",
            "reference_run_training_clouds_per_s": round(ref_v, 1),
            "reference_ms_per_step": round(2 * B / ref_v * 1e3, 1),
            "port_clouds_per_s": round(port_v, 1), "port_over_reference": round(port_v / ref_v, 3),
-           "samples": {"reference": [round(v, 1) for v in refs], "port": [round(v, 1) for v in ports]},
+           "dense_port_clouds_per_s": round(dense_v, 1),
+           "dense_port_over_reference": round(dense_v / ref_v, 3),
+           "samples": {"reference": [round(v, 1) for v in refs], "port": [round(v, 1) for v in ports],
+                       "dense_port": [round(v, 1) for v in dense]},
            "workload": "adversarial step B=32 GT + 32 no-GT, N=1024, fp32 (run_training :426-559)",
            "method": "reference: (T(13) - T(3)) / 10 iterations of utils/trainer.py:run_training "
-                     "(iteration 0's checkpoint + test pass cancel); port: bench.cpu_baseline(10 s); "
+                     "(iteration 0's checkpoint + test pass cancel); port / dense_port: "
+                     "bench._time_adv_oracle(10 s) with the sparse / the reference's dense max-pool "
+                     "backward (bench.py's cpu_baseline times the dense one); "
                      f"median of {a.rounds} alternating rounds"}
     print(json.dumps(out, indent=1))
     if a.out:
