@@ -49,3 +49,14 @@ ab: $(SRC) $(HDR)
 	@mkdir -p build/ab
 	$(HIPCC) $(HIPFLAGS) $(ABDEFS) -shared -o build/ab/libA.so $(SRC) $(CPP) -lz
 .PHONY: ab
+
+# AddressSanitizer + UBSan host build of the HDF5 reader with a small driver
+# (tests/test_h5_asan.py feeds it truncated / corrupted files)
+ASAN_BIN := build/asan/h5check
+asan: $(ASAN_BIN)
+$(ASAN_BIN): $(PKG)/csrc/h5read.cpp tests/asan/h5check.cpp include/pcadv.h
+	@mkdir -p build/asan
+	g++ -std=c++17 -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer \
+	  -fno-sanitize-recover=undefined -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude \
+	  $(PKG)/csrc/h5read.cpp tests/asan/h5check.cpp -lz -o $@
+.PHONY: asan

@@ -33,6 +33,8 @@ int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float
                           const float*, const float*, const float*, const float*, const float*,
                           const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
                           hipStream_t, uint64_t* stamps = nullptr, int precision = 0);
+int launch_conv4_max(const float*, int, int, const float*, const float*, float*, int32_t*,
+                     hipStream_t, int);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t,
                       int add_identity_k = 0, float* mask_out = nullptr);
@@ -443,6 +445,11 @@ int pcadv_feat_fwd(const float* pts, int C, int N, const float* w1, const float*
                    void* workspace, size_t workspace_bytes, hipStream_t stream) {
   return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
                                nullptr, workspace, workspace_bytes, stream);
+}
+
+int pcadv_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4, float* gmax,
+                    int32_t* gidx, int precision, hipStream_t stream) {
+  return launch_conv4_max(x3, C, N, w4, b4, gmax, gidx, stream, precision);
 }
 
 int pcadv_feat_fwd_bf16(const float* pts, int C, int N, const float* w1, const float* b1,

@@ -734,11 +734,7 @@ size_t feat_fwd_workspace_bytes(int C, int N) {
 }
 
 template <int NP3, int NP4>
-static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split, int C, int N,
-                              const float* w1, const float* b1, const float* w2, const float* b2,
-                              const float* w3, const float* b3, const float* w4, const float* b4,
-                              float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter,
-                              hipStream_t s, uint64_t* stamps) {
+static int feat_fwd_attrs() {
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, false>),
@@ -758,6 +754,36 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
     }
     attr_set = true;
   }
+  return PCADV_OK;
+}
+
+// k_conv4_max alone over a given x3 (C x N x 128): the second launch of the
+// feature forward
+template <int NP3, int NP4>
+static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, const float* b4,
+                               float* gmax, int32_t* gidx, hipStream_t s, uint64_t* stamps) {
+  const int rc = feat_fwd_attrs<NP3, NP4>();
+  if (rc != PCADV_OK) return rc;
+  // two wave groups per 128-channel workgroup when 256-channel workgroups would
+  // leave CUs idle (the diagnostic stamps layout assumes the plain form)
+  if (4 * C < 256 && !stamps)
+    hipLaunchKernelGGL((k_conv4_max<NP4, true>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
+  else
+    hipLaunchKernelGGL((k_conv4_max<NP4, false>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
+  PC_HIP_CHECK_LAUNCH("k_conv4_max");
+  return PCADV_OK;
+}
+
+template <int NP3, int NP4>
+static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split, int C, int N,
+                              const float* w1, const float* b1, const float* w2, const float* b2,
+                              const float* w3, const float* b3, const float* w4, const float* b4,
+                              float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter,
+                              hipStream_t s, uint64_t* stamps) {
+  const int rc = feat_fwd_attrs<NP3, NP4>();
+  if (rc != PCADV_OK) return rc;
   const int T = (N + PM_P - 1) / PM_P;
   const int ntiles = C * T;
   uint64_t* mlp_stamps = stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr;
@@ -772,16 +798,16 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
                        s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3,
                        inc_counter, mlp_stamps);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
-  // two wave groups per 128-channel workgroup when 256-channel workgroups would
-  // leave CUs idle (the diagnostic stamps layout assumes the plain form)
-  if (4 * C < 256 && !stamps)
-    hipLaunchKernelGGL((k_conv4_max<NP4, true>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
-                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
-  else
-    hipLaunchKernelGGL((k_conv4_max<NP4, false>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
-                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
-  PC_HIP_CHECK_LAUNCH("k_conv4_max");
-  return PCADV_OK;
+  return launch_conv4_max_np<NP3, NP4>(x3, C, N, w4, b4, gmax, gidx, s, stamps);
+}
+
+int launch_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4, float* gmax,
+                     int32_t* gidx, hipStream_t s, int precision) {
+  PC_REQUIRE(C > 0 && N > 0, "conv4_max: bad shape C=%d N=%d", C, N);
+  PC_REQUIRE(precision == 0 || precision == 1, "conv4_max: precision %d (0 fp32, 1 bf16)",
+             precision);
+  if (precision == 1) return launch_conv4_max_np<1, 1>(x3, C, N, w4, b4, gmax, gidx, s, nullptr);
+  return launch_conv4_max_np<6, 3>(x3, C, N, w4, b4, gmax, gidx, s, nullptr);
 }
 
 // precision 0: f32-level (conv3 six bf16 products, conv4 three + the exact

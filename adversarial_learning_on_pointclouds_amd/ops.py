@@ -70,6 +70,30 @@ def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4, precision="fp32"):
     return gmax, gidx, x3
 
 
+def conv4_max(x3, w4, b4, precision="fp32", out=None):
+    """conv4 + max over points of given conv3 activations x3 (C, N, 128) ->
+    gmax (C, 1024), gidx (C, 1024) int32: pcadv_feat_fwd's second launch alone
+    (pcadv_conv4_max).  out: optional (gmax, gidx) to write into."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}")
+    lib = _lib.load()
+    _req(x3, "x3")
+    if x3.dim() != 3 or x3.shape[2] != 128:
+        raise ValueError(f"x3: expected (C, N, 128), got {tuple(x3.shape)}")
+    C, N, _ = x3.shape
+    w = _req(_mat(w4), "conv4.weight", (1024, 128))
+    _req(b4, "conv4.bias", (1024,))
+    if out is None:
+        out = (torch.empty(C, 1024, device=x3.device),
+               torch.empty(C, 1024, device=x3.device, dtype=torch.int32))
+    gmax, gidx = out
+    _req(gmax, "gmax", (C, 1024))
+    _req(gidx, "gidx", (C, 1024), torch.int32)
+    check(lib.pcadv_conv4_max(ptr(x3), C, N, ptr(w), ptr(b4), ptr(gmax), ptr(gidx),
+                              PRECISIONS[precision], stream_ptr()), "pcadv_conv4_max")
+    return gmax, gidx
+
+
 def feat_bwd(dgmax, gidx, pts, w1, b1, w2, b2, w3, w4, x3):
     """Gradients of (conv1..conv4) weights and biases given dL/dgmax."""
     lib = _lib.load()

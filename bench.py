@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--repeats", type=int, default=3,
+                    help="timed regions of --steps steps each; the median is reported")
     ap.add_argument("--points", type=int, default=1024,
                     help="points per cloud of the adv step (1024: the metric's config; 2048: "
                          "BASELINE configs[4]'s per-rank shape)")
@@ -241,6 +243,126 @@ def cpu_baseline_cls(seconds):
             "sample": f"{steps} numpy-oracle cls steps (B=32, N=1024, fp32) in {dt:.1f}s"}
 
 
+BF16_PEAK, F32_PEAK = 2500.0, 157.3  # dense TFLOP/s (MI355X_MICROARCH.md)
+
+
+def _pmc_traffic(pattern, prefixes, only_if=True):
+    """Bytes per launch (L2 -> memory, PMC FETCH_SIZE x 2 + WRITE_SIZE) of the
+    named kernels, summed, from the newest committed summary matching
+    profiles/<pattern> (tools/pmc_traffic.py), or (None, None)."""
+    if not only_if:
+        return None, None
+    prof = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    if not prof:
+        return None, None
+    kern = json.load(open(prof[-1]))["kernels"]
+    names = [next((k for k in kern if k.startswith(p)), None) for p in prefixes]
+    if not all(names):
+        return None, None
+    return round(sum(kern[n]["traffic_bytes"] for n in names)), os.path.relpath(prof[-1], REPO)
+
+
+def _graph_time(fn, reps=50):
+    """Average device time of fn() over `reps` back-to-back calls captured in
+    one HIP graph (as the kernels run inside the step graph), timed with HIP
+    events on the stream the graph is launched on (the current stream)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()  # warm
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    g.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / 1e3 / reps
+
+
+def feat_roofline(pts_all, fw, prec, traffic_pattern=None):
+    """The roofline block for the dominant kernel, k_conv4_max (conv4 + max over
+    points, models/pointnet.py:128-130), and the same figures for the feature
+    forward pair (k_point_mlp + k_conv4_max, conv1..conv4).  achieved = the
+    ALGORITHMIC f32 FLOPs of the launch (2 C N 128 1024 for conv4) over its
+    measured time, against the dense bf16 MFMA peak: the pipe these kernels
+    run on (fp32 mode emulates each f32 product with three bf16 split products
+    plus an exact f32 re-evaluation of every winner; bf16 mode one product).
+    issued_frac counts the MFMA work actually issued (split products)."""
+    from adversarial_learning_on_pointclouds_amd import ops
+    C, Np = int(pts_all.shape[0]), int(pts_all.shape[1])
+    gmax, gidx, x3 = ops.feat_fwd(pts_all, *fw, precision=prec)
+    pair_s = _graph_time(lambda: ops.feat_fwd(pts_all, *fw, precision=prec))
+    k2_s = _graph_time(lambda: ops.conv4_max(x3, fw[6], fw[7], precision=prec, out=(gmax, gidx)))
+    f4 = 2.0 * C * Np * 128 * 1024
+    f12 = 2.0 * C * Np * (3 * 64 + 64 * 64)
+    f3 = 2.0 * C * Np * 64 * 128
+    np3, np4 = (6, 3) if prec == "fp32" else (1, 1)  # bf16 products per f32 product
+    issued4 = np4 * f4
+    issued_pair = f12 * (BF16_PEAK / F32_PEAK) + np3 * f3 + np4 * f4
+    alg_bytes4 = C * Np * 128 * 4 + 1024 * 128 * 4 + C * 1024 * 8
+    alg_bytes_pair = C * Np * (3 + 128) * 4 + C * Np * 128 * 4 + C * 1024 * 8
+    traffic4, src = _pmc_traffic(traffic_pattern or "none", (f"pcadv::k_conv4_max<{np4}",),
+                                 traffic_pattern is not None)
+    traffic_pair, _ = _pmc_traffic(traffic_pattern or "none",
+                                   (f"pcadv::k_point_mlp<{np3}", f"pcadv::k_conv4_max<{np4}"),
+                                   traffic_pattern is not None)
+    ach4 = f4 / k2_s / 1e12
+    ach_pair = (f12 + f3 + f4) / pair_s / 1e12
+    return {
+        "bound": "mfma",
+        "kernel": f"k_conv4_max<{np4}> (conv4 128->1024 + max over points, {C} clouds x {Np} points)",
+        "achieved": round(ach4, 2), "peak": BF16_PEAK, "unit": "TFLOP/s",
+        "frac": round(ach4 / BF16_PEAK, 4),
+        "issued_frac": round(issued4 / k2_s / 1e12 / BF16_PEAK, 4),
+        "traffic": traffic4,
+        "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
+        "traffic_source": src,
+        "avg_launch_us": round(k2_s * 1e6, 2),
+        "algorithmic_flops_per_launch": f4,
+        "algorithmic_bytes_per_launch": alg_bytes4,
+        "issued_bf16_flops_per_launch": issued4,
+        "peak_basis": "dense bf16 MFMA 2500 TF (MI355X_MICROARCH.md), the pipe the kernel runs on; "
+                      "achieved = algorithmic f32 FLOPs / HIP-event launch time (graph of 50)",
+        "pair": {"kernel": f"k_point_mlp<{np3}> + k_conv4_max<{np4}> (conv1..conv4 + max)",
+                 "avg_us": round(pair_s * 1e6, 2), "achieved": round(ach_pair, 2),
+                 "frac": round(ach_pair / BF16_PEAK, 4),
+                 "issued_frac": round(issued_pair / pair_s / 1e12 / BF16_PEAK, 4),
+                 "algorithmic_flops": f12 + f3 + f4, "issued_bf16_equiv_flops": issued_pair,
+                 "algorithmic_bytes": alg_bytes_pair, "traffic": traffic_pair,
+                 "issued_note": "conv1-2's f32 FLOPs weighted 2500/157.3 (the f32 pipe's rate)"},
+    }
+
+
+def timed_regions(one, steps, repeats, dist=None):
+    """`repeats` timed regions of exactly `steps` steps, each bracketed by a
+    barrier + synchronize on both sides; returns the per-region seconds (max
+    over ranks)."""
+    out = []
+    for _ in range(repeats):
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            one(k)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([dt], device=torch.cuda.current_device(), dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out.append(dt)
+    return out
+
+
 def bench_cls(args):
     """BASELINE.json configs[1]: PointNetCls ModelNet40 B=32, N=1024, no
     discriminator - one run_training_pointnet_cls iteration per step
@@ -260,14 +382,15 @@ def bench_cls(args):
     graphs = [step.capture_on(*b) for b in pool]
     for k in range(args.warmup):
         graphs[k % POOL].replay()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        graphs[k % POOL].replay()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    regions = timed_regions(lambda k: graphs[k % POOL].replay(), args.steps, args.repeats)
+    dt = float(np.median(regions))
     gflop = 11.18  # algorithmic FLOPs of one cfg-2 step
     loss = float(step.losses[0].item())
+    fw = [model.feat.conv1.weight, model.feat.conv1.bias, model.feat.conv2.weight,
+          model.feat.conv2.bias, model.feat.conv3.weight, model.feat.conv3.bias,
+          model.feat.conv4.weight, model.feat.conv4.bias]
+    roof = feat_roofline(pool[(args.steps - 1) % POOL][0], fw, prec,
+                         "r*_cls_pmc_traffic.json" if prec == "bf16" else None)
     out = {
         "metric": "point-clouds/sec (cls train step, no discriminator), B=32 N=1024 ModelNet40, 1 GPU",
         "value": round(B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
@@ -281,6 +404,8 @@ def bench_cls(args):
         "config": {"workload": "run_training_pointnet_cls: PointNetCls(k=40), CE, Adam, B=32, "
                                "N=1024 (BASELINE configs[1])", "global_batch": B, "points": N,
                    "parallelism": "dp1", "hip_graph": True, "precision": prec},
+        "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
+        "roofline": roof,
         "step_flops": {"gflop_per_step": gflop,
                        "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
@@ -314,12 +439,8 @@ def bench_seg(args):
     graphs = [step.capture_on(*b) for b in pool]
     for k in range(args.warmup):
         graphs[k % 2].replay()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        graphs[k % 2].replay()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    regions = timed_regions(lambda k: graphs[k % 2].replay(), args.steps, args.repeats)
+    dt = float(np.median(regions))
     # algorithmic FLOPs per step (fc1's tiled part once per cloud;
     # sparse max backward): forward 2 N (3*64 + 64*128 + 2*128*128 + 128*512 +
     # 512*2048 + 960*256 + 256*256 + 256*128 + 128*50) per cloud, backward twice
@@ -376,20 +497,10 @@ def bench_seg(args):
     torch.cuda.synchronize()
     kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
     kflops = 2.0 * Bs * Ns * 512 * 2048
-    kpeak = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
     kissued = 3 * kflops  # three bf16 MFMA products per f32 product (hi/lo splits)
-    # HBM traffic of the same launch pair from the committed PMC passes of
-    # `bench.py --config seg` (tools/gpu_round.sh, tools/pmc_traffic.py)
-    traffic, traffic_src = None, None
-    here = os.path.dirname(os.path.abspath(__file__))
-    prof = sorted(glob.glob(os.path.join(here, "profiles", "r*_seg_pmc_traffic.json")))
-    if prof:
-        kern = json.load(open(prof[-1]))["kernels"]
-        names = ("pcadv::k_gemm_bf2_big<2>" if big else "pcadv::k_gemm_x3<2, 2, 2, 3>",
-                 "pcadv::k_max_combine")
-        if all(n in kern for n in names):
-            traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
-            traffic_src = os.path.relpath(prof[-1], here)
+    traffic, traffic_src = _pmc_traffic(
+        "r*_seg_pmc_traffic.json",
+        ("pcadv::k_gemm_bf2_big<2>" if big else "pcadv::k_gemm_x3<2, 2, 2, 3>", "pcadv::k_max_combine"))
     out = {
         "metric": "point-clouds/sec (seg train step), B=16 N=2048 ShapeNet-part, 1 GPU",
         "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
@@ -401,20 +512,22 @@ def bench_seg(args):
         "config": {"workload": "PointNetSeg(50) + CrossEntropyLoss + Adam, B=16, N=2048 "
                                "(BASELINE configs[3])", "global_batch": Bs, "points": Ns,
                    "parallelism": "dp1", "hip_graph": True},
+        "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
         "roofline": {"bound": "mfma",
                      "kernel": kname + " (conv6 512->2048 screened top-2 per 128-point tile) "
                                "+ k_max_combine (exact f32 re-evaluation)",
-                     "achieved": round(kissued / kern_s / 1e12, 2), "peak": kpeak,
-                     "unit": "TFLOP/s", "frac": round(kissued / kern_s / 1e12 / kpeak, 4),
+                     "achieved": round(kflops / kern_s / 1e12, 2), "peak": BF16_PEAK,
+                     "unit": "TFLOP/s", "frac": round(kflops / kern_s / 1e12 / BF16_PEAK, 4),
+                     "issued_frac": round(kissued / kern_s / 1e12 / BF16_PEAK, 4),
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
                      "traffic_source": traffic_src, "avg_launch_us": round(kern_s * 1e6, 2),
                      "algorithmic_flops_per_launch": kflops,
                      "algorithmic_bytes_per_launch": Bs * Ns * 512 * 4 + 2048 * 512 * 4 + Bs * 2048 * 8,
                      "issued_bf16_flops_per_launch": kissued,
-                     "fp32_equivalent_tflops": round(kflops / kern_s / 1e12, 2),
-                     "peak_basis": "dense bf16 MFMA 2500 TF; achieved = issued bf16 MFMA FLOPs "
-                                   "(3 split products per f32 product) / launch time"},
+                     "peak_basis": "dense bf16 MFMA 2500 TF, the pipe the kernel runs on; achieved = "
+                                   "algorithmic f32 FLOPs / launch time (issued_frac: the three "
+                                   "bf16 split products per f32 product)"},
         "step_flops": {"gflop_per_step": round(gflop, 2),
                        "achieved_tflops": round(gflop * args.steps / dt / 1e3, 2)},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
@@ -497,80 +610,22 @@ def main():
 
     for k in range(args.warmup):
         one(k)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one(k)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    regions = timed_regions(one, args.steps, args.repeats, dist)
+    dt = float(np.median(regions))
     losses = step.losses[:4].cpu().numpy().tolist()
     finite = all(np.isfinite(losses))
 
-    # dominant kernels: the PointNetfeat forward (k_point_mlp: conv1..conv3;
-    # k_conv4_max: conv4 + max with the exact re-evaluation), timed with HIP events on
-    # the stream they are launched on, same inputs as the step (the last resident batch).
-    # The pairs run back to back from one HIP graph, as they do inside the step graph
-    # (eager calls would add host launch gaps between pairs to the events' interval).
+    # dominant kernel k_conv4_max and the feature forward pair, timed with HIP
+    # events over the last resident batch (the step's 2B clouds)
     pg, lab, pn = pool[(args.steps - 1) % POOL]
     pts_all = torch.cat([pg, pn], 0).contiguous()
     fw = [model.feat.conv1.weight, model.feat.conv1.bias, model.feat.conv2.weight,
           model.feat.conv2.bias, model.feat.conv3.weight, model.feat.conv3.bias,
           model.feat.conv4.weight, model.feat.conv4.bias]
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(3):
-        ops.feat_fwd(pts_all, *fw, precision=adv_prec)
-    torch.cuda.synchronize()
-    reps = 50
-    pair_graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(pair_graph):
-        for _ in range(reps):
-            ops.feat_fwd(pts_all, *fw, precision=adv_prec)
-    pair_graph.replay()  # warm
-    torch.cuda.synchronize()
-    ev0.record()
-    pair_graph.replay()
-    ev1.record()
-    torch.cuda.synchronize()
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
-    # algorithmic f32 FLOPs of conv1..conv4 forward per launch (64 clouds x N points):
-    # 2 * N * (3*64 + 64*64 + 64*128 + 128*1024) per cloud
-    flops = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64 + 64 * 128 + 128 * 1024)
-    f32_equiv = flops / kern_s / 1e12
-    # The pair computes f32-level results on the matrix cores: conv1 (VALU) and
-    # conv2 (f32 MFMA) in f32, conv3 as six bf16 MFMA products of three-way
-    # splits, conv4 as three (hi/lo) plus the exact f32 re-evaluation of each
-    # winner.  Roofline against the named dense bf16 MFMA peak (MI355X_MICROARCH.md:
-    # 2.5 PF): the MFMA work issued, in bf16-MFMA-equivalent FLOPs (conv1-2's f32
-    # work weighted by the f32:bf16 peak ratio 2500/157.3), over the launch time.
-    BF16_PEAK, F32_PEAK = 2500.0, 157.3
-    f12 = 2.0 * (2 * B) * N * (3 * 64 + 64 * 64)
-    f3 = 2.0 * (2 * B) * N * (64 * 128)
-    f4 = flops - f12 - f3
-    np3, np4 = (6, 3) if adv_prec == "fp32" else (1, 1)  # bf16 products per f32 product
-    issued = f12 * (BF16_PEAK / F32_PEAK) + np3 * f3 + np4 * f4
-    achieved = issued / kern_s / 1e12
-    traffic, traffic_src = None, None
-    prof = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                     "profiles", "r*_pmc_traffic.json"))
-                  if "_seg_" not in os.path.basename(p))
-    if prof and N == 1024 and adv_prec == "fp32":  # the committed PMC passes ran the default workload
-        kern = json.load(open(prof[-1]))["kernels"]
-        # the fp32-mode instances (<6, 2> and <3, false>: the forms B = 32 runs)
-        names = [next((k for k in kern if k.startswith(p)), None)
-                 for p in ("pcadv::k_point_mlp<6", "pcadv::k_conv4_max<3")]
-        if all(names):
-            traffic = round(sum(kern[n]["traffic_bytes"] for n in names))
-            traffic_src = os.path.relpath(prof[-1], os.path.dirname(os.path.abspath(__file__)))
+    # the committed PMC passes ran the default workload (fp32, N = 1024)
+    roof = feat_roofline(pts_all, fw, adv_prec,
+                         "r*_pmc_traffic.json" if (N == 1024 and adv_prec == "fp32") else None)
+    pair = roof["pair"]
     # algorithmic FLOPs of one B=32 adversarial step (44.53 at N=2048)
     step_gflop = 22.47 if N == 1024 else 22.47 * N / 1024.0
     step_tf = step_gflop * world * args.steps / dt / 1e3
@@ -596,25 +651,15 @@ def main():
                    "parallelism": f"dp{world}", "hip_graph": use_graph},
         "world_size": world,
         "backend": ((_backend() if _backend() != "nccl" else "nccl (RCCL)") if world > 1 else None),
-        "roofline": {"bound": "mfma",
-                     "kernel": "k_point_mlp + k_conv4_max (PointNetfeat conv1..4 + max, 2 launches)",
-                     "achieved": round(achieved, 2), "peak": BF16_PEAK, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_PEAK, 4), "traffic": traffic,
-                     "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": 2 * B * N * (3 + 128) * 4 + 2 * B * 1024 * 8,
-                     "avg_launch_us": round(kern_s * 1e6, 2),
-                     "algorithmic_flops_per_launch": flops,
-                     "issued_bf16_equiv_flops_per_launch": issued,
-                     "peak_basis": "dense bf16 MFMA 2500 TF (MI355X_MICROARCH.md); achieved = issued "
-                                   "MFMA work in bf16-equivalent FLOPs: conv3 x6 and conv4 x3 split "
-                                   "products, conv1-2 f32 FLOPs x 2500/157.3",
-                     "fp32_equivalent": {
-                         "achieved_tflops": round(f32_equiv, 2), "f32_mfma_peak_tflops": F32_PEAK,
-                         "ratio_to_f32_peak": round(f32_equiv / F32_PEAK, 4),
-                         "note": "algorithmic f32 FLOPs / time; the f32 products are emulated on the "
-                                 "bf16 MFMA pipe (split operands, f32 accumulate, winners re-evaluated "
-                                 "in exact f32), so this ratio is not a roofline fraction and can exceed 1"}},
+        "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median",
+                   "per_region": "barrier + synchronize on both sides, max over ranks"},
+        "roofline": roof,
+        "fp32_equivalent": {
+            "kernel": "feature forward pair (conv1..conv4 + max)",
+            "achieved_tflops": pair["achieved"], "f32_mfma_peak_tflops": F32_PEAK,
+            "note": "algorithmic f32 FLOPs / time against the f32 MFMA peak; the f32 products are "
+                    "emulated on the bf16 pipe (split operands, f32 accumulate, winners "
+                    "re-evaluated in exact f32), so this is not a roofline fraction"},
         "step_flops": {"gflop_per_step": step_gflop, "achieved_tflops": round(step_tf, 2)},
         "losses_last_step": [round(v, 5) for v in losses],
         "finite": finite,

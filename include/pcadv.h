@@ -116,6 +116,13 @@ int pcadv_feat_fwd_bf16(const float* pts, int C, int N,
                         float* x3, float* gmax, int32_t* gidx,
                         void* workspace, size_t workspace_bytes, hipStream_t stream);
 
+/* The second launch of pcadv_feat_fwd alone: conv4 (128 -> 1024, no ReLU) +
+ * torch.max over the points (models/pointnet.py:128-130) of given conv3
+ * activations x3 [C][N][128] -> gmax, gidx [C][1024]; precision 0 = f32-level
+ * (as pcadv_feat_fwd), 1 = bf16 (as pcadv_feat_fwd_bf16). */
+int pcadv_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4,
+                    float* gmax, int32_t* gidx, int precision, hipStream_t stream);
+
 /* Bytes of workspace pcadv_feat_bwd needs for C clouds of N points. */
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N);
 

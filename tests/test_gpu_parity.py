@@ -123,6 +123,19 @@ def test_conv4_max_workgroup_forms_bitwise(precision, N):
         assert _argmax_ok(i32.cpu().numpy(), ra, r3, W4, G["feat.conv4.bias"]) == 0
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("C,N", [(64, 1024), (32, 1000), (3, 77)])
+def test_conv4_max_alone_equals_feat_fwd(precision, C, N):
+    """pcadv_conv4_max (the feature forward's second launch alone, the kernel
+    bench.py times as the dominant one) on feat_fwd's own x3 gives bitwise
+    feat_fwd's gmax / gidx."""
+    G = onp.make_params(onp.cls_spec(40), seed=61)
+    w = _feat_weights(G)
+    gmax, gidx, x3 = ops.feat_fwd(_t(_pts(62 + C, C, N)), *w, precision=precision)
+    g2, i2 = ops.conv4_max(x3, w[6], w[7], precision=precision)
+    assert torch.equal(gmax, g2) and torch.equal(gidx, i2)
+
+
 @pytest.mark.parametrize("C,N", [(4, 1024), (64, 1024), (3, 1000), (2, 300)])
 def test_feat_bwd_vs_oracle(C, N):
     G = onp.make_params(onp.cls_spec(40), seed=9)
