@@ -272,18 +272,19 @@ __device__ __forceinline__ int screen_key_asm(float v, int m_ord, int m_hi) {
       : "v"(v), "s"(m_ord), "s"(m_hi), "n"(LOWC));
   return t;
 }
-// push acc element I (row acc_row(I, 0) of the unit, plus 4 h) into a lane's top-2
-template <int I>
+// push acc element I (row acc_row(I, 0) of the unit, plus 4 h) into a lane's
+// top-2 (TOP2) or top-1 (bf16 mode, whose result is the screened winner itself)
+template <int I, bool TOP2>
 __device__ __forceinline__ void screen_one(const f32x16& acc, int m_ord, int m_hi, int& k1,
                                            int& k2) {
   const int key = screen_key_asm<31 - ((I & 3) + 8 * (I >> 2))>(acc[I], m_ord, m_hi);
-  k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1: v_med3_i32
+  if constexpr (TOP2) k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1: v_med3_i32
   k1 = max(k1, key);
 }
-template <int I0, int... J>
+template <int I0, bool TOP2, int... J>
 __device__ __forceinline__ void screen_seq(const f32x16& acc, int m_ord, int m_hi, int& k1,
                                            int& k2, std::integer_sequence<int, J...>) {
-  (screen_one<I0 + J>(acc, m_ord, m_hi, k1, k2), ...);
+  (screen_one<I0 + J, TOP2>(acc, m_ord, m_hi, k1, k2), ...);
 }
 __device__ __forceinline__ int key_row(int k) { return 31 - (k & 63); }
 __device__ __forceinline__ float key_value(int k) {
@@ -326,8 +327,15 @@ __device__ __forceinline__ bool ranks_before(float va, int ia, float vb, int ib)
 // running top-2 (r1 >= r2, tags t1, t2) of earlier steps.  Keys of different
 // steps compare by their truncated value only (the low bits are rows within a
 // step): on equal values the earlier step, i.e. the lower point index, stays.
+template <bool TOP2 = true>
 __device__ __forceinline__ void pair_merge(int n1, int u1, int n2, int u2, int& r1, int& t1,
                                            int& r2, int& t2) {
+  if constexpr (!TOP2) {  // top-1: the earlier step keeps equal truncated values
+    const bool a = (n1 & ~63) > (r1 & ~63);
+    r1 = a ? n1 : r1;
+    t1 = a ? u1 : t1;
+    return;
+  }
   const int m1 = n1 & ~63, m2 = n2 & ~63, q1 = r1 & ~63, q2 = r2 & ~63;
   const bool a = m1 > q1;
   const int sa = q1 >= m2 ? r1 : n2;
@@ -458,15 +466,15 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       if constexpr (decltype(MASKED)::value)
         if (u * 32 + acc_row(i, lane) >= N) continue;
       const int key = screen_key(acc[i], 31 - acc_row(i, 0));
-      k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1: v_med3_i32
+      if constexpr (NP4 == 3) k2 = max(min(key, k1), k2);  // median(key, k1, k2): v_med3_i32
       k1 = max(k1, key);
     }
   };
   // unmasked screening of acc elements [I, I + CNT) with the asm keys
   const int m_ord = 0x7fffffc0, m_hi = ~63;
   auto screen_fast = [&](const f32x16& acc, auto I, auto CNT, int& k1, int& k2) {
-    screen_seq<decltype(I)::value>(acc, m_ord, m_hi, k1, k2,
-                                   std::make_integer_sequence<int, decltype(CNT)::value>{});
+    screen_seq<decltype(I)::value, NP4 == 3>(acc, m_ord, m_hi, k1, k2,
+                                             std::make_integer_sequence<int, decltype(CNT)::value>{});
   };
 
   // Software pipeline over 32-point units (step s, half pt): the 24 MFMAs of a
@@ -544,7 +552,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) stage_load(s + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (decltype(SCREEN)::value) pair_merge(k1, uprev, k2, uprev, r1, t1, r2, t2);
+    if constexpr (decltype(SCREEN)::value) pair_merge<NP4 == 3>(k1, uprev, k2, uprev, r1, t1, r2, t2);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -588,11 +596,11 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     const int ul = 2 * (S - 1) + grp;
     if ((S - 1) & 1) screen_unit(accB, ul, T_{}, 0, 8, k1, k2);
     else screen_unit(accA, ul, T_{}, 0, 8, k1, k2);
-    pair_merge(k1, ul, k2, ul, r1, t1, r2, t2);
+    pair_merge<NP4 == 3>(k1, ul, k2, ul, r1, t1, r2, t2);
   } else {  // the last unit
     int k1 = KEY_NONE, k2 = KEY_NONE;
     screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2);
-    pair_merge(k1, 2 * S - 1, k2, 2 * S - 1, r1, t1, r2, t2);
+    pair_merge<NP4 == 3>(k1, 2 * S - 1, k2, 2 * S - 1, r1, t1, r2, t2);
   }
   STAMP(2);
 

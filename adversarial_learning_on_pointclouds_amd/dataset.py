@@ -247,10 +247,12 @@ class DeviceCloudLoader:
     def __len__(self):
         return self.n // self.B if self.drop_last else (self.n + self.B - 1) // self.B
 
-    def gather(self, idx, noise=None, out=None, _checked=False):
+    def gather(self, idx, noise=None, out=None, _checked=False, out_lab=None):
         """One batch for the device index tensor ``idx`` (int64, each in
         [0, len(dataset)): checked here, one host read; the epoch order of
-        __iter__ is in range by construction and skips it)."""
+        __iter__ is in range by construction and skips it).  ``out`` /
+        ``out_lab``: tensors to write the points (b, npts, 3) / labels (b, width)
+        into (a captured graph's static inputs)."""
         b = int(idx.numel())
         if idx.dtype != torch.int64 or idx.device != self.device or not idx.is_contiguous():
             raise ValueError("idx: contiguous int64 on the loader's device")
@@ -261,7 +263,12 @@ class DeviceCloudLoader:
                                  f"(min {int(lo)}, max {int(hi)})")
         pts = out if out is not None else torch.empty(b, self.npts, 3, device=self.device)
         lw = 0 if self.labels is None else int(self.labels.shape[1])
-        lab = None if self.labels is None else torch.empty(b, lw, device=self.device, dtype=torch.int64)
+        lab = None
+        if self.labels is not None:
+            lab = out_lab if out_lab is not None else torch.empty(b, lw, device=self.device,
+                                                                  dtype=torch.int64)
+            if tuple(lab.shape) != (b, lw) or lab.dtype != torch.int64 or not lab.is_contiguous():
+                raise ValueError(f"out_lab: expected contiguous int64 ({b}, {lw})")
         seg = None if self.segs is None else torch.empty(b, self.npts, device=self.device,
                                                          dtype=torch.int64)
         nz = None
@@ -286,11 +293,16 @@ class DeviceCloudLoader:
         oh.scatter_(2, lab[:, :1].unsqueeze(1), 1.0)
         return (pts, oh, seg) if self.kind == "shapenet_gt" else (pts, oh)
 
-    def __iter__(self):
+    def index_batches(self):
+        """The index slices of one epoch, in the order __iter__ gathers them
+        (a fresh permutation from the loader's generator when shuffling)."""
         if self.shuffle:
             order = torch.randperm(self.n, device=self.device, generator=self.gen)
         else:
             order = torch.arange(self.n, device=self.device)
         for k in range(len(self)):
-            idx = order[k * self.B:(k + 1) * self.B].contiguous()
-            yield self.gather(idx, _checked=True)
+            yield order[k * self.B:(k + 1) * self.B]
+
+    def __iter__(self):
+        for idx in self.index_batches():
+            yield self.gather(idx.contiguous(), _checked=True)

@@ -11,6 +11,7 @@ loop body op by op over the same HIP kernels through autograd.
 """
 from __future__ import annotations
 
+import collections
 import os
 
 import numpy as np
@@ -62,6 +63,131 @@ def _next(loader, it):
     return batch, it
 
 
+class _AsyncLossLog:
+    """The per-iteration loss lines of the training loops (utils/trainer.py:
+    561-572) without a host sync per iteration: a logged iteration's device
+    loss vector is copied to pinned host memory behind an event, and the lines
+    are emitted in iteration order once their copies have landed (polled every
+    iteration, drained before test passes, checkpoints and at the end).  The
+    lines and scalars are the reference's, only written a few iterations late."""
+
+    def __init__(self, emit, depth=256):
+        self.emit, self.depth = emit, depth
+        self.pending = collections.deque()
+        self.free = []
+
+    def push(self, i_iter, dev_vals, extra=None):
+        buf = self.free.pop() if self.free else torch.empty(dev_vals.numel(), pin_memory=True)
+        buf.copy_(dev_vals, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((i_iter, buf, ev, extra))
+        self.poll()
+        while len(self.pending) > self.depth:
+            self._pop(block=True)
+
+    def emit_now(self, i_iter, vals, extra=None):
+        self.drain()
+        self.emit(i_iter, vals, extra)
+
+    def _pop(self, block):
+        i_iter, buf, ev, extra = self.pending[0]
+        if not block and not ev.query():
+            return False
+        ev.synchronize()
+        self.pending.popleft()
+        self.emit(i_iter, buf.tolist(), extra)
+        self.free.append(buf)
+        return True
+
+    def poll(self):
+        while self.pending and self._pop(block=False):
+            pass
+
+    def drain(self):
+        while self.pending:
+            self._pop(block=True)
+
+
+class _IndexCursor:
+    """Index slices of a DeviceCloudLoader in the order the trainer's _next
+    would gather them: epoch after epoch, each a fresh pass of the loader's
+    own index_batches() (the same generator draws as iterating it)."""
+
+    def __init__(self, loader):
+        self.loader = loader
+        self.it = loader.index_batches()
+
+    def next(self):
+        try:
+            return next(self.it)
+        except StopIteration:
+            self.it = self.loader.index_batches()
+            return next(self.it)
+
+
+class _GraphedIteration:
+    """One training iteration fed by DeviceCloudLoaders as ONE HIP graph: each
+    loader's gather (+ device jitter) into static input buffers, then the
+    fused step.  Per iteration the host copies the loaders' index slices into
+    static index buffers and replays (graphs per `semi` flag, captured on first
+    use; the capture's warm-up leaves parameters, Adam state and the loaders'
+    RNG counters as they were)."""
+
+    def __init__(self, step, loaders, lab_width=1):
+        self.step, self.loaders = step, loaders
+        B, N, dev = step.B, step.N, step.device
+        self.B = B
+        self.idx = [torch.zeros(B, dtype=torch.int64, device=dev) for _ in loaders]
+        self.pts = [torch.zeros(B, N, 3, device=dev) for _ in loaders]
+        self.lab = torch.zeros(B, lab_width, dtype=torch.int64, device=dev)
+        self.graphs = {}
+
+    def _body(self, semi):
+        for k, ld in enumerate(self.loaders):
+            ld.gather(self.idx[k], out=self.pts[k], out_lab=self.lab if k == 0 else None,
+                      _checked=True)
+        if len(self.loaders) == 2:
+            self.step(self.pts[0], self.lab[:, 0], self.pts[1], semi=semi)
+        else:
+            self.step(self.pts[0], self.lab[:, 0])
+
+    def _graph(self, semi):
+        g = self.graphs.get(semi)
+        if g is None:
+            st = self.step
+            state = [t for t in (getattr(st, n, None) for n in
+                                 ("g_param", "g_m", "g_v", "d_param", "d_m", "d_v", "step_count"))
+                     if t is not None] + [ld.step for ld in self.loaders]
+            saved = [t.clone() for t in state]
+            cur = torch.cuda.current_stream()
+            side = torch.cuda.Stream(device=st.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):  # warm-up outside the capture
+                self._body(semi)
+            cur.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body(semi)
+            torch.cuda.synchronize()
+            for dst, src in zip(state, saved):
+                dst.copy_(src)
+            self.graphs[semi] = g
+        return g
+
+    def run(self, idx_slices, semi=False):
+        for buf, ix in zip(self.idx, idx_slices):
+            buf.copy_(ix)
+        self._graph(semi).replay()
+        return self.step.losses
+
+
+def _device_loaders(*loaders):
+    from .dataset import DeviceCloudLoader
+    return all(isinstance(l, DeviceCloudLoader) and l.kind in ("modelnet_gt", "modelnet_nogt")
+               for l in loaders)
+
+
 def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pools, args):
     if not (isinstance(model, PointNetCls) and isinstance(model_D, DeepConvDiscNet)):
         return False
@@ -102,7 +228,15 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
               history_pool_gt, history_pool_nogt, train_logger, test_logger, writer, args,
               semi_loss=None):
     """The iteration loop shared by run_training (semi_loss None) and
-    run_training_semi (pseudo-label term from iteration semi_start + 1)."""
+    run_training_semi (pseudo-label term from iteration semi_start + 1).
+
+    Fast path: with the hot path's configuration (see _fusable) every
+    iteration whose GT and no-GT batches have the same shape is one fused
+    native step; when both loaders are DeviceCloudLoaders the batch gathers
+    and the step replay as one HIP graph per iteration (args.use_graph, default
+    on), fed by the loaders' own epoch orders.  Loss lines are read
+    asynchronously (no host sync per iteration), every args.log_every
+    iterations (default 1, as the reference logs every iteration)."""
     gt_label, nogt_label = 1, 0
     max_test_accu = float("-inf")
     max_train_epoch = 0
@@ -111,36 +245,76 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
     if semi_loss is not None:
         fused = fused and _semi_fusable(semi_loss)
     step = None
-    log_every = int(getattr(args, "log_every", 1))
+    log_every = max(1, int(getattr(args, "log_every", 1)))
+    graphed = (fused and bool(getattr(args, "use_graph", True))
+               and _device_loaders(trainloader_gt, trainloader_nogt)
+               and trainloader_gt.B == trainloader_nogt.B
+               and trainloader_gt.npts == trainloader_nogt.npts
+               and trainloader_gt.B <= MAX_FUSED_B)
+    gi = None
+    if graphed:  # the loaders' own epoch orders replace the (fresh) iterators given
+        cur_gt, cur_ng = _IndexCursor(trainloader_gt), _IndexCursor(trainloader_nogt)
+    tb = getattr(args, "tensorboard", False) and writer is not None
+
+    def emit(i_iter, vals, semi_on):
+        loss_D_value = vals[2] + vals[3]
+        train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss_adv = {3:.3f} "
+                          "loss_D = {4:.3f}".format(i_iter, args.total_iterations, vals[0],
+                                                    vals[1], loss_D_value))
+        if tb:
+            writer.add_scalar("Loss/train_cls", vals[0], i_iter)
+            writer.add_scalar("Loss/train_adv", vals[1], i_iter)
+            writer.add_scalar("Loss/train_disc", loss_D_value, i_iter)
+            if semi_loss is not None:
+                writer.add_scalar("Loss/train_semi", vals[4] if semi_on else 0.0, i_iter)
+
+    log = _AsyncLossLog(emit)
+
+    def fused_step(B, N):
+        nonlocal step
+        if step is None or step.N != N or step.B < B:
+            if step is not None:  # the replacement adopts the Adam state: count included
+                step.sync_optimizer_state()
+            step = AdvTrainStep(model, model_D, B, N,
+                                optimizer=optimizer, optimizer_D=optimizer_D,
+                                lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
+                                seed=int(getattr(args, "seed", 0)) + i_iter,
+                                device=args.device,
+                                lambda_semi=float(getattr(args, "lambda_semi", 1.0)),
+                                semi_th=float(getattr(args, "semi_TH", 0.8)))
+        return step
 
     for i_iter in range(args.total_iterations):
         model.train()
         model_D.train()
-        batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
-        pts, cls = batch
-        pts_nogt, targetloader_nogt_iter = _next(trainloader_nogt, targetloader_nogt_iter)
-        pts = pts.float().to(args.device).contiguous()
-        cls = cls.long().to(args.device).contiguous()
-        pts_nogt = pts_nogt.float().to(args.device).contiguous()
         semi_on = semi_loss is not None and args.semi_start > 0 and i_iter > args.semi_start
+        losses = None
+        if graphed:
+            ig, ing = cur_gt.next(), cur_ng.next()
+            if ig.numel() == trainloader_gt.B and ing.numel() == trainloader_nogt.B:
+                st = fused_step(trainloader_gt.B, trainloader_gt.npts)
+                if gi is None or gi.step is not st:
+                    gi = _GraphedIteration(st, (trainloader_gt, trainloader_nogt))
+                losses = gi.run((ig, ing), semi=semi_on)
+            else:  # a ragged last batch: gathered eagerly
+                pts, cls = trainloader_gt.gather(ig.contiguous(), _checked=True)
+                pts_nogt = trainloader_nogt.gather(ing.contiguous(), _checked=True)
+        else:
+            batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
+            pts, cls = batch
+            pts_nogt, targetloader_nogt_iter = _next(trainloader_nogt, targetloader_nogt_iter)
+        if losses is None:
+            pts = pts.float().to(args.device).contiguous()
+            cls = cls.long().to(args.device).contiguous()
+            pts_nogt = pts_nogt.float().to(args.device).contiguous()
+            if fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B:
+                losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls, pts_nogt, semi=semi_on)
 
-        if fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B:
-            if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
-                if step is not None:  # the replacement adopts the Adam state: count included
-                    step.sync_optimizer_state()
-                step = AdvTrainStep(model, model_D, pts.shape[0], pts.shape[1],
-                                    optimizer=optimizer, optimizer_D=optimizer_D,
-                                    lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
-                                    seed=int(getattr(args, "seed", 0)) + i_iter,
-                                    device=args.device,
-                                    lambda_semi=float(getattr(args, "lambda_semi", 1.0)),
-                                    semi_th=float(getattr(args, "semi_TH", 0.8)))
-            losses = step(pts, cls, pts_nogt, semi=semi_on)
-            vals = losses.tolist() if (i_iter % log_every == 0) else None
-            if vals is not None:
-                loss_cls_value, loss_adv_value = vals[0], vals[1]
-                loss_D_value = vals[2] + vals[3]
-                loss_semi_value = vals[4] if semi_on else 0.0
+        if losses is not None:
+            if i_iter % log_every == 0:
+                log.push(i_iter, losses, semi_on)
+            else:
+                log.poll()
         else:
             # unequal GT / no-GT batches (a loader's ragged last batch): the
             # reference's body through autograd over the same kernels; the torch
@@ -182,23 +356,12 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             optimizer_D.step()
             if step is not None:
                 step.after_torch_step()
-            vals = True
-            loss_cls_value, loss_adv_value = l.item(), loss_adv.item()
-            loss_D_value = loss_D1.item() + loss_D2.item()
-
-        if vals is not None:
-            train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss_adv = {3:.3f} "
-                              "loss_D = {4:.3f}".format(i_iter, args.total_iterations,
-                                                        loss_cls_value, loss_adv_value,
-                                                        loss_D_value))
-            if getattr(args, "tensorboard", False) and writer is not None:
-                writer.add_scalar("Loss/train_cls", loss_cls_value, i_iter)
-                writer.add_scalar("Loss/train_adv", loss_adv_value, i_iter)
-                writer.add_scalar("Loss/train_disc", loss_D_value, i_iter)
-                if semi_loss is not None:
-                    writer.add_scalar("Loss/train_semi", loss_semi_value, i_iter)
+            if i_iter % log_every == 0:
+                log.emit_now(i_iter, [l.item(), loss_adv.item(), loss_D1.item(), loss_D2.item(),
+                                      loss_semi_value], semi_on)
 
         if i_iter % args.iter_save_epoch == 0:
+            log.drain()
             if step is not None:
                 step.sync_optimizer_state()
             if semi_loss is None:
@@ -207,12 +370,14 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                 tag = int(round(i_iter / len(trainloader_gt)))
             _save(model, model_D, args, "train_epoch_{}".format(tag))
         if i_iter % args.iter_test_epoch == 0:
+            log.drain()
             curr_accu, _ = run_testing(testloader, model, cls_loss, test_logger, i_iter, writer, args)
             if max_test_accu < curr_accu:
                 max_test_accu = curr_accu
                 max_train_epoch = i_iter // args.iter_test_epoch
                 _save(model, model_D, args, "train_best")
 
+    log.drain()
     if step is not None:
         step.sync_optimizer_state()
     if getattr(args, "tensorboard", False) and writer is not None:
@@ -265,20 +430,53 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
              and cls_loss.reduction == "mean" and cls_loss.label_smoothing == 0.0
              and str(args.device).split(":")[0] == "cuda")
     step = None
+    graphed = (fused and bool(getattr(args, "use_graph", True)) and _device_loaders(trainloader_gt)
+               and trainloader_gt.B <= MAX_FUSED_B)
+    gi = None
+    if graphed:
+        cursor = _IndexCursor(trainloader_gt)
+    log_every = max(1, int(getattr(args, "log_every", 1)))
+
+    def emit(i_iter, vals, regu):
+        train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
+            i_iter, args.total_iterations, vals[0], regu))
+
+    log = _AsyncLossLog(emit)
+
+    def fused_step(B, N):
+        nonlocal step
+        if step is None or step.N != N or step.B < B:
+            if step is not None:
+                step.sync_optimizer_state()
+            step = ClsTrainStep(model, B, N, optimizer=optimizer, lambda_cls=args.lambda_cls,
+                                seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)
+        return step
+
     for i_iter in range(args.total_iterations):
         model.train()
-        batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
-        pts, cls = batch
-        pts, cls = pts.float().to(args.device).contiguous(), cls.long().to(args.device).contiguous()
         l_regu = None
-        if fused and pts.shape[0] <= MAX_FUSED_B:
-            if step is None or step.N != pts.shape[1] or step.B < pts.shape[0]:
-                if step is not None:
-                    step.sync_optimizer_state()
-                step = ClsTrainStep(model, pts.shape[0], pts.shape[1], optimizer=optimizer,
-                                    lambda_cls=args.lambda_cls,
-                                    seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)
-            l_value = float(step(pts, cls)[0].item())
+        losses = None
+        if graphed:
+            ix = cursor.next()
+            if ix.numel() == trainloader_gt.B:
+                st = fused_step(trainloader_gt.B, trainloader_gt.npts)
+                if gi is None or gi.step is not st:
+                    gi = _GraphedIteration(st, (trainloader_gt,))
+                losses = gi.run((ix,))
+            else:
+                pts, cls = trainloader_gt.gather(ix.contiguous(), _checked=True)
+        else:
+            batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
+            pts, cls = batch
+        if losses is None:
+            pts, cls = pts.float().to(args.device).contiguous(), cls.long().to(args.device).contiguous()
+            if fused and pts.shape[0] <= MAX_FUSED_B:
+                losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls)
+        if losses is not None:
+            if i_iter % log_every == 0:
+                log.push(i_iter, losses, 0.0)
+            else:
+                log.poll()
         else:
             if step is not None:
                 step.sync_optimizer_state()
@@ -293,20 +491,22 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
             optimizer.step()
             if step is not None:
                 step.after_torch_step()
-            l_value = l.item()
-        train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
-            i_iter, args.total_iterations, l_value, 0.0 if l_regu is None else l_regu.item()))
+            if i_iter % log_every == 0:
+                log.emit_now(i_iter, [l.item()], 0.0 if l_regu is None else l_regu.item())
         if i_iter % args.iter_save_epoch == 0:
+            log.drain()
             if step is not None:
                 step.sync_optimizer_state()
             torch.save(model.state_dict(), os.path.join(
                 args.exp_dir, "model_train_epoch_{}.pth".format(i_iter // len(trainloader_gt))))
         if i_iter % args.iter_test_epoch == 0:
+            log.drain()
             curr_accu, _ = run_testing(testloader, model, cls_loss, test_logger, i_iter, writer, args)
             if max_test_accu < curr_accu:
                 max_test_accu = curr_accu
                 max_train_epoch = i_iter // args.iter_test_epoch
                 torch.save(model.state_dict(), os.path.join(args.exp_dir, "model_train_best.pth"))
+    log.drain()
     if step is not None:
         step.sync_optimizer_state()
     train_logger.info("Max test accuracy: {:.4f}".format(max_test_accu))

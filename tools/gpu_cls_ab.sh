@@ -8,6 +8,6 @@ for i in 1 2 3; do
   for v in A B; do
     if [ $v = A ]; then lib=build/ab/libA.so; else lib=adversarial_learning_on_pointclouds_amd/lib/libpcadv.so; fi
     PCADV_LIB=$lib timeout -k 10 200 python bench.py --config cls --steps 300 --warmup 30 --no-cpu > gpurun_out/cab_$v$i.log 2>&1 || { echo "bench $v failed"; exit 1; }
-    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if '\"metric\"' in l][-1]); print('$v', d['ms_per_step'])" gpurun_out/cab_$v$i.log
+    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if '\"metric\"' in l][-1]); print('$v', d['ms_per_step'], d.get('roofline', {}).get('avg_launch_us'), d.get('roofline', {}).get('pair', {}).get('avg_us'))" gpurun_out/cab_$v$i.log
   done
 done
