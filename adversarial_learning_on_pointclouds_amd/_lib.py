@@ -118,6 +118,9 @@ SIGNATURES = {
     "pcadv_gather_clouds": (_i, [_vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, ctypes.c_double,
                                  ctypes.c_double, _vp, _u64, _vp,
                                  _vp, _vp, _vp, _vp]),
+    "pcadv_gather_clouds_at": (_i, [_vp, _i64, _i, _i, _vp, _vp, _i, _vp, _i, _vp, ctypes.c_double,
+                                    ctypes.c_double, _u64, _vp, _vp, _vp, _vp, _vp]),
+    "pcadv_iter_epilogue": (_i, [_vp, _i, _vp, _i, _vp, _i, _vp, _vp]),
     "pcadv_row_ce_workspace_bytes": (_sz, [_i]),
     "pcadv_row_ce": (_i, [_vp, _i64, _vp, _i, _i, _f, _vp, _vp, _vp, _sz, _vp]),
     "pcadv_adv_step_workspace_bytes": (_sz, [_i, _i]),

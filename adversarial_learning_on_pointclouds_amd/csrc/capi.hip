@@ -95,7 +95,8 @@ int launch_cmx_bwd(const float*, const float*, const int32_t*, const float*, lon
                    int, int, const float*, float*, float*, float*, long long, int, hipStream_t);
 int launch_gather_clouds(const float*, int64_t, int, int, const int64_t*, int, const int64_t*, int,
                          const int64_t*, double, double, const double*, uint64_t, const int32_t*,
-                         float*, int64_t*, int64_t*, hipStream_t);
+                         float*, int64_t*, int64_t*, hipStream_t, const int32_t* cursor = nullptr);
+int launch_iter_epilogue(int32_t*, int, const float*, int, float*, int, int32_t*, hipStream_t);
 size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
                   size_t, hipStream_t);
@@ -657,6 +658,22 @@ int pcadv_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
                         int64_t* out_seg, hipStream_t stream) {
   return launch_gather_clouds(src, n_src, npts, src_npts, idx, B, src_lab, lab_width, src_seg,
                               sigma, clip, noise, seed, step, out, out_lab, out_seg, stream);
+}
+
+int pcadv_gather_clouds_at(const float* src, int64_t n_src, int npts, int src_npts,
+                           const int64_t* order, const int32_t* cursor, int B,
+                           const int64_t* src_lab, int lab_width, const int64_t* src_seg,
+                           double sigma, double clip, uint64_t seed, const int32_t* step,
+                           float* out, int64_t* out_lab, int64_t* out_seg, hipStream_t stream) {
+  PC_REQUIRE(cursor, "gather_clouds_at: cursor required");
+  return launch_gather_clouds(src, n_src, npts, src_npts, order, B, src_lab, lab_width, src_seg,
+                              sigma, clip, nullptr, seed, step, out, out_lab, out_seg, stream,
+                              cursor);
+}
+
+int pcadv_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl,
+                        float* ring, int slots, int32_t* ring_count, hipStream_t stream) {
+  return launch_iter_epilogue(counters, ncounters, losses, nl, ring, slots, ring_count, stream);
 }
 
 size_t pcadv_row_ce_workspace_bytes(int M) { return row_ce_workspace_bytes(M); }

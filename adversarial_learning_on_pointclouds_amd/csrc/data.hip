@@ -22,11 +22,12 @@ k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_
                 int lab_width, const int64_t* __restrict__ src_seg, double sigma_d, double clip_d,
                 const double* __restrict__ noise, uint64_t seed, const int32_t* __restrict__ step,
                 float* __restrict__ out, int64_t* __restrict__ out_lab,
-                int64_t* __restrict__ out_seg) {
+                int64_t* __restrict__ out_seg, const int32_t* __restrict__ cursor) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)B * npts) return;
   const int b = (int)(t / npts), p = (int)(t % npts);
-  const int64_t c = idx[b];
+  // cursor: batch k = *cursor of an epoch order held in idx (a graph-fed loader)
+  const int64_t c = idx[(cursor ? (int64_t)*cursor * B : 0) + b];
   // DeviceCloudLoader.gather() rejects out-of-range indices on the host before
   // the launch (its own epoch order is in range by construction); this guard
   // only keeps a bad index from reading outside the split
@@ -69,7 +70,7 @@ int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts
                          const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
                          const int64_t* src_seg, double sigma, double clip, const double* noise,
                          uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
-                         int64_t* out_seg, hipStream_t s) {
+                         int64_t* out_seg, hipStream_t s, const int32_t* cursor) {
   PC_REQUIRE(src && idx && out && n_src > 0 && B > 0 && npts > 0 && src_npts >= npts,
              "gather_clouds: bad arguments (n_src=%lld B=%d npts=%d src_npts=%d)",
              (long long)n_src, B, npts, src_npts);
@@ -79,8 +80,36 @@ int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts
   const int64_t n = (int64_t)B * npts;
   hipLaunchKernelGGL(k_gather_clouds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src,
                      n_src, npts, src_npts, idx, B, src_lab, lab_width, src_seg, sigma, clip, noise,
-                     seed, step, out, out_lab, out_seg);
+                     seed, step, out, out_lab, out_seg, cursor);
   PC_HIP_CHECK_LAUNCH("k_gather_clouds");
+  return PCADV_OK;
+}
+
+// The end of a graph-replayed training iteration: every counter += 1 (the
+// loaders' RNG steps and batch cursors) and the step's loss vector into slot
+// (*ring_count % slots) of a loss ring, *ring_count += 1.  One wave.
+__global__ void __launch_bounds__(64)
+k_iter_epilogue(int32_t* __restrict__ counters, int ncounters, const float* __restrict__ losses,
+                int nl, float* __restrict__ ring, int slots, int32_t* __restrict__ ring_count) {
+  const int t = threadIdx.x;
+  if (ring && ring_count) {
+    const int slot = (int)((uint32_t)*ring_count % (uint32_t)slots);
+    if (t < nl) ring[(size_t)slot * nl + t] = losses[t];
+  }
+  if (t < ncounters) counters[t] += 1;
+  __syncthreads();  // every lane has read *ring_count
+  if (t == 0 && ring && ring_count) *ring_count += 1;
+}
+
+int launch_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl, float* ring,
+                         int slots, int32_t* ring_count, hipStream_t s) {
+  PC_REQUIRE(ncounters >= 0 && ncounters <= 64 && (ncounters == 0 || counters),
+             "iter_epilogue: %d counters (at most 64)", ncounters);
+  PC_REQUIRE(!ring || (ring_count && losses && nl > 0 && nl <= 64 && slots > 0),
+             "iter_epilogue: bad loss ring (nl=%d slots=%d)", nl, slots);
+  hipLaunchKernelGGL(k_iter_epilogue, dim3(1), dim3(64), 0, s, counters, ncounters, losses, nl,
+                     ring, slots, ring_count);
+  PC_HIP_CHECK_LAUNCH("k_iter_epilogue");
   return PCADV_OK;
 }
 

@@ -265,6 +265,11 @@ __device__ __forceinline__ int screen_key(float v, int lowc) {
 template <int LOWC>
 __device__ __forceinline__ int screen_key_asm(float v, int m_ord, int m_hi) {
   int t;
+#if PCADV_C4_DIAG & 4  // diagnostic builds only: one instruction, order wrong for negative values
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=&v"(t) : "v"(v), "s"(m_hi), "n"(LOWC));
+  (void)m_ord;
+  return t;
+#endif
   asm("v_ashrrev_i32 %0, 31, %1\n\t"
       "v_bitop3_b32 %0, %1, %0, %2 bitop3:0x78\n\t"
       "v_bitop3_b32 %0, %0, %3, %4 bitop3:0xea"

@@ -293,15 +293,33 @@ class DeviceCloudLoader:
         oh.scatter_(2, lab[:, :1].unsqueeze(1), 1.0)
         return (pts, oh, seg) if self.kind == "shapenet_gt" else (pts, oh)
 
-    def index_batches(self):
-        """The index slices of one epoch, in the order __iter__ gathers them
-        (a fresh permutation from the loader's generator when shuffling)."""
+    def epoch_order(self):
+        """One epoch's order of the split: a fresh permutation from the loader's
+        generator when shuffling (what __iter__ draws at the start of an epoch)."""
         if self.shuffle:
-            order = torch.randperm(self.n, device=self.device, generator=self.gen)
-        else:
-            order = torch.arange(self.n, device=self.device)
+            return torch.randperm(self.n, device=self.device, generator=self.gen)
+        return torch.arange(self.n, device=self.device)
+
+    def index_batches(self):
+        """The index slices of one epoch, in the order __iter__ gathers them."""
+        order = self.epoch_order()
         for k in range(len(self)):
             yield order[k * self.B:(k + 1) * self.B]
+
+    def gather_at(self, order, cursor, out, out_lab=None):
+        """Batch *cursor (device int32) of the epoch order `order` (int64, on the
+        device) into `out` / `out_lab`: the graph-replayed form of gather (no
+        host copy per batch).  The step counter is NOT advanced here: the
+        caller advances it and the cursor (pcadv_iter_epilogue)."""
+        lw = 0 if self.labels is None else int(self.labels.shape[1])
+        if out_lab is None and self.labels is not None:
+            raise ValueError("gather_at: out_lab required for a labelled split")
+        P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        check(self.lib.pcadv_gather_clouds_at(P(self.pts), self.n, self.npts, self.npts, P(order),
+                                              P(cursor), self.B, P(self.labels), lw, None,
+                                              self.sigma, self.clip, self.seed, P(self.step),
+                                              P(out), P(out_lab), None, stream_ptr()),
+              "pcadv_gather_clouds_at")
 
     def __iter__(self):
         for idx in self.index_batches():

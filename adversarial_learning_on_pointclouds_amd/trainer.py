@@ -63,94 +63,147 @@ def _next(loader, it):
     return batch, it
 
 
-class _AsyncLossLog:
+class _LossRing:
     """The per-iteration loss lines of the training loops (utils/trainer.py:
-    561-572) without a host sync per iteration: a logged iteration's device
-    loss vector is copied to pinned host memory behind an event, and the lines
-    are emitted in iteration order once their copies have landed (polled every
-    iteration, drained before test passes, checkpoints and at the end).  The
-    lines and scalars are the reference's, only written a few iterations late."""
+    561-572) without a host sync per iteration.  Each fused iteration's device
+    loss vector goes into slot (count % slots) of a device ring
+    (pcadv_iter_epilogue: inside the iteration's graph when it is replayed);
+    every slots / 2 iterations one asynchronous copy of the ring to pinned
+    host memory is queued, and the lines are emitted in iteration order once
+    a copy has landed (polled every iteration; drained before test passes,
+    checkpoints, autograd iterations and at the end).  The lines and scalars
+    are the reference's, written a few iterations late."""
 
-    def __init__(self, emit, depth=256):
-        self.emit, self.depth = emit, depth
-        self.pending = collections.deque()
+    def __init__(self, emit, nl, device, slots=64):
+        from . import _lib
+        self.lib = _lib.load()
+        self.emit, self.nl, self.slots, self.half = emit, nl, slots, slots // 2
+        self.ring = torch.zeros(slots, nl, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.n_written = 0          # host mirror of *count
+        self.pending = []           # (slot, i_iter, extra) written, not yet copied
+        self.inflight = collections.deque()
         self.free = []
 
-    def push(self, i_iter, dev_vals, extra=None):
-        buf = self.free.pop() if self.free else torch.empty(dev_vals.numel(), pin_memory=True)
-        buf.copy_(dev_vals, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.pending.append((i_iter, buf, ev, extra))
+    def write(self, losses, counters=None, ncounters=0):
+        """Enqueue the epilogue: losses -> ring slot, counters[0:ncounters] += 1."""
+        from ._lib import check, stream_ptr
+        import ctypes
+        P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        check(self.lib.pcadv_iter_epilogue(P(counters), ncounters, P(losses), self.nl,
+                                           P(self.ring), self.slots, P(self.count), stream_ptr()),
+              "pcadv_iter_epilogue")
+
+    def record(self, i_iter, extra, log=True):
+        """After each fused iteration (its epilogue wrote the next slot)."""
+        slot = self.n_written % self.slots
+        self.n_written += 1
+        if log:
+            self.pending.append((slot, i_iter, extra))
+        if self.n_written % self.half == 0:
+            self.flush()
         self.poll()
-        while len(self.pending) > self.depth:
+
+    def flush(self):
+        if not self.pending:
+            return
+        if self.free:
+            buf, ev = self.free.pop()
+        else:
+            buf, ev = torch.empty(self.slots, self.nl, pin_memory=True), torch.cuda.Event()
+        buf.copy_(self.ring, non_blocking=True)  # stream-ordered before any later rewrite
+        ev.record()
+        self.inflight.append((buf, ev, self.pending))
+        self.pending = []
+
+    def _pop(self, block):
+        buf, ev, entries = self.inflight[0]
+        if not ev.query():
+            if not block:
+                return False
+            ev.synchronize()
+        self.inflight.popleft()
+        rows = buf.tolist()
+        for slot, i_iter, extra in entries:
+            self.emit(i_iter, rows[slot], extra)
+        self.free.append((buf, ev))
+        return True
+
+    def poll(self):
+        while self.inflight and self._pop(block=False):
+            pass
+
+    def drain(self):
+        self.flush()
+        while self.inflight:
             self._pop(block=True)
 
     def emit_now(self, i_iter, vals, extra=None):
         self.drain()
         self.emit(i_iter, vals, extra)
 
-    def _pop(self, block):
-        i_iter, buf, ev, extra = self.pending[0]
-        if not block and not ev.query():
-            return False
-        ev.synchronize()
-        self.pending.popleft()
-        self.emit(i_iter, buf.tolist(), extra)
-        self.free.append(buf)
-        return True
-
-    def poll(self):
-        while self.pending and self._pop(block=False):
-            pass
-
-    def drain(self):
-        while self.pending:
-            self._pop(block=True)
-
-
-class _IndexCursor:
-    """Index slices of a DeviceCloudLoader in the order the trainer's _next
-    would gather them: epoch after epoch, each a fresh pass of the loader's
-    own index_batches() (the same generator draws as iterating it)."""
-
-    def __init__(self, loader):
-        self.loader = loader
-        self.it = loader.index_batches()
-
-    def next(self):
-        try:
-            return next(self.it)
-        except StopIteration:
-            self.it = self.loader.index_batches()
-            return next(self.it)
-
 
 class _GraphedIteration:
     """One training iteration fed by DeviceCloudLoaders as ONE HIP graph: each
-    loader's gather (+ device jitter) into static input buffers, then the
-    fused step.  Per iteration the host copies the loaders' index slices into
-    static index buffers and replays (graphs per `semi` flag, captured on first
-    use; the capture's warm-up leaves parameters, Adam state and the loaders'
-    RNG counters as they were)."""
+    loader's batch gathered (+ device jitter) into static input buffers from a
+    static copy of its epoch order at a device batch cursor
+    (pcadv_gather_clouds_at), the fused step, then pcadv_iter_epilogue
+    (loaders' RNG steps and cursors += 1, losses into the loss ring).  Per
+    iteration the host only replays; at an epoch start it rewrites the order
+    (the loader's own epoch_order(): the draws iterating it would make) and
+    zeroes the cursor.  Ragged batches (drop_last=False) are gathered eagerly
+    from the same order, their cursors advanced alike.  Graphs per `semi`
+    flag, captured on first use; the capture's warm-up leaves parameters, Adam
+    state, counters and the ring as they were."""
 
-    def __init__(self, step, loaders, lab_width=1):
-        self.step, self.loaders = step, loaders
+    def __init__(self, step, loaders, ring, lab_width=1):
+        self.step, self.loaders, self.ring = step, loaders, ring
         B, N, dev = step.B, step.N, step.device
-        self.B = B
-        self.idx = [torch.zeros(B, dtype=torch.int64, device=dev) for _ in loaders]
+        L = len(loaders)
+        self.B, self.L = B, L
+        self.counters = torch.zeros(2 * L, dtype=torch.int32, device=dev)  # RNG steps | cursors
+        for k, ld in enumerate(loaders):
+            self.counters[k:k + 1].copy_(ld.step)
+            ld.step = self.counters[k:k + 1]  # the loader keeps using it (eager gathers too)
+        self.order = [torch.zeros(ld.n, dtype=torch.int64, device=dev) for ld in loaders]
+        self.pos = [None] * L  # host: next batch of the current epoch
         self.pts = [torch.zeros(B, N, 3, device=dev) for _ in loaders]
         self.lab = torch.zeros(B, lab_width, dtype=torch.int64, device=dev)
         self.graphs = {}
 
-    def _body(self, semi):
+    def next_batches(self):
+        """Advance every loader by one batch: [(batch index k, size)]."""
+        out = []
         for k, ld in enumerate(self.loaders):
-            ld.gather(self.idx[k], out=self.pts[k], out_lab=self.lab if k == 0 else None,
-                      _checked=True)
-        if len(self.loaders) == 2:
+            if self.pos[k] is None or self.pos[k] >= len(ld):
+                self.order[k].copy_(ld.epoch_order())
+                self.counters[self.L + k:self.L + k + 1].zero_()
+                self.pos[k] = 0
+            kk = self.pos[k]
+            self.pos[k] += 1
+            out.append((kk, min(ld.B, ld.n - kk * ld.B)))
+        return out
+
+    def eager_batches(self, batches):
+        """Gather this iteration's batches eagerly (a ragged one among them):
+        the loaders' own gather (RNG step advanced there), cursors += 1."""
+        outs = []
+        for k, (ld, (kk, size)) in enumerate(zip(self.loaders, batches)):
+            idx = self.order[k][kk * ld.B:kk * ld.B + size].contiguous()
+            outs.append(ld.gather(idx, _checked=True))
+        self.counters[self.L:] += 1
+        return outs
+
+    def _body(self, semi):
+        L = self.L
+        for k, ld in enumerate(self.loaders):
+            ld.gather_at(self.order[k], self.counters[L + k:L + k + 1], self.pts[k],
+                         self.lab if (k == 0 and ld.labels is not None) else None)
+        if L == 2:
             self.step(self.pts[0], self.lab[:, 0], self.pts[1], semi=semi)
         else:
             self.step(self.pts[0], self.lab[:, 0])
+        self.ring.write(self.step.losses, self.counters, 2 * L)
 
     def _graph(self, semi):
         g = self.graphs.get(semi)
@@ -158,7 +211,7 @@ class _GraphedIteration:
             st = self.step
             state = [t for t in (getattr(st, n, None) for n in
                                  ("g_param", "g_m", "g_v", "d_param", "d_m", "d_v", "step_count"))
-                     if t is not None] + [ld.step for ld in self.loaders]
+                     if t is not None] + [self.counters, self.ring.count, self.ring.ring]
             saved = [t.clone() for t in state]
             cur = torch.cuda.current_stream()
             side = torch.cuda.Stream(device=st.device)
@@ -175,9 +228,7 @@ class _GraphedIteration:
             self.graphs[semi] = g
         return g
 
-    def run(self, idx_slices, semi=False):
-        for buf, ix in zip(self.idx, idx_slices):
-            buf.copy_(ix)
+    def replay(self, semi=False):
         self._graph(semi).replay()
         return self.step.losses
 
@@ -252,8 +303,6 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                and trainloader_gt.npts == trainloader_nogt.npts
                and trainloader_gt.B <= MAX_FUSED_B)
     gi = None
-    if graphed:  # the loaders' own epoch orders replace the (fresh) iterators given
-        cur_gt, cur_ng = _IndexCursor(trainloader_gt), _IndexCursor(trainloader_nogt)
     tb = getattr(args, "tensorboard", False) and writer is not None
 
     def emit(i_iter, vals, semi_on):
@@ -268,7 +317,9 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             if semi_loss is not None:
                 writer.add_scalar("Loss/train_semi", vals[4] if semi_on else 0.0, i_iter)
 
-    log = _AsyncLossLog(emit)
+    log = _LossRing(emit, 6, args.device)
+    if graphed:  # the loaders' own epoch orders replace the (fresh) iterators given
+        B0, N0 = trainloader_gt.B, trainloader_gt.npts
 
     def fused_step(B, N):
         nonlocal step
@@ -285,20 +336,22 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
         return step
 
     for i_iter in range(args.total_iterations):
-        model.train()
-        model_D.train()
+        # trainer.py:432-433; inside this loop only run_testing changes the modes
+        # (model.eval()), so the recursive train() is re-applied only then
+        if i_iter == 0 or not model.training:
+            model.train()
+        if i_iter == 0 or not model_D.training:
+            model_D.train()
         semi_on = semi_loss is not None and args.semi_start > 0 and i_iter > args.semi_start
         losses = None
         if graphed:
-            ig, ing = cur_gt.next(), cur_ng.next()
-            if ig.numel() == trainloader_gt.B and ing.numel() == trainloader_nogt.B:
-                st = fused_step(trainloader_gt.B, trainloader_gt.npts)
-                if gi is None or gi.step is not st:
-                    gi = _GraphedIteration(st, (trainloader_gt, trainloader_nogt))
-                losses = gi.run((ig, ing), semi=semi_on)
-            else:  # a ragged last batch: gathered eagerly
-                pts, cls = trainloader_gt.gather(ig.contiguous(), _checked=True)
-                pts_nogt = trainloader_nogt.gather(ing.contiguous(), _checked=True)
+            if gi is None:
+                gi = _GraphedIteration(fused_step(B0, N0), (trainloader_gt, trainloader_nogt), log)
+            bt = gi.next_batches()
+            if all(size == B0 for _, size in bt):
+                losses = gi.replay(semi=semi_on)
+            else:  # a ragged last batch: gathered eagerly from the same epoch order
+                (pts, cls), pts_nogt = gi.eager_batches(bt)
         else:
             batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
             pts, cls = batch
@@ -309,12 +362,10 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             pts_nogt = pts_nogt.float().to(args.device).contiguous()
             if fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B:
                 losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls, pts_nogt, semi=semi_on)
+                log.write(losses)
 
         if losses is not None:
-            if i_iter % log_every == 0:
-                log.push(i_iter, losses, semi_on)
-            else:
-                log.poll()
+            log.record(i_iter, semi_on, log=i_iter % log_every == 0)
         else:
             # unequal GT / no-GT batches (a loader's ragged last batch): the
             # reference's body through autograd over the same kernels; the torch
@@ -433,15 +484,13 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
     graphed = (fused and bool(getattr(args, "use_graph", True)) and _device_loaders(trainloader_gt)
                and trainloader_gt.B <= MAX_FUSED_B)
     gi = None
-    if graphed:
-        cursor = _IndexCursor(trainloader_gt)
     log_every = max(1, int(getattr(args, "log_every", 1)))
 
     def emit(i_iter, vals, regu):
         train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
             i_iter, args.total_iterations, vals[0], regu))
 
-    log = _AsyncLossLog(emit)
+    log = _LossRing(emit, 1, args.device)
 
     def fused_step(B, N):
         nonlocal step
@@ -453,18 +502,19 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
         return step
 
     for i_iter in range(args.total_iterations):
-        model.train()
+        if i_iter == 0 or not model.training:  # only run_testing's eval() changes it here
+            model.train()
         l_regu = None
         losses = None
         if graphed:
-            ix = cursor.next()
-            if ix.numel() == trainloader_gt.B:
-                st = fused_step(trainloader_gt.B, trainloader_gt.npts)
-                if gi is None or gi.step is not st:
-                    gi = _GraphedIteration(st, (trainloader_gt,))
-                losses = gi.run((ix,))
+            if gi is None:
+                gi = _GraphedIteration(fused_step(trainloader_gt.B, trainloader_gt.npts),
+                                       (trainloader_gt,), log)
+            bt = gi.next_batches()
+            if bt[0][1] == trainloader_gt.B:
+                losses = gi.replay()
             else:
-                pts, cls = trainloader_gt.gather(ix.contiguous(), _checked=True)
+                (pts, cls), = gi.eager_batches(bt)
         else:
             batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
             pts, cls = batch
@@ -472,11 +522,9 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
             pts, cls = pts.float().to(args.device).contiguous(), cls.long().to(args.device).contiguous()
             if fused and pts.shape[0] <= MAX_FUSED_B:
                 losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls)
+                log.write(losses)
         if losses is not None:
-            if i_iter % log_every == 0:
-                log.push(i_iter, losses, 0.0)
-            else:
-                log.poll()
+            log.record(i_iter, 0.0, log=i_iter % log_every == 0)
         else:
             if step is not None:
                 step.sync_optimizer_state()

@@ -47,10 +47,11 @@ def parse():
     ap.add_argument("--points", type=int, default=1024,
                     help="points per cloud of the adv step (1024: the metric's config; 2048: "
                          "BASELINE configs[4]'s per-rank shape)")
-    ap.add_argument("--config", choices=["adv", "seg", "cls"], default="adv",
+    ap.add_argument("--config", choices=["adv", "seg", "cls", "trainer"], default="adv",
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
-                         "supervised PointNetCls step of configs[1]")
+                         "supervised PointNetCls step of configs[1]; trainer: run_training "
+                         "end to end over DeviceCloudLoaders")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="feature-forward precision (default: bf16 for --config cls, the dtype "
                          "BASELINE configs[1] names; fp32 for adv and seg)")
@@ -415,6 +416,102 @@ def bench_cls(args):
     print(json.dumps(out), flush=True)
 
 
+def _synthetic_modelnet(n_gt, n_nogt, seed=5000):
+    """ModelNetDatasetGT / _noGT objects over in-memory synthetic clouds (the
+    HDF5 files are not in the image): same attributes as the file-backed ones,
+    data_augmentation on (the reference default, dataset/modelNetData.py:19)."""
+    from adversarial_learning_on_pointclouds_amd import dataset as D
+    rng = np.random.default_rng(seed)
+    gt = D.ModelNetDatasetGT.__new__(D.ModelNetDatasetGT)
+    gt.sample_list, gt.npoints, gt.data_augmentation = None, N, True
+    gt.select_data = rng.uniform(-1, 1, (n_gt, N, 3)).astype(np.float32)
+    gt.select_labels = rng.integers(0, 40, n_gt).astype(np.int32)
+    ng = D.ModelNetDataset_noGT.__new__(D.ModelNetDataset_noGT)
+    ng.sample_list, ng.npoints, ng.data_augmentation = None, N, True
+    ng.select_data = rng.uniform(-1, 1, (n_nogt, N, 3)).astype(np.float32)
+    return gt, ng
+
+
+def bench_trainer(args):
+    """The drop-in loop a user of the reference calls: trainer.run_training
+    (utils/trainer.py:403-608) over two DeviceCloudLoaders (GT / no-GT split
+    resident in HBM, each batch gathered and jittered on the device), B=32 +
+    32, N=1024, loss lines logged every iteration (read asynchronously).
+    Steady state = (T(W + K) - T(W)) / K over two fresh runs (iteration 0's
+    test pass, checkpoint and graph capture cancel), median of --repeats."""
+    import argparse as ap_
+    import logging
+    import tempfile
+    from adversarial_learning_on_pointclouds_amd import dataset as D
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    dev = torch.device("cuda", 0)
+    gt_ds, ng_ds = _synthetic_modelnet(1024, 4096)
+    log = logging.getLogger("bench_trainer")
+    log.addHandler(logging.NullHandler())
+    log.propagate = False
+
+    def run(iters, use_graph):
+        model, model_D = make_models(dev, seed=0)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        gt = D.DeviceCloudLoader(gt_ds, B, seed=1, drop_last=True)
+        ng = D.DeviceCloudLoader(ng_ds, B, seed=2, drop_last=True)
+        te = [next(iter(gt))]
+        a = ap_.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                          iter_test_epoch=10 ** 9, exp_dir=tempfile.mkdtemp(prefix="bench_tr_"),
+                          tensorboard=False, lambda_cls=1.0, lambda_adv=0.001, batch_size=B,
+                          use_graph=use_graph, log_every=1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), te, model, model_D,
+                             torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(), opt, opt_D,
+                             ImagePool(0), ImagePool(0), log, log, None, a)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    W, K = args.warmup, args.steps
+    run(W, True)  # first-use costs (library load, allocator) out of the timed runs
+    per, per_eager = [], []
+    for _ in range(args.repeats):
+        per.append((run(W + K, True) - run(W, True)) / K)
+    for _ in range(max(1, args.repeats // 3)):
+        per_eager.append((run(W + K, False) - run(W, False)) / K)
+    dt = float(np.median(per))
+    # the graph-replay step over resident batches (the headline bench's timed loop)
+    model, model_D = make_models(dev, seed=0)
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+    step = AdvTrainStep(model, model_D, B, N, seed=1234, device=dev)
+    rng = np.random.default_rng(1000)
+    bufs = (torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
+            torch.from_numpy(rng.integers(0, 40, B)).to(dev),
+            torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev))
+    g = step.capture_on(*bufs)
+    for _ in range(W):
+        g.replay()
+    reg = timed_regions(lambda k: g.replay(), K, args.repeats)
+    replay = float(np.median(reg)) / K
+    out = {
+        "metric": "point-clouds/sec (run_training over DeviceCloudLoader, adv step), B=32 N=1024, 1 GPU",
+        "value": round(2 * B / dt, 1), "unit": "clouds/s", "n_gpus": 1, "steps": K, "warmup": W,
+        "ms_per_step": round(dt * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (f32-level, as the headline line)",
+        "data": "synthetic in-memory ModelNet-shaped split (1024 GT + 4096 no-GT clouds), resident "
+                "in HBM, device gather + jitter per batch",
+        "config": {"workload": "trainer.run_training (utils/trainer.py:403-608) fed by two "
+                               "DeviceCloudLoaders, loss lines every iteration (async)",
+                   "global_batch": 2 * B, "points": N, "parallelism": "dp1",
+                   "hip_graph": "gathers + fused step, one graph per iteration"},
+        "timing": {"per_step_s": [round(v, 7) for v in per],
+                   "method": "(T(W+K) - T(W)) / K of whole run_training calls, median"},
+        "eager_ms_per_step": round(float(np.median(per_eager)) * 1e3, 4),
+        "graph_replay_ms_per_step": round(replay * 1e3, 4),
+        "ratio_to_graph_replay": round(dt / replay, 4),
+    }
+    print(json.dumps(out), flush=True)
+
+
 def bench_seg(args):
     """BASELINE.json configs[3]: PointNetSeg ShapeNet-part B=16, N=2048, one
     run_training_pointnet_seg iteration (forward, per-point CE, backward, Adam)
@@ -559,6 +656,8 @@ def main():
         return bench_seg(args)
     if args.config == "cls":
         return bench_cls(args)
+    if args.config == "trainer":
+        return bench_trainer(args)
     if _backend() != "nccl":  # rehearsal: ranks may share a GPU
         local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)

@@ -325,6 +325,25 @@ int pcadv_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
                         uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
                         int64_t* out_seg, hipStream_t stream);
 
+/* pcadv_gather_clouds for a graph-replayed loader: batch k = *cursor of the
+ * epoch order `order` (int64, k * B + b -> source cloud), so a captured graph
+ * gathers a new batch on every replay with no host copy; the caller advances
+ * *cursor and *step (pcadv_iter_epilogue) and rewrites `order` at each epoch
+ * (DeviceCloudLoader.index_batches' order). */
+int pcadv_gather_clouds_at(const float* src, int64_t n_src, int npts, int src_npts,
+                           const int64_t* order, const int32_t* cursor, int B,
+                           const int64_t* src_lab, int lab_width, const int64_t* src_seg,
+                           double sigma, double clip, uint64_t seed, const int32_t* step,
+                           float* out, int64_t* out_lab, int64_t* out_seg, hipStream_t stream);
+
+/* The end of a graph-replayed training iteration (trainer.py): counters[i] += 1
+ * for i < ncounters (<= 64: loaders' RNG steps and batch cursors), and, when
+ * ring is given, losses[0..nl) into slot (*ring_count % slots) of the [slots][nl]
+ * loss ring, then *ring_count += 1 (the host reads the ring every `slots`
+ * iterations instead of copying the losses out every iteration). */
+int pcadv_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl,
+                        float* ring, int slots, int32_t* ring_count, hipStream_t stream);
+
 /* CrossEntropyLoss over rows (the per-point segmentation loss, mean over M
  * points): *loss, and dlogits = scale * dL/dlogits (same stride ld). */
 size_t pcadv_row_ce_workspace_bytes(int M);
