@@ -253,7 +253,9 @@ def _pmc_traffic(pattern, prefixes, only_if=True):
     profiles/<pattern> (tools/pmc_traffic.py), or (None, None)."""
     if not only_if:
         return None, None
-    prof = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    prof = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", pattern))
+                  if pattern != "r*_pmc_traffic.json"
+                  or not any(t in os.path.basename(p) for t in ("_seg_", "_cls_")))
     if not prof:
         return None, None
     kern = json.load(open(prof[-1]))["kernels"]

@@ -4,7 +4,7 @@
 # traffic summaries and one step's kernel timeline.  Runs on the CPU here.
 set -euo pipefail
 cd "$(dirname "$0")/.."
-tag=${1:-r01}
+tag=${1:-r03}
 o=gpurun_out
 p=profiles
 line() { grep '"metric"' "$1" | tail -1; }
@@ -12,13 +12,14 @@ line "$o/${tag}_bench.log" > "$p/${tag}_bench.json"
 line "$o/${tag}_bench_seg.log" > "$p/${tag}_seg_bench.json"
 line "$o/${tag}_bench_cls.log" > "$p/${tag}_cls_bench.json"
 line "$o/${tag}_bench_n2048.log" > "$p/${tag}_bench_n2048.json"
-cp "$o/${tag}_trace/run_kernel_stats.csv" "$p/${tag}_kernel_stats.csv"
-cp "$o/${tag}_trace_seg/run_kernel_stats.csv" "$p/${tag}_seg_kernel_stats.csv"
-python tools/kstats.py "$o/${tag}_trace/run_kernel_trace.csv" > "$p/${tag}_kernel_trace_summary.txt"
-python tools/kstats.py "$o/${tag}_trace_seg/run_kernel_trace.csv" > "$p/${tag}_seg_kernel_trace_summary.txt"
+line "$o/${tag}_bench_trainer.log" > "$p/${tag}_trainer_bench.json"
+for c in "" _cls _seg; do
+  cp "$o/${tag}_trace$c/run_kernel_stats.csv" "$p/${tag}${c}_kernel_stats.csv"
+  python tools/kstats.py "$o/${tag}_trace$c/run_kernel_trace.csv" > "$p/${tag}${c}_kernel_trace_summary.txt"
+  python tools/pmc_traffic.py "$o/${tag}_pmc_fetch$c" "$o/${tag}_pmc_write$c" "$p/${tag}${c}_pmc_traffic.json" > /dev/null
+done
 python tools/step_timeline.py "$o/${tag}_trace/run_kernel_trace.csv" > "$p/${tag}_step_timeline.txt"
-python tools/pmc_traffic.py "$o/${tag}_pmc_fetch" "$o/${tag}_pmc_write" "$p/${tag}_pmc_traffic.json" > /dev/null
-python tools/pmc_traffic.py "$o/${tag}_pmc_fetch_seg" "$o/${tag}_pmc_write_seg" "$p/${tag}_seg_pmc_traffic.json" > /dev/null
-cp "$o/${tag}_pytest.log" "$p/${tag}_pytest_gpu.log"
-cp "$o/${tag}_smoke.log" "$p/${tag}_smoke.log"
+python tools/step_timeline.py "$o/${tag}_trace_cls/run_kernel_trace.csv" > "$p/${tag}_cls_step_timeline.txt" || true
+if [ -f "$o/${tag}_pytest.log" ]; then cp "$o/${tag}_pytest.log" "$p/${tag}_pytest_gpu.log"; fi
+if [ -f "$o/${tag}_smoke.log" ]; then cp "$o/${tag}_smoke.log" "$p/${tag}_smoke.log"; fi
 echo "refreshed $p/${tag}_*"
