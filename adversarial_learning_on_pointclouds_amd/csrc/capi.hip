@@ -100,6 +100,8 @@ int launch_iter_epilogue(int32_t*, int, const float*, int, float*, int, int32_t*
 size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
                   size_t, hipStream_t);
+int launch_cls_head(const float*, const float*, float, const float*, const float*, const int64_t*,
+                    int, float, float*, float*, float*, float*, hipStream_t);
 
 // ---- workspace carve for the fused step ------------------------------------
 struct StepWs {
@@ -110,6 +112,7 @@ struct StepWs {
   float* ddp;           // D conv1 input-gradient partials [512 / 16][B][40] (chained)
   float *mask;
   float *lpart, *lpart3, *dslabs, *dout;
+  float* rowloss;  // the cls step's per-row CE / B (k_cls_head)
   int32_t* gidx;
   int* sortrec;  // the feature backward's hit sort, done early (feat_sort.h)
   void* feat_ws;
@@ -154,6 +157,7 @@ static StepWs carve(int B, int N, char* base) {
   w.lpart3 = take(3 * (size_t)disc_rowblocks(B));
   w.dslabs = take((size_t)disc_rowblocks(B) * disc_tail_slab_floats());
   w.dout = take(R);
+  w.rowloss = take(C);
   w.sortrec = reinterpret_cast<int*>(take(feat_sort_record_ints((int)C, N)));
   w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
   if (feat_fwd_workspace_bytes((int)C, N) > w.feat_ws_bytes)
@@ -356,8 +360,8 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
 // feature_transform=False; BASELINE configs[1]): PointNetCls on B labelled
 // clouds, loss = lambda_cls * CE, backward, Adam on the generator only.  The
 // same kernels as the adversarial step minus the discriminator: the feature
-// forward over C = B clouds, fc1, fc2 + dropout, fc3 (k_linear_fwd), the CE and
-// its gradient (k_row_ce), the head backward (k_linear_bwd x3), the sparse
+// forward over C = B clouds, fc1, fc2 + dropout, fc3 + the CE + fc3's input
+// gradient (k_cls_head), the head backward (k_linear_bwd x2), the sparse
 // feature backward and one Adam launch.
 static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(a && a->B > 0 && a->B <= 256 && a->N > 0 && a->pts_gt && a->labels && a->g_param &&
@@ -391,24 +395,20 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
                            PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s, 0,
                            mask ? nullptr : w.mask));
-  PC_TRY(launch_linear_fwd(w.h2, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, logits, C, 40, 256,
-                           PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, s));
-  // CrossEntropyLoss (train_classification.py:199) and lambda_cls * dCE/dlogits
-  PC_TRY(launch_row_ce(logits, 40, a->labels, B, 40, a->lambda_cls, a->losses, w.dlogits,
-                       w.dslabs, (size_t)disc_rowblocks(B) * disc_tail_slab_floats() * sizeof(float),
-                       s));
-  // data gradients stored as the layer below's dz (see adv_step)
+  // fc3, CrossEntropyLoss (train_classification.py:199), lambda_cls * dCE/dlogits
+  // and fc3's input gradient, stored as fc2's dz (k_cls_head)
+  PC_TRY(launch_cls_head(w.h2, w.mask, a->drop_p, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, a->labels,
+                         B, a->lambda_cls, logits, w.dlogits, w.dh2, w.rowloss, s));
   {
+    // fc2's backward; fc3's weight gradient and the CE batch mean ride along
     LinBwdExtra ex{};
-    ex.dx_act = PCADV_ACT_RELU;  // x = fc2 output, with its dropout
-    ex.dx_mask = w.mask;
-    ex.dx_keep = 1.0f / (1.0f - a->drop_p);
-    PC_TRY(launch_linear_bwd(w.dlogits, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h2,
-                             G + PCADV_G_FC3_W, w.dh2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C,
-                             C, 40, 256, s, &ex));
-  }
-  {
-    LinBwdExtra ex{};
+    ex.job[0] = LinBwdJob{w.dlogits, w.h2, gG + PCADV_G_FC3_W, gG + PCADV_G_FC3_B, C, 40, 256};
+    ex.njobs = 1;
+    ex.red_src = w.rowloss;
+    ex.red_dst = a->losses;
+    ex.red_n = 1;
+    ex.red_cnt = B;
+    ex.red_ld = 1;
     ex.dx_act = PCADV_ACT_RELU;  // x = fc1 output
     PC_TRY(launch_linear_bwd(w.dh2, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.h1,
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,

@@ -685,6 +685,88 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
 }
 
 // ---------------------------------------------------------------------------
+// k_cls_head: run_training_pointnet_cls's head end (utils/trainer.py:254-268):
+// fc3 (models/pointnet.py:202), log_softmax + CrossEntropyLoss
+// (train_classification.py:199), lambda_cls x its gradient and fc3's input
+// gradient - stored as fc2's dz (relu'(h2) x dropout mask x keep) - one
+// workgroup per 16 rows, in place of three launches.  fc3's weight gradient
+// and the batch mean of the CE (rowloss[r] = CE_r / B, summed in row order)
+// ride in fc2's backward launch (a LinBwdJob over dlogits x h2, its slab sum).
+// ---------------------------------------------------------------------------
+struct ClsHeadLds {
+  float w3[40 * 260];                 // fc3 weight [40][256], padded rows
+  float b3[40];
+  alignas(16) float h2[TR * 260];     // the block's fc2 output rows
+  alignas(16) float g[TR * 260];      // relu'(h2) x dropout mask x keep
+  float lg[TR * 44];                  // logits
+  float dl[TR * 44];                  // lambda dCE / dlogits
+  float rl[TR];
+  int lab[TR];
+  alignas(16) float scratch[12 * 256];
+};
+
+__global__ void __launch_bounds__(TT)
+k_cls_head(const float* __restrict__ h2, const float* __restrict__ drop_mask, float keep,
+           const float* __restrict__ w3, const float* __restrict__ b3,
+           const int64_t* __restrict__ labels, int B, float lambda_cls, float* __restrict__ logits,
+           float* __restrict__ dlogits, float* __restrict__ dz2, float* __restrict__ rowloss) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  ClsHeadLds& L = *reinterpret_cast<ClsHeadLds*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * TR, nr = min(TR, B - r0);
+  TSTAMP(0, 0);
+  {
+    const Fill f[4] = {{L.h2, 260, h2 + (size_t)r0 * 256, TR, 256, nr},
+                       {L.g, 260, drop_mask + (size_t)r0 * 256, TR, 256, drop_mask ? nr : 0},
+                       {L.w3, 260, w3, 40, 256, 40}, {L.b3, 40, b3, 1, 40, 1}};
+    if (tid < nr) L.lab[tid] = (int)labels[r0 + tid];
+    lds_fill<4, 5>(f);  // 4618 float4: <= 5 per thread
+  }
+  __syncthreads();
+  TSTAMP(0, 1);
+  // g = relu'(h2) x mask x keep (the mask rows were staged into g)
+  for (int e = tid; e < TR * 256; e += TT) {
+    const int r = e >> 8, k = e & 255;
+    const float m = drop_mask ? L.g[r * 260 + k] * keep : 1.f;
+    L.g[r * 260 + k] = L.h2[r * 260 + k] > 0.f ? m : 0.f;
+  }
+  // fc3: reduction chunks of 64 (as k_head_fwd)
+  rows_layer<256, 40, B_OK, ACT_NONE, 64>(L.h2, 260, L.w3, 260, L.b3, L.lg, 44, L.scratch);
+  TSTAMP(0, 2);
+  // log_softmax, CE and its gradient (as k_row_ce_wave): one wave per row
+  {
+    const int row = wave;
+    const float v = lane < 40 ? L.lg[row * 44 + lane] : -INFINITY;
+    float mx = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float e = lane < 40 ? expf(v - mx) : 0.f;
+    float se = e;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+    const float lse = mx + logf(se);
+    float dl = 0.f;
+    if (row < nr) {
+      const int y = L.lab[row];
+      dl = (expf(v - lse) - (lane == y ? 1.f : 0.f)) * (lambda_cls / (float)B);
+      const float rloss = lse - __shfl(v, y);
+      if (lane < 40) {
+        logits[(size_t)(r0 + row) * 40 + lane] = v;
+        dlogits[(size_t)(r0 + row) * 40 + lane] = dl;
+      }
+      if (lane == 0) rowloss[r0 + row] = rloss / (float)B;
+    }
+    if (lane < 40) L.dl[row * 44 + lane] = dl;
+  }
+  __syncthreads();
+  TSTAMP(0, 3);
+  // fc3 input gradient, stored as fc2's dz: dl W3 x g
+  rows_layer<40, 256, B_KO, ACT_NONE>(L.dl, 44, L.w3, 260, nullptr, dz2 + (size_t)r0 * 256, 256,
+                                      nullptr, nr, TR, 0, OutMask{L.g, 260, L.g, 1.f});
+  TSTAMP(0, 4);
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 template <typename K>
@@ -714,6 +796,23 @@ int launch_head_fwd(const float* h2, const float* w3, const float* b3, const int
   hipLaunchKernelGGL(k_head_fwd, dim3(head_rowblocks(B) * HF_SPLIT), dim3(TT), sizeof(HeadFwdLds), s, h2, w3,
                      b3, labels, B, lambda_cls, logits, dlogits, din, dw1, db1, d1, lpart);
   PC_HIP_CHECK_LAUNCH("k_head_fwd");
+  return PCADV_OK;
+}
+
+int launch_cls_head(const float* h2, const float* drop_mask, float drop_p, const float* w3,
+                    const float* b3, const int64_t* labels, int B, float lambda_cls, float* logits,
+                    float* dlogits, float* dz2, float* rowloss, hipStream_t s) {
+  static bool once = false;
+  if (!once) {
+    if (set_lds(k_cls_head, sizeof(ClsHeadLds), "cls_head") != PCADV_OK) return PCADV_EHIP;
+    once = true;
+  }
+  PC_REQUIRE(B > 0 && h2 && w3 && b3 && labels && logits && dlogits && dz2 && rowloss,
+             "cls_head: bad arguments");
+  const float keep = 1.0f / (1.0f - drop_p);  // as the linear kernels' dropout scale
+  hipLaunchKernelGGL(k_cls_head, dim3((B + TR - 1) / TR), dim3(TT), sizeof(ClsHeadLds), s, h2,
+                     drop_mask, keep, w3, b3, labels, B, lambda_cls, logits, dlogits, dz2, rowloss);
+  PC_HIP_CHECK_LAUNCH("k_cls_head");
   return PCADV_OK;
 }
 
