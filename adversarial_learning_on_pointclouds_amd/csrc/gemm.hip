@@ -805,6 +805,12 @@ k_gemm_bf2_big(GemmP p) {
   }
 }
 
+// diagnostic / A-B switches read from the environment ("1" = on)
+static bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
 // the 256-tile kernel takes a plane-operand GEMM when its columns come in
 // whole 256-blocks and the grid still gives every CU work (>= 256 tiles);
 // PCADV_GEMM_BIG=0 keeps the 128-tile kernel (A/B and bitwise checks)
@@ -934,6 +940,26 @@ k_gemm_small(GemmP p) {
 // fixed order (bitwise reproducible): a workgroup takes 32 consecutive e
 // (coalesced) x 8 interleaved z-subsets (one per half-wave), combined through
 // LDS.  The output index is 2-D: out + g * ldg + (e / N) * ldo + e % N.
+// one z-subset's share (z = zs, zs + 8, ...) of a slab sum, four loads in flight
+__device__ __forceinline__ float slab_subset(const float* src, long long stride, int nz, int zs) {
+  float s = 0.f;
+  int z = zs;
+  for (; z + 24 < nz; z += 32) {
+    const float a0 = src[(size_t)z * stride], a1 = src[(size_t)(z + 8) * stride];
+    const float a2 = src[(size_t)(z + 16) * stride], a3 = src[(size_t)(z + 24) * stride];
+    s += ((a0 + a1) + a2) + a3;
+  }
+  for (; z < nz; z += 8) s += src[(size_t)z * stride];
+  return s;
+}
+// the eight subsets' partials of element el, in subset order
+__device__ __forceinline__ float slab_combine(const float (&part)[8][33], int el) {
+  float t = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) t += part[q][el];
+  return t;
+}
+
 __global__ void __launch_bounds__(256)
 k_slab_sum(const float* __restrict__ in, long long stride, int nz, long long E,
            float* __restrict__ out, long long ldg, int N, long long ldo, int accumulate) {
@@ -941,25 +967,75 @@ k_slab_sum(const float* __restrict__ in, long long stride, int nz, long long E,
   const long long e = (long long)blockIdx.x * 32 + el;
   const int g = blockIdx.y;
   __shared__ float part[8][33];
-  float s = 0.f;
-  if (e < E) {
-    const float* src = in + (size_t)g * nz * stride + e;
-    int z = zs;
-    for (; z + 24 < nz; z += 32) {  // four independent loads in flight
-      const float a0 = src[(size_t)z * stride], a1 = src[(size_t)(z + 8) * stride];
-      const float a2 = src[(size_t)(z + 16) * stride], a3 = src[(size_t)(z + 24) * stride];
-      s += ((a0 + a1) + a2) + a3;
-    }
-    for (; z < nz; z += 8) s += src[(size_t)z * stride];
-  }
-  part[zs][el] = s;
+  part[zs][el] = e < E ? slab_subset(in + (size_t)g * nz * stride + e, stride, nz, zs) : 0.f;
   __syncthreads();
   if (zs == 0 && e < E) {
-    float t = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) t += part[q][el];
+    const float t = slab_combine(part, el);
     float* dst = out + (size_t)g * ldg + (size_t)(e / N) * ldo + (e % N);
     *dst = accumulate ? *dst + t : t;
+  }
+}
+
+// The finishing reductions of one weight-gradient launch in ONE launch, bitwise
+// the same sums as k_slab_sum's separate launches: blocks [0, nb_dw) sum the dW
+// slabs (as k_slab_sum (dw)); the blocks after them take 32 output channels
+// each and form the per-group sums of the slabs' column sums (kept in LDS,
+// written to gs when asked) and then db from them (or from the column sums
+// directly when there is one group and no per-group output).
+constexpr int WF_MAXG = 64;
+__global__ void __launch_bounds__(256)
+k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __restrict__ dw, int N,
+               long long ldo, int acc_dw, int nb_dw, const float* __restrict__ csum, int O,
+               int groups, int zpg, int from_groups, float* __restrict__ gs, float* __restrict__ db,
+               int acc_db) {
+  const int tid = threadIdx.x, el = tid & 31, zs = tid >> 5;
+  __shared__ float part[8][33];
+  if ((int)blockIdx.x < nb_dw) {
+    const long long e = (long long)blockIdx.x * 32 + el;
+    part[zs][el] = e < E ? slab_subset(slabs + e, E, nz, zs) : 0.f;
+    __syncthreads();
+    if (zs == 0 && e < E) {
+      const float t = slab_combine(part, el);
+      float* dst = dw + (size_t)(e / N) * ldo + (e % N);
+      *dst = acc_dw ? *dst + t : t;
+    }
+    return;
+  }
+  const int o = ((int)blockIdx.x - nb_dw) * 32 + el;
+  const bool ok = o < O;
+  if (!from_groups) {
+    part[zs][el] = ok ? slab_subset(csum + o, O, nz, zs) : 0.f;
+    __syncthreads();
+    if (zs == 0 && ok) {
+      const float t = slab_combine(part, el);
+      db[o] = acc_db ? db[o] + t : t;
+    }
+    return;
+  }
+  __shared__ float gsl[WF_MAXG][33];
+  for (int g = 0; g < groups; ++g) {
+    part[zs][el] = ok ? slab_subset(csum + (size_t)g * zpg * O + o, O, zpg, zs) : 0.f;
+    __syncthreads();
+    if (zs == 0) {
+      const float t = slab_combine(part, el);
+      gsl[g][el] = t;
+      if (gs && ok) gs[(size_t)g * O + o] = t;
+    }
+    __syncthreads();
+  }
+  if (!db) return;
+  // db over the groups: the same subset order, reading the group sums from LDS
+  {
+    float s = 0.f;
+    int z = zs;
+    for (; z + 24 < groups; z += 32) s += ((gsl[z][el] + gsl[z + 8][el]) + gsl[z + 16][el]) + gsl[z + 24][el];
+    for (; z < groups; z += 8) s += gsl[z][el];
+    part[zs][el] = ok ? s : 0.f;
+  }
+  __syncthreads();
+  if (zs == 0 && ok) {
+    const float t = slab_combine(part, el);
+    db[o] = acc_db ? db[o] + t : t;
   }
 }
 
@@ -1332,6 +1408,18 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
   p.csum = csum;
   PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(p, w.nz, s)));
   const long long E = (long long)O * Kin;
+  if (w.groups <= WF_MAXG && !getenv_flag("PCADV_WGRAD_SPLIT_FINISH")) {
+    // dW, the per-group sums and db in one launch (k_wgrad_finish)
+    const int nb_dw = (int)((E + 31) / 32);
+    const int nb_cs = csum ? (O + 31) / 32 : 0;
+    const bool from_groups = w.groups > 1 || gsum;
+    hipLaunchKernelGGL(k_wgrad_finish, dim3((unsigned)(nb_dw + nb_cs)), dim3(256), 0, s,
+                       static_cast<const float*>(slabs), E, w.nz, dw, Kin, ldo, accumulate, nb_dw,
+                       static_cast<const float*>(csum), O, w.groups, w.zpg, from_groups ? 1 : 0,
+                       gsum, db, accumulate);
+    PC_HIP_CHECK_LAUNCH("k_wgrad_finish");
+    return PCADV_OK;
+  }
   hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((E + 31) / 32), 1), dim3(256), 0, s,
                      static_cast<const float*>(slabs), E, w.nz, E, dw, 0LL, Kin, ldo, accumulate);
   PC_HIP_CHECK_LAUNCH("k_slab_sum (dw)");

@@ -273,9 +273,28 @@ def test_gemm_weight_grad(rows, rpg, O, K):
     if rpg:
         rg = d64.reshape(G, rpg, O).sum(1)
         assert np.abs(gs.cpu().numpy() - rg).max() <= 1e-5 * max(1.0, np.abs(d64).sum(0).max())
-    a, a_db = dW.clone(), db.clone()
+    a, a_db, a_gs = dW.clone(), db.clone(), gs.clone()
     check(lib.pcadv_gemm_wgrad(*args), "wgrad")
     assert torch.equal(a, dW) and torch.equal(a_db, db)  # fixed-order slabs: bitwise reproducible
+    # the one-launch finishing reductions (k_wgrad_finish) against the separate
+    # k_slab_sum launches, plain and accumulating: bitwise the same sums
+    acc = args[:12] + (1,) + args[13:]
+    outs = {}
+    for split in ("0", "1"):
+        os.environ["PCADV_WGRAD_SPLIT_FINISH"] = split
+        try:
+            dW.copy_(a), db.copy_(a_db), gs.fill_(0)
+            check(lib.pcadv_gemm_wgrad(*args), "wgrad")
+            plain = (dW.clone(), db.clone(), gs.clone())
+            check(lib.pcadv_gemm_wgrad(*acc), "wgrad accumulate")
+            outs[split] = plain + (dW.clone(), db.clone())
+        finally:
+            del os.environ["PCADV_WGRAD_SPLIT_FINISH"]
+    for x, y in zip(outs["0"], outs["1"]):
+        assert torch.equal(x, y)
+    assert torch.equal(outs["0"][0], a) and torch.equal(outs["0"][1], a_db)
+    if rpg:
+        assert torch.equal(outs["0"][2], a_gs)
 
 
 def test_colsum_and_group_colsum():
