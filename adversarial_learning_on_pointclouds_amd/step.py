@@ -266,6 +266,28 @@ class AdvTrainStep:
         self._restore(saved)
         return g
 
+    def capture_seq(self, batches, apply_adam=True):
+        """Capture len(batches) consecutive steps, step i reading the resident
+        buffers batches[i] = (pts_gt, labels, pts_nogt), into ONE HIP graph (the
+        device step counter advances per step, so each draws its own dropout
+        masks and D labels).  One replay = len(batches) iterations with one
+        graph-launch overhead; state is left as it was before the capture."""
+        saved = self._snapshot()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(*batches[0], apply_adam=apply_adam)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        args = [self._args(pg, lab, pn, None, None, apply_adam, False, 0) for pg, lab, pn in batches]
+        self._keep.extend(args)
+        with torch.cuda.graph(g):
+            for a in args:
+                check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (capture)")
+        torch.cuda.synchronize()
+        self._restore(saved)
+        return g
+
     def capture(self):
         """Capture one step over static input buffers; returns the buffers
         (pts_gt, labels, pts_nogt) to fill before replay()."""
@@ -407,6 +429,26 @@ class ClsTrainStep:
         self._keep.append(a)
         with torch.cuda.graph(g):
             check(self.lib.pcadv_cls_step(ctypes.byref(a), stream_ptr()), "pcadv_cls_step (capture)")
+        torch.cuda.synchronize()
+        for dst, src in zip((self.g_param, self.g_m, self.g_v, self.step_count), saved):
+            dst.copy_(src)
+        return g
+
+    def capture_seq(self, batches):
+        """len(batches) consecutive steps (batches[i] = (pts, labels)) in ONE
+        HIP graph, as AdvTrainStep.capture_seq (state restored)."""
+        saved = [t.clone() for t in (self.g_param, self.g_m, self.g_v, self.step_count)]
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(*batches[0])
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        args = [self._args(pts, lab, None, True) for pts, lab in batches]
+        self._keep.extend(args)
+        with torch.cuda.graph(g):
+            for a in args:
+                check(self.lib.pcadv_cls_step(ctypes.byref(a), stream_ptr()), "pcadv_cls_step (capture)")
         torch.cuda.synchronize()
         for dst, src in zip((self.g_param, self.g_m, self.g_v, self.step_count), saved):
             dst.copy_(src)

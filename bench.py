@@ -54,6 +54,11 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--graph-steps", type=int, default=1,
+                    help="steps captured per HIP graph (adv / cls, one GPU): a replay runs that "
+                         "many consecutive iterations over the resident batch pool; a timed "
+                         "region still runs exactly --steps steps (the remainder as one-step "
+                         "graphs)")
     ap.add_argument("--repeats", type=int, default=3,
                     help="timed regions of --steps steps each; the median is reported")
     ap.add_argument("--points", type=int, default=1024,
@@ -352,6 +357,20 @@ def feat_roofline(pts_all, fw, prec, traffic_pattern=None):
     }
 
 
+def graph_runner(single, seq, G):
+    """Per-step callable for warm-up / timed_regions over `total` steps: step
+    k replays single[k % POOL] or, inside a whole group of G steps, the G-step
+    graph `seq` (batches 0..G-1 of the pool) once at the group's last step."""
+    def run(k, total):
+        full = (total // G) * G if seq is not None else 0
+        if k < full:
+            if k % G == G - 1:
+                seq.replay()
+        else:
+            single[k % POOL].replay()
+    return run
+
+
 def timed_regions(one, steps, repeats, dist=None):
     """`repeats` timed regions of exactly `steps` steps, each bracketed by a
     barrier + synchronize on both sides; returns the per-region seconds (max
@@ -395,9 +414,11 @@ def bench_cls(args):
         pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
                      torch.from_numpy(rng.integers(0, 40, B)).to(dev)))
     graphs = [step.capture_on(*b) for b in pool]
+    G = max(1, min(args.graph_steps, POOL))
+    run = graph_runner(graphs, step.capture_seq(pool[:G]) if G > 1 else None, G)
     for k in range(args.warmup):
-        graphs[k % POOL].replay()
-    regions = timed_regions(lambda k: graphs[k % POOL].replay(), args.steps, args.repeats)
+        run(k, args.warmup)
+    regions = timed_regions(lambda k: run(k, args.steps), args.steps, args.repeats)
     dt = float(np.median(regions))
     gflop = 11.18  # algorithmic FLOPs of one cfg-2 step
     loss = float(step.losses[0].item())
@@ -418,7 +439,7 @@ def bench_cls(args):
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
         "config": {"workload": "run_training_pointnet_cls: PointNetCls(k=40), CE, Adam, B=32, "
                                "N=1024 (BASELINE configs[1])", "global_batch": B, "points": N,
-                   "parallelism": "dp1", "hip_graph": True, "precision": prec},
+                   "parallelism": "dp1", "hip_graph": True, "steps_per_graph": G, "precision": prec},
         "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
         "roofline": roof,
         "step_flops": {"gflop_per_step": gflop,
@@ -707,23 +728,28 @@ def main():
                      torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev)))
     use_graph = not args.no_graph
     graphs = []
+    G = 1
+    seq = None
     if use_graph:
         if runner is not None:
             graphs = [runner.capture(*pool[k]) for k in range(POOL)]
         else:
             graphs = [step.capture_on(*pool[k]) for k in range(POOL)]
+            G = max(1, min(args.graph_steps, POOL))
+            seq = step.capture_seq(pool[:G]) if G > 1 else None
+    run = graph_runner(graphs, seq, G)
 
-    def one(k):
+    def one(k, total):
         if use_graph:
-            graphs[k % POOL].replay()
+            run(k, total)
         elif runner is not None:
             runner(*pool[k % POOL])
         else:
             step(*pool[k % POOL])
 
     for k in range(args.warmup):
-        one(k)
-    regions = timed_regions(one, args.steps, args.repeats, dist)
+        one(k, args.warmup)
+    regions = timed_regions(lambda k: one(k, args.steps), args.steps, args.repeats, dist)
     dt = float(np.median(regions))
     losses = step.losses[:4].cpu().numpy().tolist()
     finite = all(np.isfinite(losses))
@@ -761,7 +787,7 @@ def main():
         "config": {"workload": "adversarial cls step: PointNetCls(k=40)+DeepConvDiscNet(40,1), "
                                f"B=32 GT + 32 noGT clouds/GPU, N={N}, Adam x2",
                    "global_batch": 2 * B * world, "points": N,
-                   "parallelism": f"dp{world}", "hip_graph": use_graph},
+                   "parallelism": f"dp{world}", "hip_graph": use_graph, "steps_per_graph": G},
         "world_size": world,
         "backend": ((_backend() if _backend() != "nccl" else "nccl (RCCL)") if world > 1 else None),
         "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median",
