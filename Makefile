@@ -58,5 +58,5 @@ $(ASAN_BIN): $(PKG)/csrc/h5read.cpp tests/asan/h5check.cpp include/pcadv.h
 	@mkdir -p build/asan
 	g++ -std=c++17 -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer \
 	  -fno-sanitize-recover=undefined -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude \
-	  $(PKG)/csrc/h5read.cpp tests/asan/h5check.cpp -lz -o $@
+	  $(PKG)/csrc/h5read.cpp tests/asan/h5check.cpp -lz -o $@.tmp.$$$$ && mv -f $@.tmp.$$$$ $@
 .PHONY: asan

@@ -80,6 +80,7 @@ SIGNATURES = {
     "pcadv_feat_fwd": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 3 + [_vp, _sz, _vp]),
     "pcadv_feat_fwd_bf16": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 3 + [_vp, _sz, _vp]),
     "pcadv_conv4_max": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
+    "pcadv_conv4_max_bf16": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "pcadv_feat_bwd_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_feat_bwd": (_i, [_vp, _vp, _vp, _i, _i] + [_vp] * 7 + [_vp] * 8 + [_vp, _sz, _vp]),
     "pcadv_conv_max_fwd": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp]),
@@ -146,6 +147,8 @@ def load():
                 "There is no CPU fallback for the pcadv ops.")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("PCADV_LIB") and not hasattr(lib, name):
+                continue  # an older library picked for an A/B timing run
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
