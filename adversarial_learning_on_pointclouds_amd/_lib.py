@@ -80,7 +80,6 @@ SIGNATURES = {
     "pcadv_feat_fwd": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 3 + [_vp, _sz, _vp]),
     "pcadv_feat_fwd_bf16": (_i, [_vp, _i, _i] + [_vp] * 8 + [_vp] * 3 + [_vp, _sz, _vp]),
     "pcadv_conv4_max": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
-    "pcadv_conv4_max_bf16": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "pcadv_feat_bwd_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_feat_bwd": (_i, [_vp, _vp, _vp, _i, _i] + [_vp] * 7 + [_vp] * 8 + [_vp, _sz, _vp]),
     "pcadv_conv_max_fwd": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp]),

@@ -24,6 +24,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
+    assert sorted(_lib.SIGNATURES) == syms  # nothing bound that the header does not declare
     assert lib.pcadv_abi_version() == 5
 
 
