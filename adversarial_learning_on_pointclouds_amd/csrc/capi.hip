@@ -101,7 +101,8 @@ size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
                   size_t, hipStream_t);
 int launch_cls_head(const float*, const float*, float, const float*, const float*, const int64_t*,
-                    int, float, float*, float*, float*, float*, hipStream_t);
+                    int, float, float*, float*, float*, float*, hipStream_t, const int32_t*, int,
+                    int, int*);
 
 // ---- workspace carve for the fused step ------------------------------------
 struct StepWs {
@@ -398,7 +399,8 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   // fc3, CrossEntropyLoss (train_classification.py:199), lambda_cls * dCE/dlogits
   // and fc3's input gradient, stored as fc2's dz (k_cls_head)
   PC_TRY(launch_cls_head(w.h2, w.mask, a->drop_p, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, a->labels,
-                         B, a->lambda_cls, logits, w.dlogits, w.dh2, w.rowloss, s));
+                         B, a->lambda_cls, logits, w.dlogits, w.dh2, w.rowloss, s, w.gidx, C, N,
+                         w.sortrec));
   {
     // fc2's backward; fc3's weight gradient and the CE batch mean ride along
     LinBwdExtra ex{};
@@ -426,7 +428,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr);
+                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec);
 }
 
 }  // namespace pcadv

@@ -709,10 +709,24 @@ __global__ void __launch_bounds__(TT)
 k_cls_head(const float* __restrict__ h2, const float* __restrict__ drop_mask, float keep,
            const float* __restrict__ w3, const float* __restrict__ b3,
            const int64_t* __restrict__ labels, int B, float lambda_cls, float* __restrict__ logits,
-           float* __restrict__ dlogits, float* __restrict__ dz2, float* __restrict__ rowloss) {
+           float* __restrict__ dlogits, float* __restrict__ dz2, float* __restrict__ rowloss,
+           const int32_t* __restrict__ gidx, int C, int N, int* __restrict__ sortrec) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  ClsHeadLds& L = *reinterpret_cast<ClsHeadLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nrb = (B + TR - 1) / TR;
+  if ((int)blockIdx.x >= nrb) {
+    // the feature backward's hit sort (feat_sort.h) on the CUs this launch
+    // leaves idle, as k_disc_tail does for the adversarial step
+    static_assert(TT == 2 * FS_T && sizeof(ClsHeadLds) >= 2 * sizeof(SortLds), "sort geometry");
+    const int nch = (N + FS_PCH - 1) / FS_PCH, half = tid / FS_T;
+    const int id = 2 * ((int)blockIdx.x - nrb) + half, cc = id / nch, ch = id % nch;
+    SortLds& S = reinterpret_cast<SortLds*>(smem)[half];
+    const bool valid = cc < C;
+    chunk_sort(gidx + (size_t)(valid ? cc : 0) * FS_MAXO, FS_MAXO, ch * FS_PCH, tid % FS_T, valid,
+               S, sortrec + (size_t)id * FS_REC);
+    return;
+  }
+  ClsHeadLds& L = *reinterpret_cast<ClsHeadLds*>(smem);
   const int r0 = blockIdx.x * TR, nr = min(TR, B - r0);
   TSTAMP(0, 0);
   {
@@ -799,9 +813,12 @@ int launch_head_fwd(const float* h2, const float* w3, const float* b3, const int
   return PCADV_OK;
 }
 
+// sortrec (optional): also run the feature backward's hit sort over the C
+// clouds' argmax gidx [C][1024] into sortrec (feat_sort_record_ints(C, N))
 int launch_cls_head(const float* h2, const float* drop_mask, float drop_p, const float* w3,
                     const float* b3, const int64_t* labels, int B, float lambda_cls, float* logits,
-                    float* dlogits, float* dz2, float* rowloss, hipStream_t s) {
+                    float* dlogits, float* dz2, float* rowloss, hipStream_t s,
+                    const int32_t* gidx, int C, int N, int* sortrec) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_cls_head, sizeof(ClsHeadLds), "cls_head") != PCADV_OK) return PCADV_EHIP;
@@ -809,9 +826,12 @@ int launch_cls_head(const float* h2, const float* drop_mask, float drop_p, const
   }
   PC_REQUIRE(B > 0 && h2 && w3 && b3 && labels && logits && dlogits && dz2 && rowloss,
              "cls_head: bad arguments");
+  PC_REQUIRE(!sortrec || (gidx && C > 0 && N > 0), "cls_head: the hit sort needs gidx, C and N");
+  const int nsort = sortrec ? (C * ((N + FS_PCH - 1) / FS_PCH) + 1) / 2 : 0;
   const float keep = 1.0f / (1.0f - drop_p);  // as the linear kernels' dropout scale
-  hipLaunchKernelGGL(k_cls_head, dim3((B + TR - 1) / TR), dim3(TT), sizeof(ClsHeadLds), s, h2,
-                     drop_mask, keep, w3, b3, labels, B, lambda_cls, logits, dlogits, dz2, rowloss);
+  hipLaunchKernelGGL(k_cls_head, dim3((B + TR - 1) / TR + nsort), dim3(TT), sizeof(ClsHeadLds), s,
+                     h2, drop_mask, keep, w3, b3, labels, B, lambda_cls, logits, dlogits, dz2,
+                     rowloss, gidx, C, N, sortrec);
   PC_HIP_CHECK_LAUNCH("k_cls_head");
   return PCADV_OK;
 }
