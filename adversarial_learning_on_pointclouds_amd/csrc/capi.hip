@@ -66,6 +66,7 @@ int launch_disc_tail(const float*, int, const float*, const float*, const float*
 size_t feat_sort_record_ints(int C, int N);
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
+int chunk_stamps_read(uint64_t* host);
 int lin_stamps_read(uint64_t* host, int reset);
 #endif
 int launch_head_bwd(const float*, const float*, const float*, float, const float*, int,
@@ -479,6 +480,7 @@ size_t pcadv_feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_workspace_
 
 #ifdef PCADV_STAMPS
 int pcadv_tail_stamps(uint64_t* host) { return tail_stamps_read(host); }
+int pcadv_chunk_stamps(uint64_t* host) { return chunk_stamps_read(host); }
 int pcadv_lin_stamps(uint64_t* host, int reset) { return lin_stamps_read(host, reset); }
 
 // diagnostic build only: pcadv_feat_bwd with per-workgroup phase timestamps

@@ -72,7 +72,13 @@ static_assert(FS_PCH == BW_PCH && FS_MAXO == BW_MAXO && FS_T == BW_T, "feat_sort
 // backward: the generator from fc1 on (segment 0) and the discriminator
 // (segment 1), in trailing workgroups of k_feat_bwd_chunk (NT = BW_T threads);
 // V4 float4 per thread and pass, blocks [0, nb0) on segment 0.
-constexpr int FIN_ADAM_V4 = 4;  // float4 per thread in the chunk launch's Adam workgroups
+#ifndef PCADV_FIN_ADAM_V4
+#define PCADV_FIN_ADAM_V4 4
+#endif
+#ifndef PCADV_TRAIL_ADAM_FIRST
+#define PCADV_TRAIL_ADAM_FIRST 0
+#endif
+constexpr int FIN_ADAM_V4 = PCADV_FIN_ADAM_V4;  // float4 per thread in the chunk launch's Adam workgroups
 template <int NT, int V4>
 __device__ void adam_range(int b, int nb, float* p, float* m, float* v, const float* g, int64_t n,
                            float lr, const FinAdam& fa) {
@@ -188,6 +194,18 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
 }
 
 
+#ifdef PCADV_STAMPS
+// diagnostic build only: the stamps of a launch given no stamps buffer (the
+// chunk launch inside a step): [y * gridDim.x + x][32], trailing workgroups
+// stamp slot 0 (start) and 14 (end) and carry -1 in slot 15
+__device__ uint64_t g_chunk_stamps[1024][32];
+int chunk_stamps_read(uint64_t* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chunk_stamps), sizeof(g_chunk_stamps)) == hipSuccess
+             ? PCADV_OK
+             : PCADV_EHIP;
+}
+#endif
+
 // PRE: phases 1-3 (the hit sort) were done ahead of this launch (feat_sort.h,
 // records at sortrec): load them and gather the hits' gradients instead.
 template <bool PRE>
@@ -207,13 +225,27 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   // dispatched last, so they take the CU slots of the chunks that finish first
   // while the two-batch chunks run on.
   if ((int)blockIdx.y >= nclouds) {
+#ifdef PCADV_STAMPS
+    const size_t wg_ = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (!stamps && threadIdx.x == 0 && wg_ < 1024) g_chunk_stamps[wg_][0] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int b = ((int)blockIdx.y - nclouds) * (int)gridDim.x + (int)blockIdx.x;
     constexpr int NDW4 = BW_MAXO / (BW_T / 64 / DW4_WPC);
-    if (b < NDW4)
-      dw4_block<BW_T / 64>(b, reinterpret_cast<float4(*)[64]>(smem), dg, gidx, nclouds, N, O, x3,
+    const int nad = nb_adam0 + nb_adam1;
+    const bool is_dw4 = PCADV_TRAIL_ADAM_FIRST ? (b >= nad && b - nad < NDW4) : b < NDW4;
+    const int bd = PCADV_TRAIL_ADAM_FIRST ? b - nad : b, ba = PCADV_TRAIL_ADAM_FIRST ? b : b - NDW4;
+    if (is_dw4)
+      dw4_block<BW_T / 64>(bd, reinterpret_cast<float4(*)[64]>(smem), dg, gidx, nclouds, N, O, x3,
                            dw4, db4);
-    else if (b - NDW4 < nb_adam0 + nb_adam1)
-      adam_block<BW_T, FIN_ADAM_V4>(b - NDW4, nb_adam0, nb_adam1, fa);
+    else if (ba >= 0 && ba < nad)
+      adam_block<BW_T, FIN_ADAM_V4>(ba, nb_adam0, nb_adam1, fa);
+#ifdef PCADV_STAMPS
+    __syncthreads();
+    if (!stamps && threadIdx.x == 0 && wg_ < 1024) {
+      g_chunk_stamps[wg_][14] = __builtin_amdgcn_s_memrealtime();
+      g_chunk_stamps[wg_][15] = is_dw4 ? -1 : -2;
+    }
+#endif
     return;
   }
   BwdLds& L = *reinterpret_cast<BwdLds*>(smem);
@@ -221,10 +253,11 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   // diagnostic build only: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
   // 32 slots per workgroup: 0-15 by thread 0 (below); 16 + batch by thread 128
   // (wave 2) when its dZ3 gather loop is done; 24 + k: phase a of batch 1
-  uint64_t* st_ = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 32;
-#define BSTAMP(k) do { if (stamps && threadIdx.x == 0 && (k) < 15) st_[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define GSTAMP(k) do { if (stamps && threadIdx.x == 128 && (k) < 8) st_[16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define ASTAMP(k) do { if (stamps && threadIdx.x == 0 && b0 == 0) st_[24 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  const size_t wgi_ = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+  uint64_t* st_ = stamps ? stamps + wgi_ * 32 : (wgi_ < 1024 ? g_chunk_stamps[wgi_] : nullptr);
+#define BSTAMP(k) do { if (st_ && threadIdx.x == 0 && (k) < 15) st_[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define GSTAMP(k) do { if (st_ && threadIdx.x == 128 && (k) < 8) st_[16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define ASTAMP(k) do { if (st_ && threadIdx.x == 0 && b0 == 0) st_[24 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define BSTAMP(k) do { } while (0)
 #define GSTAMP(k) do { } while (0)
@@ -689,7 +722,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   else if (tid < 448) slab[SL_DB1 + tid - 384] = acc_b;
 #ifdef PCADV_STAMPS
   __syncthreads();
-  if (stamps && threadIdx.x == 0) { st_[14] = __builtin_amdgcn_s_memrealtime(); st_[15] = nact; }
+  if (st_ && threadIdx.x == 0) { st_[14] = __builtin_amdgcn_s_memrealtime(); st_[15] = nact; }
 #endif
 #undef BSTAMP
 #undef GSTAMP

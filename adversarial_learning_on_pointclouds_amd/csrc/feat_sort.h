@@ -36,6 +36,12 @@ struct SortLds {
 __device__ __forceinline__ void chunk_sort(const int32_t* __restrict__ gidx_c, int O, int p0, int t,
                                            bool valid, SortLds& L, int* __restrict__ rec) {
   const int lane = t & 63, wave = t >> 6;
+  int ga[2];  // the argmax rows, loaded before the counters are cleared
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int o = u * FS_T + t;
+    ga[u] = valid && o < O ? gidx_c[o] : -1;
+  }
   if (t < FS_PCH) {
     L.rcnt[t] = 0;
     L.fill[t] = 0;
@@ -44,8 +50,7 @@ __device__ __forceinline__ void chunk_sort(const int32_t* __restrict__ gidx_c, i
   int hrow[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int o = u * FS_T + t;
-    const int a = valid && o < O ? gidx_c[o] : -1;
+    const int a = ga[u];
     const bool hit = a >= p0 && a < p0 + FS_PCH;
     hrow[u] = hit ? a - p0 : -1;
     if (hit) atomicAdd(&L.rcnt[a - p0], 1);
