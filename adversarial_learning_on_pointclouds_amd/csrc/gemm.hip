@@ -1362,13 +1362,23 @@ int launch_split_bf2(const float* x, long long ld, int rows, int cols, void* hi,
 // forms db[o] (+)= sum dZ[.][o] and the per-group sums gsum[g][o] from the
 // column sums the slabs take of the staged dZ.  Enough slabs to give the
 // launch ~768 workgroups, each slab at least 128 rows.
+#ifndef PCADV_WGRAD_WGS
+#define PCADV_WGRAD_WGS 512  // one dispatch round (two 61 KB-LDS workgroups per CU)
+#endif
+#ifndef PCADV_WGRAD_FLOOR
+#define PCADV_WGRAD_FLOOR 0
+#endif
 struct WgradPlan { int groups, grp, zpg, len, nz; };
 static WgradPlan wgrad_plan(int rows, int O, int Kin, int rows_per_group) {
   WgradPlan w{};
   w.grp = rows_per_group > 0 ? rows_per_group : rows;
   w.groups = rows / w.grp;
   const int tiles = ((O + GM_BM - 1) / GM_BM) * ((Kin + GM_BN - 1) / GM_BN);
-  const int want = (768 + tiles * w.groups - 1) / (tiles * w.groups);
+#if PCADV_WGRAD_FLOOR
+  const int want = max(1, PCADV_WGRAD_WGS / (tiles * w.groups));
+#else
+  const int want = (PCADV_WGRAD_WGS + tiles * w.groups - 1) / (tiles * w.groups);
+#endif
   w.zpg = max(1, min(want, (w.grp + 127) / 128));
   w.len = (w.grp + w.zpg - 1) / w.zpg;
   w.zpg = (w.grp + w.len - 1) / w.len;

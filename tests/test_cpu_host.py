@@ -62,9 +62,9 @@ def test_workspace_sizes():
     # segmentation engine: point-axis slabs of the weight gradient (32 x O x K),
     # per-128-point-tile top-2 keys of conv6 + max, CE partials
     # 64 output tiles -> 12 slabs of the point axis (~768 workgroups); 16 clouds x 3
-    nz = 12
+    nz = 8  # 64 tiles x 8 slabs: the 512 workgroups of one dispatch round
     assert lib.pcadv_gemm_wgrad_workspace_bytes(32768, 2048, 512, 0) == (nz * 2048 * (512 + 1) + 2048) * 4 + 512
-    nz = 16 * 3
+    nz = 16 * 2
     assert lib.pcadv_gemm_wgrad_workspace_bytes(32768, 256, 960, 2048) == (nz * 256 * (960 + 1) + 16 * 256) * 4 + 512
     assert lib.pcadv_gemm_wgrad_workspace_bytes(300, 64, 3, 7) == 0  # rows % rows_per_group
     assert lib.pcadv_conv_max_x3_workspace_bytes(16, 2048, 2048) == 16 * 16 * 2048 * 8 + 256
