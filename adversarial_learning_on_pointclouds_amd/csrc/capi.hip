@@ -82,7 +82,8 @@ int launch_gemm_bf2(const void*, const void*, long long, const void*, const void
 int launch_split_bf2(const float*, long long, int, int, void*, void*, long long, hipStream_t);
 size_t gemm_wgrad_workspace_bytes(int, int, int, int);
 int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int, int, float*,
-                      long long, float*, float*, int, int, void*, size_t, hipStream_t);
+                      long long, float*, float*, int, int, void*, size_t, hipStream_t, int defer);
+int wgrad_flush(hipStream_t);
 size_t colsum_workspace_bytes(int, int);
 int launch_colsum(const float*, const float*, long long, long long, int, int, float*, int, void*,
                   size_t, hipStream_t);
@@ -609,8 +610,18 @@ int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, 
                      int Kin, float* dw, int64_t ldo, float* db, float* gsum, int rows_per_group,
                      int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
   return launch_gemm_wgrad(dz, ldz, x, ldx, rows, O, Kin, dw, ldo, db, gsum, rows_per_group,
-                           accumulate, workspace, workspace_bytes, stream);
+                           accumulate, workspace, workspace_bytes, stream, 0);
 }
+
+int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows,
+                           int O, int Kin, float* dw, int64_t ldo, float* db, float* gsum,
+                           int rows_per_group, int accumulate, void* workspace,
+                           size_t workspace_bytes, hipStream_t stream) {
+  return launch_gemm_wgrad(dz, ldz, x, ldx, rows, O, Kin, dw, ldo, db, gsum, rows_per_group,
+                           accumulate, workspace, workspace_bytes, stream, 1);
+}
+
+int pcadv_wgrad_flush(hipStream_t stream) { return wgrad_flush(stream); }
 
 size_t pcadv_colsum_workspace_bytes(int M, int N) { return colsum_workspace_bytes(M, N); }
 

@@ -983,15 +983,26 @@ k_slab_sum(const float* __restrict__ in, long long stride, int nz, long long E,
 // written to gs when asked) and then db from them (or from the column sums
 // directly when there is one group and no per-group output).
 constexpr int WF_MAXG = 64;
-__global__ void __launch_bounds__(256)
-k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __restrict__ dw, int N,
-               long long ldo, int acc_dw, int nb_dw, const float* __restrict__ csum, int O,
-               int groups, int zpg, int from_groups, float* __restrict__ gs, float* __restrict__ db,
-               int acc_db) {
+// One weight gradient's finishing reductions (the arguments of k_wgrad_finish)
+struct WfDesc {
+  const float* slabs; long long E; int nz; float* dw; int N; long long ldo; int acc_dw; int nb_dw;
+  const float* csum; int O; int groups; int zpg; int from_groups; float* gs; float* db;
+  int acc_db;
+};
+__device__ __forceinline__ void wgrad_finish_block(const WfDesc& w, int blk, float (&part)[8][33],
+                                                   float (&gsl)[WF_MAXG][33]) {
+  const float* __restrict__ slabs = w.slabs;
+  const long long E = w.E;
+  const int nz = w.nz, N = w.N, acc_dw = w.acc_dw, nb_dw = w.nb_dw, O = w.O, groups = w.groups;
+  const int zpg = w.zpg, from_groups = w.from_groups, acc_db = w.acc_db;
+  const long long ldo = w.ldo;
+  float* __restrict__ dw = w.dw;
+  const float* __restrict__ csum = w.csum;
+  float* __restrict__ gs = w.gs;
+  float* __restrict__ db = w.db;
   const int tid = threadIdx.x, el = tid & 31, zs = tid >> 5;
-  __shared__ float part[8][33];
-  if ((int)blockIdx.x < nb_dw) {
-    const long long e = (long long)blockIdx.x * 32 + el;
+  if (blk < nb_dw) {
+    const long long e = (long long)blk * 32 + el;
     part[zs][el] = e < E ? slab_subset(slabs + e, E, nz, zs) : 0.f;
     __syncthreads();
     if (zs == 0 && e < E) {
@@ -1001,7 +1012,7 @@ k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __re
     }
     return;
   }
-  const int o = ((int)blockIdx.x - nb_dw) * 32 + el;
+  const int o = (blk - nb_dw) * 32 + el;
   const bool ok = o < O;
   if (!from_groups) {
     part[zs][el] = ok ? slab_subset(csum + o, O, nz, zs) : 0.f;
@@ -1012,7 +1023,6 @@ k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __re
     }
     return;
   }
-  __shared__ float gsl[WF_MAXG][33];
   for (int g = 0; g < groups; ++g) {
     part[zs][el] = ok ? slab_subset(csum + (size_t)g * zpg * O + o, O, zpg, zs) : 0.f;
     __syncthreads();
@@ -1037,6 +1047,38 @@ k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __re
     const float t = slab_combine(part, el);
     db[o] = acc_db ? db[o] + t : t;
   }
+}
+
+__global__ void __launch_bounds__(256)
+k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __restrict__ dw, int N,
+               long long ldo, int acc_dw, int nb_dw, const float* __restrict__ csum, int O,
+               int groups, int zpg, int from_groups, float* __restrict__ gs, float* __restrict__ db,
+               int acc_db) {
+  __shared__ float part[8][33];
+  __shared__ float gsl[WF_MAXG][33];
+  const WfDesc w{slabs, E, nz, dw, N, ldo, acc_dw, nb_dw, csum, O, groups, zpg, from_groups, gs, db,
+                 acc_db};
+  wgrad_finish_block(w, (int)blockIdx.x, part, gsl);
+}
+
+// Several weight gradients' finishing reductions in one launch (deferred by
+// launch_gemm_wgrad(..., defer = 1) until pcadv_wgrad_flush): block b belongs
+// to the descriptor whose block range [blk0[i], blk0[i + 1]) holds it; every
+// sum is bitwise the one k_wgrad_finish forms.
+constexpr int WF_BATCH = 16;
+struct WfBatch {
+  WfDesc d[WF_BATCH];
+  int blk0[WF_BATCH + 1];
+  int n;
+};
+__global__ void __launch_bounds__(256)
+k_wgrad_finish_batch(WfBatch bt) {
+  __shared__ float part[8][33];
+  __shared__ float gsl[WF_MAXG][33];
+  const int b = (int)blockIdx.x;
+  int i = 0;
+  for (int j = 1; j < bt.n; ++j) i = b >= bt.blk0[j] ? j : i;
+  wgrad_finish_block(bt.d[i], b - bt.blk0[i], part, gsl);
 }
 
 // column sums of an M x N matrix (row stride ld), optionally masked by [Y > 0]
@@ -1392,9 +1434,34 @@ size_t gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) 
   return ((size_t)w.nz * O * Kin + (size_t)w.nz * O + (size_t)w.groups * O) * sizeof(float) + 512;
 }
 
+// the deferred finishing reductions of this thread's weight gradients
+static thread_local WfBatch g_wf_pending{};
+
+int wgrad_flush(hipStream_t s) {
+  WfBatch& b = g_wf_pending;
+  if (b.n == 0) return PCADV_OK;
+  const int nblk = b.blk0[b.n];
+  hipLaunchKernelGGL(k_wgrad_finish_batch, dim3((unsigned)nblk), dim3(256), 0, s, b);
+  b.n = 0;
+  b.blk0[0] = 0;
+  PC_HIP_CHECK_LAUNCH("k_wgrad_finish_batch");
+  return PCADV_OK;
+}
+
+static int wgrad_defer(const WfDesc& d, int nb, hipStream_t s) {
+  if (nb <= 0) return PCADV_OK;
+  if (g_wf_pending.n == WF_BATCH) PC_TRY_GEMM(wgrad_flush(s));
+  WfBatch& b = g_wf_pending;
+  b.d[b.n] = d;
+  b.blk0[b.n + 1] = b.blk0[b.n] + nb;
+  ++b.n;
+  return PCADV_OK;
+}
+
 int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long ldx, int rows,
                       int O, int Kin, float* dw, long long ldo, float* db, float* gsum,
-                      int rows_per_group, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+                      int rows_per_group, int accumulate, void* ws, size_t ws_bytes, hipStream_t s,
+                      int defer) {
   PC_REQUIRE(dz && x && dw && rows > 0 && O > 0 && Kin > 0 && ldo >= Kin && ldz >= O && ldx >= Kin,
              "gemm_wgrad: bad shape rows=%d O=%d Kin=%d", rows, O, Kin);
   PC_REQUIRE(!gsum || (rows_per_group > 0 && rows % rows_per_group == 0),
@@ -1418,6 +1485,26 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
   p.csum = csum;
   PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(p, w.nz, s)));
   const long long E = (long long)O * Kin;
+  if (defer) {
+    // the dW slab sums (and db, unless the per-group sums are wanted now) wait
+    // for wgrad_flush, which runs every deferred finish in one launch
+    PC_REQUIRE(w.groups <= WF_MAXG, "gemm_wgrad: %d groups cannot be deferred", w.groups);
+    const int nb_dw = (int)((E + 31) / 32);
+    const int nb_cs = csum ? (O + 31) / 32 : 0;
+    const bool from_groups = w.groups > 1 || gsum;
+    const WfDesc all{slabs, E, w.nz, dw, Kin, ldo, accumulate, nb_dw, csum, O, w.groups, w.zpg,
+                     from_groups ? 1 : 0, gsum, db, accumulate};
+    if (!gsum) return wgrad_defer(all, nb_dw + nb_cs, s);
+    hipLaunchKernelGGL(k_wgrad_finish, dim3((unsigned)nb_cs), dim3(256), 0, s,
+                       static_cast<const float*>(slabs), E, w.nz, dw, Kin, ldo, accumulate, 0,
+                       static_cast<const float*>(csum), O, w.groups, w.zpg, 1, gsum, db, accumulate);
+    PC_HIP_CHECK_LAUNCH("k_wgrad_finish (groups)");
+    WfDesc dwo = all;
+    dwo.csum = nullptr;
+    dwo.gs = nullptr;
+    dwo.db = nullptr;
+    return wgrad_defer(dwo, nb_dw, s);
+  }
   if (w.groups <= WF_MAXG && !getenv_flag("PCADV_WGRAD_SPLIT_FINISH")) {
     // dW, the per-group sums and db in one launch (k_wgrad_finish)
     const int nb_dw = (int)((E + 31) / 32);

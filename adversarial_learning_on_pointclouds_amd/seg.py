@@ -63,6 +63,8 @@ class _Engine:
 
     def __init__(self):
         self.lib = _lib.load()
+        self._pending = []  # workspaces of the deferred weight-gradient finishes
+
 
     def gemm(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, cmask=None, ldm=0, bias=None,
              bias_rows=None, rows_per_group=0, relu=False, accumulate=False, precise=False,
@@ -96,13 +98,24 @@ class _Engine:
               "pcadv_split_bf2")
 
     def wgrad(self, dz, ldz, x, ldx, rows, O, K, dw, ldo, *, db=None, gsum=None, rpg=0, dz_off=0,
-              x_off=0, dw_off=0):
+              x_off=0, dw_off=0, defer=False):
+        """defer: the finishing slab sums of dw (and db) wait for flush(), which
+        runs all pending ones in one launch; the workspace is held until then."""
         nb = self.lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K, rpg)
         ws = _ws(nb, dz.device)
-        check(self.lib.pcadv_gemm_wgrad(_p(dz, dz_off), ldz, _p(x, x_off), ldx, rows, O, K,
-                                        _p(dw, dw_off), ldo, None if db is None else _p(db),
-                                        None if gsum is None else _p(gsum), rpg, 0, _p(ws),
-                                        ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
+        fn = self.lib.pcadv_gemm_wgrad_defer if defer else self.lib.pcadv_gemm_wgrad
+        check(fn(_p(dz, dz_off), ldz, _p(x, x_off), ldx, rows, O, K, _p(dw, dw_off), ldo,
+                 None if db is None else _p(db), None if gsum is None else _p(gsum), rpg, 0, _p(ws),
+                 ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
+        if defer:
+            self._pending.append(ws)
+
+    def flush(self):
+        """Enqueue the deferred weight-gradient finishes (one launch)."""
+        try:
+            check(self.lib.pcadv_wgrad_flush(stream_ptr()), "pcadv_wgrad_flush")
+        finally:
+            self._pending.clear()  # stream order keeps the slabs until the launch has read them
 
     def colsum(self, x, ld, M, N, out, *, ymask=None, ldm=0, x_off=0, m_off=0):
         nb = self.lib.pcadv_colsum_workspace_bytes(M, N)
@@ -118,6 +131,11 @@ class _Engine:
 
 
 _ENGINE = None
+
+
+# weight gradients' finishing slab sums deferred and run in one launch at the
+# end of the backward (PCADV_WGRAD_DEFER=0: one launch after each, for A/B runs)
+_DEFER = os.environ.get("PCADV_WGRAD_DEFER", "1") != "0"
 
 
 def _engine():
@@ -260,24 +278,24 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         return torch.empty_like(like) if hasattr(like, "shape") else torch.empty(like, device=dev)
     # ---- fc4 .. fc2 -------------------------------------------------------
     dW4 = _g(18, Wf[3]); db4 = _g(19, ncls)
-    E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128, db=db4)
+    E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128, db=db4, defer=_DEFER)
     dh3 = torch.empty(M, 128, device=dev)
     E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3, ldm=128, precise=_DGRAD_PRECISE)
     dW3 = _g(16, Wf[2]); db3 = _g(17, 128)
-    E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, db=db3)
+    E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, db=db3, defer=_DEFER)
     dh2 = torch.empty(M, 256, device=dev)
     E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2, ldm=256, precise=_DGRAD_PRECISE)
     dW2 = _g(14, Wf[1]); db2 = _g(15, 256)
-    E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, db=db2)
+    E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, db=db2, defer=_DEFER)
     dh1 = torch.empty(M, 256, device=dev)
     E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1, ldm=256, precise=_DGRAD_PRECISE)
     # ---- fc1: local columns (+ per-cloud sums s1), then the tiled columns --
     W1 = Wf[0]
     dW1 = _g(12, W1); db1 = _g(13, 256)
     s1 = torch.empty(B, 256, device=dev)  # per-cloud sums of dz1
-    E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N)
-    E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960)
-    E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008)
+    E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N, defer=_DEFER)
+    E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, defer=_DEFER)
+    E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008, defer=_DEFER)
     dloc = torch.empty(M, _LOC, device=dev)
     E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc, ldm=_LOC, precise=_DGRAD_PRECISE)
     dg = torch.empty(B, 2048, device=dev)
@@ -300,12 +318,14 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         dbc[i] = _g(2 * i + 1, O)
         if i > 0:
             E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i],
-                    x_off=_OFF[i - 1])
+                    x_off=_OFF[i - 1], defer=_DEFER)
             E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, cmask=xloc, ldm=_LOC,
                    accumulate=True, precise=_DGRAD_PRECISE, a_off=_OFF[i], m_off=_OFF[i - 1],
                    c_off=_OFF[i - 1])
         else:
-            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i])
+            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i], defer=_DEFER)
+    # every weight gradient's slab sums (deferred above) in one launch
+    E.flush()
     grads = []
     for i in range(6):
         grads += [dWc[i].view(O_shape(i)), dbc[i]]

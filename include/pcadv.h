@@ -258,6 +258,17 @@ size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_g
 int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows, int O,
                      int Kin, float* dw, int64_t ldo, float* db, float* gsum, int rows_per_group,
                      int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream);
+/* The same weight gradient with its finishing slab sums deferred: the GEMM is
+ * enqueued now, the dw (and db) sums join this thread's pending list and run,
+ * with every other pending one, in ONE launch at pcadv_wgrad_flush (gsum, when
+ * given, is formed now).  dw, db and the workspace must stay valid and
+ * untouched until the flush is enqueued; results are bitwise those of
+ * pcadv_gemm_wgrad. */
+int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows,
+                           int O, int Kin, float* dw, int64_t ldo, float* db, float* gsum,
+                           int rows_per_group, int accumulate, void* workspace,
+                           size_t workspace_bytes, hipStream_t stream);
+int pcadv_wgrad_flush(hipStream_t stream);
 
 /* Column sums (bias gradients): out[n] (+)= sum_m x[m][n] [ymask[m][n] > 0];
  * pcadv_group_colsum writes one row of sums per rows_per_group rows. */

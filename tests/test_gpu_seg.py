@@ -297,6 +297,47 @@ def test_gemm_weight_grad(rows, rpg, O, K):
         assert torch.equal(outs["0"][2], a_gs)
 
 
+def test_gemm_weight_grad_deferred_batch_is_bitwise():
+    """pcadv_gemm_wgrad_defer + pcadv_wgrad_flush: the finishing slab sums of
+    several weight gradients (plain, accumulating, with per-group sums, and
+    more than one batch of descriptors) run in one launch per flush and give
+    bitwise the results of the immediate pcadv_gemm_wgrad calls."""
+    lib = _lib.load()
+    shapes = [(300, 100, 96, 40), (32768, 2048, 96, 40), (32768, 0, 256, 960), (16, 0, 256, 2048),
+              (4096, 0, 64, 3)] * 4  # 20 > one batch of 16 descriptors
+    cases = []
+    for i, (rows, rpg, O, K) in enumerate(shapes):
+        rng = np.random.default_rng(100 + i)
+        dZ = _t(rng.standard_normal((rows, O)).astype(np.float32))
+        X = _t(rng.standard_normal((rows, K)).astype(np.float32))
+        G = rows // rpg if rpg else 1
+        nb = lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K, rpg)
+        acc = i % 3 == 2
+        init = _t(rng.standard_normal((O, K)).astype(np.float32)), _t(rng.standard_normal(O).astype(np.float32))
+        cases.append((rows, rpg, O, K, G, nb, acc, dZ, X, init))
+
+    def run(defer):
+        outs, keep = [], []
+        fn = lib.pcadv_gemm_wgrad_defer if defer else lib.pcadv_gemm_wgrad
+        for rows, rpg, O, K, G, nb, acc, dZ, X, (w0, b0) in cases:
+            dW, db = w0.clone(), b0.clone()
+            gs = torch.zeros(G, O, device=DEV)
+            ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+            keep.append(ws)
+            check(fn(_p(dZ), O, _p(X), K, rows, O, K, _p(dW), K, _p(db), _p(gs) if rpg else None,
+                     rpg, int(acc), _p(ws), nb, stream_ptr()), "wgrad")
+            outs.append((dW, db, gs))
+        if defer:
+            check(lib.pcadv_wgrad_flush(stream_ptr()), "flush")
+        torch.cuda.synchronize()
+        return outs
+
+    for a, b in zip(run(False), run(True)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    check(lib.pcadv_wgrad_flush(stream_ptr()), "flush of an empty list")
+
+
 def test_colsum_and_group_colsum():
     lib = _lib.load()
     rng = np.random.default_rng(5)
