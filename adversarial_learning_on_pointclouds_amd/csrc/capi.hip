@@ -84,6 +84,8 @@ size_t gemm_wgrad_workspace_bytes(int, int, int, int);
 int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int, int, float*,
                       long long, float*, float*, int, int, void*, size_t, hipStream_t, int defer);
 int wgrad_flush(hipStream_t);
+int gemm_pair_begin(hipStream_t);
+int gemm_pair_end(hipStream_t);
 size_t colsum_workspace_bytes(int, int);
 int launch_colsum(const float*, const float*, long long, long long, int, int, float*, int, void*,
                   size_t, hipStream_t);
@@ -622,6 +624,9 @@ int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t
 }
 
 int pcadv_wgrad_flush(hipStream_t stream) { return wgrad_flush(stream); }
+
+int pcadv_gemm_pair_begin(hipStream_t stream) { return gemm_pair_begin(stream); }
+int pcadv_gemm_pair_end(hipStream_t stream) { return gemm_pair_end(stream); }
 
 size_t pcadv_colsum_workspace_bytes(int M, int N) { return colsum_workspace_bytes(M, N); }
 

@@ -264,9 +264,11 @@ __device__ __forceinline__ void epilogue_rows(const GemmP& p, float* C, const fl
 
 // VEC bit 0 / bit 1: A / B staged by 16-byte loads (vector-aligned, no
 // vector straddles an edge), else by dword loads
+// The body of one workgroup of k_gemm_x3: linear block id lin of a
+// gx x gy x gz grid (k_gemm_x3 passes its own; the pair kernel below runs two
+// GEMMs' workgroups in one launch)
 template <int TA, int TB, int MODE, int NP, int VEC>
-__global__ void __launch_bounds__(GM_T)
-k_gemm_x3(GemmP p) {
+__device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, int gy, int gzn) {
   constexpr int NPL = NP == 6 ? 3 : 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GemmLds& L = *reinterpret_cast<GemmLds*>(smem);
@@ -278,9 +280,7 @@ k_gemm_x3(GemmP p) {
   // sharing a row tile of A run together on one XCD and read it from its L2
   int tx, ty, tz;
   {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int n = gx * gy * gridDim.z;
-    const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int n = gx * gy * gzn;
     const int xcd = lin & 7, q = n >> 3, rr = n & 7;
     const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (lin >> 3);
     tz = t / (gx * gy);
@@ -580,6 +580,33 @@ k_gemm_x3(GemmP p) {
       else epilogue_rows_plain<MODE>(p, C, stage, ES, c4, tid >> 4, 16, 8, m0, n);
     }
   }
+}
+
+template <int TA, int TB, int MODE, int NP, int VEC>
+__global__ void __launch_bounds__(GM_T)
+k_gemm_x3(GemmP p) {
+  gemm_x3_body<TA, TB, MODE, NP, VEC>(
+      p, (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)), (int)gridDim.x,
+      (int)gridDim.y, (int)gridDim.z);
+}
+
+// A weight gradient (six products, TA = TB = 1, slabs) and an independent data
+// gradient (TA = 0, TB = 1, three products) in ONE launch: workgroups
+// [0, n_first) run the first of the two, the rest the second (wfirst: the
+// weight gradient first).  Each keeps its own grid geometry and XCD order, so
+// every output is bitwise what its own launch gives; the pair saves a launch
+// boundary and lets the two fill each other's idle CUs (the segmentation
+// backward's per-layer weight and data gradients both read that layer's dz).
+struct PairGeom { int n, gx, gy, gz; };
+template <int VW, int MD, int VD>
+__global__ void __launch_bounds__(GM_T)
+k_gemm_x3_pair(GemmP pw, PairGeom gw, GemmP pd, PairGeom gd, int wfirst) {
+  const int b = (int)blockIdx.x;
+  const int nfirst = wfirst ? gw.n : gd.n;
+  const bool w = (b < nfirst) == (wfirst != 0);
+  const int lin = b < nfirst ? b : b - nfirst;
+  if (w) gemm_x3_body<1, 1, 0, 6, VW>(pw, lin, gw.gx, gw.gy, gw.gz);
+  else gemm_x3_body<0, 1, MD, 3, VD>(pd, lin, gd.gx, gd.gy, gd.gz);
 }
 
 // ---------------------------------------------------------------------------
@@ -1241,21 +1268,128 @@ static bool fits31(long long rows, long long ld, int esz) {
   return rows >= 0 && ld >= 0 && (rows * ld + 16) * esz < 0x7fffffffLL;
 }
 
+template <typename K>
+static int gemm_lds_attr(K kern) {
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)sizeof(GemmLds)) != hipSuccess) {
+    set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(GemmLds));
+    return PCADV_EHIP;
+  }
+  return PCADV_OK;
+}
+
 template <int TA, int TB, int MODE, int NP, int VEC>
-static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s) {
+static int gemm_launch_direct(const GemmP& p, dim3 grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_x3<TA, TB, MODE, NP, VEC>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(GemmLds)) != hipSuccess) {
-      set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(GemmLds));
-      return PCADV_EHIP;
-    }
+    PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3<TA, TB, MODE, NP, VEC>));
     attr = true;
   }
   hipLaunchKernelGGL((k_gemm_x3<TA, TB, MODE, NP, VEC>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
   PC_HIP_CHECK_LAUNCH("k_gemm_x3");
   return PCADV_OK;
+}
+
+// Pair recording (pcadv_gemm_pair_begin / _end): the first weight-gradient or
+// data-gradient GEMM launched after begin waits; the next one of the other
+// kind launches both as one k_gemm_x3_pair.  Anything else launched by the
+// engine first enqueues the waiting GEMM alone (stream order is kept).
+struct PendingGemm {
+  bool on, has;
+  int kind;  // 0: weight gradient <1, 1, 0, 6, v>; 1: data gradient <0, 1, mode, 3, v>
+  int v, mode;
+  GemmP p;
+  dim3 grid;
+};
+static thread_local PendingGemm g_pair{};
+
+static PairGeom pair_geom(dim3 g) {
+  return PairGeom{(int)(g.x * g.y * g.z), (int)g.x, (int)g.y, (int)g.z};
+}
+
+static int gemm_pair_flush(hipStream_t s) {
+  if (!g_pair.has) return PCADV_OK;
+  g_pair.has = false;
+  const GemmP& p = g_pair.p;
+  const dim3 g = g_pair.grid;
+  if (g_pair.kind == 0) {
+    switch (g_pair.v) {
+      case 1: return gemm_launch_direct<1, 1, 0, 6, 1>(p, g, s);
+      case 2: return gemm_launch_direct<1, 1, 0, 6, 2>(p, g, s);
+      default: return gemm_launch_direct<1, 1, 0, 6, 3>(p, g, s);
+    }
+  }
+  if (g_pair.mode == 0)
+    return g_pair.v == 2 ? gemm_launch_direct<0, 1, 0, 3, 2>(p, g, s)
+                         : gemm_launch_direct<0, 1, 0, 3, 3>(p, g, s);
+  return g_pair.v == 2 ? gemm_launch_direct<0, 1, 1, 3, 2>(p, g, s)
+                       : gemm_launch_direct<0, 1, 1, 3, 3>(p, g, s);
+}
+
+template <int VW, int MD, int VD>
+static int gemm_pair_launch(const GemmP& pw, dim3 gw, const GemmP& pd, dim3 gd, int wfirst,
+                            hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3_pair<VW, MD, VD>));
+    attr = true;
+  }
+  const PairGeom a = pair_geom(gw), b = pair_geom(gd);
+  hipLaunchKernelGGL((k_gemm_x3_pair<VW, MD, VD>), dim3((unsigned)(a.n + b.n)), dim3(GM_T),
+                     sizeof(GemmLds), s, pw, a, pd, b, wfirst);
+  PC_HIP_CHECK_LAUNCH("k_gemm_x3_pair");
+  return PCADV_OK;
+}
+
+template <int TA, int TB, int MODE, int NP, int VEC>
+static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s) {
+  constexpr bool is_w = TA == 1 && TB == 1 && MODE == 0 && NP == 6 && VEC >= 1;
+  constexpr bool is_d = TA == 0 && TB == 1 && (MODE == 0 || MODE == 1) && NP == 3 && VEC >= 2;
+  if constexpr (is_w || is_d) {
+    if (g_pair.on) {
+      if (g_pair.has && g_pair.kind == (is_w ? 1 : 0)) {  // the pair's second GEMM
+        g_pair.has = false;
+        if constexpr (is_w) {
+          const GemmP& pd = g_pair.p;
+          const dim3 gd = g_pair.grid;
+          if (g_pair.mode == 0)
+            return g_pair.v == 2 ? gemm_pair_launch<VEC, 0, 2>(p, grid, pd, gd, 0, s)
+                                 : gemm_pair_launch<VEC, 0, 3>(p, grid, pd, gd, 0, s);
+          return g_pair.v == 2 ? gemm_pair_launch<VEC, 1, 2>(p, grid, pd, gd, 0, s)
+                               : gemm_pair_launch<VEC, 1, 3>(p, grid, pd, gd, 0, s);
+        } else {
+          const GemmP& pw = g_pair.p;
+          const dim3 gw = g_pair.grid;
+          switch (g_pair.v) {
+            case 1: return gemm_pair_launch<1, MODE, VEC>(pw, gw, p, grid, 1, s);
+            case 2: return gemm_pair_launch<2, MODE, VEC>(pw, gw, p, grid, 1, s);
+            default: return gemm_pair_launch<3, MODE, VEC>(pw, gw, p, grid, 1, s);
+          }
+        }
+      }
+      PC_TRY_GEMM(gemm_pair_flush(s));  // a waiting GEMM of the same kind goes alone
+      g_pair.has = true;
+      g_pair.kind = is_w ? 0 : 1;
+      g_pair.v = VEC;
+      g_pair.mode = MODE;
+      g_pair.p = p;
+      g_pair.grid = grid;
+      return PCADV_OK;
+    }
+  }
+  PC_TRY_GEMM(gemm_pair_flush(s));
+  return gemm_launch_direct<TA, TB, MODE, NP, VEC>(p, grid, s);
+}
+
+int gemm_pair_begin(hipStream_t s) {
+  PC_TRY_GEMM(gemm_pair_flush(s));
+  g_pair.on = true;
+  return PCADV_OK;
+}
+int gemm_pair_end(hipStream_t s) {
+  g_pair.on = false;
+  return gemm_pair_flush(s);
 }
 
 // the staging form of each operand: 16-byte loads where the operand allows
@@ -1438,6 +1572,7 @@ size_t gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) 
 static thread_local WfBatch g_wf_pending{};
 
 int wgrad_flush(hipStream_t s) {
+  PC_TRY_GEMM(gemm_pair_flush(s));  // a waiting GEMM writes slabs this launch reads
   WfBatch& b = g_wf_pending;
   if (b.n == 0) return PCADV_OK;
   const int nblk = b.blk0[b.n];
@@ -1485,6 +1620,7 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
   p.csum = csum;
   PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(p, w.nz, s)));
   const long long E = (long long)O * Kin;
+  if (!defer) PC_TRY_GEMM(gemm_pair_flush(s));  // the finishing launches read its slabs
   if (defer) {
     // the dW slab sums (and db, unless the per-group sums are wanted now) wait
     // for wgrad_flush, which runs every deferred finish in one launch
@@ -1495,6 +1631,7 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
     const WfDesc all{slabs, E, w.nz, dw, Kin, ldo, accumulate, nb_dw, csum, O, w.groups, w.zpg,
                      from_groups ? 1 : 0, gsum, db, accumulate};
     if (!gsum) return wgrad_defer(all, nb_dw + nb_cs, s);
+    PC_TRY_GEMM(gemm_pair_flush(s));  // the slabs' GEMM may be waiting for its pair
     hipLaunchKernelGGL(k_wgrad_finish, dim3((unsigned)nb_cs), dim3(256), 0, s,
                        static_cast<const float*>(slabs), E, w.nz, dw, Kin, ldo, accumulate, 0,
                        static_cast<const float*>(csum), O, w.groups, w.zpg, 1, gsum, db, accumulate);

@@ -22,6 +22,7 @@ layer); tests/test_gpu_seg.py holds the tolerances.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -110,6 +111,20 @@ class _Engine:
         if defer:
             self._pending.append(ws)
 
+    @contextlib.contextmanager
+    def pair(self):
+        """A weight-gradient GEMM and an independent data-gradient GEMM issued
+        inside run as ONE launch (pcadv_gemm_pair_begin / _end); PCADV_GEMM_PAIR=0:
+        two launches, for A/B runs."""
+        if not _PAIR:
+            yield
+            return
+        check(self.lib.pcadv_gemm_pair_begin(stream_ptr()), "pcadv_gemm_pair_begin")
+        try:
+            yield
+        finally:
+            check(self.lib.pcadv_gemm_pair_end(stream_ptr()), "pcadv_gemm_pair_end")
+
     def flush(self):
         """Enqueue the deferred weight-gradient finishes (one launch)."""
         try:
@@ -136,6 +151,8 @@ _ENGINE = None
 # weight gradients' finishing slab sums deferred and run in one launch at the
 # end of the backward (PCADV_WGRAD_DEFER=0: one launch after each, for A/B runs)
 _DEFER = os.environ.get("PCADV_WGRAD_DEFER", "1") != "0"
+# each layer's weight and data gradients in one launch (_Engine.pair)
+_PAIR = os.environ.get("PCADV_GEMM_PAIR", "1") != "0"
 
 
 def _engine():
@@ -278,26 +295,30 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         return torch.empty_like(like) if hasattr(like, "shape") else torch.empty(like, device=dev)
     # ---- fc4 .. fc2 -------------------------------------------------------
     dW4 = _g(18, Wf[3]); db4 = _g(19, ncls)
-    E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128, db=db4, defer=_DEFER)
     dh3 = torch.empty(M, 128, device=dev)
-    E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3, ldm=128, precise=_DGRAD_PRECISE)
+    with E.pair():
+        E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128, db=db4, defer=_DEFER)
+        E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3, ldm=128, precise=_DGRAD_PRECISE)
     dW3 = _g(16, Wf[2]); db3 = _g(17, 128)
-    E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, db=db3, defer=_DEFER)
     dh2 = torch.empty(M, 256, device=dev)
-    E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2, ldm=256, precise=_DGRAD_PRECISE)
+    with E.pair():
+        E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, db=db3, defer=_DEFER)
+        E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2, ldm=256, precise=_DGRAD_PRECISE)
     dW2 = _g(14, Wf[1]); db2 = _g(15, 256)
-    E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, db=db2, defer=_DEFER)
     dh1 = torch.empty(M, 256, device=dev)
-    E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1, ldm=256, precise=_DGRAD_PRECISE)
+    with E.pair():
+        E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, db=db2, defer=_DEFER)
+        E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1, ldm=256, precise=_DGRAD_PRECISE)
     # ---- fc1: local columns (+ per-cloud sums s1), then the tiled columns --
     W1 = Wf[0]
     dW1 = _g(12, W1); db1 = _g(13, 256)
     s1 = torch.empty(B, 256, device=dev)  # per-cloud sums of dz1
-    E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N, defer=_DEFER)
+    dloc = torch.empty(M, _LOC, device=dev)
+    with E.pair():  # the data gradient first: the weight gradient's group sums follow its launch
+        E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc, ldm=_LOC, precise=_DGRAD_PRECISE)
+        E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N, defer=_DEFER)
     E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, defer=_DEFER)
     E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008, defer=_DEFER)
-    dloc = torch.empty(M, _LOC, device=dev)
-    E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc, ldm=_LOC, precise=_DGRAD_PRECISE)
     dg = torch.empty(B, 2048, device=dev)
     E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=_DGRAD_PRECISE)
     if dgmax_out is not None:
@@ -317,11 +338,12 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         dWc[i] = _g(2 * i, W[i])
         dbc[i] = _g(2 * i + 1, O)
         if i > 0:
-            E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i],
-                    x_off=_OFF[i - 1], defer=_DEFER)
-            E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, cmask=xloc, ldm=_LOC,
-                   accumulate=True, precise=_DGRAD_PRECISE, a_off=_OFF[i], m_off=_OFF[i - 1],
-                   c_off=_OFF[i - 1])
+            with E.pair():
+                E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i],
+                        x_off=_OFF[i - 1], defer=_DEFER)
+                E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, cmask=xloc, ldm=_LOC,
+                       accumulate=True, precise=_DGRAD_PRECISE, a_off=_OFF[i], m_off=_OFF[i - 1],
+                       c_off=_OFF[i - 1])
         else:
             E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i], defer=_DEFER)
     # every weight gradient's slab sums (deferred above) in one launch

@@ -269,6 +269,14 @@ int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t
                            int rows_per_group, int accumulate, void* workspace,
                            size_t workspace_bytes, hipStream_t stream);
 int pcadv_wgrad_flush(hipStream_t stream);
+/* Pair a weight-gradient GEMM (pcadv_gemm_wgrad[_defer]) with an independent
+ * data-gradient GEMM (pcadv_gemm with ta = 0, tb = 1): between begin and end
+ * the first of the two waits and the second launches both as ONE kernel
+ * (their workgroups side by side, each output bitwise its own launch's).  Only
+ * those two calls may sit between begin and end on this thread; end enqueues a
+ * GEMM still waiting. */
+int pcadv_gemm_pair_begin(hipStream_t stream);
+int pcadv_gemm_pair_end(hipStream_t stream);
 
 /* Column sums (bias gradients): out[n] (+)= sum_m x[m][n] [ymask[m][n] > 0];
  * pcadv_group_colsum writes one row of sums per rows_per_group rows. */

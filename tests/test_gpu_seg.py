@@ -246,6 +246,34 @@ def test_seg_forward_planes_path_is_bitwise_the_f32_path():
         assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("B,N", [(2, 700), (4, 2048)])
+def test_seg_backward_paired_and_deferred_launches_are_bitwise(B, N):
+    """The backward's launch forms: each layer's weight and data gradients as
+    one paired launch (_Engine.pair) and the weight gradients' slab sums
+    deferred to one launch (pcadv_wgrad_flush) give bitwise the gradients of
+    one launch per GEMM and per finishing reduction."""
+    from adversarial_learning_on_pointclouds_amd import seg as segmod
+    torch.manual_seed(5)
+    m = PointNetSeg(50).to(DEV)
+    params = list(m.parameters())
+    pts = torch.rand(B, N, 3, device=DEV) * 2 - 1
+    cls = torch.zeros(B, 1, 16, device=DEV)
+    cls[:, 0, 3] = 1
+    fw = seg_forward(pts, cls, params)
+    dl = torch.randn(B * N, 50, device=DEV) * 1e-3
+    saved = segmod._PAIR, segmod._DEFER
+    outs = []
+    try:
+        for pair, defer in ((False, False), (True, False), (False, True), (True, True)):
+            segmod._PAIR, segmod._DEFER = pair, defer
+            outs.append([g.clone() for g in seg_backward(fw, dl)])
+    finally:
+        segmod._PAIR, segmod._DEFER = saved
+    for got in outs[1:]:
+        for k, (x, y) in enumerate(zip(outs[0], got)):
+            assert torch.equal(x, y), k
+
+
 @pytest.mark.parametrize("rows,rpg,O,K", [(300, 100, 96, 40), (32768, 2048, 96, 40),
                                           (32768, 0, 256, 960), (16, 0, 256, 2048),
                                           (4096, 0, 64, 3)])
