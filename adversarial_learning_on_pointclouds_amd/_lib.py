@@ -109,6 +109,8 @@ SIGNATURES = {
                                     _vp, _sz, _vp]),
     "pcadv_wgrad_flush": (_i, [_vp]),
     "pcadv_gemm_pair_begin": (_i, [_vp]),
+    "pcadv_wgrad_small": (_i, [_vp, _i64, _i, _i, _vp, _i64, _i, _vp, _vp, _i64, _i, _vp, _i64, _i,
+                               _vp]),
     "pcadv_gemm_pair_end": (_i, [_vp]),
     "pcadv_colsum_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_colsum": (_i, [_vp, _vp, _i64, _i64, _i, _i, _vp, _i, _vp, _sz, _vp]),

@@ -85,6 +85,8 @@ int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int
                       long long, float*, float*, int, int, void*, size_t, hipStream_t, int defer);
 int wgrad_flush(hipStream_t);
 int gemm_pair_begin(hipStream_t);
+int launch_wgrad_small(const float*, long long, int, int, const float*, long long, int, float*,
+                       const float*, long long, int, float*, long long, int, hipStream_t);
 int gemm_pair_end(hipStream_t);
 size_t colsum_workspace_bytes(int, int);
 int launch_colsum(const float*, const float*, long long, long long, int, int, float*, int, void*,
@@ -626,6 +628,13 @@ int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t
 int pcadv_wgrad_flush(hipStream_t stream) { return wgrad_flush(stream); }
 
 int pcadv_gemm_pair_begin(hipStream_t stream) { return gemm_pair_begin(stream); }
+
+int pcadv_wgrad_small(const float* s, int64_t lds, int B, int O, const float* x0, int64_t ldx0,
+                      int K0, float* dw0, const float* x1, int64_t ldx1, int K1, float* dw1,
+                      int64_t ldo, int accumulate, hipStream_t stream) {
+  return launch_wgrad_small(s, lds, B, O, x0, ldx0, K0, dw0, x1, ldx1, K1, dw1, ldo, accumulate,
+                            stream);
+}
 int pcadv_gemm_pair_end(hipStream_t stream) { return gemm_pair_end(stream); }
 
 size_t pcadv_colsum_workspace_bytes(int M, int N) { return colsum_workspace_bytes(M, N); }

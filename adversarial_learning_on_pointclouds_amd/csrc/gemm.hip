@@ -1568,6 +1568,56 @@ size_t gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) 
   return ((size_t)w.nz * O * Kin + (size_t)w.nz * O + (size_t)w.groups * O) * sizeof(float) + 512;
 }
 
+// Weight gradients over a few rows (fc1's tiled global columns: the B
+// per-cloud sums s[b][o] times gmax / the class vector, pointnet.py:306-310):
+// dw[o][k] (+)= sum_{b < B} s[b][o] x[b][k] in exact f32, b in order (fixed,
+// deterministic), four k per thread; up to two x operands (jobs) per launch,
+// blocks [0, nb0) on job 0.  Replaces a six-product slab GEMM over B = 16
+// rows (one k-tile of work on a 128 x 128 tile engine).
+struct WsmJob { const float* x; long long ldx; int K; float* dw; };
+__global__ void __launch_bounds__(256)
+k_wgrad_small(const float* __restrict__ s, long long lds, int B, int O, long long ldo, int accumulate,
+              WsmJob j0, WsmJob j1, int nb0) {
+  const bool second = (int)blockIdx.x >= nb0;
+  const WsmJob j = second ? j1 : j0;
+  const int blk = second ? (int)blockIdx.x - nb0 : (int)blockIdx.x;
+  const int kq = (j.K + 3) / 4;  // k quads per output row
+  const long long e = (long long)blk * 256 + threadIdx.x;
+  if (e >= (long long)O * kq) return;
+  const int o = (int)(e / kq), k = 4 * (int)(e % kq);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float sv = s[(size_t)b * lds + o];
+    const float* xr = j.x + (size_t)b * j.ldx + k;
+    a0 = fmaf(sv, xr[0], a0);
+    if (k + 1 < j.K) a1 = fmaf(sv, xr[1], a1);
+    if (k + 2 < j.K) a2 = fmaf(sv, xr[2], a2);
+    if (k + 3 < j.K) a3 = fmaf(sv, xr[3], a3);
+  }
+  float* d = j.dw + (size_t)o * ldo + k;
+  const float r[4] = {a0, a1, a2, a3};
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (k + t < j.K) d[t] = accumulate ? d[t] + r[t] : r[t];
+}
+
+int launch_wgrad_small(const float* s, long long lds, int B, int O, const float* x0, long long ldx0,
+                       int K0, float* dw0, const float* x1, long long ldx1, int K1, float* dw1,
+                       long long ldo, int accumulate, hipStream_t st) {
+  PC_REQUIRE(s && x0 && dw0 && B > 0 && O > 0 && K0 > 0 && lds >= O && ldx0 >= K0 && ldo >= K0 &&
+                 (!x1 || (dw1 && K1 > 0 && ldx1 >= K1 && ldo >= K1)),
+             "wgrad_small: bad shape B=%d O=%d K0=%d K1=%d", B, O, K0, K1);
+  PC_TRY_GEMM(gemm_pair_flush(st));
+  const long long n0 = (long long)O * ((K0 + 3) / 4), n1 = x1 ? (long long)O * ((K1 + 3) / 4) : 0;
+  const int nb0 = (int)((n0 + 255) / 256), nb1 = (int)((n1 + 255) / 256);
+  const WsmJob j0{x0, ldx0, K0, dw0};
+  const WsmJob j1{x1 ? x1 : x0, x1 ? ldx1 : ldx0, x1 ? K1 : K0, x1 ? dw1 : dw0};
+  hipLaunchKernelGGL(k_wgrad_small, dim3((unsigned)(nb0 + nb1)), dim3(256), 0, st, s, lds, B, O,
+                     ldo, accumulate, j0, j1, nb0);
+  PC_HIP_CHECK_LAUNCH("k_wgrad_small");
+  return PCADV_OK;
+}
+
 // the deferred finishing reductions of this thread's weight gradients
 static thread_local WfBatch g_wf_pending{};
 

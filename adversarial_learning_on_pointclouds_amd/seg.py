@@ -153,6 +153,7 @@ _ENGINE = None
 _DEFER = os.environ.get("PCADV_WGRAD_DEFER", "1") != "0"
 # each layer's weight and data gradients in one launch (_Engine.pair)
 _PAIR = os.environ.get("PCADV_GEMM_PAIR", "1") != "0"
+_SMALL = os.environ.get("PCADV_WGRAD_SMALL", "1") != "0"  # fc1's per-cloud columns: exact f32 kernel
 
 
 def _engine():
@@ -317,8 +318,15 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
     with E.pair():  # the data gradient first: the weight gradient's group sums follow its launch
         E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc, ldm=_LOC, precise=_DGRAD_PRECISE)
         E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N, defer=_DEFER)
-    E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, defer=_DEFER)
-    E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008, defer=_DEFER)
+    # the tiled global and class columns: B per-cloud rows, exact f32, one launch
+    if not _SMALL:
+        E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, defer=_DEFER)
+        E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008,
+                defer=_DEFER)
+    else:
+        check(E.lib.pcadv_wgrad_small(_p(s1), 256, B, 256, _p(gmax), 2048, 2048, _p(dW1, 960),
+                                      _p(cvec), cvec.shape[1], cvec.shape[1], _p(dW1, 3008), 3024,
+                                      0, stream_ptr()), "pcadv_wgrad_small")
     dg = torch.empty(B, 2048, device=dev)
     E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=_DGRAD_PRECISE)
     if dgmax_out is not None:

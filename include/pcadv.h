@@ -276,6 +276,12 @@ int pcadv_wgrad_flush(hipStream_t stream);
  * those two calls may sit between begin and end on this thread; end enqueues a
  * GEMM still waiting. */
 int pcadv_gemm_pair_begin(hipStream_t stream);
+/* Weight gradient over a few rows in exact f32 (rows in order):
+ * dw0[o][k] (+)= sum_{b < B} s[b][o] x0[b][k] for k < K0, and the same with
+ * x1 / K1 / dw1 when x1 is given, in one launch (fc1's per-cloud columns). */
+int pcadv_wgrad_small(const float* s, int64_t lds, int B, int O, const float* x0, int64_t ldx0,
+                      int K0, float* dw0, const float* x1, int64_t ldx1, int K1, float* dw1,
+                      int64_t ldo, int accumulate, hipStream_t stream);
 int pcadv_gemm_pair_end(hipStream_t stream);
 
 /* Column sums (bias gradients): out[n] (+)= sum_m x[m][n] [ymask[m][n] > 0];

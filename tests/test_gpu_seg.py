@@ -325,6 +325,35 @@ def test_gemm_weight_grad(rows, rpg, O, K):
         assert torch.equal(outs["0"][2], a_gs)
 
 
+@pytest.mark.parametrize("B,O,K0,K1,acc", [(16, 256, 2048, 16, 0), (3, 70, 5, 0, 1), (16, 256, 2048, 50, 1)])
+def test_wgrad_small_matches_f64(B, O, K0, K1, acc):
+    """pcadv_wgrad_small (fc1's per-cloud columns): dw[o][k] (+)= sum_b s[b][o] x[b][k]
+    in f32 with rows in order; one or two operands per launch, into a wider dw
+    with a column offset; tolerance 1e-5 relative to the f64 product."""
+    lib = _lib.load()
+    rng = np.random.default_rng(B * 7 + K1)
+    s = rng.standard_normal((B, O)).astype(np.float32)
+    x0 = rng.standard_normal((B, K0)).astype(np.float32)
+    x1 = rng.standard_normal((B, max(K1, 1))).astype(np.float32)
+    ldo = 3 + K0 + max(K1, 1) + 2
+    w0 = rng.standard_normal((O, ldo)).astype(np.float32)
+    dW, ds, dx0, dx1 = _t(w0), _t(s), _t(x0), _t(x1)  # held: the launch reads them
+    check(lib.pcadv_wgrad_small(_p(ds), O, B, O, _p(dx0), K0, K0, _p(dW, 3),
+                                _p(dx1) if K1 else None, K1, K1, _p(dW, 3 + K0) if K1 else None,
+                                ldo, acc, stream_ptr()), "pcadv_wgrad_small")
+    torch.cuda.synchronize()
+    want = w0.astype(np.float64)
+    base = want.copy()
+    want[:, 3:3 + K0] = acc * base[:, 3:3 + K0] + s.astype(np.float64).T @ x0
+    if K1:
+        want[:, 3 + K0:3 + K0 + K1] = acc * base[:, 3 + K0:3 + K0 + K1] + s.astype(np.float64).T @ x1[:, :K1]
+    got = dW.cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
+    # columns outside the two jobs untouched
+    assert np.array_equal(got[:, :3], w0[:, :3])
+    assert np.array_equal(got[:, 3 + K0 + K1:], w0[:, 3 + K0 + K1:])
+
+
 def test_gemm_weight_grad_deferred_batch_is_bitwise():
     """pcadv_gemm_wgrad_defer + pcadv_wgrad_flush: the finishing slab sums of
     several weight gradients (plain, accumulating, with per-group sums, and
