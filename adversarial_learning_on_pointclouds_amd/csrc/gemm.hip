@@ -23,6 +23,7 @@
 // consumer (the weight gradient, the next data gradient, the bias sums) reads
 // dZ already masked.
 #include "common.h"
+#include <type_traits>
 
 namespace pcadv {
 
@@ -639,11 +640,28 @@ struct GemmBigLds {
   };
 };
 
-template <int MODE>
+// LDS-DMA form (GL = true; whole tiles only: M % 256 == 0 per launch / cloud
+// and K % 32 == 0): the planes go global -> LDS by buffer_load ... lds, no
+// staging registers and no ds_write pass.  The image is lane-linear (one
+// wave-instruction fills 1 KB = 16 rows of 64 B), so the fragment reads are
+// kept conflict-free by an XOR swizzle of the 16-B chunk inside each row,
+// chunk' = chunk ^ ((row >> 2) & 3), applied on the global source address.
+struct GemmGlLds {
+  union {
+    struct {
+      alignas(16) __bf16 a[2][GB_BM * GM_BK];  // [hi, lo][m][k], swizzled chunks
+      alignas(16) __bf16 b[2][GB_BN * GM_BK];
+    } op[2];
+    alignas(16) float stage[GB_BM * GB_ES];
+  };
+};
+
+template <int MODE, bool GL>
 __global__ void __launch_bounds__(GB_T)
 k_gemm_bf2_big(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GemmBigLds& L = *reinterpret_cast<GemmBigLds*>(smem);
+  GemmGlLds& G = *reinterpret_cast<GemmGlLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int wm = wave >> 2, wn = wave & 3;
@@ -743,6 +761,84 @@ k_gemm_bf2_big(GemmP p) {
     }
   };
 
+  if constexpr (GL) {
+    // wave w issues eight of the tile's 64 LDS-DMA loads, i < 8: operand
+    // i >> 2 (A, B), plane (i >> 1) & 1, 16-row block 2 w + (i & 1) (operand
+    // and plane compile-time, so the resources stay in SGPRs); lane l fills
+    // row 16 block + l / 4, physical chunk l & 3 = logical chunk
+    // (l & 3) ^ ((l >> 4) & 3) (the row's (row >> 2) & 3)
+    const int lr = lane >> 2, lc = (lane & 3) ^ ((lane >> 4) & 3);
+    const int wsc = __builtin_amdgcn_readfirstlane(wave);  // scalar: soffset and the LDS base (M0)
+    const uint32_t alane = (uint32_t)(lr * p.ldap + 8 * lc) * 2u;
+    const uint32_t blane = (uint32_t)(lr * p.ldbp + 8 * lc) * 2u;
+    const uint32_t arow0 = (uint32_t)m0 * (uint32_t)p.ldap * 2u, brow0 = (uint32_t)n0 * (uint32_t)p.ldbp * 2u;
+    auto issue = [&](int k0, int buf) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int opb = i >> 2, q = (i >> 1) & 1, rb16 = 2 * wsc + (i & 1);
+        const __amdgpu_buffer_rsrc_t rs = opb ? brsc[q] : arsc[q];
+        const uint32_t so = (opb ? brow0 + (uint32_t)(16 * rb16) * (uint32_t)p.ldbp * 2u
+                                 : arow0 + (uint32_t)(16 * rb16) * (uint32_t)p.ldap * 2u) + (uint32_t)k0 * 2u;
+        __bf16* dst = (opb ? G.op[buf].b[q] : G.op[buf].a[q]) + 16 * rb16 * GM_BK;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16,
+                                                 opb ? blane : alane, (int)so, 0, 0);
+      }
+    };
+    // fragments of one 16-deep k-block (48 VGPRs): B [j][plane], A [i][plane]
+    auto read_kb = [&](int buf, int kb, bf16x8g (&fa)[4][2], bf16x8g (&fb)[2][2]) {
+      const int c = 2 * kb + h;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = 64 * wn + 32 * j + r;
+        const int off = row * GM_BK + 8 * (c ^ ((row >> 2) & 3));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) fb[j][q] = *reinterpret_cast<const bf16x8g*>(&G.op[buf].b[q][off]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 128 * wm + 32 * i + r;
+        const int off = row * GM_BK + 8 * (c ^ ((row >> 2) & 3));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) fa[i][q] = *reinterpret_cast<const bf16x8g*>(&G.op[buf].a[q][off]);
+      }
+    };
+    auto mfma_kb = [&](const bf16x8g (&fa)[4][2], const bf16x8g (&fb)[2][2]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma_bf16g(fa[i][1], fb[j][0], acc[i][j]);
+          acc[i][j] = mfma_bf16g(fa[i][0], fb[j][1], acc[i][j]);
+          acc[i][j] = mfma_bf16g(fa[i][0], fb[j][0], acc[i][j]);
+        }
+    };
+    // two LDS buffers, one barrier per tile, placed between the tile's two
+    // k-blocks: behind it tile t + 1 is visible (every wave waited for its own
+    // DMA) and every read of tile t's buffer is done (they were issued a
+    // barrier earlier), so tile t + 2's DMA goes into that buffer and tile
+    // t + 1's fragments are read while k-block 1 of tile t multiplies
+    const int nt = K / GM_BK;
+    bf16x8g fa0[4][2], fb0[2][2], fa1[4][2], fb1[2][2];
+    issue(0, 0);
+    __syncthreads();
+    if (nt > 1) issue(GM_BK, 1);
+    read_kb(0, 0, fa0, fb0);
+    read_kb(0, 1, fa1, fb1);
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      mfma_kb(fa0, fb0);
+      if (t + 1 < nt) {
+        __syncthreads();
+        if (t + 2 < nt) issue((t + 2) * GM_BK, buf);
+        read_kb(buf ^ 1, 0, fa0, fb0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_kb(fa1, fb1);
+      if (t + 1 < nt) read_kb(buf ^ 1, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // the epilogue's stage overlays the operand buffers
+  } else {
   // one register set: tile t + 1 is loaded right after tile t is stored, and
   // the sched_barrier keeps those loads ahead of tile t's MFMAs (at 256 VGPRs
   // the scheduler otherwise sinks them below the MFMAs, where their registers
@@ -777,6 +873,7 @@ k_gemm_bf2_big(GemmP p) {
     mfma_tile(0);
   }
 #endif
+  }
 
   if constexpr (MODE == 2) {
     // per column, the top-2 (value, row) of this wave's 128 rows: the wave's
@@ -856,22 +953,34 @@ static bool use_gemm_big(int M, int N, int rows_per_group, int mode, long long l
   const long long tiles = (long long)((M + GB_BM - 1) / GB_BM) * (N / GB_BN);
   return tiles >= 256;
 }
-template <int MODE>
-static int gemm_big_launch(const GemmP& p, hipStream_t s) {
+// LDS-DMA staging for whole tiles (PCADV_GEMM_GLDS=0 keeps register staging:
+// same MFMAs in the same order, bitwise the same results)
+static bool gemm_glds_enabled() {
+  const char* e = getenv("PCADV_GEMM_GLDS");
+  return !(e && e[0] == '0');
+}
+template <int MODE, bool GL>
+static int gemm_big_launch_t(const GemmP& p, hipStream_t s) {
+  using Lds = typename std::conditional<GL, GemmGlLds, GemmBigLds>::type;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_bf2_big<MODE>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(GemmBigLds)) != hipSuccess) {
-      set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(GemmBigLds));
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_bf2_big<MODE, GL>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds)) != hipSuccess) {
+      set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(Lds));
       return PCADV_EHIP;
     }
     attr = true;
   }
   const dim3 grid((p.M + GB_BM - 1) / GB_BM, p.N / GB_BN, 1);
-  hipLaunchKernelGGL((k_gemm_bf2_big<MODE>), grid, dim3(GB_T), sizeof(GemmBigLds), s, p);
+  hipLaunchKernelGGL((k_gemm_bf2_big<MODE, GL>), grid, dim3(GB_T), sizeof(Lds), s, p);
   PC_HIP_CHECK_LAUNCH("k_gemm_bf2_big");
   return PCADV_OK;
+}
+template <int MODE>
+static int gemm_big_launch(const GemmP& p, hipStream_t s) {
+  const bool whole = (MODE == 2 ? p.rows_per_group : p.M) % GB_BM == 0 && p.K % GM_BK == 0;
+  return whole && gemm_glds_enabled() ? gemm_big_launch_t<MODE, true>(p, s)
+                                      : gemm_big_launch_t<MODE, false>(p, s);
 }
 
 // Skinny GEMM (M <= 16 rows per workgroup: one row per cloud, e.g. fc1's
