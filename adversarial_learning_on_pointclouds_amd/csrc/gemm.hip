@@ -498,6 +498,79 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
     }
   };
 
+  if constexpr ((VEC & 4) != 0) {
+    // LDS-DMA form for plane operands (VEC bit 2; TA = TB = 2, whole tiles:
+    // M, N % 128, K % 32, one k-range), as k_gemm_bf2_big<MODE, true>: two
+    // 32 KB buffers of unpadded 64-B rows, the 16-B chunk XOR-swizzled by
+    // (row >> 2) & 3 on the source address; wave w issues 8 of the tile's 32
+    // buffer_load ... lds (operand i >> 2, plane (i >> 1) & 1, 16-row block
+    // 2 w + (i & 1)); one barrier per tile between its two k-blocks
+    static_assert(TA == 2 && TB == 2 && MODE != 2, "LDS-DMA staging: plane operands, modes 0 / 1");
+    __bf16* const gl = reinterpret_cast<__bf16*>(smem);  // [buf][A hi, A lo, B hi, B lo][128 x 32]
+    constexpr int PL = GM_BM * GM_BK;                     // bf16 per plane tile
+    const int wsc = __builtin_amdgcn_readfirstlane(wave);
+    const int lr = lane >> 2, lc = (lane & 3) ^ ((lane >> 4) & 3);
+    const uint32_t alane = (uint32_t)(lr * p.ldap + 8 * lc) * 2u;
+    const uint32_t blane = (uint32_t)(lr * p.ldbp + 8 * lc) * 2u;
+    const uint32_t arow0 = (uint32_t)m0 * (uint32_t)p.ldap * 2u, brow0 = (uint32_t)n0 * (uint32_t)p.ldbp * 2u;
+    auto issue = [&](int k0, int buf) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int opb = i >> 2, q = (i >> 1) & 1, rb16 = 2 * wsc + (i & 1);
+        const __amdgpu_buffer_rsrc_t rs = opb ? (q ? brsl : brs) : (q ? arsl : ars);
+        const uint32_t so = (opb ? brow0 + (uint32_t)(16 * rb16) * (uint32_t)p.ldbp * 2u
+                                 : arow0 + (uint32_t)(16 * rb16) * (uint32_t)p.ldap * 2u) + (uint32_t)k0 * 2u;
+        __bf16* dst = gl + (size_t)(buf * 4 + 2 * opb + q) * PL + 16 * rb16 * GM_BK;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16,
+                                                 opb ? blane : alane, (int)so, 0, 0);
+      }
+    };
+    // one k-block's fragments: [plane][tile] of A and B (32 VGPRs)
+    auto read_kb = [&](int buf, int kb, bf16x8g (&fa)[2][2], bf16x8g (&fb)[2][2]) {
+      const int c = 2 * kb + h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ra_ = 64 * wm + 32 * t + r, rb_ = 64 * wn + 32 * t + r;
+        const int oa = ra_ * GM_BK + 8 * (c ^ ((ra_ >> 2) & 3));
+        const int ob = rb_ * GM_BK + 8 * (c ^ ((rb_ >> 2) & 3));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          fa[q][t] = *reinterpret_cast<const bf16x8g*>(gl + (size_t)(buf * 4 + q) * PL + oa);
+          fb[q][t] = *reinterpret_cast<const bf16x8g*>(gl + (size_t)(buf * 4 + 2 + q) * PL + ob);
+        }
+      }
+    };
+    auto mfma_kb = [&](const bf16x8g (&fa)[2][2], const bf16x8g (&fb)[2][2]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma_bf16g(fa[1][i], fb[0][j], acc[i][j]);
+          acc[i][j] = mfma_bf16g(fa[0][i], fb[1][j], acc[i][j]);
+          acc[i][j] = mfma_bf16g(fa[0][i], fb[0][j], acc[i][j]);
+        }
+    };
+    const int nt = (kz1 - kz0) / GM_BK;
+    bf16x8g fa0[2][2], fb0[2][2], fa1[2][2], fb1[2][2];
+    issue(kz0, 0);
+    __syncthreads();
+    if (nt > 1) issue(kz0 + GM_BK, 1);
+    read_kb(0, 0, fa0, fb0);
+    read_kb(0, 1, fa1, fb1);
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      mfma_kb(fa0, fb0);
+      if (t + 1 < nt) {
+        __syncthreads();
+        if (t + 2 < nt) issue(kz0 + (t + 2) * GM_BK, buf);
+        read_kb(buf ^ 1, 0, fa0, fb0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_kb(fa1, fb1);
+      if (t + 1 < nt) read_kb(buf ^ 1, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   // one register set: tile t + 1 is loaded right after tile t is stored; the
   // sched_barrier keeps those loads ahead of tile t's MFMAs (as
   // k_gemm_bf2_big), so one tile's MFMAs cover the next tile's loads
@@ -510,6 +583,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
     load_tile(ra, rb, k0 + GM_BK);
     __builtin_amdgcn_sched_barrier(0);
     mfma_tile();
+  }
   }
 
   if (do_csum) {  // fixed-order reduction over the 8 k-lanes of each column group
@@ -1088,6 +1162,18 @@ __device__ __forceinline__ float slab_subset(const float* src, long long stride,
   for (; z < nz; z += 8) s += src[(size_t)z * stride];
   return s;
 }
+// slab_subset on four consecutive elements (16-B loads; the same sums per element)
+__device__ __forceinline__ f32x4 slab_subset4(const float* src, long long stride, int nz, int zs) {
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  int z = zs;
+  auto ld = [&](int zz) { return *reinterpret_cast<const f32x4*>(src + (size_t)zz * stride); };
+  for (; z + 24 < nz; z += 32) {
+    const f32x4 a0 = ld(z), a1 = ld(z + 8), a2 = ld(z + 16), a3 = ld(z + 24);
+    s += ((a0 + a1) + a2) + a3;
+  }
+  for (; z < nz; z += 8) s += ld(z);
+  return s;
+}
 // the eight subsets' partials of element el, in subset order
 __device__ __forceinline__ float slab_combine(const float (&part)[8][33], int el) {
   float t = 0.f;
@@ -1125,8 +1211,17 @@ struct WfDesc {
   const float* csum; int O; int groups; int zpg; int from_groups; float* gs; float* db;
   int acc_db;
 };
-__device__ __forceinline__ void wgrad_finish_block(const WfDesc& w, int blk, float (&part)[8][33],
-                                                   float (&gsl)[WF_MAXG][33]) {
+// dW blocks take WF_DWE consecutive elements (four per thread, 16-B loads when
+// the slab stride allows) x the 8 z-subsets; column-sum blocks 32 channels
+constexpr int WF_DWE = 128;
+struct WfLds {
+  float part[8][33];
+  float gsl[WF_MAXG][33];
+  float pw[8][WF_DWE + 4];
+};
+__device__ __forceinline__ void wgrad_finish_block(const WfDesc& w, int blk, WfLds& L) {
+  float (&part)[8][33] = L.part;
+  float (&gsl)[WF_MAXG][33] = L.gsl;
   const float* __restrict__ slabs = w.slabs;
   const long long E = w.E;
   const int nz = w.nz, N = w.N, acc_dw = w.acc_dw, nb_dw = w.nb_dw, O = w.O, groups = w.groups;
@@ -1138,11 +1233,23 @@ __device__ __forceinline__ void wgrad_finish_block(const WfDesc& w, int blk, flo
   float* __restrict__ db = w.db;
   const int tid = threadIdx.x, el = tid & 31, zs = tid >> 5;
   if (blk < nb_dw) {
-    const long long e = (long long)blk * 32 + el;
-    part[zs][el] = e < E ? slab_subset(slabs + e, E, nz, zs) : 0.f;
+    const long long e0 = (long long)blk * WF_DWE + 4 * el;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (E % 4 == 0) {
+      if (e0 < E) v = slab_subset4(slabs + e0, E, nz, zs);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (e0 + t < E) v[t] = slab_subset(slabs + e0 + t, E, nz, zs);
+    }
+    *reinterpret_cast<f32x4*>(&L.pw[zs][4 * el]) = v;
     __syncthreads();
-    if (zs == 0 && e < E) {
-      const float t = slab_combine(part, el);
+    // thread tid < 128 finishes element blk * 128 + tid (coalesced stores)
+    const long long e = (long long)blk * WF_DWE + tid;
+    if (tid < WF_DWE && e < E) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += L.pw[q][tid];
       float* dst = dw + (size_t)(e / N) * ldo + (e % N);
       *dst = acc_dw ? *dst + t : t;
     }
@@ -1190,11 +1297,10 @@ k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __re
                long long ldo, int acc_dw, int nb_dw, const float* __restrict__ csum, int O,
                int groups, int zpg, int from_groups, float* __restrict__ gs, float* __restrict__ db,
                int acc_db) {
-  __shared__ float part[8][33];
-  __shared__ float gsl[WF_MAXG][33];
+  __shared__ WfLds L;
   const WfDesc w{slabs, E, nz, dw, N, ldo, acc_dw, nb_dw, csum, O, groups, zpg, from_groups, gs, db,
                  acc_db};
-  wgrad_finish_block(w, (int)blockIdx.x, part, gsl);
+  wgrad_finish_block(w, (int)blockIdx.x, L);
 }
 
 // Several weight gradients' finishing reductions in one launch (deferred by
@@ -1209,12 +1315,11 @@ struct WfBatch {
 };
 __global__ void __launch_bounds__(256)
 k_wgrad_finish_batch(WfBatch bt) {
-  __shared__ float part[8][33];
-  __shared__ float gsl[WF_MAXG][33];
+  __shared__ WfLds L;
   const int b = (int)blockIdx.x;
   int i = 0;
   for (int j = 1; j < bt.n; ++j) i = b >= bt.blk0[j] ? j : i;
-  wgrad_finish_block(bt.d[i], b - bt.blk0[i], part, gsl);
+  wgrad_finish_block(bt.d[i], b - bt.blk0[i], L);
 }
 
 // column sums of an M x N matrix (row stride ld), optionally masked by [Y > 0]
@@ -1378,24 +1483,30 @@ static bool fits31(long long rows, long long ld, int esz) {
 }
 
 template <typename K>
-static int gemm_lds_attr(K kern) {
+static int gemm_lds_attr(K kern, size_t bytes = sizeof(GemmLds)) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)sizeof(GemmLds)) != hipSuccess) {
-    set_error("gemm: cannot reserve %zu bytes of LDS", sizeof(GemmLds));
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
+    set_error("gemm: cannot reserve %zu bytes of LDS", bytes);
     return PCADV_EHIP;
   }
   return PCADV_OK;
+}
+
+// LDS of k_gemm_x3: the register-staged tile, or (VEC bit 2) two LDS-DMA
+// buffers of 4 plane tiles of 128 x 32 bf16
+template <int VEC>
+constexpr size_t gemm_x3_lds_bytes() {
+  return (VEC & 4) ? (sizeof(GemmLds) > 65536 ? sizeof(GemmLds) : 65536) : sizeof(GemmLds);
 }
 
 template <int TA, int TB, int MODE, int NP, int VEC>
 static int gemm_launch_direct(const GemmP& p, dim3 grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3<TA, TB, MODE, NP, VEC>));
+    PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3<TA, TB, MODE, NP, VEC>, gemm_x3_lds_bytes<VEC>()));
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_x3<TA, TB, MODE, NP, VEC>), grid, dim3(GM_T), sizeof(GemmLds), s, p);
+  hipLaunchKernelGGL((k_gemm_x3<TA, TB, MODE, NP, VEC>), grid, dim3(GM_T), gemm_x3_lds_bytes<VEC>(), s, p);
   PC_HIP_CHECK_LAUNCH("k_gemm_x3");
   return PCADV_OK;
 }
@@ -1613,6 +1724,12 @@ int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const voi
   p.cp[0] = static_cast<__bf16*>(c_hi); p.cp[1] = static_cast<__bf16*>(c_lo); p.ldcp = ldcp;
   p.grp = K; p.zpg = 1; p.ksplit_len = K;
   if (use_gemm_big(M, N, 0, 0, lda, ldb)) return accumulate ? gemm_big_launch<1>(p, s) : gemm_big_launch<0>(p, s);
+  if (M % GM_BM == 0 && N % GM_BN == 0 && K % GM_BK == 0 && gemm_glds_enabled()) {
+    PC_TRY_GEMM(gemm_pair_flush(s));
+    const dim3 grid(M / GM_BM, N / GM_BN, 1);
+    return accumulate ? gemm_launch_direct<2, 2, 1, 3, 7>(p, grid, s)
+                      : gemm_launch_direct<2, 2, 0, 3, 7>(p, grid, s);
+  }
   return accumulate ? gemm_launch<2, 2, 1, 3>(p, 1, s) : gemm_launch<2, 2, 0, 3>(p, 1, s);
 }
 
@@ -1784,7 +1901,7 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
     // the dW slab sums (and db, unless the per-group sums are wanted now) wait
     // for wgrad_flush, which runs every deferred finish in one launch
     PC_REQUIRE(w.groups <= WF_MAXG, "gemm_wgrad: %d groups cannot be deferred", w.groups);
-    const int nb_dw = (int)((E + 31) / 32);
+    const int nb_dw = (int)((E + WF_DWE - 1) / WF_DWE);
     const int nb_cs = csum ? (O + 31) / 32 : 0;
     const bool from_groups = w.groups > 1 || gsum;
     const WfDesc all{slabs, E, w.nz, dw, Kin, ldo, accumulate, nb_dw, csum, O, w.groups, w.zpg,
@@ -1803,7 +1920,7 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
   }
   if (w.groups <= WF_MAXG && !getenv_flag("PCADV_WGRAD_SPLIT_FINISH")) {
     // dW, the per-group sums and db in one launch (k_wgrad_finish)
-    const int nb_dw = (int)((E + 31) / 32);
+    const int nb_dw = (int)((E + WF_DWE - 1) / WF_DWE);
     const int nb_cs = csum ? (O + 31) / 32 : 0;
     const bool from_groups = w.groups > 1 || gsum;
     hipLaunchKernelGGL(k_wgrad_finish, dim3((unsigned)(nb_dw + nb_cs)), dim3(256), 0, s,

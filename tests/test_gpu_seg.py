@@ -188,6 +188,57 @@ def test_gemm_bf2_256_tiles_bitwise(M, N, K, acc):
     assert ((big[0].double() - ref).abs() <= bound).all()
 
 
+@pytest.mark.parametrize("M,N,K,acc", [(4096, 256, 960, 0), (8192, 128, 64, 1), (2048, 384, 256, 0)])
+def test_gemm_bf2_128_tiles_lds_dma_bitwise(M, N, K, acc):
+    """The 128-tile plane GEMM staged by LDS-DMA (whole tiles; PCADV_GEMM_GLDS=0
+    keeps register staging): C, its planes and the bias / per-group bias /
+    mask / accumulate epilogue bitwise the register-staged kernel's."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g)
+    b = torch.randn(N, device=DEV, generator=g)
+    rpg = 1024
+    br = torch.randn(M // rpg, N, device=DEV, generator=g)
+    Y = torch.randn(M, N, device=DEV, generator=g)
+    base = torch.randn(M, N, device=DEV, generator=g)
+    ah, al = _planes(A)
+    wh, wl = _planes(W)
+
+    def run():
+        C = base.clone()
+        ch = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        cl = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        check(lib.pcadv_gemm_bf2(_pb(ah), _pb(al), K, _pb(wh), _pb(wl), K, _p(C), N,
+                                 _pb(ch), _pb(cl), N, M, N, K, _p(b), _p(br), rpg, 1, acc,
+                                 _p(Y) if acc else None, N if acc else 0, stream_ptr()), "gemm_bf2")
+        torch.cuda.synchronize()
+        return C, ch, cl
+
+    saved = os.environ.get("PCADV_GEMM_GLDS")
+    try:
+        os.environ["PCADV_GEMM_GLDS"] = "1"
+        dma = run()
+        os.environ["PCADV_GEMM_GLDS"] = "0"
+        reg = run()
+    finally:
+        if saved is None:
+            del os.environ["PCADV_GEMM_GLDS"]
+        else:
+            os.environ["PCADV_GEMM_GLDS"] = saved
+    for x, y in zip(dma, reg):
+        assert torch.equal(x, y)
+    A64, W64 = A.double(), W.double()
+    ref = A64 @ W64.T + b.double() + br.double()[torch.arange(M, device=DEV) // rpg]
+    if acc:
+        ref = ref + base.double()
+    ref = ref.clamp_min(0)
+    if acc:
+        ref = ref * (Y > 0)
+    bound = 2e-5 * (A64.abs() @ W64.abs().T) + 2e-6 * (1 + base.double().abs())
+    assert ((dma[0].double() - ref).abs() <= bound).all()
+
+
 def test_conv_max_bf2_256_tiles_bitwise():
     """conv6's screened max on the 256-tile kernel (one top-2 record per
     128-row half) gives gmax / gidx bitwise equal to the 128-tile kernel,
