@@ -602,7 +602,9 @@ def bench_seg(args):
 
     xp, w6p = fw["xp"], fw["W6p"]
     big = os.environ.get("PCADV_GEMM_BIG", "1") != "0"
-    gname = "k_gemm_bf2_big<2>" if big else "k_gemm_x3<2,2,2,3>"
+    glds = os.environ.get("PCADV_GEMM_GLDS", "1") != "0"
+    gname = (f"k_gemm_bf2_big<2, {'true' if glds else 'false'}> (operands staged by "
+             f"{'LDS-DMA' if glds else 'registers'})") if big else "k_gemm_x3<2,2,2,3>"
     kname = f"pcadv_conv_max_bf2: {gname}" if xp is not None else "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3>"
 
     def cmx():
@@ -632,7 +634,7 @@ def bench_seg(args):
     kissued = 3 * kflops  # three bf16 MFMA products per f32 product (hi/lo splits)
     traffic, traffic_src = _pmc_traffic(
         "r*_seg_pmc_traffic.json",
-        ("pcadv::k_gemm_bf2_big<2>" if big else "pcadv::k_gemm_x3<2, 2, 2, 3>", "pcadv::k_max_combine"))
+        ("pcadv::k_gemm_bf2_big<2" if big else "pcadv::k_gemm_x3<2, 2, 2, 3>", "pcadv::k_max_combine"))
     out = {
         "metric": "point-clouds/sec (seg train step), B=16 N=2048 ShapeNet-part, 1 GPU",
         "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
