@@ -962,9 +962,9 @@ k_gemm_bf2_big(GemmP p) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int row = 32 * i + acc_row(e, lane);
-          if (m0 + 128 * wm + row < Mlim) {
+          if (GL || m0 + 128 * wm + row < Mlim) {  // GL: whole tiles, every row is in range
             const int key = gkey(acc[i][j][e], row);
-            k2 = max(min(key, k1), k2);
+            k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1
             k1 = max(k1, key);
           }
         }
@@ -1771,15 +1771,25 @@ int launch_split_bf2(const float* x, long long ld, int rows, int cols, void* hi,
 #define PCADV_WGRAD_FLOOR 0
 #endif
 struct WgradPlan { int groups, grp, zpg, len, nz; };
+// the workgroups a weight gradient's slab plan aims at (PCADV_WGRAD_WGS
+// overrides the default, read once: the workspace size follows the plan)
+static int wgrad_wgs() {
+  static const int v = [] {
+    const char* e = getenv("PCADV_WGRAD_WGS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : PCADV_WGRAD_WGS;
+  }();
+  return v;
+}
 static WgradPlan wgrad_plan(int rows, int O, int Kin, int rows_per_group) {
   WgradPlan w{};
   w.grp = rows_per_group > 0 ? rows_per_group : rows;
   w.groups = rows / w.grp;
   const int tiles = ((O + GM_BM - 1) / GM_BM) * ((Kin + GM_BN - 1) / GM_BN);
 #if PCADV_WGRAD_FLOOR
-  const int want = max(1, PCADV_WGRAD_WGS / (tiles * w.groups));
+  const int want = max(1, wgrad_wgs() / (tiles * w.groups));
 #else
-  const int want = (PCADV_WGRAD_WGS + tiles * w.groups - 1) / (tiles * w.groups);
+  const int want = (wgrad_wgs() + tiles * w.groups - 1) / (tiles * w.groups);
 #endif
   w.zpg = max(1, min(want, (w.grp + 127) / 128));
   w.len = (w.grp + w.zpg - 1) / w.zpg;
