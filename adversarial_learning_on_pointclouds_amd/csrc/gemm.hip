@@ -1547,9 +1547,23 @@ static int gemm_pair_flush(hipStream_t s) {
                        : gemm_launch_direct<0, 1, 1, 3, 3>(p, g, s);
 }
 
+// which GEMM's workgroups a pair dispatches first: the weight gradient's
+// (its slab workgroups run the longest; A/B on two boxes 1.139 -> 1.125 and
+// 1.182 -> 1.167 ms against the issue order); PCADV_PAIR_WFIRST=0: the data
+// gradient's, =i: the GEMM issued first.  Outputs bitwise the same either way.
+static int pair_wfirst(int issued) {
+  static const int v = [] {
+    const char* e = getenv("PCADV_PAIR_WFIRST");
+    if (e && e[0] == '0') return 0;
+    if (e && e[0] == 'i') return -1;
+    return 1;
+  }();
+  return v < 0 ? issued : v;
+}
 template <int VW, int MD, int VD>
 static int gemm_pair_launch(const GemmP& pw, dim3 gw, const GemmP& pd, dim3 gd, int wfirst,
                             hipStream_t s) {
+  wfirst = pair_wfirst(wfirst);
   static bool attr = false;
   if (!attr) {
     PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3_pair<VW, MD, VD>));
