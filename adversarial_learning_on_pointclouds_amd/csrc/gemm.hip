@@ -1737,8 +1737,13 @@ int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const voi
              "gemm_bf2: output planes need N %% 4, ldcp %% 4 and 16-B aligned C");
   p.cp[0] = static_cast<__bf16*>(c_hi); p.cp[1] = static_cast<__bf16*>(c_lo); p.ldcp = ldcp;
   p.grp = K; p.zpg = 1; p.ksplit_len = K;
-  if (use_gemm_big(M, N, 0, 0, lda, ldb)) return accumulate ? gemm_big_launch<1>(p, s) : gemm_big_launch<0>(p, s);
-  if (M % GM_BM == 0 && N % GM_BN == 0 && K % GM_BK == 0 && gemm_glds_enabled()) {
+  // whole 128-tiles: the LDS-DMA 128-tile kernel, also where the 256-tile one
+  // would apply (conv5: 1.1211 -> 1.1180 ms A/B, two workgroups per CU over
+  // four k-tiles beat one); PCADV_GEMM_BIG_PLAIN=1 keeps the 256 tiles there
+  const bool gl128 = M % GM_BM == 0 && N % GM_BN == 0 && K % GM_BK == 0 && gemm_glds_enabled();
+  if ((!gl128 || getenv_flag("PCADV_GEMM_BIG_PLAIN")) && use_gemm_big(M, N, 0, 0, lda, ldb))
+    return accumulate ? gemm_big_launch<1>(p, s) : gemm_big_launch<0>(p, s);
+  if (gl128) {
     PC_TRY_GEMM(gemm_pair_flush(s));
     const dim3 grid(M / GM_BM, N / GM_BN, 1);
     return accumulate ? gemm_launch_direct<2, 2, 1, 3, 7>(p, grid, s)

@@ -121,17 +121,21 @@ def test_gemm_bf2_is_bitwise_the_f32_staged_gemm(M, N, K):
 
 
 def _with_gemm_big(enabled, fn):
-    saved = os.environ.get("PCADV_GEMM_BIG")
+    # PCADV_GEMM_BIG_PLAIN: the 256-tile kernel also where whole 128-tiles would
+    # take the LDS-DMA 128-tile kernel, so the plain modes are exercised too
+    saved = {k: os.environ.get(k) for k in ("PCADV_GEMM_BIG", "PCADV_GEMM_BIG_PLAIN")}
     os.environ["PCADV_GEMM_BIG"] = "1" if enabled else "0"
+    os.environ["PCADV_GEMM_BIG_PLAIN"] = "1"
     try:
         out = fn()
         torch.cuda.synchronize()
         return out
     finally:
-        if saved is None:
-            del os.environ["PCADV_GEMM_BIG"]
-        else:
-            os.environ["PCADV_GEMM_BIG"] = saved
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 def _planes(x):
