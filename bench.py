@@ -26,9 +26,12 @@ import time
 
 import numpy as np
 
-# graph dispatch without packet capture, as the package sets it (see its
-# __init__); must be in the environment before torch initialises HIP
-if os.environ.get("PCADV_GRAPH_PACKET_CAPTURE", "0") != "1":
+# This entry point opts in to graph replay through the stream dispatch path
+# (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0, the same as the package's
+# use_stream_graph_dispatch(); importing the package never sets it).  It must
+# be in the environment before torch initialises HIP; the JSON line records it
+# ("runtime").  --runtime-graph-dispatch keeps the HIP runtime's default.
+if "--runtime-graph-dispatch" not in sys.argv:
     os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 import torch  # noqa: E402
 
@@ -72,6 +75,9 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="feature-forward precision (default: bf16 for --config cls, the dtype "
                          "BASELINE configs[1] names; fp32 for adv and seg)")
+    ap.add_argument("--runtime-graph-dispatch", action="store_true",
+                    help="leave DEBUG_CLR_GRAPH_PACKET_CAPTURE unset (the HIP runtime's default "
+                         "graph dispatch) instead of the stream dispatch path this bench opts in to")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: start the --gpus ranks, form the process group, "
                          "print the JSON world/backend line; no GPU work")
