@@ -49,6 +49,25 @@ _i64 = ctypes.c_int64
 _u64 = ctypes.c_uint64
 
 
+class WgradDesc(ctypes.Structure):
+    """Mirror of pcadv_wgrad_desc (include/pcadv.h)."""
+
+    _fields_ = [("dz", _vp), ("ldz", _i64), ("x", _vp), ("ldx", _i64), ("rows", _i), ("O", _i),
+                ("Kin", _i), ("dw", _vp), ("ldo", _i64), ("db", _vp), ("gsum", _vp),
+                ("rows_per_group", _i), ("accumulate", _i), ("workspace", _vp),
+                ("workspace_bytes", _sz)]
+
+
+class GemmDesc(ctypes.Structure):
+    """Mirror of pcadv_gemm_desc (include/pcadv.h)."""
+
+    _fields_ = [("a", _vp), ("lda", _i64), ("ta", _i), ("b", _vp), ("ldb", _i64), ("tb", _i),
+                ("c", _vp), ("ldc", _i64), ("M", _i), ("N", _i), ("K", _i), ("bias", _vp),
+                ("bias_rows", _vp), ("rows_per_group", _i), ("relu", _i), ("accumulate", _i),
+                ("cmask", _vp), ("ldm", _i64), ("precise", _i), ("c_hi", _vp), ("c_lo", _vp),
+                ("ldcp", _i64)]
+
+
 class AdvArgs(ctypes.Structure):
     """Mirror of pcadv_adv_args (include/pcadv.h)."""
 
@@ -105,13 +124,10 @@ SIGNATURES = {
     "pcadv_gemm_wgrad_workspace_bytes": (_sz, [_i, _i, _i, _i]),
     "pcadv_gemm_wgrad": (_i, [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _vp, _vp, _i, _i, _vp,
                               _sz, _vp]),
-    "pcadv_gemm_wgrad_defer": (_i, [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _vp, _vp, _i, _i,
-                                    _vp, _sz, _vp]),
-    "pcadv_wgrad_flush": (_i, [_vp]),
-    "pcadv_gemm_pair_begin": (_i, [_vp]),
+    "pcadv_gemm_wgrad_slabs": (_i, [ctypes.POINTER(WgradDesc), ctypes.POINTER(GemmDesc), _vp]),
+    "pcadv_wgrad_finish": (_i, [ctypes.POINTER(WgradDesc), _i, _vp]),
     "pcadv_wgrad_small": (_i, [_vp, _i64, _i, _i, _vp, _i64, _i, _vp, _vp, _i64, _i, _vp, _i64, _i,
                                _vp]),
-    "pcadv_gemm_pair_end": (_i, [_vp]),
     "pcadv_colsum_workspace_bytes": (_sz, [_i, _i]),
     "pcadv_colsum": (_i, [_vp, _vp, _i64, _i64, _i, _i, _vp, _i, _vp, _sz, _vp]),
     "pcadv_group_colsum": (_i, [_vp, _vp, _i64, _i64, _i, _i, _i, _vp, _vp]),

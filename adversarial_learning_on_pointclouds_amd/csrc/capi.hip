@@ -82,12 +82,11 @@ int launch_gemm_bf2(const void*, const void*, long long, const void*, const void
 int launch_split_bf2(const float*, long long, int, int, void*, void*, long long, hipStream_t);
 size_t gemm_wgrad_workspace_bytes(int, int, int, int);
 int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int, int, float*,
-                      long long, float*, float*, int, int, void*, size_t, hipStream_t, int defer);
-int wgrad_flush(hipStream_t);
-int gemm_pair_begin(hipStream_t);
+                      long long, float*, float*, int, int, void*, size_t, hipStream_t);
+int launch_gemm_wgrad_slabs(const pcadv_wgrad_desc*, const pcadv_gemm_desc*, hipStream_t);
+int launch_wgrad_finish(const pcadv_wgrad_desc*, int, hipStream_t);
 int launch_wgrad_small(const float*, long long, int, int, const float*, long long, int, float*,
                        const float*, long long, int, float*, long long, int, hipStream_t);
-int gemm_pair_end(hipStream_t);
 size_t colsum_workspace_bytes(int, int);
 int launch_colsum(const float*, const float*, long long, long long, int, int, float*, int, void*,
                   size_t, hipStream_t);
@@ -614,20 +613,17 @@ int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, 
                      int Kin, float* dw, int64_t ldo, float* db, float* gsum, int rows_per_group,
                      int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
   return launch_gemm_wgrad(dz, ldz, x, ldx, rows, O, Kin, dw, ldo, db, gsum, rows_per_group,
-                           accumulate, workspace, workspace_bytes, stream, 0);
+                           accumulate, workspace, workspace_bytes, stream);
 }
 
-int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows,
-                           int O, int Kin, float* dw, int64_t ldo, float* db, float* gsum,
-                           int rows_per_group, int accumulate, void* workspace,
-                           size_t workspace_bytes, hipStream_t stream) {
-  return launch_gemm_wgrad(dz, ldz, x, ldx, rows, O, Kin, dw, ldo, db, gsum, rows_per_group,
-                           accumulate, workspace, workspace_bytes, stream, 1);
+int pcadv_gemm_wgrad_slabs(const pcadv_wgrad_desc* w, const pcadv_gemm_desc* g,
+                           hipStream_t stream) {
+  return launch_gemm_wgrad_slabs(w, g, stream);
 }
 
-int pcadv_wgrad_flush(hipStream_t stream) { return wgrad_flush(stream); }
-
-int pcadv_gemm_pair_begin(hipStream_t stream) { return gemm_pair_begin(stream); }
+int pcadv_wgrad_finish(const pcadv_wgrad_desc* w, int n, hipStream_t stream) {
+  return launch_wgrad_finish(w, n, stream);
+}
 
 int pcadv_wgrad_small(const float* s, int64_t lds, int B, int O, const float* x0, int64_t ldx0,
                       int K0, float* dw0, const float* x1, int64_t ldx1, int K1, float* dw1,
@@ -635,7 +631,6 @@ int pcadv_wgrad_small(const float* s, int64_t lds, int B, int O, const float* x0
   return launch_wgrad_small(s, lds, B, O, x0, ldx0, K0, dw0, x1, ldx1, K1, dw1, ldo, accumulate,
                             stream);
 }
-int pcadv_gemm_pair_end(hipStream_t stream) { return gemm_pair_end(stream); }
 
 size_t pcadv_colsum_workspace_bytes(int M, int N) { return colsum_workspace_bytes(M, N); }
 

@@ -1303,8 +1303,8 @@ k_wgrad_finish(const float* __restrict__ slabs, long long E, int nz, float* __re
   wgrad_finish_block(w, (int)blockIdx.x, L);
 }
 
-// Several weight gradients' finishing reductions in one launch (deferred by
-// launch_gemm_wgrad(..., defer = 1) until pcadv_wgrad_flush): block b belongs
+// Several weight gradients' finishing reductions in one launch
+// (launch_wgrad_finish, after their launch_gemm_wgrad_slabs calls): block b belongs
 // to the descriptor whose block range [blk0[i], blk0[i + 1]) holds it; every
 // sum is bitwise the one k_wgrad_finish forms.
 constexpr int WF_BATCH = 16;
@@ -1511,10 +1511,11 @@ static int gemm_launch_direct(const GemmP& p, dim3 grid, hipStream_t s) {
   return PCADV_OK;
 }
 
-// Pair recording (pcadv_gemm_pair_begin / _end): the first weight-gradient or
-// data-gradient GEMM launched after begin waits; the next one of the other
-// kind launches both as one k_gemm_x3_pair.  Anything else launched by the
-// engine first enqueues the waiting GEMM alone (stream order is kept).
+// Pairing inside ONE call (pcadv_gemm_wgrad_slabs): a slot on the caller's
+// stack.  With slot->on, the first pairable weight-gradient or data-gradient
+// GEMM waits in the slot; the next one of the other kind launches both as one
+// k_gemm_x3_pair; gemm_slot_flush enqueues a GEMM still waiting.  Nothing
+// outlives the call.
 struct PendingGemm {
   bool on, has;
   int kind;  // 0: weight gradient <1, 1, 0, 6, v>; 1: data gradient <0, 1, mode, 3, v>
@@ -1522,29 +1523,28 @@ struct PendingGemm {
   GemmP p;
   dim3 grid;
 };
-static thread_local PendingGemm g_pair{};
 
 static PairGeom pair_geom(dim3 g) {
   return PairGeom{(int)(g.x * g.y * g.z), (int)g.x, (int)g.y, (int)g.z};
 }
 
-static int gemm_pair_flush(hipStream_t s) {
-  if (!g_pair.has) return PCADV_OK;
-  g_pair.has = false;
-  const GemmP& p = g_pair.p;
-  const dim3 g = g_pair.grid;
-  if (g_pair.kind == 0) {
-    switch (g_pair.v) {
+static int gemm_slot_flush(PendingGemm& slot, hipStream_t s) {
+  if (!slot.has) return PCADV_OK;
+  slot.has = false;
+  const GemmP& p = slot.p;
+  const dim3 g = slot.grid;
+  if (slot.kind == 0) {
+    switch (slot.v) {
       case 1: return gemm_launch_direct<1, 1, 0, 6, 1>(p, g, s);
       case 2: return gemm_launch_direct<1, 1, 0, 6, 2>(p, g, s);
       default: return gemm_launch_direct<1, 1, 0, 6, 3>(p, g, s);
     }
   }
-  if (g_pair.mode == 0)
-    return g_pair.v == 2 ? gemm_launch_direct<0, 1, 0, 3, 2>(p, g, s)
-                         : gemm_launch_direct<0, 1, 0, 3, 3>(p, g, s);
-  return g_pair.v == 2 ? gemm_launch_direct<0, 1, 1, 3, 2>(p, g, s)
-                       : gemm_launch_direct<0, 1, 1, 3, 3>(p, g, s);
+  if (slot.mode == 0)
+    return slot.v == 2 ? gemm_launch_direct<0, 1, 0, 3, 2>(p, g, s)
+                       : gemm_launch_direct<0, 1, 0, 3, 3>(p, g, s);
+  return slot.v == 2 ? gemm_launch_direct<0, 1, 1, 3, 2>(p, g, s)
+                     : gemm_launch_direct<0, 1, 1, 3, 3>(p, g, s);
 }
 
 // which GEMM's workgroups a pair dispatches first: the weight gradient's
@@ -1577,53 +1577,42 @@ static int gemm_pair_launch(const GemmP& pw, dim3 gw, const GemmP& pd, dim3 gd, 
 }
 
 template <int TA, int TB, int MODE, int NP, int VEC>
-static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s) {
+static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s, PendingGemm* slot) {
   constexpr bool is_w = TA == 1 && TB == 1 && MODE == 0 && NP == 6 && VEC >= 1;
   constexpr bool is_d = TA == 0 && TB == 1 && (MODE == 0 || MODE == 1) && NP == 3 && VEC >= 2;
   if constexpr (is_w || is_d) {
-    if (g_pair.on) {
-      if (g_pair.has && g_pair.kind == (is_w ? 1 : 0)) {  // the pair's second GEMM
-        g_pair.has = false;
+    if (slot && slot->on) {
+      if (slot->has && slot->kind == (is_w ? 1 : 0)) {  // the pair's second GEMM
+        slot->has = false;
         if constexpr (is_w) {
-          const GemmP& pd = g_pair.p;
-          const dim3 gd = g_pair.grid;
-          if (g_pair.mode == 0)
-            return g_pair.v == 2 ? gemm_pair_launch<VEC, 0, 2>(p, grid, pd, gd, 0, s)
-                                 : gemm_pair_launch<VEC, 0, 3>(p, grid, pd, gd, 0, s);
-          return g_pair.v == 2 ? gemm_pair_launch<VEC, 1, 2>(p, grid, pd, gd, 0, s)
-                               : gemm_pair_launch<VEC, 1, 3>(p, grid, pd, gd, 0, s);
+          const GemmP& pd = slot->p;
+          const dim3 gd = slot->grid;
+          if (slot->mode == 0)
+            return slot->v == 2 ? gemm_pair_launch<VEC, 0, 2>(p, grid, pd, gd, 0, s)
+                                : gemm_pair_launch<VEC, 0, 3>(p, grid, pd, gd, 0, s);
+          return slot->v == 2 ? gemm_pair_launch<VEC, 1, 2>(p, grid, pd, gd, 0, s)
+                              : gemm_pair_launch<VEC, 1, 3>(p, grid, pd, gd, 0, s);
         } else {
-          const GemmP& pw = g_pair.p;
-          const dim3 gw = g_pair.grid;
-          switch (g_pair.v) {
+          const GemmP& pw = slot->p;
+          const dim3 gw = slot->grid;
+          switch (slot->v) {
             case 1: return gemm_pair_launch<1, MODE, VEC>(pw, gw, p, grid, 1, s);
             case 2: return gemm_pair_launch<2, MODE, VEC>(pw, gw, p, grid, 1, s);
             default: return gemm_pair_launch<3, MODE, VEC>(pw, gw, p, grid, 1, s);
           }
         }
       }
-      PC_TRY_GEMM(gemm_pair_flush(s));  // a waiting GEMM of the same kind goes alone
-      g_pair.has = true;
-      g_pair.kind = is_w ? 0 : 1;
-      g_pair.v = VEC;
-      g_pair.mode = MODE;
-      g_pair.p = p;
-      g_pair.grid = grid;
+      PC_TRY_GEMM(gemm_slot_flush(*slot, s));  // a waiting GEMM of the same kind goes alone
+      slot->has = true;
+      slot->kind = is_w ? 0 : 1;
+      slot->v = VEC;
+      slot->mode = MODE;
+      slot->p = p;
+      slot->grid = grid;
       return PCADV_OK;
     }
   }
-  PC_TRY_GEMM(gemm_pair_flush(s));
   return gemm_launch_direct<TA, TB, MODE, NP, VEC>(p, grid, s);
-}
-
-int gemm_pair_begin(hipStream_t s) {
-  PC_TRY_GEMM(gemm_pair_flush(s));
-  g_pair.on = true;
-  return PCADV_OK;
-}
-int gemm_pair_end(hipStream_t s) {
-  g_pair.on = false;
-  return gemm_pair_flush(s);
 }
 
 // the staging form of each operand: 16-byte loads where the operand allows
@@ -1638,26 +1627,27 @@ static int gemm_vec_flags(const GemmP& p) {
 }
 
 template <int TA, int TB, int MODE, int NP>
-static int gemm_launch_grid(const GemmP& p, dim3 grid, hipStream_t s) {
+static int gemm_launch_grid(const GemmP& p, dim3 grid, hipStream_t s, PendingGemm* slot) {
   switch (gemm_vec_flags<TA, TB>(p)) {
-    case 3: return gemm_launch_v<TA, TB, MODE, NP, 3>(p, grid, s);
-    case 2: return gemm_launch_v<TA, TB, MODE, NP, 2>(p, grid, s);
-    case 1: return gemm_launch_v<TA, TB, MODE, NP, 1>(p, grid, s);
-    default: return gemm_launch_v<TA, TB, MODE, NP, 0>(p, grid, s);
+    case 3: return gemm_launch_v<TA, TB, MODE, NP, 3>(p, grid, s, slot);
+    case 2: return gemm_launch_v<TA, TB, MODE, NP, 2>(p, grid, s, slot);
+    case 1: return gemm_launch_v<TA, TB, MODE, NP, 1>(p, grid, s, slot);
+    default: return gemm_launch_v<TA, TB, MODE, NP, 0>(p, grid, s, slot);
   }
 }
 template <int TA, int TB, int MODE, int NP>
-static int gemm_launch(const GemmP& p, int nz, hipStream_t s) {
+static int gemm_launch(const GemmP& p, int nz, hipStream_t s, PendingGemm* slot = nullptr) {
   return gemm_launch_grid<TA, TB, MODE, NP>(
-      p, dim3((p.M + GM_BM - 1) / GM_BM, (p.N + GM_BN - 1) / GM_BN, nz), s);
+      p, dim3((p.M + GM_BM - 1) / GM_BM, (p.N + GM_BN - 1) / GM_BN, nz), s, slot);
 }
 
 // C[M][N] (+)= op(A) op(B)^T: see the header comment for ta / tb.
-int launch_gemm(const float* a, long long lda, int ta, const float* b, long long ldb, int tb,
-                float* c, long long ldc, int M, int N, int K, const float* bias,
-                const float* bias_rows, int rows_per_group, int relu, int accumulate,
-                const float* cmask, long long ldm, int precise, void* c_hi, void* c_lo,
-                long long ldcp, hipStream_t s) {
+static int launch_gemm_impl(const float* a, long long lda, int ta, const float* b, long long ldb,
+                            int tb, float* c, long long ldc, int M, int N, int K,
+                            const float* bias, const float* bias_rows, int rows_per_group,
+                            int relu, int accumulate, const float* cmask, long long ldm,
+                            int precise, void* c_hi, void* c_lo, long long ldcp, hipStream_t s,
+                            PendingGemm* slot) {
   PC_REQUIRE(a && b && c && M > 0 && N > 0 && K > 0, "gemm: bad shape M=%d N=%d K=%d", M, N, K);
   PC_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M), "gemm: bad lda %lld (ta=%d)", lda, ta);
   PC_REQUIRE((tb == 0 && ldb >= K) || (tb == 1 && ldb >= N), "gemm: bad ldb %lld (tb=%d)", ldb, tb);
@@ -1699,8 +1689,18 @@ int launch_gemm(const float* a, long long lda, int ta, const float* b, long long
     return accumulate ? gemm_launch<1, 1, 1, 6>(p, 1, s) : gemm_launch<1, 1, 0, 6>(p, 1, s);
   }
   if (ta == 0 && tb == 0) return accumulate ? gemm_launch<0, 0, 1, 3>(p, 1, s) : gemm_launch<0, 0, 0, 3>(p, 1, s);
-  if (ta == 0 && tb == 1) return accumulate ? gemm_launch<0, 1, 1, 3>(p, 1, s) : gemm_launch<0, 1, 0, 3>(p, 1, s);
+  if (ta == 0 && tb == 1)
+    return accumulate ? gemm_launch<0, 1, 1, 3>(p, 1, s, slot) : gemm_launch<0, 1, 0, 3>(p, 1, s, slot);
   return accumulate ? gemm_launch<1, 1, 1, 3>(p, 1, s) : gemm_launch<1, 1, 0, 3>(p, 1, s);
+}
+
+int launch_gemm(const float* a, long long lda, int ta, const float* b, long long ldb, int tb,
+                float* c, long long ldc, int M, int N, int K, const float* bias,
+                const float* bias_rows, int rows_per_group, int relu, int accumulate,
+                const float* cmask, long long ldm, int precise, void* c_hi, void* c_lo,
+                long long ldcp, hipStream_t s) {
+  return launch_gemm_impl(a, lda, ta, b, ldb, tb, c, ldc, M, N, K, bias, bias_rows, rows_per_group,
+                          relu, accumulate, cmask, ldm, precise, c_hi, c_lo, ldcp, s, nullptr);
 }
 
 // Both operands as bf16 hi / lo planes (the 2-way splits of f32 matrices, made
@@ -1744,7 +1744,6 @@ int launch_gemm_bf2(const void* a_hi, const void* a_lo, long long lda, const voi
   if ((!gl128 || getenv_flag("PCADV_GEMM_BIG_PLAIN")) && use_gemm_big(M, N, 0, 0, lda, ldb))
     return accumulate ? gemm_big_launch<1>(p, s) : gemm_big_launch<0>(p, s);
   if (gl128) {
-    PC_TRY_GEMM(gemm_pair_flush(s));
     const dim3 grid(M / GM_BM, N / GM_BN, 1);
     return accumulate ? gemm_launch_direct<2, 2, 1, 3, 7>(p, grid, s)
                       : gemm_launch_direct<2, 2, 0, 3, 7>(p, grid, s);
@@ -1862,7 +1861,6 @@ int launch_wgrad_small(const float* s, long long lds, int B, int O, const float*
   PC_REQUIRE(s && x0 && dw0 && B > 0 && O > 0 && K0 > 0 && lds >= O && ldx0 >= K0 && ldo >= K0 &&
                  (!x1 || (dw1 && K1 > 0 && ldx1 >= K1 && ldo >= K1)),
              "wgrad_small: bad shape B=%d O=%d K0=%d K1=%d", B, O, K0, K1);
-  PC_TRY_GEMM(gemm_pair_flush(st));
   const long long n0 = (long long)O * ((K0 + 3) / 4), n1 = x1 ? (long long)O * ((K1 + 3) / 4) : 0;
   const int nb0 = (int)((n0 + 255) / 256), nb1 = (int)((n1 + 255) / 256);
   const WsmJob j0{x0, ldx0, K0, dw0};
@@ -1873,80 +1871,78 @@ int launch_wgrad_small(const float* s, long long lds, int B, int O, const float*
   return PCADV_OK;
 }
 
-// the deferred finishing reductions of this thread's weight gradients
-static thread_local WfBatch g_wf_pending{};
-
-int wgrad_flush(hipStream_t s) {
-  PC_TRY_GEMM(gemm_pair_flush(s));  // a waiting GEMM writes slabs this launch reads
-  WfBatch& b = g_wf_pending;
-  if (b.n == 0) return PCADV_OK;
-  const int nblk = b.blk0[b.n];
-  hipLaunchKernelGGL(k_wgrad_finish_batch, dim3((unsigned)nblk), dim3(256), 0, s, b);
-  b.n = 0;
-  b.blk0[0] = 0;
-  PC_HIP_CHECK_LAUNCH("k_wgrad_finish_batch");
-  return PCADV_OK;
-}
-
-static int wgrad_defer(const WfDesc& d, int nb, hipStream_t s) {
-  if (nb <= 0) return PCADV_OK;
-  if (g_wf_pending.n == WF_BATCH) PC_TRY_GEMM(wgrad_flush(s));
-  WfBatch& b = g_wf_pending;
-  b.d[b.n] = d;
-  b.blk0[b.n + 1] = b.blk0[b.n] + nb;
-  ++b.n;
-  return PCADV_OK;
-}
-
-int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long ldx, int rows,
-                      int O, int Kin, float* dw, long long ldo, float* db, float* gsum,
-                      int rows_per_group, int accumulate, void* ws, size_t ws_bytes, hipStream_t s,
-                      int defer) {
+// A weight gradient's slab GEMM: its plan, its GemmP and the slab / column-sum
+// regions of its workspace (shared by the one-call and the split forms)
+struct WgradJob {
+  WgradPlan w;
+  GemmP p;
+  float* slabs;
+  float* csum;
+  long long E;
+};
+static int wgrad_prepare(const float* dz, long long ldz, const float* x, long long ldx, int rows,
+                         int O, int Kin, float* dw, long long ldo, float* db, float* gsum,
+                         int rows_per_group, void* ws, size_t ws_bytes, WgradJob& j) {
   PC_REQUIRE(dz && x && dw && rows > 0 && O > 0 && Kin > 0 && ldo >= Kin && ldz >= O && ldx >= Kin,
              "gemm_wgrad: bad shape rows=%d O=%d Kin=%d", rows, O, Kin);
   PC_REQUIRE(!gsum || (rows_per_group > 0 && rows % rows_per_group == 0),
              "gemm_wgrad: per-group sums need rows %% rows_per_group == 0");
   PC_REQUIRE(fits31(rows, ldz, 4) && fits31(rows, ldx, 4), "gemm_wgrad: operands must span < 2 GB");
   PC_REQUIRE(rows_per_group <= 0 || rows % rows_per_group == 0, "gemm_wgrad: rows %% rows_per_group");
-  const WgradPlan w = wgrad_plan(rows, O, Kin, rows_per_group);
+  j.w = wgrad_plan(rows, O, Kin, rows_per_group);
   PC_REQUIRE(ws && ws_bytes >= gemm_wgrad_workspace_bytes(rows, O, Kin, rows_per_group),
              "gemm_wgrad: workspace");
-  float* slabs = static_cast<float*>(ws);
-  float* csum = (db || gsum) ? slabs + (size_t)w.nz * O * Kin : nullptr;
-  GemmP p{};
+  j.slabs = static_cast<float*>(ws);
+  j.csum = (db || gsum) ? j.slabs + (size_t)j.w.nz * O * Kin : nullptr;
+  GemmP& p = j.p;
+  p = GemmP{};
   p.a = dz; p.lda = ldz; p.b = x; p.ldb = ldx;
-  p.c = slabs; p.ldc = Kin;
+  p.c = j.slabs; p.ldc = Kin;
   p.M = O; p.N = Kin; p.K = rows;
   p.avec = ldz % 4 == 0 && ((uintptr_t)dz & 15) == 0;
   p.bvec = ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
   p.cvec = Kin % 4 == 0;
-  p.grp = w.grp; p.zpg = w.zpg; p.ksplit_len = w.len;
+  p.grp = j.w.grp; p.zpg = j.w.zpg; p.ksplit_len = j.w.len;
   p.slab_stride = (long long)O * Kin;
-  p.csum = csum;
-  PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(p, w.nz, s)));
-  const long long E = (long long)O * Kin;
-  if (!defer) PC_TRY_GEMM(gemm_pair_flush(s));  // the finishing launches read its slabs
-  if (defer) {
-    // the dW slab sums (and db, unless the per-group sums are wanted now) wait
-    // for wgrad_flush, which runs every deferred finish in one launch
-    PC_REQUIRE(w.groups <= WF_MAXG, "gemm_wgrad: %d groups cannot be deferred", w.groups);
-    const int nb_dw = (int)((E + WF_DWE - 1) / WF_DWE);
-    const int nb_cs = csum ? (O + 31) / 32 : 0;
-    const bool from_groups = w.groups > 1 || gsum;
-    const WfDesc all{slabs, E, w.nz, dw, Kin, ldo, accumulate, nb_dw, csum, O, w.groups, w.zpg,
-                     from_groups ? 1 : 0, gsum, db, accumulate};
-    if (!gsum) return wgrad_defer(all, nb_dw + nb_cs, s);
-    PC_TRY_GEMM(gemm_pair_flush(s));  // the slabs' GEMM may be waiting for its pair
-    hipLaunchKernelGGL(k_wgrad_finish, dim3((unsigned)nb_cs), dim3(256), 0, s,
-                       static_cast<const float*>(slabs), E, w.nz, dw, Kin, ldo, accumulate, 0,
-                       static_cast<const float*>(csum), O, w.groups, w.zpg, 1, gsum, db, accumulate);
-    PC_HIP_CHECK_LAUNCH("k_wgrad_finish (groups)");
-    WfDesc dwo = all;
-    dwo.csum = nullptr;
-    dwo.gs = nullptr;
-    dwo.db = nullptr;
-    return wgrad_defer(dwo, nb_dw, s);
+  p.csum = j.csum;
+  j.E = (long long)O * Kin;
+  return PCADV_OK;
+}
+
+// the per-group sums (gsum, or the workspace's scratch rows) of the slabs'
+// column sums and db from them, by separate k_slab_sum launches: the form for
+// more groups than k_wgrad_finish keeps in LDS
+static int wgrad_colsums_split(const WgradJob& j, int O, float* db, float* gsum, int accumulate,
+                               hipStream_t s) {
+  const bool from_groups = j.w.groups > 1 || gsum;
+  float* gs = gsum ? gsum : j.csum + (size_t)j.w.nz * O;
+  if (from_groups) {
+    hipLaunchKernelGGL(k_slab_sum, dim3((O + 31) / 32, j.w.groups), dim3(256), 0, s,
+                       static_cast<const float*>(j.csum), (long long)O, j.w.zpg, (long long)O, gs,
+                       (long long)O, O, 0LL, 0);
+    PC_HIP_CHECK_LAUNCH("k_slab_sum (groups)");
   }
+  if (db) {
+    hipLaunchKernelGGL(k_slab_sum, dim3((O + 31) / 32, 1), dim3(256), 0, s,
+                       static_cast<const float*>(from_groups ? gs : j.csum), (long long)O,
+                       from_groups ? j.w.groups : j.w.nz, (long long)O, db, 0LL, O, 0LL,
+                       accumulate);
+    PC_HIP_CHECK_LAUNCH("k_slab_sum (db)");
+  }
+  return PCADV_OK;
+}
+
+int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long ldx, int rows,
+                      int O, int Kin, float* dw, long long ldo, float* db, float* gsum,
+                      int rows_per_group, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+  WgradJob j;
+  PC_TRY_GEMM(wgrad_prepare(dz, ldz, x, ldx, rows, O, Kin, dw, ldo, db, gsum, rows_per_group, ws,
+                            ws_bytes, j));
+  PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(j.p, j.w.nz, s)));
+  const WgradPlan& w = j.w;
+  const long long E = j.E;
+  float* slabs = j.slabs;
+  float* csum = j.csum;
   if (w.groups <= WF_MAXG && !getenv_flag("PCADV_WGRAD_SPLIT_FINISH")) {
     // dW, the per-group sums and db in one launch (k_wgrad_finish)
     const int nb_dw = (int)((E + WF_DWE - 1) / WF_DWE);
@@ -1962,24 +1958,81 @@ int launch_gemm_wgrad(const float* dz, long long ldz, const float* x, long long 
   hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((E + 31) / 32), 1), dim3(256), 0, s,
                      static_cast<const float*>(slabs), E, w.nz, E, dw, 0LL, Kin, ldo, accumulate);
   PC_HIP_CHECK_LAUNCH("k_slab_sum (dw)");
-  if (csum) {
-    // per-group sums of the slabs' column sums, then their total
-    float* gs = gsum ? gsum : csum + (size_t)w.nz * O;
-    if (w.groups > 1 || gsum) {
-      hipLaunchKernelGGL(k_slab_sum, dim3((O + 31) / 32, w.groups), dim3(256), 0, s,
-                         static_cast<const float*>(csum), (long long)O, w.zpg, (long long)O, gs,
-                         (long long)O, O, 0LL, 0);
-      PC_HIP_CHECK_LAUNCH("k_slab_sum (groups)");
-    }
-    if (db) {
-      const bool from_groups = w.groups > 1 || gsum;
-      hipLaunchKernelGGL(k_slab_sum, dim3((O + 31) / 32, 1), dim3(256), 0, s,
-                         static_cast<const float*>(from_groups ? gs : csum), (long long)O,
-                         from_groups ? w.groups : w.nz, (long long)O, db, 0LL, O, 0LL, accumulate);
-      PC_HIP_CHECK_LAUNCH("k_slab_sum (db)");
+  if (csum) PC_TRY_GEMM(wgrad_colsums_split(j, O, db, gsum, accumulate, s));
+  return PCADV_OK;
+}
+
+static int wgrad_prepare_d(const pcadv_wgrad_desc& d, WgradJob& j) {
+  return wgrad_prepare(d.dz, d.ldz, d.x, d.ldx, d.rows, d.O, d.Kin, d.dw, d.ldo, d.db, d.gsum,
+                       d.rows_per_group, d.workspace, d.workspace_bytes, j);
+}
+
+// The slab GEMM of w (+ gsum and its db now, when asked) and optionally the
+// data-gradient GEMM g, paired into one launch where both forms allow it.
+// The dw (and db) sums are left to launch_wgrad_finish.
+int launch_gemm_wgrad_slabs(const pcadv_wgrad_desc* wd, const pcadv_gemm_desc* g, hipStream_t s) {
+  PC_REQUIRE(wd, "gemm_wgrad_slabs: null descriptor");
+  const pcadv_wgrad_desc& d = *wd;
+  WgradJob j;
+  PC_TRY_GEMM(wgrad_prepare_d(d, j));
+  PendingGemm slot{};
+  slot.on = g != nullptr;
+  PC_TRY_GEMM((gemm_launch<1, 1, 0, 6>(j.p, j.w.nz, s, &slot)));
+  if (g)
+    PC_TRY_GEMM(launch_gemm_impl(g->a, g->lda, g->ta, g->b, g->ldb, g->tb, g->c, g->ldc, g->M, g->N,
+                                 g->K, g->bias, g->bias_rows, g->rows_per_group, g->relu,
+                                 g->accumulate, g->cmask, g->ldm, g->precise, g->c_hi, g->c_lo,
+                                 g->ldcp, s, &slot));
+  PC_TRY_GEMM(gemm_slot_flush(slot, s));  // a GEMM that found no partner goes alone
+  if (d.gsum) {  // fc1's per-cloud sums are needed at once: finish the column sums now
+    if (j.w.groups <= WF_MAXG) {
+      hipLaunchKernelGGL(k_wgrad_finish, dim3((unsigned)((d.O + 31) / 32)), dim3(256), 0, s,
+                         static_cast<const float*>(j.slabs), j.E, j.w.nz, d.dw, d.Kin, d.ldo,
+                         d.accumulate, 0, static_cast<const float*>(j.csum), d.O, j.w.groups,
+                         j.w.zpg, 1, d.gsum, d.db, d.accumulate);
+      PC_HIP_CHECK_LAUNCH("k_wgrad_finish (groups)");
+    } else {
+      PC_TRY_GEMM(wgrad_colsums_split(j, d.O, d.db, d.gsum, d.accumulate, s));
     }
   }
   return PCADV_OK;
+}
+
+// The finishing sums of n weight gradients whose slabs launch_gemm_wgrad_slabs
+// enqueued: one k_wgrad_finish_batch launch per WF_BATCH descriptors, bitwise
+// the sums of launch_gemm_wgrad.  Column sums over more groups than the batch
+// kernel keeps in LDS take the separate k_slab_sum form.
+int launch_wgrad_finish(const pcadv_wgrad_desc* ds, int n, hipStream_t s) {
+  PC_REQUIRE(n >= 0 && (ds || n == 0), "wgrad_finish: bad descriptor list (n=%d)", n);
+  WfBatch b{};
+  auto flush = [&]() -> int {
+    if (b.n == 0) return PCADV_OK;
+    hipLaunchKernelGGL(k_wgrad_finish_batch, dim3((unsigned)b.blk0[b.n]), dim3(256), 0, s, b);
+    PC_HIP_CHECK_LAUNCH("k_wgrad_finish_batch");
+    b.n = 0;
+    b.blk0[0] = 0;
+    return PCADV_OK;
+  };
+  for (int i = 0; i < n; ++i) {
+    const pcadv_wgrad_desc& d = ds[i];
+    WgradJob j;
+    PC_TRY_GEMM(wgrad_prepare_d(d, j));
+    const int nb_dw = (int)((j.E + WF_DWE - 1) / WF_DWE);
+    const bool from_groups = j.w.groups > 1 || d.gsum;
+    // gsum's column sums (and db) were finished by the slabs call
+    const bool cs = j.csum && !d.gsum;
+    const bool cs_here = cs && !(from_groups && j.w.groups > WF_MAXG);
+    if (cs && !cs_here) PC_TRY_GEMM(wgrad_colsums_split(j, d.O, d.db, nullptr, d.accumulate, s));
+    const int nb_cs = cs_here ? (d.O + 31) / 32 : 0;
+    const WfDesc w{j.slabs, j.E, j.w.nz, d.dw, d.Kin, d.ldo, d.accumulate, nb_dw,
+                   cs_here ? j.csum : nullptr, d.O, j.w.groups, j.w.zpg, from_groups ? 1 : 0,
+                   nullptr, cs_here ? d.db : nullptr, d.accumulate};
+    if (b.n == WF_BATCH) PC_TRY_GEMM(flush());
+    b.d[b.n] = w;
+    b.blk0[b.n + 1] = b.blk0[b.n] + nb_dw + nb_cs;
+    ++b.n;
+  }
+  return flush();
 }
 
 constexpr int CS_ROWS = 128;  // rows per colsum chunk (enough workgroups to fill the chip)
@@ -2058,9 +2111,9 @@ int launch_conv_max_x3(const float* x, long long ldx, int C, int Npts, int K, co
     if (planes && use_gemm_big(C * Npts, O, Npts, 2, ldxp, K)) {
       PC_TRY_GEMM(gemm_big_launch<2>(p, s));
     } else if (planes) {
-      PC_TRY_GEMM((gemm_launch_grid<2, 2, 2, 3>(p, grid, s)));
+      PC_TRY_GEMM((gemm_launch_grid<2, 2, 2, 3>(p, grid, s, nullptr)));
     } else {
-      PC_TRY_GEMM((gemm_launch_grid<0, 0, 2, 3>(p, grid, s)));
+      PC_TRY_GEMM((gemm_launch_grid<0, 0, 2, 3>(p, grid, s, nullptr)));
     }
   }
   const int pairs = C * O;

@@ -314,6 +314,18 @@ class DeviceCloudLoader:
         lw = 0 if self.labels is None else int(self.labels.shape[1])
         if out_lab is None and self.labels is not None:
             raise ValueError("gather_at: out_lab required for a labelled split")
+        B = self.B
+
+        def need(t, name, shape, dtype):
+            if (t.device != self.device or t.dtype != dtype or tuple(t.shape) != shape
+                    or not t.is_contiguous()):
+                raise ValueError(f"gather_at: {name} must be contiguous {dtype} {shape} on "
+                                 f"{self.device} (got {t.dtype} {tuple(t.shape)} on {t.device})")
+        need(out, "out", (B, self.npts, 3), torch.float32)
+        if self.labels is not None:
+            need(out_lab, "out_lab", (B, lw), torch.int64)
+        need(order, "order", (self.n,), torch.int64)
+        need(cursor, "cursor", (1,), torch.int32)
         P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         check(self.lib.pcadv_gather_clouds_at(P(self.pts), self.n, self.npts, self.npts, P(order),
                                               P(cursor), self.B, P(self.labels), lw, None,

@@ -22,7 +22,6 @@ layer); tests/test_gpu_seg.py holds the tolerances.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
 
@@ -64,8 +63,6 @@ class _Engine:
 
     def __init__(self):
         self.lib = _lib.load()
-        self._pending = []  # workspaces of the deferred weight-gradient finishes
-
 
     def gemm(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, cmask=None, ldm=0, bias=None,
              bias_rows=None, rows_per_group=0, relu=False, accumulate=False, precise=False,
@@ -98,39 +95,69 @@ class _Engine:
         check(self.lib.pcadv_split_bf2(_p(x), c, r, c, _pb(hi), _pb(lo), c, stream_ptr()),
               "pcadv_split_bf2")
 
+    def gemm_desc(self, a, lda, b, ldb, c, ldc, M, N, K, *, ta=0, tb=0, cmask=None, ldm=0,
+                  bias=None, bias_rows=None, rows_per_group=0, relu=False, accumulate=False,
+                  precise=False, a_off=0, b_off=0, c_off=0, m_off=0):
+        """pcadv_gemm's arguments as a pcadv_gemm_desc (for wgrad(..., pair=))."""
+        return _lib.GemmDesc(_p(a, a_off), lda, ta, _p(b, b_off), ldb, tb, _p(c, c_off), ldc, M, N,
+                             K, None if bias is None else _p(bias),
+                             None if bias_rows is None else _p(bias_rows), rows_per_group,
+                             int(relu), int(accumulate), None if cmask is None else _p(cmask, m_off),
+                             ldm, int(precise), None, None, 0)
+
+    def gemm_run(self, g):
+        """Enqueue a pcadv_gemm_desc as its own launch."""
+        check(self.lib.pcadv_gemm(g.a, g.lda, g.ta, g.b, g.ldb, g.tb, g.c, g.ldc, g.M, g.N, g.K,
+                                  g.bias, g.bias_rows, g.rows_per_group, g.relu, g.accumulate,
+                                  g.cmask, g.ldm, g.precise, g.c_hi, g.c_lo, g.ldcp, stream_ptr()),
+              "pcadv_gemm")
+
     def wgrad(self, dz, ldz, x, ldx, rows, O, K, dw, ldo, *, db=None, gsum=None, rpg=0, dz_off=0,
-              x_off=0, dw_off=0, defer=False):
-        """defer: the finishing slab sums of dw (and db) wait for flush(), which
-        runs all pending ones in one launch; the workspace is held until then."""
+              x_off=0, dw_off=0, fin=None, pair=None):
+        """dw (+ db, gsum) = dz^T x over fixed-order slabs.
+
+        fin: a caller-owned list; the finishing dw (and db) sums are then left to
+        finish(fin), which runs all of them in one launch (the workspace rides in
+        the list until then).  pair: a pcadv_gemm_desc (an independent data
+        gradient) enqueued in the same launch as the slab GEMM.  Nothing is held
+        by the library between calls: dropping `fin` abandons the sums."""
         nb = self.lib.pcadv_gemm_wgrad_workspace_bytes(rows, O, K, rpg)
         ws = _ws(nb, dz.device)
-        fn = self.lib.pcadv_gemm_wgrad_defer if defer else self.lib.pcadv_gemm_wgrad
-        check(fn(_p(dz, dz_off), ldz, _p(x, x_off), ldx, rows, O, K, _p(dw, dw_off), ldo,
-                 None if db is None else _p(db), None if gsum is None else _p(gsum), rpg, 0, _p(ws),
-                 ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
-        if defer:
-            self._pending.append(ws)
-
-    @contextlib.contextmanager
-    def pair(self):
-        """A weight-gradient GEMM and an independent data-gradient GEMM issued
-        inside run as ONE launch (pcadv_gemm_pair_begin / _end); PCADV_GEMM_PAIR=0:
-        two launches, for A/B runs."""
-        if not _PAIR:
-            yield
+        if fin is None and pair is None:
+            check(self.lib.pcadv_gemm_wgrad(
+                _p(dz, dz_off), ldz, _p(x, x_off), ldx, rows, O, K, _p(dw, dw_off), ldo,
+                None if db is None else _p(db), None if gsum is None else _p(gsum), rpg, 0, _p(ws),
+                ws.numel(), stream_ptr()), "pcadv_gemm_wgrad")
             return
-        check(self.lib.pcadv_gemm_pair_begin(stream_ptr()), "pcadv_gemm_pair_begin")
-        try:
-            yield
-        finally:
-            check(self.lib.pcadv_gemm_pair_end(stream_ptr()), "pcadv_gemm_pair_end")
+        d = _lib.WgradDesc(_p(dz, dz_off), ldz, _p(x, x_off), ldx, rows, O, K, _p(dw, dw_off), ldo,
+                           None if db is None else _p(db), None if gsum is None else _p(gsum), rpg,
+                           0, _p(ws), ws.numel())
+        check(self.lib.pcadv_gemm_wgrad_slabs(ctypes.byref(d),
+                                              None if pair is None else ctypes.byref(pair),
+                                              stream_ptr()), "pcadv_gemm_wgrad_slabs")
+        if fin is None:
+            check(self.lib.pcadv_wgrad_finish(ctypes.byref(d), 1, stream_ptr()), "pcadv_wgrad_finish")
+        else:
+            fin.append((d, ws))
 
-    def flush(self):
-        """Enqueue the deferred weight-gradient finishes (one launch)."""
-        try:
-            check(self.lib.pcadv_wgrad_flush(stream_ptr()), "pcadv_wgrad_flush")
-        finally:
-            self._pending.clear()  # stream order keeps the slabs until the launch has read them
+    def finish(self, fin):
+        """Enqueue the finishing sums of the weight gradients collected in fin
+        (one launch); the workspaces are released after it is enqueued (stream
+        order keeps them until the launch has read them)."""
+        if not fin:
+            return
+        arr = (_lib.WgradDesc * len(fin))(*[d for d, _ in fin])
+        check(self.lib.pcadv_wgrad_finish(arr, len(fin), stream_ptr()), "pcadv_wgrad_finish")
+        fin.clear()
+
+    def wgrad_and_gemm(self, fin, wargs, wkw, g):
+        """One layer's weight gradient (wgrad(*wargs, **wkw)) and its data gradient
+        g (a pcadv_gemm_desc): one paired launch, or two (PCADV_GEMM_PAIR=0)."""
+        if _PAIR:
+            self.wgrad(*wargs, fin=fin, pair=g, **wkw)
+        else:
+            self.wgrad(*wargs, fin=fin, **wkw)
+            self.gemm_run(g)
 
     def colsum(self, x, ld, M, N, out, *, ymask=None, ldm=0, x_off=0, m_off=0):
         nb = self.lib.pcadv_colsum_workspace_bytes(M, N)
@@ -294,35 +321,40 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         if out is not None:
             return out[k].view(like.shape) if hasattr(like, "shape") else out[k]
         return torch.empty_like(like) if hasattr(like, "shape") else torch.empty(like, device=dev)
+    # the weight gradients' finishing slab sums wait in this local list and run
+    # in one launch at the end (E.finish); an exception drops the list and
+    # nothing is left behind (the library holds no state between calls)
+    fin = [] if _DEFER else None
     # ---- fc4 .. fc2 -------------------------------------------------------
     dW4 = _g(18, Wf[3]); db4 = _g(19, ncls)
     dh3 = torch.empty(M, 128, device=dev)
-    with E.pair():
-        E.wgrad(dl, ncls, h3, 128, M, ncls, 128, dW4, 128, db=db4, defer=_DEFER)
-        E.gemm(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3, ldm=128, precise=_DGRAD_PRECISE)
+    E.wgrad_and_gemm(fin, (dl, ncls, h3, 128, M, ncls, 128, dW4, 128), dict(db=db4),
+                     E.gemm_desc(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3,
+                                 ldm=128, precise=_DGRAD_PRECISE))
     dW3 = _g(16, Wf[2]); db3 = _g(17, 128)
     dh2 = torch.empty(M, 256, device=dev)
-    with E.pair():
-        E.wgrad(dh3, 128, h2, 256, M, 128, 256, dW3, 256, db=db3, defer=_DEFER)
-        E.gemm(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2, ldm=256, precise=_DGRAD_PRECISE)
+    E.wgrad_and_gemm(fin, (dh3, 128, h2, 256, M, 128, 256, dW3, 256), dict(db=db3),
+                     E.gemm_desc(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2,
+                                 ldm=256, precise=_DGRAD_PRECISE))
     dW2 = _g(14, Wf[1]); db2 = _g(15, 256)
     dh1 = torch.empty(M, 256, device=dev)
-    with E.pair():
-        E.wgrad(dh2, 256, h1, 256, M, 256, 256, dW2, 256, db=db2, defer=_DEFER)
-        E.gemm(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1, ldm=256, precise=_DGRAD_PRECISE)
+    E.wgrad_and_gemm(fin, (dh2, 256, h1, 256, M, 256, 256, dW2, 256), dict(db=db2),
+                     E.gemm_desc(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1,
+                                 ldm=256, precise=_DGRAD_PRECISE))
     # ---- fc1: local columns (+ per-cloud sums s1), then the tiled columns --
     W1 = Wf[0]
     dW1 = _g(12, W1); db1 = _g(13, 256)
     s1 = torch.empty(B, 256, device=dev)  # per-cloud sums of dz1
     dloc = torch.empty(M, _LOC, device=dev)
-    with E.pair():  # the data gradient first: the weight gradient's group sums follow its launch
-        E.gemm(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc, ldm=_LOC, precise=_DGRAD_PRECISE)
-        E.wgrad(dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024, db=db1, gsum=s1, rpg=N, defer=_DEFER)
+    E.wgrad_and_gemm(fin, (dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024),
+                     dict(db=db1, gsum=s1, rpg=N),
+                     E.gemm_desc(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc,
+                                 ldm=_LOC, precise=_DGRAD_PRECISE))
     # the tiled global and class columns: B per-cloud rows, exact f32, one launch
     if not _SMALL:
-        E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, defer=_DEFER)
+        E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, fin=fin)
         E.wgrad(s1, 256, cvec, cvec.shape[1], B, 256, cvec.shape[1], dW1, 3024, dw_off=3008,
-                defer=_DEFER)
+                fin=fin)
     else:
         check(E.lib.pcadv_wgrad_small(_p(s1), 256, B, 256, _p(gmax), 2048, 2048, _p(dW1, 960),
                                       _p(cvec), cvec.shape[1], cvec.shape[1], _p(dW1, 3008), 3024,
@@ -346,16 +378,17 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
         dWc[i] = _g(2 * i, W[i])
         dbc[i] = _g(2 * i + 1, O)
         if i > 0:
-            with E.pair():
-                E.wgrad(dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i],
-                        x_off=_OFF[i - 1], defer=_DEFER)
-                E.gemm(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1, cmask=xloc, ldm=_LOC,
-                       accumulate=True, precise=_DGRAD_PRECISE, a_off=_OFF[i], m_off=_OFF[i - 1],
-                       c_off=_OFF[i - 1])
+            E.wgrad_and_gemm(fin, (dloc, _LOC, xloc, _LOC, M, O, K, dWc[i], K),
+                             dict(db=dbc[i], dz_off=_OFF[i], x_off=_OFF[i - 1]),
+                             E.gemm_desc(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1,
+                                         cmask=xloc, ldm=_LOC, accumulate=True,
+                                         precise=_DGRAD_PRECISE, a_off=_OFF[i],
+                                         m_off=_OFF[i - 1], c_off=_OFF[i - 1]))
         else:
-            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i], defer=_DEFER)
-    # every weight gradient's slab sums (deferred above) in one launch
-    E.flush()
+            E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i], fin=fin)
+    # every weight gradient's slab sums (collected above) in one launch
+    if fin is not None:
+        E.finish(fin)
     grads = []
     for i in range(6):
         grads += [dWc[i].view(O_shape(i)), dbc[i]]

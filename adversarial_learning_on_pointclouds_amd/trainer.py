@@ -156,7 +156,7 @@ class _GraphedIteration:
     flag, captured on first use; the capture's warm-up leaves parameters, Adam
     state, counters and the ring as they were."""
 
-    def __init__(self, step, loaders, ring, lab_width=1):
+    def __init__(self, step, loaders, ring):
         self.step, self.loaders, self.ring = step, loaders, ring
         B, N, dev = step.B, step.N, step.device
         L = len(loaders)
@@ -168,7 +168,9 @@ class _GraphedIteration:
         self.order = [torch.zeros(ld.n, dtype=torch.int64, device=dev) for ld in loaders]
         self.pos = [None] * L  # host: next batch of the current epoch
         self.pts = [torch.zeros(B, N, 3, device=dev) for _ in loaders]
-        self.lab = torch.zeros(B, lab_width, dtype=torch.int64, device=dev)
+        # the labelled split's label width (the gather writes B x width int64)
+        lw = max([int(ld.labels.shape[1]) for ld in loaders if ld.labels is not None] or [1])
+        self.lab = torch.zeros(B, lw, dtype=torch.int64, device=dev)
         self.graphs = {}
 
     def next_batches(self):

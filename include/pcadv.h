@@ -258,31 +258,43 @@ size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_g
 int pcadv_gemm_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows, int O,
                      int Kin, float* dw, int64_t ldo, float* db, float* gsum, int rows_per_group,
                      int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream);
-/* The same weight gradient with its finishing slab sums deferred: the GEMM is
- * enqueued now, the dw (and db) sums join this thread's pending list and run,
- * with every other pending one, in ONE launch at pcadv_wgrad_flush (gsum, when
- * given, is formed now).  dw, db and the workspace must stay valid and
- * untouched until the flush is enqueued; results are bitwise those of
- * pcadv_gemm_wgrad. */
-int pcadv_gemm_wgrad_defer(const float* dz, int64_t ldz, const float* x, int64_t ldx, int rows,
-                           int O, int Kin, float* dw, int64_t ldo, float* db, float* gsum,
-                           int rows_per_group, int accumulate, void* workspace,
-                           size_t workspace_bytes, hipStream_t stream);
-int pcadv_wgrad_flush(hipStream_t stream);
-/* Pair a weight-gradient GEMM (pcadv_gemm_wgrad[_defer]) with an independent
- * data-gradient GEMM (pcadv_gemm with ta = 0, tb = 1): between begin and end
- * the first of the two waits and the second launches both as ONE kernel
- * (their workgroups side by side, each output bitwise its own launch's).  Only
- * those two calls may sit between begin and end on this thread; end enqueues a
- * GEMM still waiting. */
-int pcadv_gemm_pair_begin(hipStream_t stream);
+/* Descriptor forms of pcadv_gemm_wgrad's and pcadv_gemm's arguments, for the
+ * split / paired entry points below.  A descriptor is read during the call
+ * only: the library keeps neither it nor any pointer in it. */
+typedef struct pcadv_wgrad_desc {
+  const float* dz; int64_t ldz; const float* x; int64_t ldx;
+  int rows, O, Kin; float* dw; int64_t ldo; float* db; float* gsum;
+  int rows_per_group, accumulate; void* workspace; size_t workspace_bytes;
+} pcadv_wgrad_desc;
+typedef struct pcadv_gemm_desc {
+  const float* a; int64_t lda; int ta; const float* b; int64_t ldb; int tb;
+  float* c; int64_t ldc; int M, N, K; const float* bias; const float* bias_rows;
+  int rows_per_group, relu, accumulate; const float* cmask; int64_t ldm; int precise;
+  void* c_hi; void* c_lo; int64_t ldcp;
+} pcadv_gemm_desc;
+/* pcadv_gemm_wgrad split in two calls, so that one launch can finish the slab
+ * sums of many weight gradients (the seg backward's launch count, not its
+ * values: bitwise pcadv_gemm_wgrad).
+ * pcadv_gemm_wgrad_slabs enqueues w's slab GEMM into w->workspace (and, when
+ * w->gsum is given, the per-group sums and db now); when g is non-null it also
+ * enqueues the GEMM g (a data gradient: pcadv_gemm's arguments), and where both
+ * have the engine's pairable forms (g: ta = 0, tb = 1, precise = 0, M > 32) the
+ * two run as ONE launch, their workgroups side by side, each output bitwise its
+ * own launch's.  g must neither read nor write anything w reads or writes.
+ * pcadv_wgrad_finish then enqueues the remaining dw (and db) sums of n such
+ * weight gradients in one launch (more launches above 16).  Between the two
+ * calls the caller keeps dw, db and the workspaces alive and untouched; nothing
+ * is held by the library, so a caller that abandons a backward between them
+ * simply drops its descriptors. */
+int pcadv_gemm_wgrad_slabs(const pcadv_wgrad_desc* w, const pcadv_gemm_desc* g,
+                           hipStream_t stream);
+int pcadv_wgrad_finish(const pcadv_wgrad_desc* w, int n, hipStream_t stream);
 /* Weight gradient over a few rows in exact f32 (rows in order):
  * dw0[o][k] (+)= sum_{b < B} s[b][o] x0[b][k] for k < K0, and the same with
  * x1 / K1 / dw1 when x1 is given, in one launch (fc1's per-cloud columns). */
 int pcadv_wgrad_small(const float* s, int64_t lds, int B, int O, const float* x0, int64_t ldx0,
                       int K0, float* dw0, const float* x1, int64_t ldx1, int K1, float* dw1,
                       int64_t ldo, int accumulate, hipStream_t stream);
-int pcadv_gemm_pair_end(hipStream_t stream);
 
 /* Column sums (bias gradients): out[n] (+)= sum_m x[m][n] [ymask[m][n] > 0];
  * pcadv_group_colsum writes one row of sums per rows_per_group rows. */

@@ -409,14 +409,21 @@ def test_wgrad_small_matches_f64(B, O, K0, K1, acc):
     assert np.array_equal(got[:, 3 + K0 + K1:], w0[:, 3 + K0 + K1:])
 
 
-def test_gemm_weight_grad_deferred_batch_is_bitwise():
-    """pcadv_gemm_wgrad_defer + pcadv_wgrad_flush: the finishing slab sums of
-    several weight gradients (plain, accumulating, with per-group sums, and
-    more than one batch of descriptors) run in one launch per flush and give
-    bitwise the results of the immediate pcadv_gemm_wgrad calls."""
+def _wdesc(dZ, X, rows, O, K, dW, db, gs, rpg, acc, ws, nb):
+    return _lib.WgradDesc(_p(dZ), O, _p(X), K, rows, O, K, _p(dW), K, _p(db),
+                          _p(gs) if gs is not None else None, rpg, int(acc), _p(ws), nb)
+
+
+def test_gemm_weight_grad_split_batch_is_bitwise():
+    """pcadv_gemm_wgrad_slabs + one pcadv_wgrad_finish over the descriptor
+    list: the finishing slab sums of several weight gradients (plain,
+    accumulating, with per-group sums, more groups than the batch kernel keeps
+    in LDS, and more than one batch of descriptors) give bitwise the results of
+    the one-call pcadv_gemm_wgrad.  Nothing is retained between calls: a
+    slabs call that is never finished changes nothing that follows."""
     lib = _lib.load()
     shapes = [(300, 100, 96, 40), (32768, 2048, 96, 40), (32768, 0, 256, 960), (16, 0, 256, 2048),
-              (4096, 0, 64, 3)] * 4  # 20 > one batch of 16 descriptors
+              (4096, 0, 64, 3), (8000, 100, 64, 40)] * 3  # 18 > one batch of 16; 80 groups > 64
     cases = []
     for i, (rows, rpg, O, K) in enumerate(shapes):
         rng = np.random.default_rng(100 + i)
@@ -428,26 +435,76 @@ def test_gemm_weight_grad_deferred_batch_is_bitwise():
         init = _t(rng.standard_normal((O, K)).astype(np.float32)), _t(rng.standard_normal(O).astype(np.float32))
         cases.append((rows, rpg, O, K, G, nb, acc, dZ, X, init))
 
-    def run(defer):
-        outs, keep = [], []
-        fn = lib.pcadv_gemm_wgrad_defer if defer else lib.pcadv_gemm_wgrad
-        for rows, rpg, O, K, G, nb, acc, dZ, X, (w0, b0) in cases:
+    def run(split):
+        outs, keep, fin = [], [], []
+        for n, (rows, rpg, O, K, G, nb, acc, dZ, X, (w0, b0)) in enumerate(cases):
             dW, db = w0.clone(), b0.clone()
-            gs = torch.zeros(G, O, device=DEV)
+            # per-group sums asked for on every other grouped case
+            gs = torch.zeros(G, O, device=DEV) if rpg and n % 2 == 0 else None
             ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
             keep.append(ws)
-            check(fn(_p(dZ), O, _p(X), K, rows, O, K, _p(dW), K, _p(db), _p(gs) if rpg else None,
-                     rpg, int(acc), _p(ws), nb, stream_ptr()), "wgrad")
+            if split:
+                d = _wdesc(dZ, X, rows, O, K, dW, db, gs, rpg, acc, ws, nb)
+                check(lib.pcadv_gemm_wgrad_slabs(ctypes.byref(d), None, stream_ptr()), "slabs")
+                fin.append(d)
+            else:
+                check(lib.pcadv_gemm_wgrad(_p(dZ), O, _p(X), K, rows, O, K, _p(dW), K, _p(db),
+                                           _p(gs) if gs is not None else None, rpg, int(acc),
+                                           _p(ws), nb, stream_ptr()), "wgrad")
             outs.append((dW, db, gs))
-        if defer:
-            check(lib.pcadv_wgrad_flush(stream_ptr()), "flush")
+        if split:
+            arr = (_lib.WgradDesc * len(fin))(*fin)
+            check(lib.pcadv_wgrad_finish(arr, len(fin), stream_ptr()), "finish")
         torch.cuda.synchronize()
         return outs
 
-    for a, b in zip(run(False), run(True)):
+    ref = run(False)
+    # an abandoned split weight gradient (slabs enqueued, never finished)
+    rows, rpg, O, K, G, nb, acc, dZ, X, (w0, b0) = cases[0]
+    junk = [torch.empty(nb, device=DEV, dtype=torch.uint8), w0.clone(), b0.clone()]
+    d = _wdesc(dZ, X, rows, O, K, junk[1], junk[2], None, rpg, 0, junk[0], nb)
+    check(lib.pcadv_gemm_wgrad_slabs(ctypes.byref(d), None, stream_ptr()), "abandoned slabs")
+    for a, b in zip(ref, run(True)):
         for x, y in zip(a, b):
+            assert (x is None and y is None) or torch.equal(x, y)
+    check(lib.pcadv_wgrad_finish(None, 0, stream_ptr()), "finish of an empty list")
+
+
+def test_gemm_wgrad_slabs_paired_with_data_gradient_is_bitwise():
+    """pcadv_gemm_wgrad_slabs with a data-gradient descriptor: the two GEMMs
+    in one launch give bitwise the outputs of their own launches (pcadv_gemm,
+    pcadv_gemm_wgrad), plain and accumulating, masked, with per-group sums."""
+    lib = _lib.load()
+    rng = np.random.default_rng(77)
+    M, O, K, rpg = 4096, 256, 128, 1024
+    dZ = _t(rng.standard_normal((M, O)).astype(np.float32))
+    X = _t(rng.standard_normal((M, K)).astype(np.float32))
+    W = _t(rng.standard_normal((O, K)).astype(np.float32))
+    Y = _t(rng.standard_normal((M, K)).astype(np.float32))
+    nb = lib.pcadv_gemm_wgrad_workspace_bytes(M, O, K, rpg)
+    for acc in (0, 1):
+        c0 = _t(rng.standard_normal((M, K)).astype(np.float32))
+        outs = []
+        for paired in (False, True):
+            dW, db = torch.zeros(O, K, device=DEV), torch.zeros(O, device=DEV)
+            gs = torch.zeros(M // rpg, O, device=DEV)
+            C = c0.clone()
+            ws = torch.empty(nb, device=DEV, dtype=torch.uint8)
+            g = _lib.GemmDesc(_p(dZ), O, 0, _p(W), K, 1, _p(C), K, M, K, O, None, None, 0, 0, acc,
+                              _p(Y), K, 0, None, None, 0)
+            if paired:
+                d = _wdesc(dZ, X, M, O, K, dW, db, gs, rpg, 0, ws, nb)
+                check(lib.pcadv_gemm_wgrad_slabs(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "pair")
+                check(lib.pcadv_wgrad_finish(ctypes.byref(d), 1, stream_ptr()), "finish")
+            else:
+                check(lib.pcadv_gemm_wgrad(_p(dZ), O, _p(X), K, M, O, K, _p(dW), K, _p(db), _p(gs),
+                                           rpg, 0, _p(ws), nb, stream_ptr()), "wgrad")
+                check(lib.pcadv_gemm(_p(dZ), O, 0, _p(W), K, 1, _p(C), K, M, K, O, None, None, 0, 0,
+                                     acc, _p(Y), K, 0, None, None, 0, stream_ptr()), "gemm")
+            torch.cuda.synchronize()
+            outs.append((dW, db, gs, C))
+        for x, y in zip(*outs):
             assert torch.equal(x, y)
-    check(lib.pcadv_wgrad_flush(stream_ptr()), "flush of an empty list")
 
 
 def test_colsum_and_group_colsum():
@@ -683,6 +740,40 @@ def test_seg_backward_vs_oracle_same_masks(B, N):
         grads = seg_backward(fw, _t(dout.reshape(B * N, 50)))
     ref = onp.seg_backward(S, _oracle_cache(fw, pts, cls), dout)
     for (name, r), g in zip(ref.items(), grads):
+        e = np.abs(g.cpu().numpy().reshape(r.shape) - r).max() / max(np.abs(r).max(), 1e-30)
+        assert e < 1e-4, (name, e)
+
+
+def test_seg_backward_more_clouds_than_the_batch_kernel_groups():
+    """B = 80 > 64 clouds (fc1's per-cloud sums then have more groups than the
+    finishing batch kernel keeps in LDS): the split (slabs + one finish launch)
+    and the one-call backward agree bitwise, and both match the oracle's
+    backward on this forward's activations (this raised before)."""
+    from adversarial_learning_on_pointclouds_amd import seg as segmod
+    B, N = 80, 64
+    S = onp.make_params(onp.seg_spec(50), seed=91)
+    rng = np.random.default_rng(92)
+    pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    cls = np.zeros((B, 1, 16), np.float32)
+    cls[np.arange(B), 0, rng.integers(0, 16, B)] = 1
+    seg = rng.integers(0, 50, (B, N))
+    params = [_t(v) for v in S.values()]
+    saved = segmod._PAIR, segmod._DEFER
+    outs = []
+    try:
+        with torch.no_grad():
+            fw = seg_forward(_t(pts), _t(cls), params)
+            logits = fw["logits"].cpu().numpy().reshape(B, N, 50)
+            _, dout = onp.seg_cross_entropy(logits, seg)
+            for pair, defer in ((True, True), (False, False)):
+                segmod._PAIR, segmod._DEFER = pair, defer
+                outs.append([g.clone() for g in seg_backward(fw, _t(dout.reshape(B * N, 50)))])
+    finally:
+        segmod._PAIR, segmod._DEFER = saved
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    ref = onp.seg_backward(S, _oracle_cache(fw, pts, cls), dout)
+    for (name, r), g in zip(ref.items(), outs[0]):
         e = np.abs(g.cpu().numpy().reshape(r.shape) - r).max() / max(np.abs(r).max(), 1e-30)
         assert e < 1e-4, (name, e)
 
