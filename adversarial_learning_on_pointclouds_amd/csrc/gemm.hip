@@ -666,14 +666,14 @@ k_gemm_x3(GemmP p) {
 }
 
 // A weight gradient (six products, TA = TB = 1, slabs) and an independent data
-// gradient (TA = 0, TB = 1, three products) in ONE launch: workgroups
+// gradient (TA = 0, TB = 1, NPD = three or six products) in ONE launch: workgroups
 // [0, n_first) run the first of the two, the rest the second (wfirst: the
 // weight gradient first).  Each keeps its own grid geometry and XCD order, so
 // every output is bitwise what its own launch gives; the pair saves a launch
 // boundary and lets the two fill each other's idle CUs (the segmentation
 // backward's per-layer weight and data gradients both read that layer's dz).
 struct PairGeom { int n, gx, gy, gz; };
-template <int VW, int MD, int VD>
+template <int VW, int MD, int VD, int NPD>
 __global__ void __launch_bounds__(GM_T)
 k_gemm_x3_pair(GemmP pw, PairGeom gw, GemmP pd, PairGeom gd, int wfirst) {
   const int b = (int)blockIdx.x;
@@ -681,7 +681,7 @@ k_gemm_x3_pair(GemmP pw, PairGeom gw, GemmP pd, PairGeom gd, int wfirst) {
   const bool w = (b < nfirst) == (wfirst != 0);
   const int lin = b < nfirst ? b : b - nfirst;
   if (w) gemm_x3_body<1, 1, 0, 6, VW>(pw, lin, gw.gx, gw.gy, gw.gz);
-  else gemm_x3_body<0, 1, MD, 3, VD>(pd, lin, gd.gx, gd.gy, gd.gz);
+  else gemm_x3_body<0, 1, MD, NPD, VD>(pd, lin, gd.gx, gd.gy, gd.gz);
 }
 
 // ---------------------------------------------------------------------------
@@ -1518,8 +1518,8 @@ static int gemm_launch_direct(const GemmP& p, dim3 grid, hipStream_t s) {
 // outlives the call.
 struct PendingGemm {
   bool on, has;
-  int kind;  // 0: weight gradient <1, 1, 0, 6, v>; 1: data gradient <0, 1, mode, 3, v>
-  int v, mode;
+  int kind;  // 0: weight gradient <1, 1, 0, 6, v>; 1: data gradient <0, 1, mode, np, v>
+  int v, mode, np;
   GemmP p;
   dim3 grid;
 };
@@ -1539,6 +1539,13 @@ static int gemm_slot_flush(PendingGemm& slot, hipStream_t s) {
       case 2: return gemm_launch_direct<1, 1, 0, 6, 2>(p, g, s);
       default: return gemm_launch_direct<1, 1, 0, 6, 3>(p, g, s);
     }
+  }
+  if (slot.np == 6) {
+    if (slot.mode == 0)
+      return slot.v == 2 ? gemm_launch_direct<0, 1, 0, 6, 2>(p, g, s)
+                         : gemm_launch_direct<0, 1, 0, 6, 3>(p, g, s);
+    return slot.v == 2 ? gemm_launch_direct<0, 1, 1, 6, 2>(p, g, s)
+                       : gemm_launch_direct<0, 1, 1, 6, 3>(p, g, s);
   }
   if (slot.mode == 0)
     return slot.v == 2 ? gemm_launch_direct<0, 1, 0, 3, 2>(p, g, s)
@@ -1560,17 +1567,17 @@ static int pair_wfirst(int issued) {
   }();
   return v < 0 ? issued : v;
 }
-template <int VW, int MD, int VD>
+template <int VW, int MD, int VD, int NPD>
 static int gemm_pair_launch(const GemmP& pw, dim3 gw, const GemmP& pd, dim3 gd, int wfirst,
                             hipStream_t s) {
   wfirst = pair_wfirst(wfirst);
   static bool attr = false;
   if (!attr) {
-    PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3_pair<VW, MD, VD>));
+    PC_TRY_GEMM(gemm_lds_attr(k_gemm_x3_pair<VW, MD, VD, NPD>));
     attr = true;
   }
   const PairGeom a = pair_geom(gw), b = pair_geom(gd);
-  hipLaunchKernelGGL((k_gemm_x3_pair<VW, MD, VD>), dim3((unsigned)(a.n + b.n)), dim3(GM_T),
+  hipLaunchKernelGGL((k_gemm_x3_pair<VW, MD, VD, NPD>), dim3((unsigned)(a.n + b.n)), dim3(GM_T),
                      sizeof(GemmLds), s, pw, a, pd, b, wfirst);
   PC_HIP_CHECK_LAUNCH("k_gemm_x3_pair");
   return PCADV_OK;
@@ -1579,7 +1586,7 @@ static int gemm_pair_launch(const GemmP& pw, dim3 gw, const GemmP& pd, dim3 gd, 
 template <int TA, int TB, int MODE, int NP, int VEC>
 static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s, PendingGemm* slot) {
   constexpr bool is_w = TA == 1 && TB == 1 && MODE == 0 && NP == 6 && VEC >= 1;
-  constexpr bool is_d = TA == 0 && TB == 1 && (MODE == 0 || MODE == 1) && NP == 3 && VEC >= 2;
+  constexpr bool is_d = TA == 0 && TB == 1 && (MODE == 0 || MODE == 1) && VEC >= 2;
   if constexpr (is_w || is_d) {
     if (slot && slot->on) {
       if (slot->has && slot->kind == (is_w ? 1 : 0)) {  // the pair's second GEMM
@@ -1587,18 +1594,25 @@ static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s, PendingGemm* 
         if constexpr (is_w) {
           const GemmP& pd = slot->p;
           const dim3 gd = slot->grid;
+          if (slot->np == 6) {
+            if (slot->mode == 0)
+              return slot->v == 2 ? gemm_pair_launch<VEC, 0, 2, 6>(p, grid, pd, gd, 0, s)
+                                  : gemm_pair_launch<VEC, 0, 3, 6>(p, grid, pd, gd, 0, s);
+            return slot->v == 2 ? gemm_pair_launch<VEC, 1, 2, 6>(p, grid, pd, gd, 0, s)
+                                : gemm_pair_launch<VEC, 1, 3, 6>(p, grid, pd, gd, 0, s);
+          }
           if (slot->mode == 0)
-            return slot->v == 2 ? gemm_pair_launch<VEC, 0, 2>(p, grid, pd, gd, 0, s)
-                                : gemm_pair_launch<VEC, 0, 3>(p, grid, pd, gd, 0, s);
-          return slot->v == 2 ? gemm_pair_launch<VEC, 1, 2>(p, grid, pd, gd, 0, s)
-                              : gemm_pair_launch<VEC, 1, 3>(p, grid, pd, gd, 0, s);
+            return slot->v == 2 ? gemm_pair_launch<VEC, 0, 2, 3>(p, grid, pd, gd, 0, s)
+                                : gemm_pair_launch<VEC, 0, 3, 3>(p, grid, pd, gd, 0, s);
+          return slot->v == 2 ? gemm_pair_launch<VEC, 1, 2, 3>(p, grid, pd, gd, 0, s)
+                              : gemm_pair_launch<VEC, 1, 3, 3>(p, grid, pd, gd, 0, s);
         } else {
           const GemmP& pw = slot->p;
           const dim3 gw = slot->grid;
           switch (slot->v) {
-            case 1: return gemm_pair_launch<1, MODE, VEC>(pw, gw, p, grid, 1, s);
-            case 2: return gemm_pair_launch<2, MODE, VEC>(pw, gw, p, grid, 1, s);
-            default: return gemm_pair_launch<3, MODE, VEC>(pw, gw, p, grid, 1, s);
+            case 1: return gemm_pair_launch<1, MODE, VEC, NP>(pw, gw, p, grid, 1, s);
+            case 2: return gemm_pair_launch<2, MODE, VEC, NP>(pw, gw, p, grid, 1, s);
+            default: return gemm_pair_launch<3, MODE, VEC, NP>(pw, gw, p, grid, 1, s);
           }
         }
       }
@@ -1607,6 +1621,7 @@ static int gemm_launch_v(const GemmP& p, dim3 grid, hipStream_t s, PendingGemm* 
       slot->kind = is_w ? 0 : 1;
       slot->v = VEC;
       slot->mode = MODE;
+      slot->np = NP;
       slot->p = p;
       slot->grid = grid;
       return PCADV_OK;
@@ -1685,7 +1700,8 @@ static int launch_gemm_impl(const float* a, long long lda, int ta, const float* 
   }
   if (precise) {
     if (ta == 0 && tb == 0) return accumulate ? gemm_launch<0, 0, 1, 6>(p, 1, s) : gemm_launch<0, 0, 0, 6>(p, 1, s);
-    if (ta == 0 && tb == 1) return accumulate ? gemm_launch<0, 1, 1, 6>(p, 1, s) : gemm_launch<0, 1, 0, 6>(p, 1, s);
+    if (ta == 0 && tb == 1)
+      return accumulate ? gemm_launch<0, 1, 1, 6>(p, 1, s, slot) : gemm_launch<0, 1, 0, 6>(p, 1, s, slot);
     return accumulate ? gemm_launch<1, 1, 1, 6>(p, 1, s) : gemm_launch<1, 1, 0, 6>(p, 1, s);
   }
   if (ta == 0 && tb == 0) return accumulate ? gemm_launch<0, 0, 1, 3>(p, 1, s) : gemm_launch<0, 0, 0, 3>(p, 1, s);

@@ -16,9 +16,17 @@ a per-cloud bias of fc1 (a B-row GEMM) instead of being materialised.
 conv6 + ReLU + max over points never materialises the [B*N][2048] output: a
 screened GEMM keeps per-tile candidates and the winner is re-evaluated in f32.
 
-Numerics: the GEMMs multiply bf16 hi/lo splits of the f32 operands (three
-MFMA products, f32 accumulate; relative error <= ~1.2e-5 of sum|a b| per
-layer); tests/test_gpu_seg.py holds the tolerances.
+Numerics (precision="fp32", the default, the reference's dtype): every GEMM
+multiplies the three-way bf16 splits of its f32 operands as six MFMA products
+(hi hi, hi mid, mid hi, hi lo, mid mid, lo hi; f32 accumulate): f32-level
+accuracy.  conv6's max is screened with three products and its winner (and
+near-tie runner-up) re-evaluated as an exact f32 dot product, so the pooled
+values are f32.  precision="bf16x3" (an explicitly labelled speed option,
+below fp32): the forward and data-gradient GEMMs take three products of
+hi / lo splits (relative error <= ~1.2e-5 of sum|a b| per layer), the forward
+staged from bf16 planes its producers write.  Weight gradients (sums over all
+B*N points, heavy cancellation) take six products in both modes.
+tests/test_gpu_seg.py holds the tolerances.
 """
 from __future__ import annotations
 
@@ -34,14 +42,17 @@ from ._lib import check, stream_ptr
 __all__ = ["PointNetSeg", "SegTrainStep", "seg_cross_entropy", "seg_forward", "seg_backward"]
 
 _LOC = 960                       # x1..x5 widths 64 + 128 + 128 + 128 + 512
-_FWD_PRECISE = os.environ.get("PCADV_SEG_PRECISE", "0") == "1"  # diagnostics: six-product forward
-# the forward's operands as bf16 hi / lo planes written once by their producers
-# (pcadv_gemm_bf2; bitwise the f32-staged result); PCADV_SEG_PLANES=0 stages f32
-_PLANES = os.environ.get("PCADV_SEG_PLANES", "1") == "1" and not _FWD_PRECISE
-# data gradients dX = dZ W: three products (sums over <= 960 terms; 1.2e-5 of
-# sum|a b|) unless PCADV_SEG_DGRAD_PRECISE=1 (six); weight gradients (sums over
-# all B*N points, heavy cancellation) always take six
-_DGRAD_PRECISE = os.environ.get("PCADV_SEG_DGRAD_PRECISE", "0") == "1"
+PRECISIONS = ("fp32", "bf16x3")
+# bf16x3 mode: the forward's operands as bf16 hi / lo planes written once by
+# their producers (pcadv_gemm_bf2; bitwise the f32-staged result);
+# PCADV_SEG_PLANES=0 stages f32
+_PLANES = os.environ.get("PCADV_SEG_PLANES", "1") == "1"
+
+
+def _check_precision(precision):
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision: one of {PRECISIONS}, got {precision!r}")
+    return precision
 _OFF = [0, 64, 192, 320, 448, 960]
 _CONV = [(3, 64), (64, 128), (128, 128), (128, 128), (128, 512), (512, 2048)]
 
@@ -220,7 +231,7 @@ def _weight_planes(W, Wf, wplanes=None):
     return [None] + out[:5], out[5:]
 
 
-def seg_forward(pts, cls, params, wplanes=None):
+def seg_forward(pts, cls, params, wplanes=None, precision="fp32"):
     """PointNetSeg forward (pointnet.py:282-317) on the engine.  Returns a dict
     with logits (B*N, C) point-major, gmax (B, 2048), gidx (B, 2048) and every
     activation the backward needs.  Each layer's epilogue also writes its
@@ -237,32 +248,43 @@ def seg_forward(pts, cls, params, wplanes=None):
     Wf = [params[12 + 2 * i].contiguous() for i in range(4)]
     bf = [params[13 + 2 * i].contiguous() for i in range(4)]
     ncls = Wf[3].shape[0]
-    planes = _PLANES
+    fp32 = _check_precision(precision) == "fp32"
+    planes = _PLANES and not fp32  # bf16x3: every forward GEMM staged from bf16 planes
+    pf = fp32  # six-product forward GEMMs (staged from f32, split three ways per tile)
+    # conv6's screen is three products in both modes (its winners are re-evaluated
+    # in exact f32), staged from x5's planes: conv5's epilogue writes them
+    c6p = _PLANES
     xloc = torch.empty(M, _LOC, device=dev)
     pl = lambda rows, cols: (torch.empty(rows, cols, device=dev, dtype=torch.bfloat16),  # noqa: E731
                              torch.empty(rows, cols, device=dev, dtype=torch.bfloat16))
-    if planes:
+    if c6p:
         Wp, Wfp = _weight_planes(W, Wf, wplanes)
+    if planes:
         xp = pl(M, _LOC)
+        x5p, x5ld, x5off = xp, _LOC, _OFF[4]
+    elif c6p:
+        x5p, x5ld, x5off = pl(M, 512), 512, 0
     # conv1..conv5 + ReLU into the column blocks of xloc
     E.gemm(pts, 3, W[0], 3, xloc, _LOC, M, 64, 3, bias=bc[0], relu=True, c_off=_OFF[0],
-           precise=_FWD_PRECISE, cp=xp if planes else None, ldcp=_LOC, cp_off=_OFF[0])
+           precise=pf, cp=xp if planes else None, ldcp=_LOC, cp_off=_OFF[0])
     for i in range(1, 5):
         K, O = _CONV[i]
         if planes:
             E.gemm_bf2(xp, _LOC, Wp[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
                        a_off=_OFF[i - 1], c_off=_OFF[i], cp=xp, ldcp=_LOC, cp_off=_OFF[i])
         else:
+            last = i == 4 and c6p  # conv5 also writes x5's planes for conv6's screen
             E.gemm(xloc, _LOC, W[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
-                   a_off=_OFF[i - 1], c_off=_OFF[i], precise=_FWD_PRECISE)
+                   a_off=_OFF[i - 1], c_off=_OFF[i], precise=pf, cp=x5p if last else None,
+                   ldcp=x5ld if last else 0)
     # conv6 + ReLU + max over the points of each cloud
     gmax = torch.empty(B, 2048, device=dev)
     gidx = torch.empty(B, 2048, device=dev, dtype=torch.int32)
     nb = E.lib.pcadv_conv_max_x3_workspace_bytes(B, N, 2048)
     ws = _ws(nb, dev)
-    if planes:
-        check(E.lib.pcadv_conv_max_bf2(_p(xloc, _OFF[4]), _LOC, _pb(xp[0], _OFF[4]),
-                                       _pb(xp[1], _OFF[4]), _LOC, B, N, 512, _p(W[5]),
+    if c6p:
+        check(E.lib.pcadv_conv_max_bf2(_p(xloc, _OFF[4]), _LOC, _pb(x5p[0], x5off),
+                                       _pb(x5p[1], x5off), x5ld, B, N, 512, _p(W[5]),
                                        _pb(Wp[5][0]), _pb(Wp[5][1]), _p(bc[5]), 2048, 1,
                                        _p(gmax), _p(gidx), _p(ws), ws.numel(), stream_ptr()),
               "pcadv_conv_max_bf2")
@@ -274,7 +296,7 @@ def seg_forward(pts, cls, params, wplanes=None):
     W1 = Wf[0]
     cb = torch.empty(B, 256, device=dev)
     E.gemm(gmax, 2048, W1, 3024, cb, 256, B, 256, 2048, bias=bf[0], b_off=960,
-           precise=_FWD_PRECISE)
+           precise=pf)
     E.gemm(cvec, cvec.shape[1], W1, 3024, cb, 256, B, 256, cvec.shape[1], b_off=3008,
            accumulate=True)
     h1 = torch.empty(M, 256, device=dev)
@@ -292,15 +314,16 @@ def seg_forward(pts, cls, params, wplanes=None):
         E.gemm_bf2(h3p, 128, Wfp[3], 128, logits, ncls, M, ncls, 128, bias=bf[3])
     else:
         E.gemm(xloc, _LOC, W1, 3024, h1, 256, M, 256, _LOC, bias_rows=cb, rows_per_group=N,
-               relu=True, precise=_FWD_PRECISE)
+               relu=True, precise=pf)
         E.gemm(h1, 256, Wf[1], 256, h2, 256, M, 256, 256, bias=bf[1], relu=True,
-               precise=_FWD_PRECISE)
+               precise=pf)
         E.gemm(h2, 256, Wf[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True,
-               precise=_FWD_PRECISE)
-        E.gemm(h3, 128, Wf[3], 128, logits, ncls, M, ncls, 128, bias=bf[3], precise=_FWD_PRECISE)
+               precise=pf)
+        E.gemm(h3, 128, Wf[3], 128, logits, ncls, M, ncls, 128, bias=bf[3], precise=pf)
     return dict(pts=pts, cvec=cvec, xloc=xloc, gmax=gmax, gidx=gidx, h1=h1, h2=h2, h3=h3, W=W,
                 Wf=Wf, logits=logits, dims=(B, N, ncls), xp=xp if planes else None,
-                W6p=Wp[5] if planes else None)
+                precision=precision, x5p=(x5p, x5ld, x5off) if c6p else None,
+                W6p=Wp[5] if c6p else None)
 
 
 def seg_backward(fw, dlogits, dgmax_out=None, out=None):
@@ -313,6 +336,7 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
     B, N, ncls = fw["dims"]
     M = B * N
     dev = xloc.device
+    pd = fw.get("precision", "fp32") == "fp32"  # six-product data gradients
     dl = torch.zeros(M, ncls, device=dev) if dlogits is None else dlogits.reshape(M, ncls).contiguous()
     # Every data-gradient GEMM applies the relu' of the layer below in its
     # epilogue (cmask), so each dz is stored masked once and read as is by the
@@ -330,17 +354,17 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
     dh3 = torch.empty(M, 128, device=dev)
     E.wgrad_and_gemm(fin, (dl, ncls, h3, 128, M, ncls, 128, dW4, 128), dict(db=db4),
                      E.gemm_desc(dl, ncls, Wf[3], 128, dh3, 128, M, 128, ncls, tb=1, cmask=h3,
-                                 ldm=128, precise=_DGRAD_PRECISE))
+                                 ldm=128, precise=pd))
     dW3 = _g(16, Wf[2]); db3 = _g(17, 128)
     dh2 = torch.empty(M, 256, device=dev)
     E.wgrad_and_gemm(fin, (dh3, 128, h2, 256, M, 128, 256, dW3, 256), dict(db=db3),
                      E.gemm_desc(dh3, 128, Wf[2], 256, dh2, 256, M, 256, 128, tb=1, cmask=h2,
-                                 ldm=256, precise=_DGRAD_PRECISE))
+                                 ldm=256, precise=pd))
     dW2 = _g(14, Wf[1]); db2 = _g(15, 256)
     dh1 = torch.empty(M, 256, device=dev)
     E.wgrad_and_gemm(fin, (dh2, 256, h1, 256, M, 256, 256, dW2, 256), dict(db=db2),
                      E.gemm_desc(dh2, 256, Wf[1], 256, dh1, 256, M, 256, 256, tb=1, cmask=h1,
-                                 ldm=256, precise=_DGRAD_PRECISE))
+                                 ldm=256, precise=pd))
     # ---- fc1: local columns (+ per-cloud sums s1), then the tiled columns --
     W1 = Wf[0]
     dW1 = _g(12, W1); db1 = _g(13, 256)
@@ -349,7 +373,7 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
     E.wgrad_and_gemm(fin, (dh1, 256, xloc, _LOC, M, 256, _LOC, dW1, 3024),
                      dict(db=db1, gsum=s1, rpg=N),
                      E.gemm_desc(dh1, 256, W1, 3024, dloc, _LOC, M, _LOC, 256, tb=1, cmask=xloc,
-                                 ldm=_LOC, precise=_DGRAD_PRECISE))
+                                 ldm=_LOC, precise=pd))
     # the tiled global and class columns: B per-cloud rows, exact f32, one launch
     if not _SMALL:
         E.wgrad(s1, 256, gmax, 2048, B, 256, 2048, dW1, 3024, dw_off=960, fin=fin)
@@ -360,7 +384,7 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
                                       _p(cvec), cvec.shape[1], cvec.shape[1], _p(dW1, 3008), 3024,
                                       0, stream_ptr()), "pcadv_wgrad_small")
     dg = torch.empty(B, 2048, device=dev)
-    E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=_DGRAD_PRECISE)
+    E.gemm(s1, 256, W1, 3024, dg, 2048, B, 2048, 256, tb=1, b_off=960, precise=pd)
     if dgmax_out is not None:
         dg += dgmax_out.reshape(B, 2048)
     # ---- conv6 + ReLU + max: the gradient reaches the argmax points -------
@@ -382,7 +406,7 @@ def seg_backward(fw, dlogits, dgmax_out=None, out=None):
                              dict(db=dbc[i], dz_off=_OFF[i], x_off=_OFF[i - 1]),
                              E.gemm_desc(dloc, _LOC, W[i], K, dloc, _LOC, M, K, O, tb=1,
                                          cmask=xloc, ldm=_LOC, accumulate=True,
-                                         precise=_DGRAD_PRECISE, a_off=_OFF[i],
+                                         precise=pd, a_off=_OFF[i],
                                          m_off=_OFF[i - 1], c_off=_OFF[i - 1]))
         else:
             E.wgrad(dloc, _LOC, pts, 3, M, O, K, dWc[i], K, db=dbc[i], dz_off=_OFF[i], fin=fin)
@@ -404,8 +428,9 @@ class SegNetFunction(torch.autograd.Function):
     int32 (argmax over points, non-differentiable)."""
 
     @staticmethod
-    def forward(ctx, pts, cls, *params):
-        fw = seg_forward(pts, cls, params)
+    def forward(ctx, precision, pts, cls, *params):
+        fw = seg_forward(pts, cls, params, precision=precision)
+        ctx.precision = precision
         ctx.save_for_backward(fw["pts"], fw["cvec"], fw["xloc"], fw["gmax"], fw["gidx"], fw["h1"],
                               fw["h2"], fw["h3"], *fw["W"], *fw["Wf"])
         ctx.dims = fw["dims"]
@@ -417,10 +442,10 @@ class SegNetFunction(torch.autograd.Function):
     def backward(ctx, dlogits, dgmax_out, _dgidx):
         t = ctx.saved_tensors
         fw = dict(pts=t[0], cvec=t[1], xloc=t[2], gmax=t[3], gidx=t[4], h1=t[5], h2=t[6], h3=t[7],
-                  W=list(t[8:14]), Wf=list(t[14:18]), dims=ctx.dims)
+                  W=list(t[8:14]), Wf=list(t[14:18]), dims=ctx.dims, precision=ctx.precision)
         B, N, ncls = ctx.dims
         dl = None if dlogits is None else dlogits.reshape(B * N, ncls)
-        return (None, None, *seg_backward(fw, dl, dgmax_out))
+        return (None, None, None, *seg_backward(fw, dl, dgmax_out))
 
 
 def O_shape(i):
@@ -464,9 +489,11 @@ class PointNetSeg(nn.Module):
     """models/pointnet.py:261-317.  forward(x: B x N x 3, cls: B x 1 x 16) ->
     (logits B x NUM_SEG_CLASSES x N, x_global B x 2048 x 1)."""
 
-    def __init__(self, NUM_SEG_CLASSES):
+    def __init__(self, NUM_SEG_CLASSES, *, precision="fp32"):
         super().__init__()
         self.output_dim = NUM_SEG_CLASSES
+        # "fp32" (the reference's dtype) or "bf16x3" (labelled speed option)
+        self.precision = _check_precision(precision)
         self.conv1 = nn.Conv1d(3, 64, 1)
         self.conv2 = nn.Conv1d(64, 128, 1)
         self.conv3 = nn.Conv1d(128, 128, 1)
@@ -487,7 +514,8 @@ class PointNetSeg(nn.Module):
             raise ValueError(f"cls: expected B x 1 x 16, got {tuple(cls.shape)}")
         _check_dev(x, "x")
         params = [p for _, p in self.named_parameters()]
-        return SegNetFunction.apply(x.float().contiguous(), cls.float().reshape(B, 1, 16), *params)
+        return SegNetFunction.apply(self.precision, x.float().contiguous(),
+                                    cls.float().reshape(B, 1, 16), *params)
 
     def forward(self, x, cls):
         logits, g, _ = self.forward_points(x, cls)
@@ -507,8 +535,10 @@ class SegTrainStep:
     launch over the whole network."""
 
     def __init__(self, model, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 lambda_seg=1.0, device="cuda", keep_activations=False):
+                 lambda_seg=1.0, device="cuda", keep_activations=False, precision=None):
         self.lib = _lib.load()
+        # the model's precision unless given ("fp32" / "bf16x3")
+        self.precision = _check_precision(precision or getattr(model, "precision", "fp32"))
         # keep_activations: hold the last step's forward tensors in self.fw (for
         # inspection / tests); off by default, so a step's per-point activations
         # (hundreds of MB at B=16, N=2048) are released when it returns
@@ -572,10 +602,11 @@ class SegTrainStep:
         if seg.shape != (B, N) or seg.dtype != torch.int64 or not seg.is_contiguous():
             raise ValueError("seg: expected contiguous int64 (B, N)")
         wpl = None
-        if _PLANES:
+        if _PLANES:  # every weight's planes (fp32 mode reads conv6's only)
             _engine().split(self.param, self.wph, self.wpl)
             wpl = self.wplanes
-        fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params, wplanes=wpl)
+        fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params, wplanes=wpl,
+                         precision=self.precision)
         if self.keep_activations:
             self.fw = fw  # the last step's activations (logits, x_global, argmax, ...)
         M, ncls = B * N, fw["dims"][2]

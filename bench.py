@@ -563,7 +563,10 @@ def bench_seg(args):
     Bs, Ns = 16, 2048
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = pc.PointNetSeg(50).to(dev)
+    # fp32 (the reference's dtype, six-product GEMMs) unless --precision bf16:
+    # the labelled bf16x3 speed option (three-product forward / data gradients)
+    precision = "bf16x3" if args.precision == "bf16" else "fp32"
+    model = pc.PointNetSeg(50, precision=precision).to(dev)
     init_weights(model, "xavier", verbose=False)
     step = SegTrainStep(model, device=dev)
     pool = []
@@ -596,7 +599,9 @@ def bench_seg(args):
     from adversarial_learning_on_pointclouds_amd._lib import check, stream_ptr
     import ctypes
     params = [p for p in model.parameters()]
-    fw = segmod.seg_forward(pool[(args.steps - 1) % 2][0], pool[(args.steps - 1) % 2][1], params)
+    segmod._engine().split(step.param, step.wph, step.wpl)
+    fw = segmod.seg_forward(pool[(args.steps - 1) % 2][0], pool[(args.steps - 1) % 2][1], params,
+                            wplanes=step.wplanes, precision=precision)
     lib = segmod._engine().lib
     gmax = torch.empty(Bs, 2048, device=dev)
     gidx = torch.empty(Bs, 2048, device=dev, dtype=torch.int32)
@@ -606,17 +611,18 @@ def bench_seg(args):
     b6 = params[11]
     x5 = ctypes.c_void_p(fw["xloc"].data_ptr() + 4 * segmod._OFF[4])
 
-    xp, w6p = fw["xp"], fw["W6p"]
+    x5p, w6p = fw["x5p"], fw["W6p"]
     big = os.environ.get("PCADV_GEMM_BIG", "1") != "0"
     glds = os.environ.get("PCADV_GEMM_GLDS", "1") != "0"
     gname = (f"k_gemm_bf2_big<2, {'true' if glds else 'false'}> (operands staged by "
              f"{'LDS-DMA' if glds else 'registers'})") if big else "k_gemm_x3<2,2,2,3>"
-    kname = f"pcadv_conv_max_bf2: {gname}" if xp is not None else "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3>"
+    kname = f"pcadv_conv_max_bf2: {gname}" if x5p is not None else "pcadv_conv_max_x3: k_gemm_x3<0,0,2,3>"
 
     def cmx():
-        if xp is not None:
-            check(lib.pcadv_conv_max_bf2(x5, segmod._LOC, segmod._pb(xp[0], segmod._OFF[4]),
-                                         segmod._pb(xp[1], segmod._OFF[4]), segmod._LOC, Bs, Ns, 512,
+        if x5p is not None:
+            (hi, lo), ld, off = x5p
+            check(lib.pcadv_conv_max_bf2(x5, segmod._LOC, segmod._pb(hi, off), segmod._pb(lo, off),
+                                         ld, Bs, Ns, 512,
                                          ctypes.c_void_p(W6.data_ptr()), segmod._pb(w6p[0]),
                                          segmod._pb(w6p[1]), ctypes.c_void_p(b6.data_ptr()), 2048, 1,
                                          ctypes.c_void_p(gmax.data_ptr()), ctypes.c_void_p(gidx.data_ptr()),
@@ -646,8 +652,12 @@ def bench_seg(args):
         "value": round(Bs * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16x3 (fp32-emulated: forward and data-gradient GEMMs as three bf16 hi/lo "
-                 "MFMA products, f32 accumulate; weight gradients six products)",
+        "dtype": ("fp32 (f32-level: every GEMM as six bf16 hi/mid/lo MFMA products, f32 "
+                  "accumulate; conv6's max screened with three products and every winner "
+                  "re-evaluated in exact f32)") if precision == "fp32" else
+                 ("bf16x3 (below fp32, a labelled speed option: forward and data-gradient GEMMs "
+                  "as three bf16 hi/lo MFMA products, f32 accumulate; weight gradients six "
+                  "products)"),
         "data": "synthetic (seeded U(-1,1) clouds, one-hot classes, part labels in [0,50))",
         "config": {"workload": "PointNetSeg(50) + CrossEntropyLoss + Adam, B=16, N=2048 "
                                "(BASELINE configs[3])", "global_batch": Bs, "points": Ns,

@@ -3,16 +3,18 @@ GEMM engine (csrc/gemm.hip) through its C ABI, and PointNetSeg on top of it,
 against float64 torch references, the numpy oracle and the reference goldens
 g6 (forward) / g8 (training step).  Runs on an MI355X only.
 
-Tolerances: the forward GEMMs multiply bf16 hi/lo splits (three MFMA
-products, f32 accumulate), bounded by 2e-5 * (|A| |B|^T) elementwise; the
-gradient GEMMs six products of hi/mid/lo splits (f32-level).  The forward
-outputs (logits, x_global) are held to the north_star's 1e-3 (they agree to
-~5e-6).  The backward is held to 1e-4 elementwise against the oracle's
-backward evaluated on this forward's own activations and ReLU masks.  End to
-end, gradients are compared in relative L2 (1e-2): any two f32 implementations
-of a ReLU net route a whole gradient element differently where a
-pre-activation lies within rounding of 0 (the oracle and the fp64 reference
-agree to 1e-6 only because numpy's f32 rounding flips almost none of them)."""
+Tolerances.  precision="fp32" (the default, the reference's dtype): every GEMM
+takes six MFMA products of hi/mid/lo bf16 splits (f32-level); conv6's pooled
+values are exact f32 re-evaluations.  The forward outputs (logits, x_global)
+are held to the north_star's 1e-3 (they agree to ~1e-6); the backward to 1e-4
+elementwise against the oracle's backward evaluated on this forward's own
+activations and ReLU masks, and end to end in relative L2 within 2e-3 (two f32
+implementations of a ReLU net route a whole gradient element differently where
+a pre-activation lies within rounding of 0).  conv6's argmax must be the f64
+argmax of the kernel's own conv5 activations except at proven near-ties
+(_conv6_argmax_ok).  precision="bf16x3" (a labelled speed option): the
+forward and data-gradient GEMMs take three products of hi/lo splits, bounded
+by 2e-5 * (|A| |B|^T) elementwise; end to end 1e-2."""
 import ctypes
 import os
 
@@ -292,17 +294,17 @@ def test_seg_forward_planes_path_is_bitwise_the_f32_path():
     saved = segmod._PLANES
     try:
         segmod._PLANES = True
-        a = seg_forward(pts, cls, params)
+        a = seg_forward(pts, cls, params, precision="bf16x3")
         segmod._PLANES = False
-        b = seg_forward(pts, cls, params)
+        b = seg_forward(pts, cls, params, precision="bf16x3")
     finally:
         segmod._PLANES = saved
     for k in ("xloc", "gmax", "gidx", "h1", "h2", "h3", "logits"):
         assert torch.equal(a[k], b[k]), k
 
 
-@pytest.mark.parametrize("B,N", [(2, 700), (4, 2048)])
-def test_seg_backward_paired_and_deferred_launches_are_bitwise(B, N):
+@pytest.mark.parametrize("B,N,precision", [(2, 700, "fp32"), (4, 2048, "fp32"), (4, 2048, "bf16x3")])
+def test_seg_backward_paired_and_deferred_launches_are_bitwise(B, N, precision):
     """The backward's launch forms: each layer's weight and data gradients as
     one paired launch (_Engine.pair) and the weight gradients' slab sums
     deferred to one launch (pcadv_wgrad_flush) give bitwise the gradients of
@@ -314,7 +316,7 @@ def test_seg_backward_paired_and_deferred_launches_are_bitwise(B, N):
     pts = torch.rand(B, N, 3, device=DEV) * 2 - 1
     cls = torch.zeros(B, 1, 16, device=DEV)
     cls[:, 0, 3] = 1
-    fw = seg_forward(pts, cls, params)
+    fw = seg_forward(pts, cls, params, precision=precision)
     dl = torch.randn(B * N, 50, device=DEV) * 1e-3
     saved = segmod._PAIR, segmod._DEFER
     outs = []
@@ -706,7 +708,7 @@ def test_seg_step_golden_g8():
     check_tensor_rel(fx, "gmax", g.detach().cpu().numpy(), tol=1e-3)
     check_tensor_rel(fx, "logits", logits.detach().cpu().numpy().transpose(0, 2, 1), tol=1e-3)
     for name, p in m.named_parameters():
-        check_tensor_l2(fx, "grad." + name, p.grad.cpu().numpy(), tol=1e-2)
+        check_tensor_l2(fx, "grad." + name, p.grad.cpu().numpy(), tol=2e-3)
 
 
 def _oracle_cache(fw, pts, cls):
@@ -720,6 +722,31 @@ def _oracle_cache(fw, pts, cls):
                 h1=fw["h1"].cpu().numpy().reshape(B, N, 256),
                 h2=fw["h2"].cpu().numpy().reshape(B, N, 256),
                 h3=fw["h3"].cpu().numpy().reshape(B, N, 128))
+
+
+def _conv6_argmax_ok(fw, S, tol=1e-5):
+    """conv6 + ReLU + max (pointnet.py:301-303): the pooled point of every
+    channel with a positive max must be the f64 argmax of the kernel's own
+    conv5 activations, except at near-ties (values within tol of the max,
+    relative to max(1, |max|)); the pooled value must equal the f64 value there
+    to 1e-5.  Returns the number of near-tie substitutions."""
+    B, N, _ = fw["dims"]
+    x5 = fw["xloc"][:, 448:960].double().reshape(B, N, 512)
+    W6 = torch.from_numpy(S["conv6.weight"].reshape(2048, 512)).to(DEV, torch.float64)
+    b6 = torch.from_numpy(S["conv6.bias"]).to(DEV, torch.float64)
+    gi = fw["gidx"].long()
+    near = 0
+    for c in range(B):
+        y = torch.relu(x5[c] @ W6.T + b6)           # N x 2048
+        best, am = y.max(0)
+        yg = y.gather(0, gi[c].unsqueeze(0)).squeeze(0)
+        pos = best > 0
+        lim = tol * torch.clamp(best.abs(), min=1.0)
+        assert bool((yg[pos] >= best[pos] - lim[pos]).all()), f"cloud {c}: pooled below the f64 max"
+        g = fw["gmax"][c].double()
+        assert bool(((g - best).abs() <= lim).all()), f"cloud {c}: pooled value off the f64 max"
+        near += int(((gi[c] != am) & pos).sum())
+    return near
 
 
 @pytest.mark.parametrize("B,N", [(3, 700), (2, 2048)])
@@ -802,7 +829,7 @@ def test_seg_step_vs_oracle_ragged():
     for name, p in m.named_parameters():
         a, r = p.grad.cpu().numpy(), grads[name]
         e = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
-        assert e < 1e-2, (name, e)
+        assert e < 2e-3, (name, e)
 
 
 def test_seg_deterministic():
@@ -862,13 +889,16 @@ def test_seg_train_step_matches_autograd_and_graph():
     assert torch.equal(st2.loss, st3.loss)
 
 
-def test_seg_train_step_full_size_configs3_vs_oracle():
+@pytest.mark.parametrize("precision,e2e", [("fp32", 2e-3), ("bf16x3", 1e-2)])
+def test_seg_train_step_full_size_configs3_vs_oracle(precision, e2e):
     """BASELINE configs[3] at full size (B=16, N=2048) through SegTrainStep, the
     bench's path (models/pointnet.py:261-317, utils/trainer.py:334-349): loss,
-    logits, x_global and argmax vs the numpy oracle; every gradient vs the
-    oracle's backward on this forward's own activations (1e-4 of each tensor's
-    max) and end to end (relative L2, see the module docstring); one Adam step
-    vs the oracle's Adam on the same gradients."""
+    logits and x_global vs the numpy oracle; conv6's argmax exact except at
+    proven near-ties (_conv6_argmax_ok); every gradient vs the oracle's
+    backward on this forward's own activations (1e-4 of each tensor's max) and
+    end to end in relative L2 (2e-3 in fp32 mode; the labelled bf16x3 mode's
+    three-product forward flips more ReLUs: 1e-2); one Adam step vs the
+    oracle's Adam on the same gradients."""
     from adversarial_learning_on_pointclouds_amd.seg import SegTrainStep
     from golden_util import assert_grad_close
     B, N = 16, 2048
@@ -879,7 +909,7 @@ def test_seg_train_step_full_size_configs3_vs_oracle():
     cls[np.arange(B), 0, rng.integers(0, 16, B)] = 1
     seg = rng.integers(0, 50, (B, N))
     m = _seg_model(S)
-    step = SegTrainStep(m, device=DEV, keep_activations=True)
+    step = SegTrainStep(m, device=DEV, keep_activations=True, precision=precision)
     loss = step(_t(pts), _t(cls), _t(seg, torch.int64), apply_adam=False).item()
     fw = step.fw
     rl, grads, rlog, rg, ram = onp.seg_step(S, pts, cls, seg)
@@ -889,24 +919,19 @@ def test_seg_train_step_full_size_configs3_vs_oracle():
     assert e < 1e-3, e
     g = fw["gmax"].cpu().numpy()
     assert np.abs(g - rg).max() / np.abs(rg).max() < 1e-3
-    gi = fw["gidx"].cpu().numpy()
-    assert ((gi == ram) | (rg <= 0)).mean() > 0.999  # argmax of the positive pooled channels
+    _conv6_argmax_ok(fw, S)
     # same-mask backward: the oracle's backward on this forward's activations
     _, dout = onp.seg_cross_entropy(logits, seg)
     ref = onp.seg_backward(S, _oracle_cache(fw, pts, cls), dout)
     for name, p in m.named_parameters():
         r = ref[name]
         assert_grad_close(p.grad.cpu().numpy().reshape(r.shape), r, name, 1e-4, 1e-4)
-    # end to end against the oracle's own forward (its own ReLU masks): the
-    # bf16x3 forward (error ~2^-16 of sum|ab|) flips the ReLU of pre-activations
-    # that close to 0, so conv1's gradient lands ~3e-3 off in relative L2 at
-    # this size; held to the module's 1e-2 (the same-mask check above is the
-    # strict one)
+    # end to end against the oracle's own forward (its own ReLU masks)
     for name, p in m.named_parameters():
         r = grads[name]
         a = p.grad.cpu().numpy().reshape(r.shape)
         el2 = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
-        assert el2 < 1e-2, (name, el2)
+        assert el2 < e2e, (name, el2)
     gnp = {k: q.grad.cpu().numpy() for k, q in m.named_parameters()}
     onp.Adam(S).step(gnp)
     step.adam()
