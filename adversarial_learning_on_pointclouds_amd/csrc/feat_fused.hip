@@ -581,6 +581,9 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       if (s + 1 < S) unit(s, 1, accB, accA, T_{}, F_{});
       else unit(s, 1, accB, accA, T_{}, T_{});
       __syncthreads();
+#ifdef PCADV_STAMPS
+      if ((s & 1) && 6 + (s >> 1) < 14) STAMP(6 + (s >> 1));  // every other step's end
+#endif
     }
   }
   // W4 rows of the exact re-evaluation (eight lanes per row, see below): they

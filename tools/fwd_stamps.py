@@ -63,7 +63,10 @@ def main():
     nwg = C * 4
     st = stamps[:nwg * 16].view(nwg, 16).cpu().numpy()
     # k_conv4_max thread 0: 0 start, 1 W4 + first tile staged, 2 point loop done, 3 end
-    summarize("k_conv4_max", st, [1, 2, 4, 5, 3])
+    # 6 + j: end of step 2 j + 1 (every other 64-point step, up to 8 of them)
+    S = (N + 63) // 64
+    steps = [6 + j for j in range(min(8, S // 2))]
+    summarize("k_conv4_max", st, [1] + steps + [2, 4, 5, 3])
     n1 = (C * ((N + 63) // 64) + 1) // 2
     st1 = stamps[nwg * 16:nwg * 16 + n1 * 16].view(n1, 16).cpu().numpy()
     st1 = st1[st1[:, 0] > 0]
