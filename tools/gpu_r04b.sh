@@ -17,5 +17,7 @@ timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu > gpurun_out/
 grep -o '"ms_per_step": [0-9.]*' gpurun_out/${tag}_adv.log
 timeout -k 10 120 python tools/fwd_stamps.py 64 1024 > gpurun_out/${tag}_stamps.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/${tag}_stamps.log | head -40
+timeout -k 10 120 python tools/tail_stamps.py 32 1024 > gpurun_out/${tag}_tail_stamps.log 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/${tag}_tail_stamps.log | tail -30
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o run --output-format csv -- python bench.py --no-cpu --steps 50 --warmup 10 > gpurun_out/${tag}_trace.log 2>&1 || exit $?
 python tools/kstats.py gpurun_out/${tag}_trace/run_kernel_trace.csv 2>/dev/null | head -20
