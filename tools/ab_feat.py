@@ -38,6 +38,8 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     pair = e0.elapsed_time(e1) / 300 * 1e3
+    gmax, gidx, _ = ops.feat_fwd(pts, *fw)
+    chk = (int(gidx.to(torch.int64).sum()), float(gmax.double().sum()))
     step = pc.AdvTrainStep(model, model_D, B, N, device=dev)
     gr = step.capture_on(pg, lab, pn)
     for _ in range(20):
@@ -48,7 +50,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     st = e0.elapsed_time(e1) / 300 * 1e3
-    print(f"AB {tag}: feature pair {pair:7.2f} us   step {st:7.2f} us", flush=True)
+    print(f"AB {tag}: feature pair {pair:7.2f} us   step {st:7.2f} us   check {chk}", flush=True)
 
 
 if __name__ == "__main__":
