@@ -118,6 +118,14 @@ def main():
                          ("d dX1", 6, 7), ("e wgrad", 7, 8)):
             d = (ch[:, b] - ch[:, a]) * 10 / 1e3
             print(f"  batch1 {nm:10s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+        # diagnostic sub-stamps of batch 1 (thread 0): phase a 24..26, phase c 28..30
+        for nm, a, b in (("a: start", 3, 24), ("a: conv1", 24, 25), ("a: conv2+W2 wait", 25, 26),
+                         ("a: epilogue", 26, 4), ("c: B loads", 5, 28), ("c: MFMA", 28, 29),
+                         ("c: park+barrier", 29, 30), ("c: combine", 30, 6)):
+            ok = (ch[:, a] > 0) & (ch[:, b] > 0)
+            if ok.any():
+                d = (ch[ok, b] - ch[ok, a]) * 10 / 1e3
+                print(f"    {nm:16s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
         two = nact > 32
         if two.any():
             for nm, a, b in (("a", 8, 9), ("b+combine", 9, 10), ("c dX2", 10, 11), ("d dX1", 11, 12),
