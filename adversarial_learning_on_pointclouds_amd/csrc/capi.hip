@@ -27,14 +27,12 @@ int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, in
                     const float*, const float*, const float*, const float*, const float*,
                     const float*, const float*, float*, float*, float*, float*, float*, float*,
                     float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr,
-                    const FinAdam* adam = nullptr, const int* sortrec = nullptr,
-                    const void* w3t = nullptr);
+                    const FinAdam* adam = nullptr, const int* sortrec = nullptr);
 size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
                           const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
-                          hipStream_t, uint64_t* stamps = nullptr, int precision = 0,
-                          void* w3t = nullptr);
+                          hipStream_t, uint64_t* stamps = nullptr, int precision = 0);
 int launch_conv4_max(const float*, int, int, const float*, const float*, float*, int32_t*,
                      hipStream_t, int);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
@@ -122,7 +120,6 @@ struct StepWs {
   float *lpart, *lpart3, *dslabs, *dout;
   float* rowloss;  // the cls step's per-row CE / B (k_cls_head)
   int32_t* gidx;
-  void* w3t;  // W3^T bf16 planes: written by the forward, read by the feature backward
   int* sortrec;  // the feature backward's hit sort, done early (feat_sort.h)
   void* feat_ws;
   size_t feat_ws_bytes;
@@ -168,7 +165,6 @@ static StepWs carve(int B, int N, char* base) {
   w.dout = take(R);
   w.rowloss = take(C);
   w.sortrec = reinterpret_cast<int*>(take(feat_sort_record_ints((int)C, N)));
-  w.w3t = take(W3T_BYTES / sizeof(float));
   w.feat_ws_bytes = feat_bwd_workspace_bytes((int)C, N);
   if (feat_fwd_workspace_bytes((int)C, N) > w.feat_ws_bytes)
     w.feat_ws_bytes = feat_fwd_workspace_bytes((int)C, N);
@@ -245,7 +241,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec, w.w3t);
+                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec);
 }
 
 // Part 1 of adv_step: everything before the feature backward.
@@ -277,8 +273,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
                                G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision,
-                               w.w3t));
+                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   // fc2 + dropout: a device-drawn mask is stored for the backward
@@ -400,8 +395,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
                                G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision,
-                               w.w3t));
+                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
@@ -439,7 +433,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec, w.w3t);
+                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec);
 }
 
 }  // namespace pcadv

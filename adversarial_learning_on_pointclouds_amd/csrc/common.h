@@ -26,34 +26,6 @@ __device__ __forceinline__ void split3(float v, __bf16& hi, __bf16& mid, __bf16&
   lo = (__bf16)(r1 - (float)mid);
 }
 
-// conv3's weight W3 [128][64], transposed and split three ways: bf16 planes
-// hi | mid | lo of W3^T [64][128], the B operand of the feature backward's
-// dX2 = dZ3 W3 (16-B loads of 8 consecutive output channels).  The step's
-// forward (k_point_mlp) writes them; the standalone backward makes its own.
-constexpr int W3T_PLANE = 64 * 128;                    // bf16 per plane
-constexpr size_t W3T_BYTES = 3 * (size_t)W3T_PLANE * 2;
-// part t in [0, 1024) of the planes: column i = t >> 4, channels 8 (t & 15) .. + 8
-__device__ __forceinline__ void w3t_planes_part(int t, const float* __restrict__ w3,
-                                                __bf16* __restrict__ out) {
-  const int i = t >> 4, o0 = 8 * (t & 15);
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = w3[(o0 + j) * 64 + i];
-  bf16x8 h, m, l;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 a, b, c;
-    split3(v[j], a, b, c);
-    h[j] = a;
-    m[j] = b;
-    l[j] = c;
-  }
-  bf16x8* d = reinterpret_cast<bf16x8*>(out + i * 128 + o0);
-  d[0] = h;
-  d[W3T_PLANE / 8] = m;
-  d[2 * W3T_PLANE / 8] = l;
-}
-
 // 32x32x2 f32 MFMA: exact f32 (k-ordered fma chain), 64 cycles / SIMD.
 // lane l supplies A[i=l&31][k=l>>5], B[k=l>>5][j=l&31];
 // D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5).

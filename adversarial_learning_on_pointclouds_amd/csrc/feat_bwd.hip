@@ -15,11 +15,8 @@
 //   2. active rows compacted;
 //   3. per batch of 32 active rows: recompute x1/x2 from the points, dX3 rows from the sorted
 //      hits (loads of W4 rows issued back to back) with the conv3 ReLU mask,
-//      dX2 = dZ3 W3 (v_mfma_f32_16x16x32_bf16) and dW3 += dZ3^T x2
-//      (v_mfma_f32_32x32x16_bf16) as six products of three-way bf16 splits
-//      (f32-level; dZ3 and x2 are split once, into LDS planes, W3^T comes split
-//      from the forward), dX1 = dZ2 W2 on v_mfma_f32_16x16x4_f32 and dW2 on
-//      v_mfma_f32_32x32x2_f32 (exact f32).
+//      dX2 = dZ3 W3 and dX1 = dZ2 W2 on v_mfma_f32_16x16x4_f32 (one 16x16 tile
+//      per wave), weight gradients on v_mfma_f32_32x32x2_f32.
 // Each workgroup writes its weight-gradient partials to its own slab;
 // k_feat_bwd_finish sums the slabs in a fixed order (no atomics).
 #include "common.h"
@@ -41,55 +38,17 @@ __device__ __forceinline__ f32x4m mfma16(float a, float b, f32x4m c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// six bf16 products of three-way splits (hi, mid, lo planes 0 / 1 / 2),
-// smallest terms first: an f32-level product (common.h split3)
-__device__ __forceinline__ f32x4m mfma16x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4m c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x16 mfma32x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
-}
-
-// bf16 plane images of a batch (element offsets), 16-B chunks XOR-swizzled to
-// spread the reads over the banks.  dZ3: row-major, 128 columns (256-B rows),
-// read by rows (ds_read_b128, the 16x16x32 A operand of dX2) and transposed
-// (ds_read_b64_tr_b16, the 32x32x16 A operand of dW3).  x2: column-major (a
-// column's 32 batch rows in 64 B), so the conv2 epilogue writes 4 rows per
-// ds_write_b64 and dW3's B operand is one ds_read_b128 per plane.
-__device__ __forceinline__ int dz3p_off(int row, int col) {
-  const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
-  return row * 128 + (((col >> 3) ^ sw) << 3) + (col & 7);
-}
-__device__ __forceinline__ int x2c_off(int col, int row) {
-  return col * BW_RB + (((row >> 3) ^ ((col >> 2) & 3)) << 3) + (row & 7);
-}
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-// 4 rows x 16 columns of a plane, transposed: lane i of each 16-lane group gets
-// column c0 + i of rows r0 .. r0 + 3, when lane 4q + p of the group points at
-// (row r0 + q, column c0 + 4p).  Needs every lane of the wave active.
-__device__ __forceinline__ bf16x4 lds_tr16(const __bf16* p) {
-  return __builtin_bit_cast(
-      bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p));
-}
-__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
-  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
 constexpr int BW_G = 12;      // hit groups of the dZ3 gather: half-waves of waves 2-7 (4 columns per lane)
 constexpr int BW_RBG = (BW_RB + BW_G - 1) / BW_G;  // batch rows per gather group (mask / combine)
 constexpr int BW_GD = 8;      // W4 rows in flight per gather lane
 struct BwdLds {
+  union {
+    struct {
+      int key[BW_MAXO];      // o of each hit, grouped by row (arbitrary order in a row)
+      float hg[BW_MAXO];     // g of each hit, same order
+    };
+    alignas(16) float bnd[BW_G][128];  // group g's partial dZ3 sums of its cut row (phase b)
+  };
   int so[BW_MAXO];           // o of each hit, sorted by (row, o)
   float sg[BW_MAXO];         // g, same order
   int rcnt[BW_PCH];          // hits per row of the chunk
@@ -99,29 +58,13 @@ struct BwdLds {
   int rows_list[BW_PCH];     // compact slot -> row
   int hoff[BW_PCH + 4];      // first sorted hit of each compact slot; hoff[nact] = nhits
   alignas(16) int bnd_row[BW_G];  // batch row whose hits group g continued (or -1)
+  alignas(16) float dz3[BW_RB * SZ3];
+  alignas(16) float x2[BW_RB * S64];   // recomputed conv2 output (f32, as the forward)
+  alignas(16) float x1[BW_RB * S64];   // recomputed conv1 output
+  alignas(16) float dz2[BW_RB * SZ2];
+  alignas(16) float dz1[BW_RB * SZ2];
   alignas(16) float pts[BW_RB * 4];
-  uint16_t x2m[64 * 2];      // conv2 ReLU mask (x2 > 0) of the batch rows: [column][h],
-                             // bit i = row acc_row(i, lane) of lane (column, h)
-  union {
-    struct {                 // the hit sort (before the batches)
-      int key[BW_MAXO];      // o of each hit, grouped by row (arbitrary order in a row)
-      float hg[BW_MAXO];     // g of each hit, same order
-    };
-    struct {                 // phase b and the combine
-      alignas(16) float dz3[BW_RB * SZ3];
-      alignas(16) float bnd[BW_G][128];  // group g's partial dZ3 sums of its cut row
-    };
-    struct {                 // phases c .. e
-      alignas(16) float dz2[BW_RB * SZ2];
-      alignas(16) float dz1[BW_RB * SZ2];
-    };
-  };
-  alignas(16) __bf16 dz3p[3][BW_RB * 128];  // dZ3 split three ways (combine .. e)
-  alignas(16) __bf16 x2p[3][64 * BW_RB];    // recomputed conv2 output split three ways,
-                                            // column-major (a .. e)
-  alignas(16) float x1[BW_RB * S64];        // recomputed conv1 output (f32, as the forward)
 };
-static_assert(sizeof(BwdLds) <= 80 * 1024, "two chunk workgroups per CU");
 
 static_assert(FS_PCH == BW_PCH && FS_MAXO == BW_MAXO && FS_T == BW_T, "feat_sort.h geometry");
 
@@ -274,8 +217,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
                  const float* __restrict__ w3, const float* __restrict__ w4,
                  const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps,
                  const int* __restrict__ sortrec, int nclouds, float* __restrict__ dw4,
-                 float* __restrict__ db4, FinAdam fa, int nb_adam0, int nb_adam1,
-                 const __bf16* __restrict__ w3t) {
+                 float* __restrict__ db4, FinAdam fa, int nb_adam0, int nb_adam1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // Workgroup rows past the clouds: work that needs nothing from this launch,
   // the dW4 / db4 gather and the Adam update of the parameters whose gradients
@@ -316,9 +258,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #define BSTAMP(k) do { if (st_ && threadIdx.x == 0 && (k) < 15) st_[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define GSTAMP(k) do { if (st_ && threadIdx.x == 128 && (k) < 8) st_[16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define ASTAMP(k) do { if (st_ && threadIdx.x == 0 && b0 == 0) st_[24 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define CSTAMP(k) do { if (st_ && threadIdx.x == 0 && b0 == 0) st_[28 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
-#define CSTAMP(k) do { } while (0)
 #define BSTAMP(k) do { } while (0)
 #define GSTAMP(k) do { } while (0)
 #define ASTAMP(k) do { } while (0)
@@ -329,12 +269,12 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
 
   // wave -> (row tile rt, column tile ct) of the 32 x 64 dX2 / dX1 outputs;
-  // its B fragments (W3^T planes, W2) are re-read from L2 each batch
+  // its B fragments (16x16x4, k = 4s + q) are re-read from L2 each batch
   const int rt = wave >> 2, ct = wave & 3;
   // buffer loads: 32-bit lane offsets + scalar step offsets, so no 64-bit
   // addresses are kept live across the batch loop
   const __amdgpu_buffer_rsrc_t w3r =
-      __builtin_amdgcn_make_buffer_rsrc((void*)w3t, (short)0, (int)W3T_BYTES, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)w3, (short)0, 128 * 64 * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t w2r =
       __builtin_amdgcn_make_buffer_rsrc((void*)w2, (short)0, 64 * 64 * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t w4r =
@@ -484,7 +424,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   // register accumulators that live across batches
   f32x16 a_dw3 = {}, a_dw2 = {};
   float acc_w1 = 0.f, acc_b = 0.f;
-  f32x4 db3acc = {0.f, 0.f, 0.f, 0.f};  // waves 2-7: db3 over rows grp + 12 u of every batch
 
   for (int b0 = 0; b0 < nact; b0 += BW_RB) {
     // the lane-dependent indices are re-derived in every batch: otherwise each
@@ -494,7 +433,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     asm volatile("" : "+v"(lane_l));
     const int lane = lane_l, tid = wave * 64 + lane;
     const int r32 = lane & 31, h = lane >> 5, r16 = lane & 15, q = lane >> 4;
-    const int boff = (q * 64 + 16 * ct + r16) * 4;  // this lane's W2 fragment offset
+    const int boff = (q * 64 + 16 * ct + r16) * 4;  // this lane's W3 / W2 fragment offset
     const int nb = min(BW_RB, nact - b0);
     const int sb_ = 4 + 5 * (b0 / BW_RB);
     (void)sb_;
@@ -526,20 +465,16 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       ASTAMP(0);
-      // CG rows' points read before their CG writes: the compiler cannot tell
-      // the x1 writes from the pts reads, so a row-by-row loop pays one LDS
-      // round trip per row
-#ifndef PCADV_CONV1_GROUP
-#define PCADV_CONV1_GROUP 4
-#endif
-      constexpr int CG = PCADV_CONV1_GROUP;
+      // four rows' points read before their four writes: the compiler cannot
+      // tell the x1 writes from the pts reads, so a row-by-row loop pays one
+      // LDS round trip per row
 #pragma unroll
-      for (int g = 0; g < BW_RB; g += CG) {
-        f32x4 q4[CG];
+      for (int g = 0; g < BW_RB; g += 4) {
+        f32x4 q4[4];
 #pragma unroll
-        for (int u = 0; u < CG; ++u) q4[u] = *reinterpret_cast<const f32x4*>(&L.pts[(g + u) * 4]);
+        for (int u = 0; u < 4; ++u) q4[u] = *reinterpret_cast<const f32x4*>(&L.pts[(g + u) * 4]);
 #pragma unroll
-        for (int u = 0; u < CG; ++u)
+        for (int u = 0; u < 4; ++u)
           L.x1[(g + u) * S64 + lane] = conv1_point(w1a, w1b, w1c, b1v, q4[u].x, q4[u].y, q4[u].z);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -552,33 +487,13 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc[15]));
 #endif
       ASTAMP(2);
-      // x2 = ReLU, split three ways into the planes (registers 4g .. 4g+3 are
-      // rows 8g + 4h .. + 3 of column col: one 8-B write per plane), and its
-      // mask bits (one 16-bit word per lane)
       const int col = 32 * wave + r32;
       const float bias = b2a;
-      uint32_t mbits = 0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 ph, pm, pl;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          float v = acc[i] + bias;
-          v = v > 0.f ? v : 0.f;
-          __bf16 a, b, c2;
-          split3(v, a, b, c2);
-          ph[e] = a;
-          pm[e] = b;
-          pl[e] = c2;
-          mbits |= (v > 0.f ? 1u : 0u) << i;
-        }
-        const int o = x2c_off(col, 8 * g + 4 * h);
-        *reinterpret_cast<bf16x4*>(&L.x2p[0][o]) = ph;
-        *reinterpret_cast<bf16x4*>(&L.x2p[1][o]) = pm;
-        *reinterpret_cast<bf16x4*>(&L.x2p[2][o]) = pl;
+      for (int i = 0; i < 16; ++i) {
+        const float v = acc[i] + bias;
+        L.x2[acc_row(i, lane) * S64 + col] = v > 0.f ? v : 0.f;
       }
-      L.x2m[col * 2 + h] = (uint16_t)mbits;
     }
     BSTAMP(sb_);
 
@@ -665,8 +580,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       GSTAMP(b0 / BW_RB);
     }
     __syncthreads();
-    // combine the cut rows and apply the conv3 ReLU mask; padding rows -> 0;
-    // the rows go to the dZ3 planes (split three ways) and into db3
+    // combine the cut rows and apply the conv3 ReLU mask; padding rows -> 0
     if (wave >= 2) {
       int br[BW_G];  // the groups' cut rows, read once (three 16-B LDS reads)
 #pragma unroll
@@ -681,7 +595,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       for (int u = 0; u < BW_RBG; ++u) {
         const int rr = grp + BW_G * u;
         if (rr >= BW_RB) continue;
-        const float* d = &L.dz3[rr * SZ3 + 4 * cq];
+        float* d = &L.dz3[rr * SZ3 + 4 * cq];
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (rr < nb) {
           const float2 v01 = *reinterpret_cast<const float2*>(d);
@@ -705,88 +619,27 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
           v.z = (mk & 4u) ? v.z : 0.f;
           v.w = (mk & 8u) ? v.w : 0.f;
         }
-        bf16x4 ph, pm, pl;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          __bf16 a, b, c2;
-          split3(v[e], a, b, c2);
-          ph[e] = a;
-          pm[e] = b;
-          pl[e] = c2;
-        }
-        const int o = dz3p_off(rr, 4 * cq);
-        *reinterpret_cast<bf16x4*>(&L.dz3p[0][o]) = ph;
-        *reinterpret_cast<bf16x4*>(&L.dz3p[1][o]) = pm;
-        *reinterpret_cast<bf16x4*>(&L.dz3p[2][o]) = pl;
-        db3acc += v;
+        *reinterpret_cast<float2*>(d) = make_float2(v.x, v.y);
+        *reinterpret_cast<float2*>(d + 2) = make_float2(v.z, v.w);
       }
     }
     __syncthreads();
     BSTAMP(sb_ + 1);
 
-    // ---- c. dX2 = dZ3 W3 (32 x 128 . 128 x 64): wave -> (column tile ct, k
-    //      half kh), both 16-row tiles, six 16x16x32 bf16 products per 32-deep
-    //      k step.  A = the dZ3 planes (row reads), B = the W3^T planes from L2
-    //      (lane: column 16 ct + r16, k 8q .. +8; 24 VGPRs, all in flight at
-    //      once).  The k halves meet in LDS (dz1, free until d): kh = 1 parks
-    //      its partial, kh = 0 adds it (one fixed-order add) and applies the mask
+    // ---- c. dX2 = dZ3 W3 (32 x 128 . 128 x 64), 16x16 tile per wave ---------
     {
-      const int kh = wave >> 2;
-      f32x4m acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      bf16x8 bw[2][3];
-      const int wo = ((16 * ct + r16) * 128 + 64 * kh + 8 * q) * 2;
+      f32x4m acc = {0.f, 0.f, 0.f, 0.f};
+      if (16 * rt < nb) {
+        const float* ap = L.dz3 + (16 * rt + r16) * SZ3 + q;
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          bw[ss][p] = __builtin_bit_cast(
-              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w3r, wo, ss * 64 + p * W3T_PLANE * 2, 0));
-#ifdef PCADV_STAMPS
-      asm volatile("s_waitcnt vmcnt(0)" ::"v"(bw[1][2]));
-#endif
-      CSTAMP(0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        if (16 * t < nb) {
-#pragma unroll
-          for (int ss = 0; ss < 2; ++ss) {
-            const int o = dz3p_off(16 * t + r16, 64 * kh + 32 * ss + 8 * q);
-            const bf16x8 a[3] = {*reinterpret_cast<const bf16x8*>(&L.dz3p[0][o]),
-                                 *reinterpret_cast<const bf16x8*>(&L.dz3p[1][o]),
-                                 *reinterpret_cast<const bf16x8*>(&L.dz3p[2][o])};
-            acc[t] = mfma16x6(a, bw[ss], acc[t]);
-          }
-        }
+        for (int s = 0; s < 32; ++s)
+          acc = mfma16(ap[4 * s], __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w3r, boff, s * 1024, 0)), acc);
       }
-#ifdef PCADV_STAMPS
-      asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc[1]));
-#endif
-      CSTAMP(1);
       const int col = 16 * ct + r16;
-      if (kh == 1) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) L.dz1[(16 * t + 4 * q + j) * 64 + col] = acc[t][j];
-      }
-      __syncthreads();
-      CSTAMP(2);
-      if (kh == 0) {  // every read before the first write (one LDS round trip)
-        float part[2][4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) part[t][j] = L.dz1[(16 * t + 4 * q + j) * 64 + col];
-        // rows 16 t + 4 q + j: h = q & 1, bit (j) + 4 (2 t + (q >> 1))
-        const uint32_t mw = L.x2m[col * 2 + (q & 1)];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int row = 16 * t + 4 * q + j;
-            const bool pos = (mw >> (j + 4 * (2 * t + (q >> 1)))) & 1u;
-            L.dz2[row * SZ2 + col] = pos ? acc[t][j] + part[t][j] : 0.f;
-          }
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * rt + 4 * q + j;
+        L.dz2[row * SZ2 + col] = L.x2[row * S64 + col] > 0.f ? acc[j] : 0.f;
       }
     }
     __syncthreads();
@@ -814,32 +667,14 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     __syncthreads();
     BSTAMP(sb_ + 3);
 
-    // ---- e. weight / bias gradients over the batch rows ----------------------
+    // ---- e. weight / bias gradients over the batch rows (32x32x2) ------------
     {
       const int nb2 = (nb + 1) & ~1;
-      // dW3[o][i] += sum_rows dz3[row][o] x2[row][i]; wave -> (o tile, i tile),
-      // six 32x32x16 bf16 products per 16 rows.  A: transposed reads of the
-      // dZ3 planes (lane 4qq + pp of a 16-lane group points at row 8 hh + 4 m +
-      // qq, column c0 + 4 pp; m = 0, 1 give k = 8 hh + 0..3, + 4..7); B: the
-      // lane's column of the x2 planes, rows 16 t + 8 hh .. + 8 (one 16-B read)
-      {
-        const int ot = wave >> 1, it = wave & 1;
-        const int g16 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-        const int ra = 8 * (g16 >> 1) + qq;
-        const int ca = 32 * ot + 16 * (g16 & 1) + 4 * pp;
-        const int nk = (nb + 15) >> 4;  // rows past nb are zero in the dZ3 planes
-        for (int t = 0; t < nk; ++t) {
-          bf16x8 a[3], b[3];
-          const int ob = x2c_off(32 * it + r32, 16 * t + 8 * h);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            a[p] = cat8(lds_tr16(&L.dz3p[p][dz3p_off(16 * t + ra, ca)]),
-                        lds_tr16(&L.dz3p[p][dz3p_off(16 * t + ra + 4, ca)]));
-            b[p] = *reinterpret_cast<const bf16x8*>(&L.x2p[p][ob]);
-          }
-          a_dw3 = mfma32x6(a, b, a_dw3);
-        }
-      }
+      // dW3[o][i] += sum_rows dz3[row][o] x2[row][i]; wave -> (o tile, i tile)
+      const int ot = wave >> 1, it = wave & 1;
+      const float* ap = L.dz3 + h * SZ3 + 32 * ot + r32;
+      const float* bp = L.x2 + h * S64 + 32 * it + r32;
+      for (int s = 0; s < nb2 / 2; ++s) a_dw3 = mfma32(ap[2 * s * SZ3], bp[2 * s * S64], a_dw3);
       // dW2[o][i] += sum_rows dz2[row][o] x1[row][i]; waves 0-3 rows [0,16),
       // waves 4-7 rows [16,32) of the batch, same 4 tiles
       const int t2 = wave & 3, rh = wave >> 2;
@@ -854,10 +689,12 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
         const int o = tid / 3, i = tid % 3;
 #pragma unroll 8
         for (int r = 0; r < BW_RB; ++r) acc_w1 = fmaf(L.dz1[r * SZ2 + o], L.pts[r * 4 + i], acc_w1);
-      } else if (tid >= 320 && tid < 448) {
-        const float* src = tid < 384 ? L.dz2 + (tid - 320) : L.dz1 + (tid - 384);
+      } else if (tid < 448) {
+        const float* src = tid < 320 ? L.dz3 + (tid - 192) : (tid < 384 ? L.dz2 + (tid - 320)
+                                                                        : L.dz1 + (tid - 384));
+        const int st = tid < 320 ? SZ3 : SZ2;
 #pragma unroll 8
-        for (int r = 0; r < BW_RB; ++r) acc_b += src[r * SZ2];
+        for (int r = 0; r < BW_RB; ++r) acc_b += src[r * st];
       }
     }
     __syncthreads();
@@ -873,9 +710,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     for (int r = 0; r < 16; ++r)
       slab[SL_DW3 + (32 * ot + acc_row(r, lane)) * 64 + 32 * it + r32] = a_dw3[r];
   }
-  // db3: the gather groups' partials, summed below in group order
-  float* db3p = reinterpret_cast<float*>(&L.x2p[0][0]);  // 12 x 128 floats
-  if (wave >= 2) *reinterpret_cast<f32x4*>(&db3p[((tid >> 5) - 4) * 128 + 4 * (tid & 31)]) = db3acc;
   // the two row halves of dW2 meet in LDS (waves 4-7 park theirs in dz3)
   {
     const int t2 = wave & 3;
@@ -894,12 +728,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     }
   }
   if (tid < 192) slab[SL_DW1 + tid] = acc_w1;
-  else if (tid < 320) {
-    float v = 0.f;
-#pragma unroll
-    for (int g = 0; g < BW_G; ++g) v += db3p[g * 128 + tid - 192];
-    slab[SL_DB3 + tid - 192] = v;
-  }
+  else if (tid < 320) slab[SL_DB3 + tid - 192] = acc_b;
   else if (tid < 384) slab[SL_DB2 + tid - 320] = acc_b;
   else if (tid < 448) slab[SL_DB1 + tid - 384] = acc_b;
 #ifdef PCADV_STAMPS
@@ -909,7 +738,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #undef BSTAMP
 #undef GSTAMP
 #undef ASTAMP
-#undef CSTAMP
 }
 
 // out[j] = sum over slabs in fixed order: 64 columns per block (one per lane;
@@ -994,36 +822,21 @@ k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float
   }
 }
 
-// the W3^T planes when no forward of the same step made them (the standalone
-// backward): 4 x 256 threads
-__global__ void __launch_bounds__(256) k_w3t_planes(const float* __restrict__ w3,
-                                                    __bf16* __restrict__ out) {
-  w3t_planes_part(blockIdx.x * 256 + threadIdx.x, w3, out);
-}
-
-static size_t feat_bwd_slab_bytes(int C, int N) {
+size_t feat_bwd_workspace_bytes(int C, int N) {
   const size_t nchunk = (N + BW_PCH - 1) / BW_PCH;
   return (size_t)C * nchunk * SLAB * sizeof(float);
 }
-size_t feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_slab_bytes(C, N) + W3T_BYTES; }
 
 int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, const float* pts_b,
                     int split, int C, int N, const float* w1, const float* b1, const float* w2,
                     const float* b2, const float* w3, const float* w4, const float* x3,
                     float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
                     float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s,
-                    uint64_t* stamps, const FinAdam* adam, const int* sortrec,
-                    const void* w3t) {
+                    uint64_t* stamps, const FinAdam* adam, const int* sortrec) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
   float* slabs = static_cast<float*>(ws);
-  if (!w3t) {  // the planes at the workspace's end (slab bytes are a multiple of 16)
-    __bf16* planes = reinterpret_cast<__bf16*>(static_cast<char*>(ws) + feat_bwd_slab_bytes(C, N));
-    hipLaunchKernelGGL(k_w3t_planes, dim3(4), dim3(256), 0, s, w3, planes);
-    PC_HIP_CHECK_LAUNCH("k_w3t_planes");
-    w3t = planes;
-  }
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<false>),
@@ -1057,13 +870,11 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
   if (sortrec)
     hipLaunchKernelGGL(k_feat_bwd_chunk<true>, dim3(nchunk, C + arows), dim3(BW_T), sizeof(BwdLds),
                        s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs,
-                       stamps, sortrec, C, dw4, db4, fa, nba0, nba1,
-                       static_cast<const __bf16*>(w3t));
+                       stamps, sortrec, C, dw4, db4, fa, nba0, nba1);
   else
     hipLaunchKernelGGL(k_feat_bwd_chunk<false>, dim3(nchunk, C + arows), dim3(BW_T),
                        sizeof(BwdLds), s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3,
-                       w4, x3, slabs, stamps, sortrec, C, dw4, db4, fa, nba0, nba1,
-                       static_cast<const __bf16*>(w3t));
+                       w4, x3, slabs, stamps, sortrec, C, dw4, db4, fa, nba0, nba1);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   const int nb4 = fa.on ? fin_adam_blocks(PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W, 1024, 2) : 0;
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + nb4), dim3(1024), 0, s, slabs, C * nchunk,

@@ -67,8 +67,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
             int T, int ntiles, const float* __restrict__ w1, const float* __restrict__ b1,
             const float* __restrict__ w2, const float* __restrict__ b2,
             const float* __restrict__ w3, const float* __restrict__ b3,
-            float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps,
-            __bf16* __restrict__ w3t) {
+            float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MlpLds& L = *reinterpret_cast<MlpLds*>(smem);
 #ifdef PCADV_STAMPS
@@ -134,15 +133,11 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     __syncthreads();  // (also: every wave is past the previous tile's conv3 reads)
     STAMP(3 + 5 * it);
     if (it + 1 < TPW && tile + 1 < ntiles) pv = pts_load(tile + 1);  // in flight during this tile
-    // all 16 points read before the 16 writes (a read-write-read chain pays one
-    // LDS round trip per pair: the compiler cannot tell x1 from pts)
-    {
-      f32x4 q[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) q[i] = *reinterpret_cast<const f32x4*>(&L.pts[(pg * 16 + i) * 4]);
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        L.x1[(pg * 16 + i) * S64 + c1] = conv1_point(wa, wb, wc, bb1, q[i].x, q[i].y, q[i].z);
+    for (int i = 0; i < 16; ++i) {
+      const int p = pg * 16 + i;
+      const f32x4 q = *reinterpret_cast<const f32x4*>(&L.pts[p * 4]);
+      L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
     }
     if (it == 0) split_w3();  // W3 has landed by now (after conv1 of the first tile)
     __syncthreads();
@@ -216,9 +211,6 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
   }
   STAMP(2);
 #undef STAMP
-  // the W3^T planes of this step's feature backward (w3t_planes_part)
-  if (w3t)
-    for (int t = blockIdx.x * PM_T + tid; t < 1024; t += gridDim.x * PM_T) w3t_planes_part(t, w3, w3t);
 }
 
 // ============================================================================
@@ -794,7 +786,7 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
                               const float* w1, const float* b1, const float* w2, const float* b2,
                               const float* w3, const float* b3, const float* w4, const float* b4,
                               float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter,
-                              hipStream_t s, uint64_t* stamps, void* w3t) {
+                              hipStream_t s, uint64_t* stamps) {
   const int rc = feat_fwd_attrs<NP3, NP4>();
   if (rc != PCADV_OK) return rc;
   const int T = (N + PM_P - 1) / PM_P;
@@ -805,11 +797,11 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
   if (ntiles < 1024 && !stamps)
     hipLaunchKernelGGL((k_point_mlp<NP3, 1>), dim3(ntiles), dim3(PM_T), sizeof(MlpLds), s, pts_a,
                        pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3, inc_counter,
-                       mlp_stamps, static_cast<__bf16*>(w3t));
+                       mlp_stamps);
   else
     hipLaunchKernelGGL((k_point_mlp<NP3, 2>), dim3((ntiles + 1) / 2), dim3(PM_T), sizeof(MlpLds),
                        s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3,
-                       inc_counter, mlp_stamps, static_cast<__bf16*>(w3t));
+                       inc_counter, mlp_stamps);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
   return launch_conv4_max_np<NP3, NP4>(x3, C, N, w4, b4, gmax, gidx, s, stamps);
 }
@@ -829,8 +821,7 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
                           const float* w1, const float* b1, const float* w2, const float* b2,
                           const float* w3, const float* b3, const float* w4, const float* b4,
                           float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
-                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int precision,
-                          void* w3t) {
+                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int precision) {
   (void)ws;
   (void)ws_bytes;
   PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
@@ -838,9 +829,9 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
   PC_REQUIRE(precision == 0 || precision == 1, "feat_fwd: precision %d (0 fp32, 1 bf16)", precision);
   if (precision == 1)
     return launch_feat_fwd_np<1, 1>(pts_a, pts_b, split, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3,
-                                    gmax, gidx, inc_counter, s, stamps, w3t);
+                                    gmax, gidx, inc_counter, s, stamps);
   return launch_feat_fwd_np<6, 3>(pts_a, pts_b, split, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3,
-                                  gmax, gidx, inc_counter, s, stamps, w3t);
+                                  gmax, gidx, inc_counter, s, stamps);
 }
 
 }  // namespace pcadv

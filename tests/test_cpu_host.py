@@ -69,9 +69,7 @@ def test_workspace_sizes():
     assert lib.pcadv_gemm_wgrad_workspace_bytes(300, 64, 3, 7) == 0  # rows % rows_per_group
     assert lib.pcadv_conv_max_x3_workspace_bytes(16, 2048, 2048) == 16 * 16 * 2048 * 8 + 256
     assert lib.pcadv_row_ce_workspace_bytes(32768) == 128 * 4 + 256
-    # feature backward: one 12 736-float slab per 128-point chunk + the W3^T
-    # bf16 planes (3 x 64 x 128) of the standalone call
-    assert lib.pcadv_feat_bwd_workspace_bytes(64, 1024) == 64 * 8 * 12736 * 4 + 3 * 64 * 128 * 2
+    assert lib.pcadv_feat_bwd_workspace_bytes(64, 1024) == 64 * 8 * 12736 * 4
 
 
 def test_ops_refuse_cpu_tensors():
