@@ -67,19 +67,24 @@ class PointNetfeat(nn.Module):
         if self.feature_transform:
             self.fstn = STNkd(k=64)
 
-    def forward_points(self, pts):
+    def forward_points(self, pts, with_pointfeat=False):
         """pts: C x N x 3 (point-major, as PointNetCls receives it) ->
-        (global C x 1024, trans_feat or None)."""
-        if self.feature_transform:
-            # models/pointnet.py:115-130 with the STNkd(64) feature transform;
-            # point-wise kernels + the sparse max-pool backward
+        (global C x 1024, trans_feat or None), plus the point features (C x N x 64,
+        conv2's output after the optional feature transform) with_pointfeat."""
+        if self.feature_transform or with_pointfeat:
+            # models/pointnet.py:115-130 layer by layer (point-wise kernels, the
+            # STNkd(64) feature transform if on, the sparse max-pool backward)
             x = PointwiseFunction.apply(pts.contiguous(), self.conv1.weight, self.conv1.bias,
                                         ACT_RELU)
             x = PointwiseFunction.apply(x, self.conv2.weight, self.conv2.bias, ACT_RELU)
-            trans_feat = self.fstn.forward_points(x)
-            x = TransformFunction.apply(x, trans_feat)
+            trans_feat = None
+            if self.feature_transform:
+                trans_feat = self.fstn.forward_points(x)
+                x = TransformFunction.apply(x, trans_feat)
+            pointfeat = x
             x = PointwiseFunction.apply(x, self.conv3.weight, self.conv3.bias, ACT_RELU)
-            return ConvMaxFunction.apply(x, self.conv4.weight, self.conv4.bias, False), trans_feat
+            g = ConvMaxFunction.apply(x, self.conv4.weight, self.conv4.bias, False)
+            return (g, trans_feat, pointfeat) if with_pointfeat else (g, trans_feat)
         gmax, gidx = PointFeatFunction.apply(
             pts.contiguous(), self.conv1.weight, self.conv1.bias, self.conv2.weight,
             self.conv2.bias, self.conv3.weight, self.conv3.bias, self.conv4.weight,
@@ -90,11 +95,14 @@ class PointNetfeat(nn.Module):
     def forward(self, x):
         # the reference receives B x C x N; the kernels read the point-major
         # B x N x 3 layout, which is a free view when x came from a transpose.
-        g, trans_feat = self.forward_points(x.transpose(1, 2))
         if self.global_feat:
-            return g, trans_feat
+            return self.forward_points(x.transpose(1, 2))
+        # models/pointnet.py:133-137: the global feature repeated over the points,
+        # then the point features: B x (1024 + 64) x N
         n_pts = x.size(2)
-        raise NotImplementedError("global_feat=False (per-point concat) is not on the hot path")
+        g, trans_feat, pointfeat = self.forward_points(x.transpose(1, 2), with_pointfeat=True)
+        return torch.cat([g.unsqueeze(2).expand(-1, -1, n_pts), pointfeat.transpose(1, 2)],
+                         1), trans_feat
 
 
 class PointNetCls(nn.Module):
