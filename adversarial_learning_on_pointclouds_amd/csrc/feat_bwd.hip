@@ -284,7 +284,6 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       (void*)(x3 + (size_t)c * N * 128), (short)0, N * 128 * 4, 0x00020000);
   // conv1 weights, fetched up front so they land during the hit sort
   const int ch1 = tid & 63;
-  const float b2a = wave < 2 ? b2[32 * wave + (lane & 31)] : 0.f;  // phase a's conv2 bias
   const float w1a = w1[ch1 * 3 + 0], w1b = w1[ch1 * 3 + 1], w1c = w1[ch1 * 3 + 2], b1v = b1[ch1];
   int nact;
   float ptv[2] = {0.f, 0.f};
@@ -465,17 +464,10 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       ASTAMP(0);
-      // four rows' points read before their four writes: the compiler cannot
-      // tell the x1 writes from the pts reads, so a row-by-row loop pays one
-      // LDS round trip per row
-#pragma unroll
-      for (int g = 0; g < BW_RB; g += 4) {
-        f32x4 q4[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) q4[u] = *reinterpret_cast<const f32x4*>(&L.pts[(g + u) * 4]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          L.x1[(g + u) * S64 + lane] = conv1_point(w1a, w1b, w1c, b1v, q4[u].x, q4[u].y, q4[u].z);
+#pragma unroll 8
+      for (int rr = 0; rr < BW_RB; ++rr) {
+        const f32x4 q4 = *reinterpret_cast<const f32x4*>(&L.pts[rr * 4]);
+        L.x1[rr * S64 + lane] = conv1_point(w1a, w1b, w1c, b1v, q4.x, q4.y, q4.z);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -488,7 +480,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #endif
       ASTAMP(2);
       const int col = 32 * wave + r32;
-      const float bias = b2a;
+      const float bias = b2[col];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float v = acc[i] + bias;
@@ -655,13 +647,10 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
           acc = mfma16(ap[4 * s], __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w2r, boff, s * 1024, 0)), acc);
       }
       const int col = 16 * ct + r16;
-      float xv[4];  // the masks' x1 values, read before the writes
-#pragma unroll
-      for (int j = 0; j < 4; ++j) xv[j] = L.x1[(16 * rt + 4 * q + j) * S64 + col];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = 16 * rt + 4 * q + j;
-        L.dz1[row * SZ2 + col] = xv[j] > 0.f ? acc[j] : 0.f;
+        L.dz1[row * SZ2 + col] = L.x1[row * S64 + col] > 0.f ? acc[j] : 0.f;
       }
     }
     __syncthreads();
