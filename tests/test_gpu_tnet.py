@@ -258,7 +258,7 @@ def test_pointnetfeat_dense_vs_oracle(ft):
                        if k.startswith("feat.")})
     f = f.to(DEV)
     rng = np.random.default_rng(22)
-    B, N = 2, 320  # the feature transform takes N % 64 == 0 (pcadv_pw_fwd rows per matrix)
+    B, N = 2, 512  # the feature transform takes N % 256 == 0 (its dT per-cloud row groups)
     pts = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
     x = _t(pts.transpose(0, 2, 1)).requires_grad_(True)
     out, trans = f(x)
