@@ -11,6 +11,9 @@ which = int(sys.argv[2]) if len(sys.argv) > 2 else -2
 i0 = starts[which]
 i1 = starts[which + 1] if which + 1 < len(starts) else len(rows)
 t0 = int(rows[i0]["Start_Timestamp"])
+print("# rocprofv3 kernel-trace timestamps (us from the step's first kernel). Gaps of about +-1 us "
+      "(negative ones included) are skew between dispatch records, not idle time; the step time "
+      "is bench.py's event timing.")
 prev_end = t0
 for r in rows[i0:i1]:
     s = (int(r["Start_Timestamp"]) - t0) / 1e3
