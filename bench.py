@@ -67,11 +67,13 @@ def parse():
     ap.add_argument("--points", type=int, default=1024,
                     help="points per cloud of the adv step (1024: the metric's config; 2048: "
                          "BASELINE configs[4]'s per-rank shape)")
-    ap.add_argument("--config", choices=["adv", "seg", "cls", "trainer"], default="adv",
+    ap.add_argument("--config", choices=["adv", "seg", "cls", "cls_ft", "trainer"], default="adv",
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
-                         "supervised PointNetCls step of configs[1]; trainer: run_training "
-                         "end to end over DeviceCloudLoaders")
+                         "supervised PointNetCls step of configs[1]; cls_ft: the same with "
+                         "feature_transform=True (STNkd(64) + regulariser, layer-by-layer "
+                         "kernels through autograd); trainer: run_training end to end over "
+                         "DeviceCloudLoaders")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="feature-forward precision (default: bf16 for --config cls, the dtype "
                          "BASELINE configs[1] names; fp32 for adv and seg)")
@@ -457,6 +459,85 @@ def bench_cls(args):
     print(json.dumps(_with_runtime(out)), flush=True)
 
 
+def bench_cls_ft(args):
+    """run_training_pointnet_cls with PointNetCls(k=40, feature_transform=True)
+    (utils/trainer.py:254-268: CE + 0.001 x the regulariser, Adam): the fused
+    cls step does not cover the feature transform, so this is the autograd body
+    over the layer-by-layer kernels (point-wise conv1..conv3, the STNkd(64) and
+    transform kernels, conv4 + max, the head), fp32 throughout, with
+    torch.optim.Adam(capturable=True); one HIP graph per resident batch when
+    capture works, else eager."""
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd.pointnet import feature_transform_regularizer
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = pc.PointNetCls(k=40, feature_transform=True).to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), capturable=True)
+    pool = []
+    for k in range(POOL):
+        rng = np.random.default_rng(3000 + k)
+        pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
+                     torch.from_numpy(rng.integers(0, 40, B)).to(dev)))
+    losses = torch.zeros(POOL, device=dev)
+
+    def body(pts, lab, k):
+        opt.zero_grad(set_to_none=False)
+        logits, _, trans = model(pts)
+        loss = torch.nn.functional.cross_entropy(logits, lab) + 0.001 * feature_transform_regularizer(trans)
+        loss.backward()
+        opt.step()
+        losses[k].copy_(loss.detach())
+
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # autograd / optimizer state created outside any capture
+        for k in range(3):
+            body(*pool[k % POOL], k % POOL)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graphs, why = [], None
+    if not args.no_graph:
+        try:
+            for k in range(POOL):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    body(*pool[k], k)
+                graphs.append(g)
+        except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
+            graphs, why = [], f"{type(e).__name__}: {e}"[:200]
+            torch.cuda.synchronize()
+
+    def one(k):
+        if graphs:
+            graphs[k % POOL].replay()
+        else:
+            body(*pool[k % POOL], k % POOL)
+    for k in range(args.warmup):
+        one(k)
+    regions = timed_regions(one, args.steps, args.repeats)
+    dt = float(np.median(regions))
+    loss = float(losses[(args.steps - 1) % POOL].item())
+    out = {
+        "metric": "point-clouds/sec (cls train step with feature_transform=True), B=32 N=1024 "
+                  "ModelNet40, 1 GPU",
+        "value": round(B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32 (layer-by-layer kernels: exact-f32 MFMA point-wise layers, split-product "
+                 "conv4 + exact max re-evaluation)",
+        "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
+        "config": {"workload": "run_training_pointnet_cls with PointNetCls(k=40, "
+                               "feature_transform=True): CE + 0.001 regulariser, Adam, autograd "
+                               "over the pcadv ops", "global_batch": B, "points": N,
+                   "parallelism": "dp1", "hip_graph": bool(graphs)},
+        "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
+        "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
+    }
+    if why:
+        out["graph_capture_error"] = why
+    print(json.dumps(_with_runtime(out)), flush=True)
+
+
 def _synthetic_modelnet(n_gt, n_nogt, seed=5000):
     """ModelNetDatasetGT / _noGT objects over in-memory synthetic clouds (the
     HDF5 files are not in the image): same attributes as the file-backed ones,
@@ -709,6 +790,8 @@ def main():
         return bench_seg(args)
     if args.config == "cls":
         return bench_cls(args)
+    if args.config == "cls_ft":
+        return bench_cls_ft(args)
     if args.config == "trainer":
         return bench_trainer(args)
     if _backend() != "nccl":  # rehearsal: ranks may share a GPU
