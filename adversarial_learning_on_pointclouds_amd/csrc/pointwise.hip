@@ -273,40 +273,85 @@ k_pw_bwd_weight(const float* __restrict__ dy, const float* __restrict__ yv,
   if (tid < O) slab[O * K + tid] = dbacc;
 }
 
-// K = 3 (conv1 weights over the points): thread = (o, k) with k = 3 -> bias
+// K = 3 (conv1 weights over the points): thread = (o, quarter of the slab's
+// rows), four accumulators (k = 0..2 and the bias); RB rows' operands loaded
+// before their fmas; the quarters added in order through LDS
 __global__ void __launch_bounds__(PW_T)
 k_pw_bwd_weight3(const float* __restrict__ dy, const float* __restrict__ yv, int act,
                  const float* __restrict__ x, int M, int O, float* __restrict__ slabs) {
-  const int tid = threadIdx.x;
-  const int o = tid % O, k = tid / O;  // O <= 64: 4 * O <= 256 threads
-  const int rbase = blockIdx.x * PWW_ROWS;
-  float acc = 0.f;
-  if (k < 4) {
-    for (int i = 0; i < PWW_ROWS; ++i) {
-      const int m = rbase + i;
-      if (m >= M) break;
-      float z = dy[(size_t)m * O + o];
-      if (act != ACT_NONE) z *= act_bwd(yv[(size_t)m * O + o], act);
-      acc = fmaf(z, k < 3 ? x[(size_t)m * 3 + k] : 1.f, acc);
+  __shared__ float part[4][64][4];
+  const int tid = threadIdx.x, o = tid & 63, rq = tid >> 6;  // O <= 64
+  const int rbase = blockIdx.x * PWW_ROWS + rq * (PWW_ROWS / 4);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (o < O) {
+    constexpr int RB = 16;
+    for (int i0 = 0; i0 < PWW_ROWS / 4; i0 += RB) {
+      float z[RB], xv[RB][3];
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int m = rbase + i0 + u;
+        const bool ok = m < M;
+        const size_t mm = ok ? (size_t)m : 0;
+        z[u] = ok ? dy[mm * O + o] : 0.f;
+        if (act != ACT_NONE) z[u] *= ok ? act_bwd(yv[mm * O + o], act) : 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xv[u][k] = ok ? x[mm * 3 + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < RB; ++u)
+        if (rbase + i0 + u < M) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) acc[k] = fmaf(z[u], xv[u][k], acc[k]);
+          acc[3] += z[u];
+        }
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) part[rq][o][k] = acc[k];
+  __syncthreads();
+  if (rq == 0 && o < O) {
     float* slab = slabs + (size_t)blockIdx.x * (O * 3 + O);
-    if (k < 3) slab[o * 3 + k] = acc;
-    else slab[O * 3 + o] = acc;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float v = ((part[0][o][k] + part[1][o][k]) + part[2][o][k]) + part[3][o][k];
+      if (k < 3) slab[o * 3 + k] = v;
+      else slab[O * 3 + o] = v;
+    }
   }
 }
 
-// out[g][j] = sum_{s < per} slabs[g*per + s][j] in slab order; j < W: dW,
-// j = W.. : db
-__global__ void __launch_bounds__(256)
+// out[g][j] = sum_{s < per} slabs[g*per + s][j] in a fixed order: 64 columns
+// per block (one per lane), the 16 waves take contiguous slab ranges (8 loads
+// in flight per lane), their partials added in wave order; j < W: dW, j = W.. : db
+constexpr int PWR_W = 16;  // waves per reduce block
+__global__ void __launch_bounds__(64 * PWR_W)
 k_pw_reduce(const float* __restrict__ slabs, int per, int width, int wsize,
             float* __restrict__ dw, float* __restrict__ db) {
-  const int j = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
-  if (j >= width) return;
-  const float* s = slabs + (size_t)g * per * width + j;
+  __shared__ float part[PWR_W][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane, g = blockIdx.y;
+  const int s0 = wave * per / PWR_W, s1 = (wave + 1) * per / PWR_W;
   float acc = 0.f;
-  for (int i = 0; i < per; ++i) acc += s[(size_t)i * width];
-  if (j < wsize) dw[(size_t)g * wsize + j] = acc;
-  else if (db) db[(size_t)g * (width - wsize) + j - wsize] = acc;
+  if (j < width) {
+    const float* s = slabs + (size_t)g * per * width + j;
+    int i = s0;
+    for (; i + 8 <= s1; i += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(i + u) * width];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; i < s1; ++i) acc += s[(size_t)i * width];
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && j < width) {
+    float x = part[0][lane];
+    for (int w = 1; w < PWR_W; ++w) x += part[w][lane];
+    if (j < wsize) dw[(size_t)g * wsize + j] = x;
+    else if (db) db[(size_t)g * (width - wsize) + j - wsize] = x;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -344,14 +389,33 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     // ---- dW[o,:] = sum_c g'[c,o] x[c, gidx[c,o], :], db[o] = sum_c g'[c,o]
     const int o = ((int)blockIdx.x - nxb) * 8 + wave;
     if (o >= O) return;
+    // CB clouds' gradients, argmax rows and x rows in flight at once, summed
+    // in cloud order (a cloud at a time was one dependent round trip each)
+    constexpr int CB = 16;
     float a0 = 0.f, a1 = 0.f, ab = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const size_t i = (size_t)c * O + o;
-      const float g = cm_g(dg, gmax, i);
-      const float* row = x + ((size_t)c * N + gidx[i]) * K;
-      if (lane < K) a0 = fmaf(g, row[lane], a0);
-      if (lane + 64 < K) a1 = fmaf(g, row[lane + 64], a1);
-      ab += g;
+    for (int c0 = 0; c0 < C; c0 += CB) {
+      float g[CB], v0[CB], v1[CB];
+      int r[CB];
+#pragma unroll
+      for (int u = 0; u < CB; ++u) {
+        const size_t i = (size_t)min(c0 + u, C - 1) * O + o;
+        g[u] = c0 + u < C ? cm_g(dg, gmax, i) : 0.f;
+        r[u] = gidx[i];
+      }
+#pragma unroll
+      for (int u = 0; u < CB; ++u) {
+        const float* row = x + ((size_t)min(c0 + u, C - 1) * N + r[u]) * K;
+        v0[u] = lane < K ? row[lane] : 0.f;
+        v1[u] = lane + 64 < K ? row[lane + 64] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CB; ++u) {
+        if (c0 + u < C) {
+          a0 = fmaf(g[u], v0[u], a0);
+          a1 = fmaf(g[u], v1[u], a1);
+          ab += g[u];
+        }
+      }
     }
     if (lane < K) dw[(size_t)o * K + lane] = a0;
     if (lane + 64 < K) dw[(size_t)o * K + lane + 64] = a1;
@@ -372,7 +436,10 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   for (int u = 0; u < PER; ++u) {
     const int o = u * CMB_T + tid;
     const int a = o < O ? gidx[(size_t)c * O + o] : -1;
-    const bool hit = a >= p0 && a < p0 + CMB_PCH;
+    // channels whose ReLU-before-max output is 0 carry no gradient: with the
+    // ReLU every all-negative channel's argmax is point 0, hundreds of hits on
+    // one row that one thread group would walk (they add exact zeros)
+    const bool hit = a >= p0 && a < p0 + CMB_PCH && (!gmax || gmax[(size_t)c * O + o] > 0.f);
     hrow[u] = hit ? a - p0 : -1;
     hg[u] = hit ? cm_g(dg, gmax, (size_t)c * O + o) : 0.f;
     if (hit) atomicAdd(&L.rcnt[a - p0], 1);
@@ -410,15 +477,39 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
       L.sg[s0 + rank] = hg[u];
     }
   __syncthreads();
-  // thread = (column k, row group): rows grp, grp + 4, ...; inactive rows -> 0
+  // thread = (column k, group of 32 consecutive rows): the group's hits are
+  // contiguous in (row, o) order, walked flat with HD W loads in flight; each
+  // row's sum runs over its hits in o order (rows without hits -> 0)
   const int k = tid & 127, grp = tid >> 7;
   if (k >= K) return;
-  for (int row = grp; row < CMB_PCH; row += 4) {
-    if (p0 + row >= N) break;
-    const int s0 = L.roff[row], s1 = s0 + L.rcnt[row];
-    float acc = 0.f;
-    for (int j = s0; j < s1; ++j) acc = fmaf(L.sg[j], w[(size_t)L.so[j] * K + k], acc);
-    dx[((size_t)c * N + p0 + row) * K + k] = acc;
+  constexpr int RG = CMB_PCH / 4, HD = 8;
+  const int r0 = grp * RG, r1 = min(r0 + RG, N - p0);
+  if (r1 <= r0) return;
+  const int j1 = L.roff[r1 - 1] + L.rcnt[r1 - 1];
+  float* drow = dx + ((size_t)c * N + p0) * K + k;
+  int row = r0, rend = L.roff[r0] + L.rcnt[r0];
+  float acc = 0.f;
+  for (int j = L.roff[r0]; j < j1; j += HD) {
+    float wv[HD];
+#pragma unroll
+    for (int u = 0; u < HD; ++u)
+      wv[u] = j + u < j1 ? w[(size_t)L.so[j + u] * K + k] : 0.f;
+#pragma unroll
+    for (int u = 0; u < HD; ++u) {
+      if (j + u < j1) {
+        while (j + u >= rend) {  // row done: store it, move to the next
+          drow[(size_t)row * K] = acc;
+          acc = 0.f;
+          ++row;
+          rend = L.roff[row] + L.rcnt[row];
+        }
+        acc = fmaf(L.sg[j + u], wv[u], acc);
+      }
+    }
+  }
+  for (; row < r1; ++row) {  // the last row with hits, then the rows after it
+    drow[(size_t)row * K] = acc;
+    acc = 0.f;
   }
 }
 
@@ -430,21 +521,48 @@ __global__ void __launch_bounds__(256)
 k_tnet_reg(const float* __restrict__ T, int B, int k, float* __restrict__ norms,
            const float* __restrict__ gscale, float* __restrict__ dT) {
   extern __shared__ float sm[];
-  float* t = sm;              // k x k
-  float* a = sm + k * k;      // k x k
+  const int ks = k + 1;       // LDS row stride: row j's element l for 32 consecutive j
+  float* t = sm;              //   hits 32 banks (stride k = 64 was one bank)
+  float* a = sm + k * ks;     // k x k, same stride
   __shared__ double part[256];
   const int tid = threadIdx.x, b = blockIdx.x;
   const float* tb = T + (size_t)b * k * k;
-  for (int e = tid; e < k * k; e += 256) t[e] = tb[e];
+  for (int e = tid; e < k * k; e += 256) t[(e / k) * ks + e % k] = tb[e];
   __syncthreads();
   double ss = 0.0;
-  for (int e = tid; e < k * k; e += 256) {
-    const int i = e / k, j = e % k;
-    float v = 0.f;
-    for (int l = 0; l < k; ++l) v = fmaf(t[i * k + l], t[j * k + l], v);
-    v -= (i == j) ? 1.f : 0.f;
-    a[e] = v;
-    ss += (double)v * v;
+  if (k == 64) {  // thread -> a 4 x 4 block of T T^T: 8 LDS reads per 16 fmas
+    const int i0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);
+    float v[4][4] = {};
+    for (int l = 0; l < 64; ++l) {
+      float ti[4], tj[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ti[u] = t[(i0 + u) * ks + l];
+        tj[u] = t[(j0 + u) * ks + l];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[u][q] = fmaf(ti[u], tj[q], v[u][q]);
+    }
+    // (the norm's f64 sum of squares runs in this blocked element order)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float d = v[u][q] - ((i0 + u) == (j0 + q) ? 1.f : 0.f);
+        a[(i0 + u) * ks + j0 + q] = d;
+        ss += (double)d * d;
+      }
+  } else {
+    for (int e = tid; e < k * k; e += 256) {
+      const int i = e / k, j = e % k;
+      float v = 0.f;
+      for (int l = 0; l < k; ++l) v = fmaf(t[i * ks + l], t[j * ks + l], v);
+      v -= (i == j) ? 1.f : 0.f;
+      a[i * ks + j] = v;
+      ss += (double)v * v;
+    }
   }
   part[tid] = ss;
   __syncthreads();
@@ -458,11 +576,32 @@ k_tnet_reg(const float* __restrict__ T, int B, int k, float* __restrict__ norms,
     return;
   }
   const float scale = 2.f * (*gscale) / ((float)B * n);
-  for (int e = tid; e < k * k; e += 256) {
-    const int i = e / k, j = e % k;
-    float v = 0.f;
-    for (int l = 0; l < k; ++l) v = fmaf(a[i * k + l], t[l * k + j], v);
-    dT[(size_t)b * k * k + e] = scale * v;
+  if (k == 64) {  // (T T^T - I) T in 4 x 4 blocks
+    const int i0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);
+    float v[4][4] = {};
+    for (int l = 0; l < 64; ++l) {
+      float ai[4], tl[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ai[u] = a[(i0 + u) * ks + l];
+        tl[u] = t[l * ks + j0 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[u][q] = fmaf(ai[u], tl[q], v[u][q]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dT[(size_t)b * k * k + (i0 + u) * k + j0 + q] = scale * v[u][q];
+  } else {
+    for (int e = tid; e < k * k; e += 256) {
+      const int i = e / k, j = e % k;
+      float v = 0.f;
+      for (int l = 0; l < k; ++l) v = fmaf(a[i * ks + l], t[l * ks + j], v);
+      dT[(size_t)b * k * k + e] = scale * v;
+    }
   }
 }
 
@@ -569,8 +708,8 @@ int launch_pw_bwd_weight(const float* dy, const float* y, int act, const float* 
   const int width = O * K + O;
   const int groups = rows_per_group ? M / rows_per_group : 1;
   const int per = rows_per_group ? rows_per_group / PWW_ROWS : nslab;
-  hipLaunchKernelGGL(k_pw_reduce, dim3((width + 255) / 256, groups), dim3(256), 0, s, slabs, per,
-                     width, O * K, dw, db);
+  hipLaunchKernelGGL(k_pw_reduce, dim3((width + 63) / 64, groups), dim3(64 * PWR_W), 0, s, slabs,
+                     per, width, O * K, dw, db);
   PC_HIP_CHECK_LAUNCH("k_pw_reduce");
   return PCADV_OK;
 }
@@ -591,7 +730,7 @@ int launch_convmax_bwd(const float* dg, const int32_t* gidx, const float* gmax, 
 int launch_tnet_reg(const float* T, int B, int k, float* norms, float* reg,
                     const float* gscale, float* dT, hipStream_t s) {
   PC_REQUIRE(B > 0 && k > 0 && k <= 64, "tnet_reg: unsupported B=%d k=%d", B, k);
-  const size_t lds = 2 * (size_t)k * k * sizeof(float);
+  const size_t lds = 2 * (size_t)k * (k + 1) * sizeof(float);
   if (!dT) {
     hipLaunchKernelGGL(k_tnet_reg, dim3(B), dim3(256), lds, s, T, B, k, norms, nullptr, nullptr);
     PC_HIP_CHECK_LAUNCH("k_tnet_reg");

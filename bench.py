@@ -464,15 +464,21 @@ def bench_cls_ft(args):
     (utils/trainer.py:254-268: CE + 0.001 x the regulariser, Adam): the fused
     cls step does not cover the feature transform, so this is the autograd body
     over the layer-by-layer kernels (point-wise conv1..conv3, the STNkd(64) and
-    transform kernels, conv4 + max, the head), fp32 throughout, with
-    torch.optim.Adam(capturable=True); one HIP graph per resident batch when
-    capture works, else eager."""
+    transform kernels, conv4 + max, the head), fp32 throughout, with torch's
+    Adam (fused where available, else capturable); one HIP graph per resident
+    batch when capture works, else eager."""
     import adversarial_learning_on_pointclouds_amd as pc
     from adversarial_learning_on_pointclouds_amd.pointnet import feature_transform_regularizer
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = pc.PointNetCls(k=40, feature_transform=True).to(dev).train()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), capturable=True)
+    try:  # one fused multi-tensor kernel per step where this torch build has it
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), fused=True,
+                               capturable=True)
+        adam = "torch.optim.Adam(fused=True, capturable=True)"
+    except (RuntimeError, ValueError):
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), capturable=True)
+        adam = "torch.optim.Adam(capturable=True)"
     pool = []
     for k in range(POOL):
         rng = np.random.default_rng(3000 + k)
@@ -529,7 +535,7 @@ def bench_cls_ft(args):
         "config": {"workload": "run_training_pointnet_cls with PointNetCls(k=40, "
                                "feature_transform=True): CE + 0.001 regulariser, Adam, autograd "
                                "over the pcadv ops", "global_batch": B, "points": N,
-                   "parallelism": "dp1", "hip_graph": bool(graphs)},
+                   "parallelism": "dp1", "hip_graph": bool(graphs), "optimizer": adam},
         "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),
     }
