@@ -211,10 +211,18 @@ class _GraphedIteration:
         g = self.graphs.get(semi)
         if g is None:
             st = self.step
-            state = [t for t in (getattr(st, n, None) for n in
-                                 ("g_param", "g_m", "g_v", "d_param", "d_m", "d_v", "step_count"))
-                     if t is not None] + [self.counters, self.ring.count, self.ring.ring]
-            saved = [t.clone() for t in state]
+            if hasattr(st, "graph_state"):  # a step that names its own state
+                pre = st.graph_state()
+            else:
+                pre = [t for t in (getattr(st, n, None) for n in
+                                   ("g_param", "g_m", "g_v", "d_param", "d_m", "d_v", "step_count"))
+                       if t is not None]
+            state = pre + [self.counters, self.ring.count, self.ring.ring]
+            # detached copies: a clone of a parameter would hold its
+            # AccumulateGrad node (created here, on this stream) alive into the
+            # capture, where it then runs on the wrong stream
+            with torch.no_grad():
+                saved = [t.detach().clone() for t in state]
             cur = torch.cuda.current_stream()
             side = torch.cuda.Stream(device=st.device)
             side.wait_stream(cur)
@@ -225,14 +233,69 @@ class _GraphedIteration:
             with torch.cuda.graph(g):
                 self._body(semi)
             torch.cuda.synchronize()
-            for dst, src in zip(state, saved):
-                dst.copy_(src)
+            with torch.no_grad():
+                for dst, src in zip(state, saved):
+                    dst.copy_(src)
+            if hasattr(st, "after_capture"):
+                st.after_capture()
             self.graphs[semi] = g
         return g
 
     def replay(self, semi=False):
         self._graph(semi).replay()
         return self.step.losses
+
+
+class _AutogradClsStep:
+    """run_training_pointnet_cls's autograd body (utils/trainer.py:254-268:
+    CE (x lambda_cls) + lambda_regu x the feature-transform regulariser,
+    backward, optimizer.step()) as a step _GraphedIteration can capture: the
+    layer-by-layer kernels, torch's autograd and the user's optimizer, which
+    must be capturable (e.g. torch.optim.Adam(capturable=True)).  losses =
+    [loss_cls, loss_regu] in a static device tensor."""
+
+    def __init__(self, model, optimizer, cls_loss, lambda_cls, lambda_regu, B, N, device):
+        self.model, self.opt, self.cls_loss = model, optimizer, cls_loss
+        self.lambda_cls, self.lambda_regu = lambda_cls, lambda_regu
+        self.B, self.N, self.device = B, N, torch.device(device)
+        self.losses = torch.zeros(2, device=self.device)
+        self._fresh = []
+
+    def __call__(self, pts, lab):
+        self.opt.zero_grad(set_to_none=False)
+        pred, _, high_feat = self.model(pts)
+        l = self.cls_loss(pred, lab)
+        l_regu = feature_transform_regularizer(high_feat)
+        loss = self.lambda_cls * l + self.lambda_regu * l_regu
+        loss.backward()
+        self.opt.step()
+        self.losses[0].copy_(l.detach())
+        self.losses[1].copy_(l_regu.detach())
+
+    def graph_state(self):
+        """Parameters, existing gradients and optimizer state: restored after
+        the capture's warm-up.  Optimizer state the warm-up creates (a first
+        step) is reset to its fresh zeros by after_capture()."""
+        params = [p for g in self.opt.param_groups for p in g["params"]]
+        self._fresh = [p for p in params if p not in self.opt.state or not self.opt.state[p]]
+        ts = list(params) + [p.grad for p in params if p.grad is not None]
+        for p in params:
+            if p in self.opt.state:
+                ts += [v for v in self.opt.state[p].values() if torch.is_tensor(v)]
+        return ts
+
+    def after_capture(self):
+        for p in self._fresh:
+            for v in self.opt.state.get(p, {}).values():
+                if torch.is_tensor(v):
+                    v.zero_()
+
+    @staticmethod
+    def graphable(model, optimizer, args, loader):
+        return (isinstance(model, PointNetCls) and model.feature_transform
+                and bool(getattr(args, "use_graph", True)) and _device_loaders(loader)
+                and str(args.device).split(":")[0] == "cuda"
+                and all(g.get("capturable", False) for g in optimizer.param_groups))
 
 
 def _device_loaders(*loaders):
@@ -487,12 +550,15 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
                and trainloader_gt.B <= MAX_FUSED_B)
     gi = None
     log_every = max(1, int(getattr(args, "log_every", 1)))
+    # feature_transform=True with a capturable optimizer over a DeviceCloudLoader:
+    # each full batch's gather + autograd body replayed as one HIP graph
+    ft_graphed = (not fused) and _AutogradClsStep.graphable(model, optimizer, args, trainloader_gt)
 
     def emit(i_iter, vals, regu):
         train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
-            i_iter, args.total_iterations, vals[0], regu))
+            i_iter, args.total_iterations, vals[0], vals[1] if regu is None else regu))
 
-    log = _LossRing(emit, 1, args.device)
+    log = _LossRing(emit, 2 if ft_graphed else 1, args.device)
 
     def fused_step(B, N):
         nonlocal step
@@ -508,10 +574,13 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
             model.train()
         l_regu = None
         losses = None
-        if graphed:
+        if graphed or ft_graphed:
             if gi is None:
-                gi = _GraphedIteration(fused_step(trainloader_gt.B, trainloader_gt.npts),
-                                       (trainloader_gt,), log)
+                gstep = (fused_step(trainloader_gt.B, trainloader_gt.npts) if graphed else
+                         _AutogradClsStep(model, optimizer, cls_loss, args.lambda_cls,
+                                          args.lambda_regu, trainloader_gt.B,
+                                          trainloader_gt.npts, args.device))
+                gi = _GraphedIteration(gstep, (trainloader_gt,), log)
             bt = gi.next_batches()
             if bt[0][1] == trainloader_gt.B:
                 losses = gi.replay()
@@ -526,7 +595,7 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
                 losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls)
                 log.write(losses)
         if losses is not None:
-            log.record(i_iter, 0.0, log=i_iter % log_every == 0)
+            log.record(i_iter, None if ft_graphed else 0.0, log=i_iter % log_every == 0)
         else:
             if step is not None:
                 step.sync_optimizer_state()

@@ -339,3 +339,45 @@ def test_graphed_trainer_equals_eager(tmp_path, drop_last):
     # log_every = 3 logs iterations 0, 3, 6 and trains identically
     pc_, lc, _ = _adv_run(tmp_path, True, 9, drop_last, log_every=3)
     assert torch.equal(pa, pc_) and lc == [la[0], la[3], la[6]]
+
+
+def _ft_cls_run(tmp_path, use_graph, iters):
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from oracle import pointnet_np as onp
+    rng = np.random.default_rng(41)
+    ds = D.ModelNetDatasetGT.__new__(D.ModelNetDatasetGT)  # in-memory clouds of 256 points
+    ds.sample_list, ds.npoints, ds.data_augmentation = None, 256, True
+    ds.select_data = rng.uniform(-1, 1, (8, 256, 3)).astype(np.float32)
+    ds.select_labels = rng.integers(0, 40, 8).astype(np.int32)
+    gt = D.DeviceCloudLoader(ds, 4, seed=11, drop_last=True)
+    G = onp.make_params(onp.cls_ft_spec(40), seed=42)
+    model = pc.PointNetCls(k=40, feature_transform=True)
+    model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    model.dropout.p = 0.0  # the graph's and the eager loop's torch.rand draws differ
+    model.cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), capturable=True)
+    args = argparse.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=10 ** 9, exp_dir=str(tmp_path), lambda_cls=1.0,
+                              lambda_regu=0.001, use_graph=use_graph, log_every=1, batch_size=4,
+                              tensorboard=False)
+    log = _Log()
+    te = [(torch.from_numpy(ds.select_data[:4].copy()), torch.from_numpy(ds.select_labels[:4].astype(np.int64)))]
+    trainer.run_training_pointnet_cls(gt, enumerate(gt), te, model, torch.nn.CrossEntropyLoss(),
+                                      opt, log, log, None, args)
+    params = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+    return params, [l for l in log.lines if l.startswith("iter")], opt
+
+
+def test_graphed_feature_transform_cls_loop_equals_eager(tmp_path):
+    """run_training_pointnet_cls with feature_transform=True (not covered by the
+    fused cls step) and a capturable Adam over a DeviceCloudLoader: each
+    iteration's gather + autograd body replayed as one HIP graph equals the
+    eager loop bitwise (parameters, loss / regulariser lines, Adam steps),
+    across epoch wrap-arounds (8 clouds, batches of 4)."""
+    pa, la, opt_a = _ft_cls_run(tmp_path, True, 5)
+    pb, lb, _ = _ft_cls_run(tmp_path, False, 5)
+    assert torch.equal(pa, pb)
+    assert la == lb and len(la) == 5
+    assert all(float(st["step"]) == 5 for st in opt_a.state.values())
