@@ -20,7 +20,7 @@ namespace pcadv {
 
 constexpr int PW_ROWS = 64;   // points per workgroup tile
 constexpr int PW_T = 256;     // 4 waves
-constexpr int PWW_ROWS = 256; // rows per weight-gradient slab
+constexpr int PWW_ROWS = 128; // rows per weight-gradient slab (M / 128 workgroups: 256 at 32 clouds x 1024 points)
 constexpr int PWW_SUB = 32;   // rows staged in LDS at a time by the weight kernel
 
 // A weight operand: conv layout W[o][k], or "kmajor" T[k][o] (the bmm's
