@@ -52,6 +52,24 @@ k_pw_fwd(const float* __restrict__ x, int M, WView wv, const float* __restrict__
   const int r0 = blockIdx.x * PW_ROWS, o0 = blockIdx.y * 128;
   const int O = wv.O;
   const float* w = wv.base(r0);
+  // wave -> (32-column tile, 32-row tiles): four column tiles over both row
+  // tiles, or with O - o0 = 64 two column tiles x one row tile each, so every
+  // wave works
+  const bool narrow = O - o0 <= 64;
+  const int oc = o0 + 32 * (narrow ? (wave & 1) : wave);
+  const int rt0 = narrow ? (wave >> 1) : 0, nrt = narrow ? 1 : 2;
+  const bool on = oc < O;  // O % 32 == 0: whole waves
+  const int r = lane & 31, h = lane >> 5;
+  // the weight fragments issued first: in flight during the x staging
+  f32x4 bf[K / 8];
+  if (on) {
+#pragma unroll
+    for (int g = 0; g < K / 8; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, oc + r, 8 * g + 4 * h + j);
+  }
+  const int col = oc + r;
+  const float bias = (b && on) ? b[col] : 0.f;
   for (int e = tid; e < PW_ROWS * K / 4; e += PW_T) {
     const int row = e / (K / 4), c4 = e % (K / 4);
     const f32x4 v = r0 + row < M ? *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + row) * K + 4 * c4)
@@ -59,24 +77,15 @@ k_pw_fwd(const float* __restrict__ x, int M, WView wv, const float* __restrict__
     *reinterpret_cast<f32x4*>(xs + row * SK + 4 * c4) = v;
   }
   __syncthreads();
-  const int oc = o0 + 32 * wave;
-  if (oc >= O) return;  // O % 32 == 0: whole waves leave
-  const int r = lane & 31, h = lane >> 5;
-  f32x4 bf[K / 8];
+  if (!on) return;
+  for (int t = rt0; t < rt0 + nrt; ++t) {
+    f32x16 acc = {};
+    acc = mfma_rows_x_wt<K>(xs + 32 * t * SK, SK, bf, acc, lane);
 #pragma unroll
-  for (int g = 0; g < K / 8; ++g)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, oc + r, 8 * g + 4 * h + j);
-  f32x16 acc0 = {}, acc1 = {};
-  acc0 = mfma_rows_x_wt<K>(xs, SK, bf, acc0, lane);
-  acc1 = mfma_rows_x_wt<K>(xs + 32 * SK, SK, bf, acc1, lane);
-  const int col = oc + r;
-  const float bias = b ? b[col] : 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int ra = r0 + acc_row(i, lane), rb = ra + 32;
-    if (ra < M) y[(size_t)ra * O + col] = act_fwd(acc0[i] + bias, ACT);
-    if (rb < M) y[(size_t)rb * O + col] = act_fwd(acc1[i] + bias, ACT);
+    for (int i = 0; i < 16; ++i) {
+      const int ra = r0 + 32 * t + acc_row(i, lane);
+      if (ra < M) y[(size_t)ra * O + col] = act_fwd(acc[i] + bias, ACT);
+    }
   }
 }
 
