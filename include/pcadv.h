@@ -138,7 +138,10 @@ int pcadv_feat_bwd(const float* dgmax, const int32_t* gidx, const float* pts, in
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Generic 1x1-conv (K=128 -> O, O % 128 == 0) + max over points.
- * relu_before_max=1 for the T-Nets (pointnet.py:30-31,63-64). */
+ * relu_before_max=1 for the T-Nets (pointnet.py:30-31,63-64).  O = 1024 runs
+ * on the fused forward's k_conv4_max (split-product screen, every winner
+ * re-evaluated in exact f32; with the ReLU, an all-negative channel's argmax
+ * is point 0, as torch.max over the zeros gives); other O on an f32 kernel. */
 int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, const float* b,
                        int O, int relu_before_max, float* gmax, int32_t* gidx,
                        hipStream_t stream);
