@@ -2347,13 +2347,31 @@ k_cmx_dw(const float* __restrict__ g, const float* __restrict__ gmax,
   const int o = blockIdx.x, k = blockIdx.y * 512 + threadIdx.x * 4;  // 4 columns per thread
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float sb = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float gv = gmax[(size_t)c * O + o] > 0.f ? g[(size_t)c * O + o] : 0.f;
-    sb += gv;
-    if (gv == 0.f || k >= K) continue;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(x + (size_t)(c * Npts + gidx[(size_t)c * O + o]) * ldx + k);
+  // CB clouds' gradients, argmax rows and x rows in flight at once (a cloud at
+  // a time was two dependent round trips each), summed in cloud order; a zero
+  // g' is skipped as before (0 * an infinite x would be a NaN)
+  constexpr int CB = 8;
+  const int kk = min(k, K - 4);
+  for (int c0 = 0; c0 < C; c0 += CB) {
+    float gv[CB];
+    int gi[CB];
+    f32x4 v[CB];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = fmaf(gv, v[t], acc[t]);
+    for (int u = 0; u < CB; ++u) {
+      const size_t co = (size_t)min(c0 + u, C - 1) * O + o;
+      gv[u] = (c0 + u < C && gmax[co] > 0.f) ? g[co] : 0.f;
+      gi[u] = gidx[co];
+    }
+#pragma unroll
+    for (int u = 0; u < CB; ++u)
+      v[u] = *reinterpret_cast<const f32x4*>(x + (size_t)(min(c0 + u, C - 1) * Npts + gi[u]) * ldx + kk);
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      sb += gv[u];
+      if (gv[u] == 0.f || k >= K) continue;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = fmaf(gv[u], v[u][t], acc[t]);
+    }
   }
   if (k < K) *reinterpret_cast<f32x4*>(dw + (size_t)o * K + k) = acc;
   if (blockIdx.y == 0 && threadIdx.x == 0 && db) db[o] = sb;
