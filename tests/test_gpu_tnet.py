@@ -284,3 +284,31 @@ def test_pointnetfeat_dense_vs_oracle(ft):
         _, am = onp.conv_max_fwd(x3, onp._w(G, "feat.conv4.weight"), G["feat.conv4.bias"])
         dw4 = np.einsum("bo,bok->ok", dg, x3[np.arange(B)[:, None], am])
         assert rel_err(_np(f.conv4.weight.grad)[:, :, 0], dw4) < 1e-4
+
+
+@pytest.mark.parametrize("relu,N", [(False, 333), (True, 333), (True, 64)])
+def test_conv_max_1024_ragged_vs_oracle(relu, N):
+    """The 1024-channel conv + max (feature conv4 / T-Net conv3) runs on
+    k_conv4_max: ragged point counts, the ReLU-before-max fix-up (an
+    all-negative channel pools 0 at point 0, as torch.max over the zeros), and
+    the argmax the backward routes through."""
+    rng = np.random.default_rng(90 + N + relu)
+    C, K, O = 3, 128, 1024
+    x = np.maximum(rng.normal(size=(C, N, K)), 0).astype(np.float32)
+    w = (rng.normal(size=(O, K)) / np.sqrt(K)).astype(np.float32)
+    b = (rng.normal(size=O) - (2.0 if relu else 0.0)).astype(np.float32)  # many all-negative channels
+    gmax, gidx = ops.conv_max_fwd(_t(x), _t(w), _t(b), relu)
+    gr, am = onp.conv_max_fwd(x, w, b, relu_before_max=relu)
+    assert rel_err(_np(gmax), gr) < 1e-5
+    gi = _np(gidx)
+    # exact argmax except near-ties of the f32 values (different summation orders)
+    y = np.einsum("cnk,ok->con", x.astype(np.float64), w.astype(np.float64)) + b[None, :, None]
+    if relu:
+        y = np.maximum(y, 0)
+    top = y.max(2)
+    picked = np.take_along_axis(y, gi[:, :, None].astype(np.int64), 2)[:, :, 0]
+    ok = (gi == am) | (np.abs(top - picked) <= 1e-5 * (np.abs(top) + 1e-6))
+    assert ok.all()
+    if relu:
+        zero = gr == 0
+        assert zero.any() and (gi[zero] == 0).all() and (_np(gmax)[zero] == 0).all()
