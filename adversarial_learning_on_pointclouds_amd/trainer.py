@@ -21,7 +21,8 @@ import torch.nn.functional as F
 from .discriminator import DeepConvDiscNet
 from .metric import batch_get_iou, object_names
 from .pointnet import PointNetCls, feature_transform_regularizer
-from .step import AdvTrainStep
+from ._lib import D_LAYOUT
+from .step import AdvTrainStep, _views
 from .utils import make_D_label
 
 
@@ -304,7 +305,7 @@ def _device_loaders(*loaders):
                for l in loaders)
 
 
-def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pools, args):
+def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args):
     if not (isinstance(model, PointNetCls) and isinstance(model_D, DeepConvDiscNet)):
         return False
     if model.feature_transform or model.fc3.out_features != 40:
@@ -325,7 +326,31 @@ def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pools, 
     if type(cls_loss) is not torch.nn.CrossEntropyLoss or cls_loss.weight is not None \
             or cls_loss.reduction != "mean" or cls_loss.label_smoothing != 0.0:
         return False
-    return all(p.pool_size == 0 for p in pools)
+    return True
+
+
+def _pooled_d_grads(step, model_D, gan_loss, pool_gt, pool_nogt, B, device):
+    """The discriminator half of utils/trainer.py:521-556 with image pools: after
+    a fused step ran without its Adam update (G's gradients, and its
+    classification / adversarial / semi loss lines, do not see the pools), D's
+    gradient is replaced by the reference's two backward passes on
+    pool.query(log_softmax(logits)) of this iteration's GT and no-GT logits,
+    accumulated into the flat gradient buffer the fused Adam reads (the D
+    parameters' .grad are views of it), and the D loss lines follow."""
+    logp = F.log_softmax(step.logits[:2 * B], dim=1)
+    step.d_grad.zero_()
+    d_out = model_D(pool_gt.query(logp[:B].detach()))
+    loss_d1 = gan_loss(d_out, make_D_label(d_out, 1, device, random=True)) * 0.5
+    loss_d1.backward()
+    d_out = model_D(pool_nogt.query(logp[B:].detach()))
+    loss_d2 = gan_loss(d_out, make_D_label(d_out, 0, device, random=True)) * 0.5
+    loss_d2.backward()
+    views = _views(step.d_grad, model_D, D_LAYOUT)
+    for name, p in model_D.named_parameters():
+        if p.grad is None or p.grad.data_ptr() != views[name].data_ptr():
+            raise RuntimeError(f"D parameter {name}: .grad is no longer a view of the fused "
+                               "step's gradient buffer")
+    step.losses[2:4].copy_(torch.stack((loss_d1.detach(), loss_d2.detach())))
 
 
 def _save(model, model_D, args, tag):
@@ -356,13 +381,16 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
     gt_label, nogt_label = 1, 0
     max_test_accu = float("-inf")
     max_train_epoch = 0
-    fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss,
-                     (history_pool_gt, history_pool_nogt), args)
+    fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args)
     if semi_loss is not None:
         fused = fused and _semi_fusable(semi_loss)
+    # ImagePool(pool_size > 0): the fused step's G half stands, D's gradient is
+    # recomputed on the pools' outputs (_pooled_d_grads); the pools draw from
+    # the host's `random`, so these iterations are not graphed
+    pooled = fused and (history_pool_gt.pool_size > 0 or history_pool_nogt.pool_size > 0)
     step = None
     log_every = max(1, int(getattr(args, "log_every", 1)))
-    graphed = (fused and bool(getattr(args, "use_graph", True))
+    graphed = (fused and not pooled and bool(getattr(args, "use_graph", True))
                and _device_loaders(trainloader_gt, trainloader_nogt)
                and trainloader_gt.B == trainloader_nogt.B
                and trainloader_gt.npts == trainloader_nogt.npts
@@ -426,7 +454,14 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             cls = cls.long().to(args.device).contiguous()
             pts_nogt = pts_nogt.float().to(args.device).contiguous()
             if fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B:
-                losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls, pts_nogt, semi=semi_on)
+                st = fused_step(pts.shape[0], pts.shape[1])
+                if pooled:
+                    losses = st(pts, cls, pts_nogt, apply_adam=False, semi=semi_on)
+                    _pooled_d_grads(st, model_D, gan_loss, history_pool_gt, history_pool_nogt,
+                                    pts.shape[0], args.device)
+                    st.adam()
+                else:
+                    losses = st(pts, cls, pts_nogt, semi=semi_on)
                 log.write(losses)
 
         if losses is not None:

@@ -287,6 +287,72 @@ def test_run_training_step_rebuild_keeps_adam_step_count():
         assert float(st["step"]) == iters
 
 
+def _pool_run(pool_size, fused, iters=6):
+    """run_training over host batches of 4 + 4 clouds with ImagePool(pool_size)
+    on both D inputs; fused=False forces the reference's autograd body (a
+    CrossEntropyLoss subclass is off the fused step's configuration)."""
+    import argparse
+    import random
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from oracle import pointnet_np as onp
+
+    class _CE(torch.nn.CrossEntropyLoss):
+        pass
+
+    N = 256
+    G = onp.make_params(onp.cls_spec(40), seed=41)
+    Dp = onp.make_params(onp.disc_spec(40, 1), seed=42, init="xavier")
+    rng = np.random.default_rng(43)
+    gt = [(torch.from_numpy(rng.uniform(-1, 1, (4, N, 3)).astype(np.float32)),
+           torch.from_numpy(rng.integers(0, 40, 4))) for _ in range(3)]
+    ng = [torch.from_numpy(rng.uniform(-1, 1, (4, N, 3)).astype(np.float32)) for _ in range(3)]
+    model, model_D = pc.PointNetCls(k=40), pc.DeepConvDiscNet(40, 1)
+    model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    model_D.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in Dp.items()})
+    model.dropout.p = 0.0  # no dropout draws: both bodies draw only D's soft labels from torch
+    model.cuda()
+    model_D.cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    args = argparse.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=10 ** 9, exp_dir="/tmp", tensorboard=False,
+                              lambda_cls=1.0, lambda_adv=0.01, batch_size=4)
+    pools = ImagePool(pool_size), ImagePool(pool_size)
+    random.seed(5)
+    torch.manual_seed(6)
+    log = _Log()
+    trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), [gt[0]], model, model_D,
+                         torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss() if fused else _CE(),
+                         opt, opt_D, *pools, log, log, None, args)
+    lines = [l for l in log.lines if l.startswith("iter")]
+    loss_d = np.array([float(l.split("loss_D = ")[1]) for l in lines])
+    flat = lambda m: torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().double()
+    return flat(model), flat(model_D), loss_d, pools
+
+
+def test_image_pool_on_fused_step_matches_autograd_body():
+    """ImagePool(pool_size > 0) in run_training (utils/trainer.py:521-556): the
+    fused step supplies G's half, D's gradient is recomputed on the pools'
+    outputs.  Against the reference's autograd body with the same pool draws
+    (Python `random`) and soft labels (torch), the G and D trajectories agree
+    to 1e-2 of their movement (Adam steps of ~lr per parameter, fused vs autograd
+    rounding), the D loss lines to 1e-4; without the pools D's trajectory is
+    visibly different (the pools did swap samples)."""
+    g_f, d_f, l_f, pools = _pool_run(3, True)
+    g_e, d_e, l_e, _ = _pool_run(3, False)
+    g_0, d_0, _, _ = _pool_run(0, True)
+    assert pools[0].num_imgs == 3 and pools[1].num_imgs == 3
+    G0, D0 = _pool_run(3, True, iters=0)[:2]
+    for a, b, a0 in ((g_f, g_e, G0), (d_f, d_e, D0)):
+        e = (a - b).norm() / (b - a0).norm()
+        assert e < 1e-2, e
+    np.testing.assert_allclose(l_f, l_e, rtol=1e-4, atol=1e-6)
+    e0 = (d_0 - d_e).norm() / (d_e - D0).norm()
+    assert e0 > 0.05, e0
+
+
 def _adv_run(tmp_path, use_graph, iters, drop_last, log_every=1):
     import argparse
     import adversarial_learning_on_pointclouds_amd as pc
