@@ -7,7 +7,14 @@ and returned; once full, each sample is, with probability 1/2, swapped with a
 uniformly chosen stored one (the stored one is returned), or else returned as
 is.  The draws use Python's `random` module in the same order as the
 reference (one random() per sample, one randrange(pool_size) per swap), so a
-seeded run makes the same choices."""
+seeded run makes the same choices.
+
+The draws do not depend on the data, so a query first plans on the host where
+each returned row comes from (a batch row, or a slot's content before the
+query; a slot swapped twice in one batch hands the second sample the first
+one's row) and which batch row each touched slot ends up holding, then applies
+the plan as one gather and one scatter on the device instead of a copy per
+sample."""
 from __future__ import annotations
 
 import random
@@ -40,13 +47,24 @@ class ImagePool:
                              f"on {batch.device}, but the history holds "
                              f"{tuple(self._bank.shape[1:])} {self._bank.dtype} on "
                              f"{self._bank.device}")
-        out = batch.clone()
-        for i in range(batch.shape[0]):
+        n = batch.shape[0]
+        src = list(range(n))  # out[i] = rows[src[i]] of cat(batch, bank as it was)
+        holds = {}            # slot -> batch row it holds after this query
+        for i in range(n):
             if self._filled < self.pool_size:
-                self._bank[self._filled].copy_(batch[i])
+                holds[self._filled] = i
                 self._filled += 1
             elif random.random() > 0.5:
                 slot = random.randrange(self.pool_size)
-                out[i].copy_(self._bank[slot])
-                self._bank[slot].copy_(batch[i])
+                src[i] = holds.get(slot, n + slot)
+                holds[slot] = i
+        if all(src[i] == i for i in range(n)):
+            out = batch.clone()
+        else:
+            idx = torch.tensor(src, dtype=torch.int64, device=batch.device)
+            out = torch.cat((batch, self._bank)).index_select(0, idx)
+        if holds:
+            plan = torch.tensor([list(holds), list(holds.values())], dtype=torch.int64,
+                                device=batch.device)
+            self._bank.index_copy_(0, plan[0], batch.index_select(0, plan[1]))
         return out.requires_grad_(True)

@@ -113,6 +113,42 @@ def test_image_pool_history_vs_reference_g10():
     assert pool.num_imgs == 3
 
 
+def test_image_pool_plan_equals_per_sample_history():
+    """ImagePool's planned query (one gather, one scatter) returns and keeps
+    what the per-sample loop of utils/image_pool.py:26-55 would, including a
+    slot swapped more than once within one batch (pool of 2, batches of 7)."""
+    import random
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+
+    def loop_query(bank, filled, size, batch):  # the reference's order of draws
+        out = batch.clone()
+        for i in range(batch.shape[0]):
+            if filled < size:
+                bank[filled] = batch[i]
+                filled += 1
+            elif random.random() > 0.5:
+                slot = random.randrange(size)
+                out[i] = bank[slot].clone()
+                bank[slot] = batch[i]
+        return out, filled
+
+    gen = torch.Generator().manual_seed(3)
+    for size, bsz in ((2, 7), (5, 3), (4, 4)):
+        pool = ImagePool(size)
+        bank, filled = torch.zeros(size, 6), 0
+        random.seed(size * 10 + bsz)
+        state = random.getstate()
+        for _ in range(8):
+            batch = torch.randn(bsz, 6, generator=gen)
+            random.setstate(state)
+            want, filled = loop_query(bank, filled, size, batch)
+            random.setstate(state)
+            got = pool.query(batch)
+            state = random.getstate()
+            assert torch.equal(got.detach(), want) and got.requires_grad
+            assert torch.equal(pool._bank[:filled], bank[:filled]) and pool.num_imgs == filled
+
+
 def test_init_weights_xavier_vs_reference_g10():
     """init_weights(DeepConvDiscNet, 'xavier') on a seeded torch RNG gives the
     reference's weights (utils/model_utils.py:27-58, fixture g10)."""
