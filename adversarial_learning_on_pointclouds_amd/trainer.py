@@ -247,16 +247,64 @@ class _GraphedIteration:
         return self.step.losses
 
 
-class _AutogradClsStep:
+class _AutogradStep:
+    """A trainer body run through torch's autograd and the user's optimizers, as
+    a step _GraphedIteration can capture (the layer-by-layer kernels; every
+    optimizer must be capturable, e.g. torch.optim.Adam(capturable=True)).
+    Subclasses set self.opts and self.losses (a static device tensor)."""
+
+    def _params(self):
+        return [p for o in self.opts for g in o.param_groups for p in g["params"]]
+
+    def graph_state(self):
+        """Parameters, existing gradients and optimizer state: restored after
+        the capture's warm-up.  Optimizer state the warm-up creates (a first
+        step) is reset to its fresh zeros by after_capture()."""
+        params = self._params()
+        self._fresh = [p for o in self.opts for g in o.param_groups for p in g["params"]
+                       if p not in o.state or not o.state[p]]
+        ts = list(params) + [p.grad for p in params if p.grad is not None]
+        for o in self.opts:
+            for p in (q for g in o.param_groups for q in g["params"]):
+                if p in o.state:
+                    ts += [v for v in o.state[p].values() if torch.is_tensor(v)]
+        return ts
+
+    def after_capture(self):
+        for o in self.opts:
+            for p in self._fresh:
+                for v in o.state.get(p, {}).values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+        # the graph reads and writes these gradient buffers: kept alive here and
+        # rebound after an eager iteration (rebind_grads)
+        self._grads = [(p, p.grad) for p in self._params() if p.grad is not None]
+
+    def rebind_grads(self):
+        """After an eager iteration (zero_grad(set_to_none=True) gave p.grad new
+        tensors): its gradients into the captured buffers, rebound as p.grad."""
+        for p, g in getattr(self, "_grads", ()):
+            if p.grad is None:
+                g.zero_()
+            elif p.grad is not g:
+                g.copy_(p.grad)
+            p.grad = g
+
+    @staticmethod
+    def _capturable(args, optimizers):
+        return (bool(getattr(args, "use_graph", True))
+                and str(args.device).split(":")[0] == "cuda"
+                and all(g.get("capturable", False) for o in optimizers for g in o.param_groups))
+
+
+class _AutogradClsStep(_AutogradStep):
     """run_training_pointnet_cls's autograd body (utils/trainer.py:254-268:
     CE (x lambda_cls) + lambda_regu x the feature-transform regulariser,
-    backward, optimizer.step()) as a step _GraphedIteration can capture: the
-    layer-by-layer kernels, torch's autograd and the user's optimizer, which
-    must be capturable (e.g. torch.optim.Adam(capturable=True)).  losses =
-    [loss_cls, loss_regu] in a static device tensor."""
+    backward, optimizer.step()).  losses = [loss_cls, loss_regu]."""
 
     def __init__(self, model, optimizer, cls_loss, lambda_cls, lambda_regu, B, N, device):
         self.model, self.opt, self.cls_loss = model, optimizer, cls_loss
+        self.opts = (optimizer,)
         self.lambda_cls, self.lambda_regu = lambda_cls, lambda_regu
         self.B, self.N, self.device = B, N, torch.device(device)
         self.losses = torch.zeros(2, device=self.device)
@@ -273,30 +321,80 @@ class _AutogradClsStep:
         self.losses[0].copy_(l.detach())
         self.losses[1].copy_(l_regu.detach())
 
-    def graph_state(self):
-        """Parameters, existing gradients and optimizer state: restored after
-        the capture's warm-up.  Optimizer state the warm-up creates (a first
-        step) is reset to its fresh zeros by after_capture()."""
-        params = [p for g in self.opt.param_groups for p in g["params"]]
-        self._fresh = [p for p in params if p not in self.opt.state or not self.opt.state[p]]
-        ts = list(params) + [p.grad for p in params if p.grad is not None]
-        for p in params:
-            if p in self.opt.state:
-                ts += [v for v in self.opt.state[p].values() if torch.is_tensor(v)]
-        return ts
-
-    def after_capture(self):
-        for p in self._fresh:
-            for v in self.opt.state.get(p, {}).values():
-                if torch.is_tensor(v):
-                    v.zero_()
-
     @staticmethod
     def graphable(model, optimizer, args, loader):
         return (isinstance(model, PointNetCls) and model.feature_transform
-                and bool(getattr(args, "use_graph", True)) and _device_loaders(loader)
-                and str(args.device).split(":")[0] == "cuda"
-                and all(g.get("capturable", False) for g in optimizer.param_groups))
+                and _device_loaders(loader) and _AutogradStep._capturable(args, (optimizer,)))
+
+
+def _adv_body(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pts, cls, pts_nogt,
+              pool_gt, pool_nogt, args, semi_loss=None, semi_on=False, set_to_none=True):
+    """run_training's iteration body through autograd (utils/trainer.py:449-559,
+    the semi term :716-743): returns the device losses (loss_cls, loss_adv,
+    loss_D_gt, loss_D_nogt) and the semi loss as a float (0.0 when off)."""
+    gt_label, nogt_label = 1, 0
+    optimizer.zero_grad(set_to_none=set_to_none)
+    optimizer_D.zero_grad(set_to_none=set_to_none)
+    for param in model_D.parameters():
+        param.requires_grad = False
+    pred, global_gt, high_feat = model(pts)
+    l = cls_loss(pred, cls)
+    pred_gt_softmax = F.log_softmax(pred, dim=1)
+    pred_nogt, global_nogt, high_feat = model(pts_nogt)
+    pred_nogt_softmax = F.log_softmax(pred_nogt, dim=1)
+    D_out = model_D(pred_nogt_softmax)
+    loss_adv = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=False))
+    loss = args.lambda_cls * l + args.lambda_adv * loss_adv
+    loss_semi_value = 0.0
+    if semi_on:  # utils/trainer.py:716-743
+        ignore = (D_out <= args.semi_TH).squeeze(1)
+        semi_gt = torch.argmax(pred_nogt.detach(), dim=1)
+        semi_gt[ignore] = 255
+        if int(ignore.sum().item()) < ignore.numel():
+            l_semi = semi_loss(pred_nogt, semi_gt)
+            loss_semi_value = l_semi.item()
+            loss = loss + args.lambda_semi * l_semi
+    loss.backward()
+    for param in model_D.parameters():
+        param.requires_grad = True
+    D_out = model_D(pool_gt.query(pred_gt_softmax.detach()))
+    loss_D1 = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=True)) * 0.5
+    loss_D1.backward()
+    D_out = model_D(pool_nogt.query(pred_nogt_softmax.detach()))
+    loss_D2 = gan_loss(D_out, make_D_label(D_out, nogt_label, args.device, random=True)) * 0.5
+    loss_D2.backward()
+    optimizer.step()
+    optimizer_D.step()
+    return l, loss_adv, loss_D1, loss_D2, loss_semi_value
+
+
+class _AutogradAdvStep(_AutogradStep):
+    """run_training's autograd body (_adv_body, without the semi term, whose
+    ignore test reads the host) for configurations off the fused step (e.g. a
+    feature-transform generator, other optimizers or losses).  losses =
+    [loss_cls, loss_adv, loss_D_gt, loss_D_nogt, 0, 0]."""
+
+    def __init__(self, model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pools, args,
+                 B, N):
+        self.parts = (model, model_D, optimizer, optimizer_D, gan_loss, cls_loss)
+        self.pools, self.args = pools, args
+        self.opts = (optimizer, optimizer_D)
+        self.B, self.N, self.device = B, N, torch.device(args.device)
+        self.losses = torch.zeros(6, device=self.device)
+        self._fresh = []
+
+    def __call__(self, pts, lab, pts_nogt, semi=False):
+        if semi:
+            raise ValueError("_AutogradAdvStep: the semi term is not capturable")
+        out = _adv_body(*self.parts, pts, lab, pts_nogt, *self.pools, self.args,
+                        set_to_none=False)
+        self.losses[:4].copy_(torch.stack([t.detach() for t in out[:4]]))
+
+    @staticmethod
+    def graphable(optimizer, optimizer_D, pools, args, loaders):
+        return (all(p.pool_size == 0 for p in pools) and _device_loaders(*loaders)
+                and loaders[0].B == loaders[1].B and loaders[0].npts == loaders[1].npts
+                and _AutogradStep._capturable(args, (optimizer, optimizer_D)))
 
 
 def _device_loaders(*loaders):
@@ -377,8 +475,10 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
     and the step replay as one HIP graph per iteration (args.use_graph, default
     on), fed by the loaders' own epoch orders.  Loss lines are read
     asynchronously (no host sync per iteration), every args.log_every
-    iterations (default 1, as the reference logs every iteration)."""
-    gt_label, nogt_label = 1, 0
+    iterations (default 1, as the reference logs every iteration).  Off the
+    fused step (e.g. a feature-transform generator) the body runs through
+    autograd (_adv_body); with capturable optimizers and DeviceCloudLoaders its
+    full, semi-free iterations are HIP graphs too (_AutogradAdvStep)."""
     max_test_accu = float("-inf")
     max_train_epoch = 0
     fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args)
@@ -395,6 +495,11 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                and trainloader_gt.B == trainloader_nogt.B
                and trainloader_gt.npts == trainloader_nogt.npts
                and trainloader_gt.B <= MAX_FUSED_B)
+    # off the fused step, with capturable optimizers over DeviceCloudLoaders:
+    # each full, semi-free iteration's gathers + autograd body as one HIP graph
+    ag_graphed = (not fused) and _AutogradAdvStep.graphable(
+        optimizer, optimizer_D, (history_pool_gt, history_pool_nogt), args,
+        (trainloader_gt, trainloader_nogt))
     gi = None
     tb = getattr(args, "tensorboard", False) and writer is not None
 
@@ -411,7 +516,7 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                 writer.add_scalar("Loss/train_semi", vals[4] if semi_on else 0.0, i_iter)
 
     log = _LossRing(emit, 6, args.device)
-    if graphed:  # the loaders' own epoch orders replace the (fresh) iterators given
+    if graphed or ag_graphed:  # the loaders' own epoch orders replace the (fresh) iterators given
         B0, N0 = trainloader_gt.B, trainloader_gt.npts
 
     def fused_step(B, N):
@@ -437,11 +542,14 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             model_D.train()
         semi_on = semi_loss is not None and args.semi_start > 0 and i_iter > args.semi_start
         losses = None
-        if graphed:
+        if graphed or ag_graphed:
             if gi is None:
-                gi = _GraphedIteration(fused_step(B0, N0), (trainloader_gt, trainloader_nogt), log)
+                gstep = (fused_step(B0, N0) if graphed else _AutogradAdvStep(
+                    model, model_D, optimizer, optimizer_D, gan_loss, cls_loss,
+                    (history_pool_gt, history_pool_nogt), args, B0, N0))
+                gi = _GraphedIteration(gstep, (trainloader_gt, trainloader_nogt), log)
             bt = gi.next_batches()
-            if all(size == B0 for _, size in bt):
+            if all(size == B0 for _, size in bt) and not (ag_graphed and semi_on):
                 losses = gi.replay(semi=semi_on)
             else:  # a ragged last batch: gathered eagerly from the same epoch order
                 (pts, cls), pts_nogt = gi.eager_batches(bt)
@@ -467,46 +575,20 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
         if losses is not None:
             log.record(i_iter, semi_on, log=i_iter % log_every == 0)
         else:
-            # unequal GT / no-GT batches (a loader's ragged last batch): the
-            # reference's body through autograd over the same kernels; the torch
-            # optimizers continue from the fused step's Adam state (moments are
-            # shared views, the step count is synced in and out)
+            # off the fused step, or unequal GT / no-GT batches (a loader's
+            # ragged last batch): the reference's body through autograd over the
+            # same kernels; the torch optimizers continue from the fused step's
+            # Adam state (moments are shared views, the step count is synced in
+            # and out) or from the graphed body's (its gradient buffers rebound)
             if step is not None:
                 step.sync_optimizer_state()
-            optimizer.zero_grad()
-            optimizer_D.zero_grad()
-            for param in model_D.parameters():
-                param.requires_grad = False
-            pred, global_gt, high_feat = model(pts)
-            l = cls_loss(pred, cls)
-            pred_gt_softmax = F.log_softmax(pred, dim=1)
-            pred_nogt, global_nogt, high_feat = model(pts_nogt)
-            pred_nogt_softmax = F.log_softmax(pred_nogt, dim=1)
-            D_out = model_D(pred_nogt_softmax)
-            loss_adv = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=False))
-            loss = args.lambda_cls * l + args.lambda_adv * loss_adv
-            loss_semi_value = 0.0
-            if semi_on:  # utils/trainer.py:716-743
-                ignore = (D_out <= args.semi_TH).squeeze(1)
-                semi_gt = torch.argmax(pred_nogt.detach(), dim=1)
-                semi_gt[ignore] = 255
-                if int(ignore.sum().item()) < ignore.numel():
-                    l_semi = semi_loss(pred_nogt, semi_gt)
-                    loss_semi_value = l_semi.item()
-                    loss = loss + args.lambda_semi * l_semi
-            loss.backward()
-            for param in model_D.parameters():
-                param.requires_grad = True
-            D_out = model_D(history_pool_gt.query(pred_gt_softmax.detach()))
-            loss_D1 = gan_loss(D_out, make_D_label(D_out, gt_label, args.device, random=True)) * 0.5
-            loss_D1.backward()
-            D_out = model_D(history_pool_nogt.query(pred_nogt_softmax.detach()))
-            loss_D2 = gan_loss(D_out, make_D_label(D_out, nogt_label, args.device, random=True)) * 0.5
-            loss_D2.backward()
-            optimizer.step()
-            optimizer_D.step()
+            l, loss_adv, loss_D1, loss_D2, loss_semi_value = _adv_body(
+                model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, pts, cls, pts_nogt,
+                history_pool_gt, history_pool_nogt, args, semi_loss, semi_on)
             if step is not None:
                 step.after_torch_step()
+            if gi is not None and ag_graphed:
+                gi.step.rebind_grads()
             if i_iter % log_every == 0:
                 log.emit_now(i_iter, [l.item(), loss_adv.item(), loss_D1.item(), loss_D2.item(),
                                       loss_semi_value], semi_on)
@@ -645,6 +727,8 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
             optimizer.step()
             if step is not None:
                 step.after_torch_step()
+            if gi is not None and ft_graphed:
+                gi.step.rebind_grads()
             if i_iter % log_every == 0:
                 log.emit_now(i_iter, [l.item()], 0.0 if l_regu is None else l_regu.item())
         if i_iter % args.iter_save_epoch == 0:

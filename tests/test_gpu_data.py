@@ -407,7 +407,7 @@ def test_graphed_trainer_equals_eager(tmp_path, drop_last):
     assert torch.equal(pa, pc_) and lc == [la[0], la[3], la[6]]
 
 
-def _ft_cls_run(tmp_path, use_graph, iters):
+def _ft_cls_run(tmp_path, use_graph, iters, drop_last=True):
     import argparse
     import adversarial_learning_on_pointclouds_amd as pc
     from adversarial_learning_on_pointclouds_amd import trainer
@@ -417,7 +417,7 @@ def _ft_cls_run(tmp_path, use_graph, iters):
     ds.sample_list, ds.npoints, ds.data_augmentation = None, 256, True
     ds.select_data = rng.uniform(-1, 1, (8, 256, 3)).astype(np.float32)
     ds.select_labels = rng.integers(0, 40, 8).astype(np.int32)
-    gt = D.DeviceCloudLoader(ds, 4, seed=11, drop_last=True)
+    gt = D.DeviceCloudLoader(ds, 4 if drop_last else 3, seed=11, drop_last=drop_last)
     G = onp.make_params(onp.cls_ft_spec(40), seed=42)
     model = pc.PointNetCls(k=40, feature_transform=True)
     model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
@@ -436,14 +436,90 @@ def _ft_cls_run(tmp_path, use_graph, iters):
     return params, [l for l in log.lines if l.startswith("iter")], opt
 
 
-def test_graphed_feature_transform_cls_loop_equals_eager(tmp_path):
+def _ft_adv_run(tmp_path, monkeypatch, use_graph, iters, drop_last):
+    """run_training with a feature-transform generator (off the fused step) and
+    capturable Adams over in-memory DeviceCloudLoaders (8 GT / 10 no-GT clouds
+    of 256 points, batches of 4).  Dropout p = 0 and constant D labels (0.9 /
+    0.1 for the soft ones) leave no random draw in the body, so the graphed and
+    the eager loop can be compared bitwise."""
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from oracle import pointnet_np as onp
+    monkeypatch.setattr(trainer, "make_D_label", lambda inp, value, device, random=False:
+                        torch.full(inp.shape, (0.9 if value else 0.1) if random else float(value),
+                                   device=device))
+    rng = np.random.default_rng(51)
+
+    def mem(cls, n):
+        ds = cls.__new__(cls)
+        ds.sample_list, ds.npoints, ds.data_augmentation = None, 256, True
+        ds.select_data = rng.uniform(-1, 1, (n, 256, 3)).astype(np.float32)
+        if cls is D.ModelNetDatasetGT:
+            ds.select_labels = rng.integers(0, 40, n).astype(np.int32)
+        return ds
+    gds, nds = mem(D.ModelNetDatasetGT, 8), mem(D.ModelNetDataset_noGT, 10)
+    gt = D.DeviceCloudLoader(gds, 4, seed=11, drop_last=drop_last)
+    ng = D.DeviceCloudLoader(nds, 4, seed=12, drop_last=drop_last)
+    G = onp.make_params(onp.cls_ft_spec(40), seed=52)
+    Dp = onp.make_params(onp.disc_spec(40, 1), seed=53, init="xavier")
+    model, model_D = pc.PointNetCls(k=40, feature_transform=True), pc.DeepConvDiscNet(40, 1)
+    model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    model_D.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in Dp.items()})
+    model.dropout.p = 0.0
+    model.cuda()
+    model_D.cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), capturable=True)
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999), capturable=True)
+    args = argparse.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=10 ** 9, exp_dir=str(tmp_path), tensorboard=False,
+                              lambda_cls=1.0, lambda_adv=0.01, batch_size=4, use_graph=use_graph)
+    te = [(torch.from_numpy(gds.select_data[:4].copy()),
+           torch.from_numpy(gds.select_labels[:4].astype(np.int64)))]
+    replays = []
+    replay = trainer._GraphedIteration.replay
+    monkeypatch.setattr(trainer._GraphedIteration, "replay",
+                        lambda self, semi=False: (replays.append(semi), replay(self, semi))[1])
+    log = _Log()
+    trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), te, model, model_D,
+                         torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(), opt, opt_D,
+                         ImagePool(0), ImagePool(0), log, log, None, args)
+    params = torch.cat([p.detach().reshape(-1) for p in list(model.parameters()) +
+                        list(model_D.parameters())]).cpu()
+    grads = torch.cat([p.grad.reshape(-1) for p in list(model.parameters()) +
+                       list(model_D.parameters())]).cpu()
+    return params, grads, [l for l in log.lines if l.startswith("iter")], (opt, opt_D), len(replays)
+
+
+@pytest.mark.parametrize("drop_last", [True, False])
+def test_graphed_feature_transform_adv_loop_equals_eager(tmp_path, monkeypatch, drop_last):
+    """run_training off the fused step (PointNetCls(feature_transform=True)) with
+    capturable Adams: each full iteration's gathers + autograd body replayed as
+    one HIP graph equals the eager loop bitwise (parameters, the last
+    iteration's gradients, loss lines, Adam steps), across epoch wrap-arounds
+    and, with drop_last=False, ragged batches run eagerly between replays (the
+    graph's gradient buffers rebound after them)."""
+    pa, ga, la, opts, na = _ft_adv_run(tmp_path, monkeypatch, True, 7, drop_last)
+    pb, gb, lb, _, nb = _ft_adv_run(tmp_path, monkeypatch, False, 7, drop_last)
+    # no-GT batches 4, 4 (+ a ragged 2 without drop_last) per epoch
+    assert nb == 0 and na == (7 if drop_last else 5)
+    assert torch.equal(pa, pb) and torch.equal(ga, gb)
+    assert la == lb and len(la) == 7
+    for o in opts:
+        assert all(float(st["step"]) == 7 for st in o.state.values())
+
+
+@pytest.mark.parametrize("drop_last", [True, False])
+def test_graphed_feature_transform_cls_loop_equals_eager(tmp_path, drop_last):
     """run_training_pointnet_cls with feature_transform=True (not covered by the
     fused cls step) and a capturable Adam over a DeviceCloudLoader: each
     iteration's gather + autograd body replayed as one HIP graph equals the
     eager loop bitwise (parameters, loss / regulariser lines, Adam steps),
-    across epoch wrap-arounds (8 clouds, batches of 4)."""
-    pa, la, opt_a = _ft_cls_run(tmp_path, True, 5)
-    pb, lb, _ = _ft_cls_run(tmp_path, False, 5)
+    across epoch wrap-arounds (8 clouds, batches of 4; or of 3 with the ragged
+    2-cloud batch run eagerly between replays)."""
+    pa, la, opt_a = _ft_cls_run(tmp_path, True, 5, drop_last)
+    pb, lb, _ = _ft_cls_run(tmp_path, False, 5, drop_last)
     assert torch.equal(pa, pb)
     assert la == lb and len(la) == 5
     assert all(float(st["step"]) == 5 for st in opt_a.state.values())
