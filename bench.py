@@ -67,12 +67,13 @@ def parse():
     ap.add_argument("--points", type=int, default=1024,
                     help="points per cloud of the adv step (1024: the metric's config; 2048: "
                          "BASELINE configs[4]'s per-rank shape)")
-    ap.add_argument("--config", choices=["adv", "seg", "cls", "cls_ft", "trainer"], default="adv",
+    ap.add_argument("--config", choices=["adv", "seg", "cls", "cls_ft", "adv_ft", "trainer"], default="adv",
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
                          "supervised PointNetCls step of configs[1]; cls_ft: the same with "
                          "feature_transform=True (STNkd(64) + regulariser, layer-by-layer "
-                         "kernels through autograd); trainer: run_training end to end over "
+                         "kernels through autograd); adv_ft: the adversarial iteration with "
+                         "that generator (autograd body, graphed); trainer: run_training end to end over "
                          "DeviceCloudLoaders")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="feature-forward precision (default: bf16 for --config cls, the dtype "
@@ -544,6 +545,92 @@ def bench_cls_ft(args):
     print(json.dumps(_with_runtime(out)), flush=True)
 
 
+def bench_adv_ft(args):
+    """run_training's iteration with PointNetCls(k=40, feature_transform=True) as
+    the generator (off the fused adversarial step): trainer._adv_body, i.e. the
+    reference's body (utils/trainer.py:449-559) through autograd over the
+    layer-by-layer kernels, both torch Adams capturable (fused where available),
+    one HIP graph per resident batch pair as run_training replays it
+    (_AutogradAdvStep); eager when capture fails."""
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = pc.PointNetCls(k=40, feature_transform=True).to(dev).train()
+    model_D = pc.DeepConvDiscNet(40, 1).to(dev).train()
+    opts = []
+    for m in (model, model_D):
+        try:
+            opts.append(torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999), fused=True,
+                                         capturable=True))
+            adam = "torch.optim.Adam(fused=True, capturable=True)"
+        except (RuntimeError, ValueError):
+            opts.append(torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999),
+                                         capturable=True))
+            adam = "torch.optim.Adam(capturable=True)"
+    targs = argparse.Namespace(device=str(dev), lambda_cls=1.0, lambda_adv=0.001)
+    step = trainer._AutogradAdvStep(model, model_D, opts[0], opts[1],
+                                    torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(),
+                                    (ImagePool(0), ImagePool(0)), targs, B, N)
+    pool = []
+    for k in range(POOL):
+        rng = np.random.default_rng(3500 + k)
+        pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
+                     torch.from_numpy(rng.integers(0, 40, B)).to(dev),
+                     torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev)))
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # autograd / optimizer state created outside any capture
+        for k in range(3):
+            step(*pool[k % POOL])
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graphs, why = [], None
+    if not args.no_graph:
+        try:
+            for k in range(POOL):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    step(*pool[k])
+                graphs.append(g)
+        except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
+            graphs, why = [], f"{type(e).__name__}: {e}"[:200]
+            torch.cuda.synchronize()
+
+    def one(k):
+        if graphs:
+            graphs[k % POOL].replay()
+        else:
+            step(*pool[k % POOL])
+    for k in range(args.warmup):
+        one(k)
+    regions = timed_regions(one, args.steps, args.repeats)
+    dt = float(np.median(regions))
+    vals = [float(v) for v in step.losses[:4].cpu()]
+    out = {
+        "metric": "point-clouds/sec (adversarial train step, generator with feature_transform=True), "
+                  "B=32+32 N=1024 ModelNet40, 1 GPU",
+        "value": round(2 * B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32 (layer-by-layer kernels: exact-f32 MFMA point-wise layers, split-product "
+                 "conv4 + exact max re-evaluation)",
+        "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
+        "config": {"workload": "run_training iteration with PointNetCls(k=40, feature_transform="
+                               "True) + DeepConvDiscNet(40, 1): autograd body over the pcadv ops, "
+                               "two Adams", "global_batch": 2 * B, "points": N,
+                   "parallelism": "dp1", "hip_graph": bool(graphs), "optimizer": adam},
+        "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
+        "losses_last_step": [round(v, 5) for v in vals],
+        "finite": bool(np.all(np.isfinite(vals))),
+    }
+    if why:
+        out["graph_capture_error"] = why
+    print(json.dumps(_with_runtime(out)), flush=True)
+
+
 def _synthetic_modelnet(n_gt, n_nogt, seed=5000):
     """ModelNetDatasetGT / _noGT objects over in-memory synthetic clouds (the
     HDF5 files are not in the image): same attributes as the file-backed ones,
@@ -798,6 +885,8 @@ def main():
         return bench_cls(args)
     if args.config == "cls_ft":
         return bench_cls_ft(args)
+    if args.config == "adv_ft":
+        return bench_adv_ft(args)
     if args.config == "trainer":
         return bench_trainer(args)
     if _backend() != "nccl":  # rehearsal: ranks may share a GPU
