@@ -488,7 +488,7 @@ def bench_cls_ft(args):
     losses = torch.zeros(POOL, device=dev)
 
     def body(pts, lab, k):
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad()  # captured: backward's gradients become p.grad, no accumulate adds
         logits, _, trans = model(pts)
         loss = torch.nn.functional.cross_entropy(logits, lab) + 0.001 * feature_transform_regularizer(trans)
         loss.backward()
@@ -505,11 +505,13 @@ def bench_cls_ft(args):
     graphs, why = [], None
     if not args.no_graph:
         try:
+            kept = []  # each graph's gradient buffers (the next capture drops p.grad)
             for k in range(POOL):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     body(*pool[k], k)
                 graphs.append(g)
+                kept.append([p.grad for p in model.parameters()])
         except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
             graphs, why = [], f"{type(e).__name__}: {e}"[:200]
             torch.cuda.synchronize()
@@ -590,11 +592,13 @@ def bench_adv_ft(args):
     graphs, why = [], None
     if not args.no_graph:
         try:
+            kept = []  # each graph's gradient buffers (the next capture drops p.grad)
             for k in range(POOL):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     step(*pool[k])
                 graphs.append(g)
+                kept.append([p.grad for p in list(model.parameters()) + list(model_D.parameters())])
         except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
             graphs, why = [], f"{type(e).__name__}: {e}"[:200]
             torch.cuda.synchronize()
