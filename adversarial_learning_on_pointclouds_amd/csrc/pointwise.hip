@@ -37,17 +37,8 @@ struct WView {
   __device__ float get(const float* b, int o, int k) const {
     return kmajor ? b[(size_t)k * O + o] : b[(size_t)o * K + k];
   }
-  // (o, k..k+3) / (o..o+3, k): one 16-B load where the four are contiguous
-  // (conv layout / kmajor) and the matrix is 16-B aligned (O, K, k, o are
-  // multiples of 4 here), else four 4-B loads; the same values either way
-  __device__ f32x4 get4_k(const float* b, int o, int k) const {
-    if (!kmajor && aligned16()) return *reinterpret_cast<const f32x4*>(b + (size_t)o * K + k);
-    return f32x4{get(b, o, k), get(b, o, k + 1), get(b, o, k + 2), get(b, o, k + 3)};
-  }
-  __device__ f32x4 get4_o(const float* b, int o, int k) const {
-    if (kmajor && aligned16()) return *reinterpret_cast<const f32x4*>(b + (size_t)k * O + o);
-    return f32x4{get(b, o, k), get(b, o + 1, k), get(b, o + 2, k), get(b, o + 3, k)};
-  }
+  // 16-B loads of four contiguous weights need the matrix 16-B aligned (O, K
+  // and the fragment offsets are multiples of 4 here)
   __device__ bool aligned16() const { return (reinterpret_cast<uintptr_t>(w) & 15) == 0; }
 };
 
@@ -75,8 +66,16 @@ k_pw_fwd(const float* __restrict__ x, int M, WView wv, const float* __restrict__
   // the weight fragments issued first: in flight during the x staging
   f32x4 bf[K / 8];
   if (on) {
+    if (!wv.kmajor && wv.aligned16()) {  // (o, k..k+3) contiguous: one 16-B load each
 #pragma unroll
-    for (int g = 0; g < K / 8; ++g) bf[g] = wv.get4_k(w, oc + r, 8 * g + 4 * h);
+      for (int g = 0; g < K / 8; ++g)
+        bf[g] = *reinterpret_cast<const f32x4*>(w + (size_t)(oc + r) * K + 8 * g + 4 * h);
+    } else {
+#pragma unroll
+      for (int g = 0; g < K / 8; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, oc + r, 8 * g + 4 * h + j);
+    }
   }
   const int col = oc + r;
   const float bias = (b && on) ? b[col] : 0.f;
@@ -159,8 +158,16 @@ k_pw_bwd_data(const float* __restrict__ dy, const float* __restrict__ yv, int M,
   const int r = lane & 31, h = lane >> 5;
   // B[o][k] = w[o][k]: lane (r, h) holds column kc + r at o = 8g + 4h + j
   f32x4 bf[R / 8];
+  if (wv.kmajor && wv.aligned16()) {  // (o..o+3, k) contiguous: one 16-B load each
 #pragma unroll
-  for (int g = 0; g < R / 8; ++g) bf[g] = wv.get4_o(w, 8 * g + 4 * h, kc + r);
+    for (int g = 0; g < R / 8; ++g)
+      bf[g] = *reinterpret_cast<const f32x4*>(w + (size_t)(kc + r) * wv.O + 8 * g + 4 * h);
+  } else {
+#pragma unroll
+    for (int g = 0; g < R / 8; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, 8 * g + 4 * h + j, kc + r);
+  }
   f32x16 acc0 = {}, acc1 = {};
   acc0 = mfma_rows_x_wt<R>(zs, SR, bf, acc0, lane);
   acc1 = mfma_rows_x_wt<R>(zs + 32 * SR, SR, bf, acc1, lane);
