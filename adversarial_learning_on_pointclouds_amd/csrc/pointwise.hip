@@ -153,8 +153,13 @@ k_pw_bwd_data(const float* __restrict__ dy, const float* __restrict__ yv, int M,
     *reinterpret_cast<f32x4*>(zs + row * SR + 4 * c4) = v;
   }
   __syncthreads();
-  const int kc = k0 + 32 * wave;
+  // wave -> (32-column tile, 32-row tiles): four column tiles over both row
+  // tiles, or with K - k0 = 64 two column tiles x one row tile each (as in
+  // k_pw_fwd), so every wave works; the same MFMA chain per output either way
+  const bool narrow = K - k0 <= 64;
+  const int kc = k0 + 32 * (narrow ? (wave & 1) : wave);
   if (kc >= K) return;  // K % 32 == 0
+  const int rt0 = narrow ? (wave >> 1) : 0;
   const int r = lane & 31, h = lane >> 5;
   // B[o][k] = w[o][k]: lane (r, h) holds column kc + r at o = 8g + 4h + j
   f32x4 bf[R / 8];
@@ -168,10 +173,23 @@ k_pw_bwd_data(const float* __restrict__ dy, const float* __restrict__ yv, int M,
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[g][j] = wv.get(w, 8 * g + 4 * h + j, kc + r);
   }
+  const int col = kc + r;
+  if (narrow) {
+    f32x16 acc = {};
+    acc = mfma_rows_x_wt<R>(zs + 32 * rt0 * SR, SR, bf, acc, lane);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ra = r0 + 32 * rt0 + acc_row(i, lane);
+      if (ra < M) {
+        float* p = dx + (size_t)ra * K + col;
+        *p = accumulate ? *p + acc[i] : acc[i];
+      }
+    }
+    return;
+  }
   f32x16 acc0 = {}, acc1 = {};
   acc0 = mfma_rows_x_wt<R>(zs, SR, bf, acc0, lane);
   acc1 = mfma_rows_x_wt<R>(zs + 32 * SR, SR, bf, acc1, lane);
-  const int col = kc + r;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int ra = r0 + acc_row(i, lane), rb = ra + 32;
