@@ -261,28 +261,46 @@ k_pw_bwd_weight(const float* __restrict__ dy, const float* __restrict__ yv,
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
   float dbacc = 0.f;
-  for (int sub = 0; sub < PWW_ROWS / PWW_SUB; ++sub) {
-    const int r0 = rbase + sub * PWW_SUB;
-    for (int e = tid; e < PWW_SUB * O / 4; e += PW_T) {
-      const int row = e / (O / 4), c4 = e % (O / 4);
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r0 + row < M) {
-        v = *reinterpret_cast<const f32x4*>(dy + (size_t)(r0 + row) * O + 4 * c4);
-        if (ACT != ACT_NONE) {
-          const f32x4 yy = *reinterpret_cast<const f32x4*>(yv + (size_t)(r0 + row) * O + 4 * c4);
+  // the next 32 rows' operands are loaded into registers while the current
+  // rows' MFMAs run (e = tid + PW_T * i covers each staging loop exactly)
+  static_assert((PWW_SUB * O / 4) % PW_T == 0 && (PWW_SUB * K / 4) % PW_T == 0, "staging split");
+  constexpr int NZ = PWW_SUB * O / 4 / PW_T, NX = PWW_SUB * K / 4 / PW_T;
+  f32x4 pz[NZ], py[NZ], px[NX];
+  auto load = [&](int r0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= act_bwd(yy[j], ACT);
-        }
+    for (int i = 0; i < NZ; ++i) {
+      const int e = tid + PW_T * i, row = e / (O / 4), c4 = e % (O / 4);
+      const bool in = r0 + row < M;
+      const size_t off = (size_t)(in ? r0 + row : 0) * O + 4 * c4;
+      pz[i] = in ? *reinterpret_cast<const f32x4*>(dy + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (ACT != ACT_NONE) py[i] = *reinterpret_cast<const f32x4*>(yv + off);
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int e = tid + PW_T * i, row = e / (K / 4), c4 = e % (K / 4);
+      px[i] = r0 + row < M ? *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + row) * K + 4 * c4)
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load(rbase);
+  for (int sub = 0; sub < PWW_ROWS / PWW_SUB; ++sub) {
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      const int e = tid + PW_T * i, row = e / (O / 4), c4 = e % (O / 4);
+      f32x4 v = pz[i];
+      if (ACT != ACT_NONE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= act_bwd(py[i][j], ACT);
       }
       *reinterpret_cast<f32x4*>(zs + row * SO + 4 * c4) = v;
     }
-    for (int e = tid; e < PWW_SUB * K / 4; e += PW_T) {
-      const int row = e / (K / 4), c4 = e % (K / 4);
-      const f32x4 v = r0 + row < M ? *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + row) * K + 4 * c4)
-                                   : f32x4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(xs + row * SX + 4 * c4) = v;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int e = tid + PW_T * i, row = e / (K / 4), c4 = e % (K / 4);
+      *reinterpret_cast<f32x4*>(xs + row * SX + 4 * c4) = px[i];
     }
     __syncthreads();
+    if (sub + 1 < PWW_ROWS / PWW_SUB) load(rbase + (sub + 1) * PWW_SUB);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int tile = wave + 4 * t;
