@@ -88,6 +88,7 @@ class AdvArgs(ctypes.Structure):
         ("semi", _i), ("lambda_semi", _f), ("semi_th", _f),
         ("part", _i),
         ("precision", _i),
+        ("rng_rank", _i), ("rng_world", _i),
     ]
 
 
@@ -140,9 +141,9 @@ SIGNATURES = {
     "pcadv_h5_read": (_i, [ctypes.c_char_p, ctypes.c_char_p, _i, _i64, _vp, _sz]),
     "pcadv_gather_clouds": (_i, [_vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, ctypes.c_double,
                                  ctypes.c_double, _vp, _u64, _vp,
-                                 _vp, _vp, _vp, _vp]),
+                                 _vp, _vp, _vp, _i64, _vp]),
     "pcadv_gather_clouds_at": (_i, [_vp, _i64, _i, _i, _vp, _vp, _i, _vp, _i, _vp, ctypes.c_double,
-                                    ctypes.c_double, _u64, _vp, _vp, _vp, _vp, _vp]),
+                                    ctypes.c_double, _u64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "pcadv_iter_epilogue": (_i, [_vp, _i, _vp, _i, _vp, _i, _vp, _vp]),
     "pcadv_row_ce_workspace_bytes": (_sz, [_i]),
     "pcadv_row_ce": (_i, [_vp, _i64, _vp, _i, _i, _f, _vp, _vp, _vp, _sz, _vp]),

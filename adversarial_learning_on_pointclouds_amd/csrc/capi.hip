@@ -37,7 +37,8 @@ int launch_conv4_max(const float*, int, int, const float*, const float*, float*,
                      hipStream_t, int);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t,
-                      int add_identity_k = 0, float* mask_out = nullptr);
+                      int add_identity_k = 0, float* mask_out = nullptr, int row_split = 0,
+                      int row_off_lo = 0, int row_off_hi = 0);
 int launch_pw_fwd(const float*, int, int, const float*, const float*, int, int, int, int, float*,
                   hipStream_t);
 int launch_pw_bwd_data(const float*, const float*, int, int, int, const float*, int, int, int,
@@ -62,7 +63,7 @@ int launch_disc_tail(const float*, int, const float*, const float*, const float*
                      const float*, const float*, const float*, const float*, const int32_t*,
                      uint64_t, float, float*, float*, float*, float*, hipStream_t,
                      const int32_t* gidx, int C, int N, int* sortrec, float* z4g, float* z5g,
-                     float* a4g);
+                     float* a4g, int lab_off = 0);
 size_t feat_sort_record_ints(int C, int N);
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
@@ -100,7 +101,8 @@ int launch_cmx_bwd(const float*, const float*, const int32_t*, const float*, lon
                    int, int, const float*, float*, float*, float*, long long, int, hipStream_t);
 int launch_gather_clouds(const float*, int64_t, int, int, const int64_t*, int, const int64_t*, int,
                          const int64_t*, double, double, const double*, uint64_t, const int32_t*,
-                         float*, int64_t*, int64_t*, hipStream_t, const int32_t* cursor = nullptr);
+                         float*, int64_t*, int64_t*, hipStream_t, const int32_t* cursor = nullptr,
+                         int64_t rng_row0 = 0);
 int launch_iter_epilogue(int32_t*, int, const float*, int, float*, int, int32_t*, hipStream_t);
 size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
@@ -267,6 +269,10 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
     mask = w.mask;
   }
   const int32_t* rstep = mask ? nullptr : st;
+  // device draws keyed by the global batch's rows (rank r of W holds GT rows
+  // [rB, rB + B) and no-GT rows [rB, rB + B) of the W B-cloud global batches)
+  const int W = a->rng_world > 1 ? a->rng_world : 1, rr = W > 1 ? a->rng_rank : 0;
+  PC_REQUIRE(rr >= 0 && rr < W, "adv_step: rng_rank %d not in [0, %d)", a->rng_rank, W);
 
   // ---- generator forward, both loaders in one launch (:468, :490) ----------
   PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
@@ -279,7 +285,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   // fc2 + dropout: a device-drawn mask is stored for the backward
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
                            PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s, 0,
-                           mask ? nullptr : w.mask));
+                           mask ? nullptr : w.mask, B, rr * B, (W - 1) * B + rr * B));
   const float* bmask = w.mask;  // explicit masks were staged there too
   // ---- fc3 -> log_softmax / CE (GT rows) -> D conv1 for the GT and noGT rows;
   //      D input rows are [lsm_gt; lsm_nogt; lsm_nogt] (:472, :492, :499) -----
@@ -295,7 +301,7 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   PC_TRY(launch_disc_tail(w.d3, B, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, D + PCADV_D_CONV5_W,
                           D + PCADV_D_CONV5_B, D + PCADV_D_FC_W, D + PCADV_D_FC_B, a->soft_gt,
                           a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
-                          w.dout, s, w.gidx, C, N, w.sortrec, w.z4, w.z5, w.a4));
+                          w.dout, s, w.gidx, C, N, w.sortrec, w.z4, w.z5, w.a4, rr * B));
   // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
   //      input grads of all rows (rows [2B,3B) feed the generator, D frozen).
   //      Every data gradient is stored as the layer below's dz (its activation
@@ -391,6 +397,8 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
     mask = w.mask;
   }
   const int32_t* rstep = mask ? nullptr : st;
+  const int W = a->rng_world > 1 ? a->rng_world : 1, rr = W > 1 ? a->rng_rank : 0;
+  PC_REQUIRE(rr >= 0 && rr < W, "cls_step: rng_rank %d not in [0, %d)", a->rng_rank, W);
   PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
@@ -400,7 +408,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
                            PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s, 0,
-                           mask ? nullptr : w.mask));
+                           mask ? nullptr : w.mask, B, rr * B, rr * B));
   // fc3, CrossEntropyLoss (train_classification.py:199), lambda_cls * dCE/dlogits
   // and fc3's input gradient, stored as fc2's dz (k_cls_head)
   PC_TRY(launch_cls_head(w.h2, w.mask, a->drop_p, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, a->labels,
@@ -443,7 +451,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 5; }
+int pcadv_abi_version(void) { return 6; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -679,20 +687,22 @@ int pcadv_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
                         const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
                         const int64_t* src_seg, double sigma, double clip, const double* noise,
                         uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
-                        int64_t* out_seg, hipStream_t stream) {
+                        int64_t* out_seg, int64_t rng_row0, hipStream_t stream) {
   return launch_gather_clouds(src, n_src, npts, src_npts, idx, B, src_lab, lab_width, src_seg,
-                              sigma, clip, noise, seed, step, out, out_lab, out_seg, stream);
+                              sigma, clip, noise, seed, step, out, out_lab, out_seg, stream,
+                              nullptr, rng_row0);
 }
 
 int pcadv_gather_clouds_at(const float* src, int64_t n_src, int npts, int src_npts,
                            const int64_t* order, const int32_t* cursor, int B,
                            const int64_t* src_lab, int lab_width, const int64_t* src_seg,
                            double sigma, double clip, uint64_t seed, const int32_t* step,
-                           float* out, int64_t* out_lab, int64_t* out_seg, hipStream_t stream) {
+                           float* out, int64_t* out_lab, int64_t* out_seg, int64_t rng_row0,
+                           hipStream_t stream) {
   PC_REQUIRE(cursor, "gather_clouds_at: cursor required");
   return launch_gather_clouds(src, n_src, npts, src_npts, order, B, src_lab, lab_width, src_seg,
                               sigma, clip, nullptr, seed, step, out, out_lab, out_seg, stream,
-                              cursor);
+                              cursor, rng_row0);
 }
 
 int pcadv_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl,

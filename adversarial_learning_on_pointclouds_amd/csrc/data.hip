@@ -22,7 +22,7 @@ k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_
                 int lab_width, const int64_t* __restrict__ src_seg, double sigma_d, double clip_d,
                 const double* __restrict__ noise, uint64_t seed, const int32_t* __restrict__ step,
                 float* __restrict__ out, int64_t* __restrict__ out_lab,
-                int64_t* __restrict__ out_seg, const int32_t* __restrict__ cursor) {
+                int64_t* __restrict__ out_seg, const int32_t* __restrict__ cursor, int64_t rng_row0) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)B * npts) return;
   const int b = (int)(t / npts), p = (int)(t % npts);
@@ -45,7 +45,10 @@ k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_
       o[2] = (float)((double)x2 + fmin(fmax(sg * z[2], -cl), cl));
     } else {
       const uint32_t st = step ? (uint32_t)*step : 0u;
-      const u32x4 r = philox((uint32_t)t, st, RNG_JITTER, (uint32_t)(t >> 32), (uint32_t)seed,
+      // keyed by the point's row in the global batch (a data-parallel rank's
+      // batch rows start at rng_row0), so W ranks jitter as one loader would
+      const int64_t tg = t + rng_row0 * npts;
+      const u32x4 r = philox((uint32_t)tg, st, RNG_JITTER, (uint32_t)(tg >> 32), (uint32_t)seed,
                              (uint32_t)(seed >> 32));
       // Box-Muller on two uniform pairs -> 4 normals (3 used)
       const float u1 = fmaxf(u01(r.x), 1e-7f), u2 = u01(r.y);
@@ -70,7 +73,7 @@ int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts
                          const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
                          const int64_t* src_seg, double sigma, double clip, const double* noise,
                          uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
-                         int64_t* out_seg, hipStream_t s, const int32_t* cursor) {
+                         int64_t* out_seg, hipStream_t s, const int32_t* cursor, int64_t rng_row0) {
   PC_REQUIRE(src && idx && out && n_src > 0 && B > 0 && npts > 0 && src_npts >= npts,
              "gather_clouds: bad arguments (n_src=%lld B=%d npts=%d src_npts=%d)",
              (long long)n_src, B, npts, src_npts);
@@ -80,7 +83,7 @@ int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts
   const int64_t n = (int64_t)B * npts;
   hipLaunchKernelGGL(k_gather_clouds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src,
                      n_src, npts, src_npts, idx, B, src_lab, lab_width, src_seg, sigma, clip, noise,
-                     seed, step, out, out_lab, out_seg, cursor);
+                     seed, step, out, out_lab, out_seg, cursor, rng_row0);
   PC_HIP_CHECK_LAUNCH("k_gather_clouds");
   return PCADV_OK;
 }

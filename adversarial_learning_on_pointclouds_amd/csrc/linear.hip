@@ -21,6 +21,11 @@ struct DropSpec {
   const int32_t* step;  // device step counter for the Philox draw, or nullptr
   uint64_t seed;
   float p;
+  // Philox row of output row m: m + (m < split ? off_lo : off_hi), so a rank of
+  // a data-parallel step draws the rows of the global batch it holds (the GT
+  // rows [0, split) and the no-GT rows after them shift separately); all 0 =
+  // the launch's own rows
+  int split, off_lo, off_hi;
 };
 
 // dropout source, fixed per launch (a template parameter: the operand loads
@@ -94,8 +99,11 @@ __device__ __forceinline__ float drop_scale(const GemmArgs& g, size_t i, int m, 
   const float keep = 1.0f / (1.0f - g.drop.p);
   if (DM == DM_MASK) return g.drop.mask[i] * keep;
   if (DM == DM_RNG)
-    return rng_uniform(g.drop.seed, step, RNG_DROPOUT, (uint32_t)(m * g.N + n)) >= g.drop.p ? keep
-                                                                                           : 0.f;
+  {
+    const int gm = m + (m < g.drop.split ? g.drop.off_lo : g.drop.off_hi);
+    return rng_uniform(g.drop.seed, step, RNG_DROPOUT, (uint32_t)(gm * g.N + n)) >= g.drop.p ? keep
+                                                                                             : 0.f;
+  }
   return 1.f;
 }
 
@@ -505,7 +513,8 @@ static void split_cfg(int R, int* S, int* L) {
 
 int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N,
                       int K, int act, const float* mask, const int32_t* step, uint64_t seed,
-                      float p, hipStream_t s, int add_identity_k, float* mask_out) {
+                      float p, hipStream_t s, int add_identity_k, float* mask_out,
+                      int row_split, int row_off_lo, int row_off_hi) {
   PC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 4 == 0, "linear_fwd: bad shape M=%d N=%d K=%d", M, N,
              K);
   PC_REQUIRE(add_identity_k == 0 || add_identity_k * add_identity_k == N,
@@ -513,7 +522,7 @@ int launch_linear_fwd(const float* x, const float* w, const float* b, float* y, 
   GemmArgs g{};
   g.x = x; g.w = w; g.b = b; g.y = y; g.act = act; g.diag = add_identity_k;
   g.mask_out = mask_out;
-  g.drop = DropSpec{mask, step, seed, p};
+  g.drop = DropSpec{mask, step, seed, p, row_split, row_off_lo, row_off_hi};
   g.M = M; g.N = N; g.K = K;
   int S, L;
   split_cfg(K, &S, &L);
@@ -537,7 +546,7 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
              "linear_bwd: bad shape M=%d m_w=%d N=%d K=%d", M, m_w, N, K);
   GemmArgs g{};
   g.x = x; g.w = w; g.dy = dy; g.yact = y; g.act = act;
-  g.drop = DropSpec{mask, step, seed, p};
+  g.drop = DropSpec{mask, step, seed, p, 0, 0, 0};
   g.dx = dx; g.dw = dw; g.db = db;
   g.M = M; g.N = N; g.K = K; g.m_w = m_w;
   if (extra) {

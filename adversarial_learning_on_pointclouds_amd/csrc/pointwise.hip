@@ -37,9 +37,12 @@ struct WView {
   __device__ float get(const float* b, int o, int k) const {
     return kmajor ? b[(size_t)k * O + o] : b[(size_t)o * K + k];
   }
-  // 16-B loads of four contiguous weights need the matrix 16-B aligned (O, K
+  // 16-B loads of four contiguous weights need every matrix 16-B aligned: the
+  // base and, with one matrix per rows_per_w rows, the per-matrix stride (O, K
   // and the fragment offsets are multiples of 4 here)
-  __device__ bool aligned16() const { return (reinterpret_cast<uintptr_t>(w) & 15) == 0; }
+  __device__ bool aligned16() const {
+    return (reinterpret_cast<uintptr_t>(w) & 15) == 0 && (rows_per_w == 0 || (stride & 3) == 0);
+  }
 };
 
 // ---------------------------------------------------------------------------

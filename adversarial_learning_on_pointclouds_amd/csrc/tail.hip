@@ -301,7 +301,7 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
             float lambda_adv, float* __restrict__ dd3, float* __restrict__ slabs,
             float* __restrict__ lpart3, float* __restrict__ dout, const int32_t* __restrict__ gidx,
             int C, int N, int* __restrict__ sortrec, float* __restrict__ z4g,
-            float* __restrict__ z5g, float* __restrict__ a4g) {
+            float* __restrict__ z5g, float* __restrict__ a4g, int lab_off) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DiscTailLds& L = *reinterpret_cast<DiscTailLds*>(smem);
   const int tid = threadIdx.x;
@@ -355,11 +355,12 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
       if (dout) dout[m] = x;  // the D logits (run_training_semi's confidence, trainer.py:717)
       float y, f;
       if (m < B) {
-        y = soft_gt ? ysoft : 0.7f + 0.35f * rng_uniform(seed, stepv, RNG_LABEL_GT, (uint32_t)m);
+        y = soft_gt ? ysoft : 0.7f + 0.35f * rng_uniform(seed, stepv, RNG_LABEL_GT, (uint32_t)(m + lab_off));
         f = 0.5f;
       } else if (m < 2 * B) {
         y = soft_nogt ? ysoft
-                      : 0.305f * rng_uniform(seed, stepv, RNG_LABEL_NOGT, (uint32_t)(m - B));
+                      : 0.305f * rng_uniform(seed, stepv, RNG_LABEL_NOGT,
+                                                  (uint32_t)(m - B + lab_off));
         f = 0.5f;
       } else {
         y = 1.f;
@@ -845,7 +846,7 @@ int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, c
                      const float* soft_nogt, const int32_t* step, uint64_t seed, float lambda_adv,
                      float* dd3, float* slabs, float* lpart3, float* dout, hipStream_t s,
                      const int32_t* gidx, int C, int N, int* sortrec, float* z4g, float* z5g,
-                     float* a4g) {
+                     float* a4g, int lab_off) {
   static bool once = false;
   if (!once) {
     if (set_lds(k_disc_tail, sizeof(DiscTailLds), "disc_tail") != PCADV_OK) return PCADV_EHIP;
@@ -855,7 +856,7 @@ int launch_disc_tail(const float* d3, int B, const float* w4, const float* b4, c
   const int nsort = sortrec ? (C * ((N + FS_PCH - 1) / FS_PCH) + 1) / 2 : 0;
   hipLaunchKernelGGL(k_disc_tail, dim3(disc_rowblocks(B) + nsort), dim3(TT), sizeof(DiscTailLds), s,
                      d3, B, w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3,
-                     slabs, lpart3, dout, gidx, C, N, sortrec, z4g, z5g, a4g);
+                     slabs, lpart3, dout, gidx, C, N, sortrec, z4g, z5g, a4g, lab_off);
   PC_HIP_CHECK_LAUNCH("k_disc_tail");
   return PCADV_OK;
 }

@@ -191,6 +191,43 @@ class ShapeNetDataset_noGT(data.Dataset):
         return self.select_data.shape[0]
 
 
+def _dp_rank_world(rank, world_size):
+    """(rank, world) of a loader: as given, else the initialised default
+    torch.distributed group's, else (0, 1)."""
+    import torch.distributed as dist
+    if world_size is None:
+        world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    if rank is None:
+        rank = dist.get_rank() if world_size > 1 else 0
+    rank, world_size = int(rank), int(world_size)
+    if world_size < 1 or not 0 <= rank < world_size:
+        raise ValueError(f"rank {rank} of world size {world_size}")
+    return rank, world_size
+
+
+def _broadcast_int(v):
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        raise RuntimeError("a data-parallel DeviceCloudLoader without a seed needs an initialised "
+                           "process group (to share rank 0's seed); pass seed= on every rank")
+    t = torch.tensor([int(v)], dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    dist.broadcast(t, src=0)
+    return int(t.item())
+
+
+def shard_order(order, B, rank, world):
+    """Rank `rank`'s rows of each whole global batch of an epoch order: the
+    global batches are order[k W B : (k + 1) W B] and this rank takes their
+    rows [rank B, rank B + B), concatenated in batch order (a ragged tail of
+    fewer than W B clouds is dropped).  Works on any 1-D tensor (host or
+    device)."""
+    Bg = B * world
+    nb = order.numel() // Bg
+    return order[:nb * Bg].reshape(nb, world, B)[:, rank].reshape(-1).contiguous()
+
+
 class DeviceCloudLoader:
     """A DataLoader over one of the datasets above whose whole split lives in
     HBM (ModelNet40 train: 9 840 x 1 024 x 3 f32 = 121 MB of the 288 GB).
@@ -207,13 +244,27 @@ class DeviceCloudLoader:
     one from torch's default generator, so two loaders built alike draw
     independent jitter as the reference's np.random does.  The dataset kind is
     mixed into the Philox key too: a GT and a no-GT loader given the same
-    seed still draw different fields."""
+    seed still draw different fields.
+
+    Data parallelism (``world_size`` > 1, ``rank``; default: the initialised
+    torch.distributed group's, else one process): ``batch_size`` is the
+    per-rank batch B.  Every rank draws the same epoch permutation (the seed
+    is rank 0's, broadcast when it is not given) and takes rows
+    [rank B, rank B + B) of each global batch of world_size x B clouds
+    (shard_order), jittered with the Philox draws of those global rows; so
+    the ranks' batches are exactly the slices of a one-process loader of
+    batch world_size x B with the same seed.  A ragged last global batch is
+    dropped (drop_last is forced on): unequal shards would not average to the
+    global batch's mean losses."""
 
     _KIND_TAG = {"modelnet_gt": 1, "modelnet_nogt": 2, "shapenet_gt": 3, "shapenet_nogt": 4}
 
     def __init__(self, dataset, batch_size, shuffle=True, seed=None, device="cuda", drop_last=False,
-                 sigma=0.01, clip=0.05):
+                 sigma=0.01, clip=0.05, rank=None, world_size=None):
         self.lib = _lib.load()
+        self.rank, self.world = _dp_rank_world(rank, world_size)
+        if self.world > 1:
+            drop_last = True
         self.ds, self.B, self.shuffle, self.drop_last = dataset, int(batch_size), shuffle, drop_last
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -238,6 +289,8 @@ class DeviceCloudLoader:
         self.clip = float(clip)
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            if self.world > 1:  # one permutation and one jitter field for every rank
+                seed = _broadcast_int(seed)
         self.seed = (int(seed) ^ (self._KIND_TAG[self.kind] << 58)) & 0xFFFFFFFFFFFFFFFF
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed))
@@ -245,7 +298,14 @@ class DeviceCloudLoader:
         self.noise = None
 
     def __len__(self):
-        return self.n // self.B if self.drop_last else (self.n + self.B - 1) // self.B
+        Bg = self.B * self.world  # the global batch
+        return self.n // Bg if self.drop_last else (self.n + Bg - 1) // Bg
+
+    @property
+    def order_len(self):
+        """Length of epoch_order(): the split, or this rank's shard of the
+        whole global batches."""
+        return self.n if self.world == 1 else len(self) * self.B
 
     def gather(self, idx, noise=None, out=None, _checked=False, out_lab=None):
         """One batch for the device index tensor ``idx`` (int64, each in
@@ -280,7 +340,7 @@ class DeviceCloudLoader:
         check(self.lib.pcadv_gather_clouds(P(self.pts), self.n, self.npts, self.npts, P(idx), b,
                                            P(self.labels), lw, P(self.segs), self.sigma, self.clip,
                                            P(nz), self.seed, P(self.step), P(pts), P(lab), P(seg),
-                                           stream_ptr()), "pcadv_gather_clouds")
+                                           self.rank * self.B, stream_ptr()), "pcadv_gather_clouds")
         self.step += 1
         return self._pack(pts, lab, seg)
 
@@ -295,10 +355,15 @@ class DeviceCloudLoader:
 
     def epoch_order(self):
         """One epoch's order of the split: a fresh permutation from the loader's
-        generator when shuffling (what __iter__ draws at the start of an epoch)."""
+        generator when shuffling (what __iter__ draws at the start of an epoch);
+        under data parallelism this rank's shard of it (shard_order)."""
         if self.shuffle:
-            return torch.randperm(self.n, device=self.device, generator=self.gen)
-        return torch.arange(self.n, device=self.device)
+            order = torch.randperm(self.n, device=self.device, generator=self.gen)
+        else:
+            order = torch.arange(self.n, device=self.device)
+        if self.world > 1:
+            order = shard_order(order, self.B, self.rank, self.world)
+        return order
 
     def index_batches(self):
         """The index slices of one epoch, in the order __iter__ gathers them."""
@@ -324,13 +389,14 @@ class DeviceCloudLoader:
         need(out, "out", (B, self.npts, 3), torch.float32)
         if self.labels is not None:
             need(out_lab, "out_lab", (B, lw), torch.int64)
-        need(order, "order", (self.n,), torch.int64)
+        need(order, "order", (self.order_len,), torch.int64)
         need(cursor, "cursor", (1,), torch.int32)
         P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         check(self.lib.pcadv_gather_clouds_at(P(self.pts), self.n, self.npts, self.npts, P(order),
                                               P(cursor), self.B, P(self.labels), lw, None,
                                               self.sigma, self.clip, self.seed, P(self.step),
-                                              P(out), P(out_lab), None, stream_ptr()),
+                                              P(out), P(out_lab), None, self.rank * self.B,
+                                              stream_ptr()),
               "pcadv_gather_clouds_at")
 
     def __iter__(self):

@@ -42,9 +42,17 @@ def _avg_async(t, group=None):
 
 class DataParallelAdvStep:
     """Wraps an AdvTrainStep-like object exposing grads(), adam(), grad_flat,
-    g_param, d_param and losses."""
+    g_param, d_param and losses.
 
-    def __init__(self, step, group=None, broadcast_params=True, overlap=None):
+    Device-drawn dropout masks and soft D labels are keyed by the GLOBAL
+    batch's rows (global_rng, default): this rank is taken to hold rows
+    [rank B, rank B + B) of the global GT and no-GT batches, the step's seed
+    becomes rank 0's, and so the ranks draw exactly the slices of the
+    one-process step on the global batch (pcadv_adv_args.rng_rank / rng_world).
+    global_rng=False keeps the step's own keying (every rank then draws the
+    SAME masks for its local rows unless the seeds differ)."""
+
+    def __init__(self, step, group=None, broadcast_params=True, overlap=None, global_rng=True):
         """overlap: bucket the all-reduce around the feature backward (default:
         when the step supports parts and the backend is RCCL)."""
         self.step, self.group = step, group
@@ -52,6 +60,14 @@ class DataParallelAdvStep:
         if broadcast_params:  # identical initial weights on every rank
             dist.broadcast(step.g_param, src=0, group=group)
             dist.broadcast(step.d_param, src=0, group=group)
+        if global_rng and hasattr(step, "set_rng_rank"):
+            step.set_rng_rank(dist.get_rank(group), dist.get_world_size(group))
+            seed = torch.tensor([step.seed & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64,
+                                device=step.g_param.device if dist.get_backend(group) == "nccl"
+                                else "cpu")
+            dist.broadcast(seed, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                           group=group)
+            step.seed = int(seed.item())
 
     def _split(self):
         if self.overlap is not None:

@@ -99,12 +99,18 @@ class AdvTrainStep:
     trainer.py:561-572).  semi=True adds run_training_semi's pseudo-label term
     (utils/trainer.py:716-743: lambda_semi x CrossEntropyLoss(ignore_index=255)
     of the no-GT logits against their argmax, clouds with D <= semi_th ignored).
+    rng_rank / rng_world: this step is rank rng_rank of a data-parallel job of
+    rng_world ranks, each holding the rows [rank B, rank B + B) of the global
+    GT and no-GT batches: the device-drawn masks and labels are those of the
+    one-process step on the global batch (pcadv_adv_args.rng_rank, ABI 6).
     """
 
     def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
                  lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
-                 seed=0, device="cuda", lambda_semi=1.0, semi_th=0.8, precision="fp32"):
+                 seed=0, device="cuda", lambda_semi=1.0, semi_th=0.8, precision="fp32",
+                 rng_rank=0, rng_world=1):
         self.lib = _lib.load()
+        self.set_rng_rank(rng_rank, rng_world)
         self.model, self.model_D = model, model_D
         self.precision = _precision(precision)
         self.B, self.N = int(B), int(N)
@@ -194,7 +200,28 @@ class AdvTrainStep:
         a.lambda_semi, a.semi_th = hp["lambda_semi"], hp["semi_th"]
         a.part = int(part)
         a.precision = self.precision
+        a.rng_rank, a.rng_world = self.rng_rank, self.rng_world
         return a
+
+    def sync_hyper(self):
+        """Re-read lr / betas / eps from the optimizers (a scheduler may have
+        changed them); a graph captured before keeps the old values, so the
+        trainer recaptures when they change."""
+        opt, opt_d = (self.optimizers + (None,))[:2] if hasattr(self, "optimizers") else \
+            (self.optimizer, None)
+        if opt is not None:
+            g = opt.param_groups[0]
+            self.hp.update(lr=float(g["lr"]), betas=tuple(float(b) for b in g["betas"]),
+                           eps=float(g["eps"]))
+        if opt_d is not None:
+            self.hp["lr_D"] = float(opt_d.param_groups[0]["lr"])
+
+    def set_rng_rank(self, rank, world):
+        """Key the device draws by the global batch's rows (data parallelism)."""
+        rank, world = int(rank), int(world)
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError(f"rng rank {rank} of {world}")
+        self.rng_rank, self.rng_world = rank, world
 
     # gradients that are final before the feature backward: g_grad[G_FC1_W:] and
     # all of D, contiguous in grad_flat (part 1 of a split step)
@@ -345,8 +372,9 @@ class ClsTrainStep:
     operands (configs[1] is quoted in bf16); everything else f32."""
 
     def __init__(self, model, B, N, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 lambda_cls=1.0, seed=0, device="cuda", precision="fp32"):
+                 lambda_cls=1.0, seed=0, device="cuda", precision="fp32", rng_rank=0, rng_world=1):
         self.lib = _lib.load()
+        self.set_rng_rank(rng_rank, rng_world)
         self.model = model
         self.precision = _precision(precision)
         self.B, self.N = int(B), int(N)
@@ -409,7 +437,11 @@ class ClsTrainStep:
         a.workspace = self.workspace.data_ptr()
         a.workspace_bytes = self.workspace.numel()
         a.precision = self.precision
+        a.rng_rank, a.rng_world = self.rng_rank, self.rng_world
         return a
+
+    set_rng_rank = AdvTrainStep.set_rng_rank
+    sync_hyper = AdvTrainStep.sync_hyper
 
     def __call__(self, pts, labels, mask=None, apply_adam=True):
         a = self._args(pts, labels, mask, apply_adam)

@@ -144,6 +144,28 @@ class _LossRing:
         self.emit(i_iter, vals, extra)
 
 
+def _opt_hyper(opts):
+    """The hyperparameters a captured optimizer step bakes in, per group."""
+    def f(v):
+        return float(v.item()) if torch.is_tensor(v) else float(v)
+    return tuple((f(g["lr"]), tuple(f(b) for b in g.get("betas", ())), f(g.get("eps", 0.0)),
+                  f(g.get("weight_decay", 0.0))) for o in opts for g in o.param_groups)
+
+
+def _detached_snapshot(state):
+    """Copies of the tensors a capture's warm-up changes.  Detached, under
+    no_grad: a clone of a parameter made with grad mode on would hold its
+    AccumulateGrad node (created on the launching stream) alive into the
+    capture, where it then runs on the wrong stream (the HIP runtime crashed
+    at capture end).  Checked, so a future state list cannot bring it back."""
+    with torch.no_grad():
+        saved = [t.detach().clone() for t in state]
+    bad = [i for i, t in enumerate(saved) if t.grad_fn is not None or t.requires_grad]
+    if bad:
+        raise RuntimeError(f"capture state snapshot {bad} carries autograd history")
+    return saved
+
+
 class _GraphedIteration:
     """One training iteration fed by DeviceCloudLoaders as ONE HIP graph: each
     loader's batch gathered (+ device jitter) into static input buffers from a
@@ -157,8 +179,13 @@ class _GraphedIteration:
     flag, captured on first use; the capture's warm-up leaves parameters, Adam
     state, counters and the ring as they were."""
 
-    def __init__(self, step, loaders, ring):
+    def __init__(self, step, loaders, ring, optimizers=()):
         self.step, self.loaders, self.ring = step, loaders, ring
+        # a capture bakes the optimizers' Python-float hyperparameters (lr,
+        # betas, eps) into its kernels: a change (a scheduler, the reference's
+        # adjust_learning_rate) drops the graphs and recaptures
+        self.optimizers = tuple(o for o in optimizers if o is not None)
+        self._hyper = _opt_hyper(self.optimizers)
         B, N, dev = step.B, step.N, step.device
         L = len(loaders)
         self.B, self.L = B, L
@@ -166,7 +193,7 @@ class _GraphedIteration:
         for k, ld in enumerate(loaders):
             self.counters[k:k + 1].copy_(ld.step)
             ld.step = self.counters[k:k + 1]  # the loader keeps using it (eager gathers too)
-        self.order = [torch.zeros(ld.n, dtype=torch.int64, device=dev) for ld in loaders]
+        self.order = [torch.zeros(ld.order_len, dtype=torch.int64, device=dev) for ld in loaders]
         self.pos = [None] * L  # host: next batch of the current epoch
         self.pts = [torch.zeros(B, N, 3, device=dev) for _ in loaders]
         # the labelled split's label width (the gather writes B x width int64)
@@ -184,7 +211,7 @@ class _GraphedIteration:
                 self.pos[k] = 0
             kk = self.pos[k]
             self.pos[k] += 1
-            out.append((kk, min(ld.B, ld.n - kk * ld.B)))
+            out.append((kk, min(ld.B, ld.order_len - kk * ld.B)))
         return out
 
     def eager_batches(self, batches):
@@ -212,18 +239,8 @@ class _GraphedIteration:
         g = self.graphs.get(semi)
         if g is None:
             st = self.step
-            if hasattr(st, "graph_state"):  # a step that names its own state
-                pre = st.graph_state()
-            else:
-                pre = [t for t in (getattr(st, n, None) for n in
-                                   ("g_param", "g_m", "g_v", "d_param", "d_m", "d_v", "step_count"))
-                       if t is not None]
-            state = pre + [self.counters, self.ring.count, self.ring.ring]
-            # detached copies: a clone of a parameter would hold its
-            # AccumulateGrad node (created here, on this stream) alive into the
-            # capture, where it then runs on the wrong stream
-            with torch.no_grad():
-                saved = [t.detach().clone() for t in state]
+            state = self._state()
+            saved = _detached_snapshot(state)
             cur = torch.cuda.current_stream()
             side = torch.cuda.Stream(device=st.device)
             side.wait_stream(cur)
@@ -242,9 +259,111 @@ class _GraphedIteration:
             self.graphs[semi] = g
         return g
 
+    def _check_hyper(self):
+        h = _opt_hyper(self.optimizers)
+        if h != self._hyper:
+            self.graphs.clear()
+            if hasattr(self.step, "sync_hyper"):
+                self.step.sync_hyper()
+            self._hyper = h
+
     def replay(self, semi=False):
+        self._check_hyper()
         self._graph(semi).replay()
         return self.step.losses
+
+    def _state(self):
+        st = self.step
+        if hasattr(st, "graph_state"):  # a step that names its own state
+            pre = st.graph_state()
+        else:
+            pre = [t for t in (getattr(st, n, None) for n in
+                               ("g_param", "g_m", "g_v", "d_param", "d_m", "d_v", "step_count"))
+                   if t is not None]
+        return pre + [self.counters, self.ring.count, self.ring.ring]
+
+
+class _DPIteration(_GraphedIteration):
+    """_GraphedIteration for a data-parallel rank (DeviceCloudLoaders sharded
+    over the process group, AdvTrainStep keyed to this rank's global rows):
+    the iteration runs as four HIP graphs around the eager RCCL all-reduces of
+    DataParallelAdvStep (bucketed, overlapped with the feature backward):
+    [gathers + step part 1] | all-reduce(AVG) of the early gradient bucket and
+    of the loss vector | [step part 2] | all-reduce of the late bucket beside
+    [Adam of the early bucket's parameters] | [Adam of conv1..conv4 + the
+    iteration epilogue].  With equal shards the replicas take exactly the
+    one-process step on the global batch (CE / BCE are batch means; the
+    logged losses are the ranks' average, i.e. the global batch's)."""
+
+    def __init__(self, step, loaders, ring, group=None, optimizers=()):
+        super().__init__(step, loaders, ring, optimizers)
+        self.group = group
+
+    def _part(self, k, semi):
+        st, L = self.step, self.L
+        if k == 1:
+            for i, ld in enumerate(self.loaders):
+                ld.gather_at(self.order[i], self.counters[L + i:L + i + 1], self.pts[i],
+                             self.lab if (i == 0 and ld.labels is not None) else None)
+            st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=1)
+        elif k == 2:
+            st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=2)
+        elif k == 3:
+            st.adam(part=1)
+        else:
+            st.adam(part=2)
+            self.ring.write(st.losses, self.counters, 2 * L)
+
+    def _graph(self, semi):
+        gs = self.graphs.get(semi)
+        if gs is None:
+            state = self._state()
+            saved = _detached_snapshot(state)
+            cur = torch.cuda.current_stream()
+            side = torch.cuda.Stream(device=self.step.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):  # warm-up outside the capture (no collectives)
+                for k in (1, 2, 3, 4):
+                    self._part(k, semi)
+            cur.wait_stream(side)
+            gs = []
+            for k in (1, 2, 3, 4):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._part(k, semi)
+                gs.append(g)
+            torch.cuda.synchronize()
+            with torch.no_grad():
+                for dst, src in zip(state, saved):
+                    dst.copy_(src)
+            self.graphs[semi] = gs
+        return gs
+
+    def replay(self, semi=False):
+        from .distributed import _avg_async
+        self._check_hyper()
+        g1, g2, g3, g4 = self._graph(semi)
+        st = self.step
+        g1.replay()
+        done = _avg_async(st.early_grads(), self.group)
+        done_loss = _avg_async(st.losses, self.group)
+        g2.replay()
+        done()
+        done_late = _avg_async(st.late_grads(), self.group)
+        g3.replay()  # the early bucket's Adam beside the late all-reduce
+        done_late()
+        done_loss()
+        g4.replay()
+        return st.losses
+
+
+def _dp_world(*loaders):
+    """World size of data-parallel (sharded) DeviceCloudLoaders, 1 if none;
+    every loader must agree."""
+    ws = {int(getattr(l, "world", 1)) for l in loaders}
+    if len(ws) != 1:
+        raise ValueError(f"loaders sharded over different world sizes {sorted(ws)}")
+    return ws.pop()
 
 
 class _AutogradStep:
@@ -458,6 +577,9 @@ def _pooled_d_grads(step, model_D, gan_loss, pool_gt, pool_nogt, B, device):
 
 
 def _save(model, model_D, args, tag):
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+        return  # data parallel: the replicas are identical, rank 0 writes
     torch.save(model.state_dict(), os.path.join(args.exp_dir, "model_{}.pth".format(tag)))
     torch.save(model_D.state_dict(), os.path.join(args.exp_dir, "modelD_{}.pth".format(tag)))
 
@@ -508,6 +630,23 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
         (trainloader_gt, trainloader_nogt))
     gi = None
     tb = getattr(args, "tensorboard", False) and writer is not None
+    # data parallelism: DeviceCloudLoaders sharded over the process group
+    # (DeviceCloudLoader(..., world_size=W)); every iteration is the fused step
+    # on this rank's shard, graphed around the gradient all-reduces (_DPIteration)
+    world = _dp_world(trainloader_gt, trainloader_nogt) if _device_loaders(
+        trainloader_gt, trainloader_nogt) else 1
+    rank = 0
+    if world > 1:
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != world:
+            raise RuntimeError(f"loaders sharded over {world} ranks: initialise a process group of "
+                               "that size first")
+        if not graphed:
+            raise NotImplementedError(
+                "data-parallel run_training runs the fused step graphed over DeviceCloudLoaders: "
+                "PointNetCls(k=40) + DeepConvDiscNet(40, 1), Adam, CE / BCE, ImagePool(0), equal "
+                "GT / no-GT batches (args.use_graph on)")
+        rank = dist.get_rank()
 
     def emit(i_iter, vals, semi_on):
         loss_D_value = vals[2] + vals[3]
@@ -536,7 +675,12 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                                 seed=int(getattr(args, "seed", 0)) + i_iter,
                                 device=args.device,
                                 lambda_semi=float(getattr(args, "lambda_semi", 1.0)),
-                                semi_th=float(getattr(args, "semi_TH", 0.8)))
+                                semi_th=float(getattr(args, "semi_TH", 0.8)),
+                                rng_rank=rank, rng_world=world)
+            if world > 1:  # identical replicas: rank 0's parameters and seed
+                from .distributed import DataParallelAdvStep
+                DataParallelAdvStep(step, broadcast_params=True)
+        step.sync_hyper()  # lr / betas / eps as the optimizers hold them now
         return step
 
     for i_iter in range(args.total_iterations):
@@ -553,7 +697,10 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                 gstep = (fused_step(B0, N0) if graphed else _AutogradAdvStep(
                     model, model_D, optimizer, optimizer_D, gan_loss, cls_loss,
                     (history_pool_gt, history_pool_nogt), args, B0, N0))
-                gi = _GraphedIteration(gstep, (trainloader_gt, trainloader_nogt), log)
+                gi = (_DPIteration(gstep, (trainloader_gt, trainloader_nogt), log,
+                                   optimizers=(optimizer, optimizer_D)) if world > 1
+                      else _GraphedIteration(gstep, (trainloader_gt, trainloader_nogt), log,
+                                             optimizers=(optimizer, optimizer_D)))
             bt = gi.next_batches()
             if all(size == B0 for _, size in bt) and not (ag_graphed and semi_on):
                 losses = gi.replay(semi=semi_on)
@@ -690,6 +837,7 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
                 step.sync_optimizer_state()
             step = ClsTrainStep(model, B, N, optimizer=optimizer, lambda_cls=args.lambda_cls,
                                 seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)
+        step.sync_hyper()
         return step
 
     for i_iter in range(args.total_iterations):
@@ -703,7 +851,7 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
                          _AutogradClsStep(model, optimizer, cls_loss, args.lambda_cls,
                                           args.lambda_regu, trainloader_gt.B,
                                           trainloader_gt.npts, args.device))
-                gi = _GraphedIteration(gstep, (trainloader_gt,), log)
+                gi = _GraphedIteration(gstep, (trainloader_gt,), log, optimizers=(optimizer,))
             bt = gi.next_batches()
             if bt[0][1] == trainloader_gt.B:
                 losses = gi.replay()

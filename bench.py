@@ -914,7 +914,8 @@ def main():
 
     model, model_D = make_models(dev, seed=0)
     adv_prec = args.precision or "fp32"
-    step = AdvTrainStep(model, model_D, B, N, seed=1234 + rank, device=dev, precision=adv_prec)
+    # DataParallelAdvStep keys the device draws by global rows (rank 0's seed)
+    step = AdvTrainStep(model, model_D, B, N, seed=1234, device=dev, precision=adv_prec)
     # PCADV_BENCH_OVERLAP=1 forces the bucketed all-reduce (the RCCL default) in a gloo rehearsal
     overlap = {"1": True, "0": False}.get(os.environ.get("PCADV_BENCH_OVERLAP", ""))
     runner = DataParallelAdvStep(step, overlap=overlap) if dist is not None else None

@@ -281,8 +281,8 @@ typedef struct pcadv_gemm_desc {
  * pcadv_gemm_wgrad_slabs enqueues w's slab GEMM into w->workspace (and, when
  * w->gsum is given, the per-group sums and db now); when g is non-null it also
  * enqueues the GEMM g (a data gradient: pcadv_gemm's arguments), and where both
- * have the engine's pairable forms (g: ta = 0, tb = 1, precise = 0, M > 32) the
- * two run as ONE launch, their workgroups side by side, each output bitwise its
+ * have the engine's pairable forms (g: ta = 0, tb = 1, either precision, M > 32,
+ * operands vectorisable: 16-B aligned rows, VEC >= 2) the two run as ONE launch, their workgroups side by side, each output bitwise its
  * own launch's.  g must neither read nor write anything w reads or writes.
  * pcadv_wgrad_finish then enqueues the remaining dw (and db) sums of n such
  * weight gradients in one launch (more launches above 16).  Between the two
@@ -356,14 +356,17 @@ int pcadv_h5_read(const char* path, const char* name, int out_type, int64_t keep
  * nullable) gathered alongside.  Jitter (dataset/modelNetData.py:80-91):
  * + clip(sigma * z, -clip, clip) per coordinate (sigma = 0: none), z from
  * `noise` ([B][npts][3] f64 standard normals, computed in f64 like numpy) or,
- * when noise is NULL, Philox normals keyed by (seed, *step, point).  Indices
- * must lie in [0, n_src) (checked by the caller; out-of-range rows are left
- * untouched). */
+ * when noise is NULL, Philox normals keyed by (seed, *step, point), the point
+ * of batch row b counted as row rng_row0 + b (0 for a one-process loader; a
+ * data-parallel rank r holding rows [rB, rB + B) of each global batch passes
+ * rB, so the ranks jitter exactly as one loader of the global batch would;
+ * ABI version 6).  Indices must lie in [0, n_src) (checked by the caller;
+ * out-of-range rows are left untouched). */
 int pcadv_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
                         const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
                         const int64_t* src_seg, double sigma, double clip, const double* noise,
                         uint64_t seed, const int32_t* step, float* out, int64_t* out_lab,
-                        int64_t* out_seg, hipStream_t stream);
+                        int64_t* out_seg, int64_t rng_row0, hipStream_t stream);
 
 /* pcadv_gather_clouds for a graph-replayed loader: batch k = *cursor of the
  * epoch order `order` (int64, k * B + b -> source cloud), so a captured graph
@@ -374,7 +377,8 @@ int pcadv_gather_clouds_at(const float* src, int64_t n_src, int npts, int src_np
                            const int64_t* order, const int32_t* cursor, int B,
                            const int64_t* src_lab, int lab_width, const int64_t* src_seg,
                            double sigma, double clip, uint64_t seed, const int32_t* step,
-                           float* out, int64_t* out_lab, int64_t* out_seg, hipStream_t stream);
+                           float* out, int64_t* out_lab, int64_t* out_seg, int64_t rng_row0,
+                           hipStream_t stream);
 
 /* The end of a graph-replayed training iteration (trainer.py): counters[i] += 1
  * for i < ncounters (<= 64: loaders' RNG steps and batch cursors), and, when
@@ -443,6 +447,14 @@ typedef struct pcadv_adv_args {
    * pcadv_feat_fwd_bf16; the head, the discriminator and every backward stay
    * f32).  ABI version 5. */
   int precision;
+  /* Data parallelism (ABI version 6): rank rng_rank of rng_world (<= 1: one
+   * process) holding GT rows [rank B, rank B + B) and no-GT rows [rank B,
+   * rank B + B) of the rng_world B-cloud global batches.  The device-drawn
+   * dropout masks and soft D labels are keyed by those global rows, so with
+   * the same rng_seed and step count the ranks draw exactly the slices of the
+   * one-process step on the global batch (the dropout row of no-GT row j is
+   * rng_world B + j, as in the one-process [GT; no-GT] batch). */
+  int rng_rank, rng_world;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

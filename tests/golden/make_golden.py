@@ -336,6 +336,113 @@ def main(ref_root, only=None):
             summarize("grad." + name, p.grad.numpy(), out)
         np.savez_compressed(os.path.join(HERE, "g12_stn3d.npz"), **out)
 
+    # ---------------- G13: run_training off the fused step ----
+    # utils/trainer.py:426-559 for 3 iterations in three configurations:
+    #   ft_pool0:    PointNetCls(feature_transform=True) + ImagePool(0)
+    #                (the graphed autograd body, trainer._AutogradAdvStep);
+    #   plain_pool3: PointNetCls(feature_transform=False) + ImagePool(3) on both
+    #                D inputs (the fused step + trainer._pooled_d_grads);
+    #   ft_pool3:    both (the eager autograd body, trainer._adv_body).
+    # Dropout masks and soft labels injected as in G3; the pools draw from
+    # Python `random` seeded with random_seed (utils/image_pool.py:45-47:
+    # random.uniform(0, 1), random.randint(0, pool_size - 1)).
+    def g13():
+        import random
+        iters, B, data_seed = 3, B_SMALL, 131
+        out = dict(iters=iters, B=B, N=N_PTS, data_seed=data_seed, g_seed=13, d_seed=14,
+                   random_seed=1313, lambda_cls=1.0, lambda_adv=0.01)
+        rng = np.random.default_rng(data_seed)
+        batches_gt, batches_ng, masks, soft = [], [], [], []
+        for _ in range(iters):
+            batches_gt.append((rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32),
+                               rng.integers(0, 40, B).astype(np.int64)))
+            batches_ng.append(rng.uniform(-1, 1, (B, N_PTS, 3)).astype(np.float32))
+            masks.append(make_mask(rng, B))
+            masks.append(make_mask(rng, B))
+            soft.append(rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32))
+            soft.append(rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32))
+        out["pts_gt"] = np.stack([a for a, _ in batches_gt])
+        out["labels"] = np.stack([b for _, b in batches_gt])
+        out["pts_nogt"] = np.stack(batches_ng)
+        out["masks"] = np.stack(masks).reshape(iters, 2, B, 256)
+        out["soft"] = np.stack(soft).reshape(iters, 2, B)
+        for cfg, ft, pool in (("ft_pool0", True, 0), ("plain_pool3", False, 3),
+                              ("ft_pool3", True, 3)):
+            Gp = onp.make_params(onp.cls_ft_spec(40) if ft else onp.cls_spec(40), seed=13)
+            Dp = onp.make_params(onp.disc_spec(40, 1), seed=14, init="xavier")
+            model = load(PointNetCls(k=40, feature_transform=ft), Gp)
+            model.dropout = MaskDropout([m.copy() for m in masks])
+            model_D = load(DeepConvDiscNet(40, 1), Dp)
+            soft_q = [s.copy() for s in soft]
+            orig = rtrainer.make_D_label
+
+            def make_D_label(input, value, device, random=False, _q=soft_q):
+                if random:
+                    return torch.from_numpy(_q.pop(0)).to(device)
+                return orig(input, value, device, random=False)
+
+            rec = {"cls": [], "gan": []}
+
+            class Rec(nn.Module):
+                def __init__(self, inner, key):
+                    super().__init__()
+                    self.inner, self.key = inner, key
+
+                def forward(self, a, b):
+                    r = self.inner(a, b)
+                    rec[self.key].append(float(r.item()))
+                    return r
+
+            optimizer = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+            optimizer_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+            args = argparse.Namespace(device=torch.device("cpu"), total_iterations=iters,
+                                      lambda_cls=1.0, lambda_adv=0.01, iter_save_epoch=10 ** 9,
+                                      iter_test_epoch=10 ** 9,
+                                      exp_dir=tempfile.mkdtemp(prefix="g13_"), tensorboard=False,
+                                      batch_size=B)
+            gt_list = [(torch.from_numpy(a), torch.from_numpy(b)) for a, b in batches_gt]
+            ng_list = [torch.from_numpy(a) for a in batches_ng]
+            logger = logging.getLogger("golden13")
+            logger.addHandler(logging.NullHandler())
+            logger.propagate = False
+            pools = (ImagePool(pool), ImagePool(pool))
+            random.seed(1313)
+            rtrainer.make_D_label = make_D_label
+            try:
+                rtrainer.run_training(
+                    trainloader_gt=gt_list, trainloader_nogt=ng_list,
+                    trainloader_gt_iter=enumerate(list(gt_list)),
+                    targetloader_nogt_iter=enumerate(list(ng_list)),
+                    testloader=[gt_list[0]], model=model, model_D=model_D,
+                    gan_loss=Rec(nn.BCEWithLogitsLoss(), "gan"),
+                    cls_loss=Rec(nn.CrossEntropyLoss(), "cls"),
+                    optimizer=optimizer, optimizer_D=optimizer_D,
+                    history_pool_gt=pools[0], history_pool_nogt=pools[1],
+                    train_logger=logger, test_logger=logger, writer=None, args=args)
+            finally:
+                rtrainer.make_D_label = orig
+            assert not masks or len(model.dropout.masks) == 0
+            gan = np.array(rec["gan"]).reshape(iters, 3)
+            out[cfg + ".feature_transform"] = int(ft)
+            out[cfg + ".pool_size"] = pool
+            out[cfg + ".loss_cls"] = np.array([rec["cls"][0]] + rec["cls"][2:])
+            out[cfg + ".loss_adv"] = gan[:, 0]
+            out[cfg + ".loss_D_gt"] = gan[:, 1] * 0.5
+            out[cfg + ".loss_D_nogt"] = gan[:, 2] * 0.5
+            if pool:
+                out[cfg + ".pool_gt"] = torch.cat(pools[0].images).numpy()
+                out[cfg + ".pool_nogt"] = torch.cat(pools[1].images).numpy()
+            for name, p in model.named_parameters():
+                summarize(cfg + ".gradG." + name, p.grad.numpy(), out)
+                summarize(cfg + ".paramG." + name, p.detach().numpy(), out)
+            for name, p in model_D.named_parameters():
+                summarize(cfg + ".gradD." + name, p.grad.numpy(), out)
+                summarize(cfg + ".paramD." + name, p.detach().numpy(), out)
+        np.savez_compressed(os.path.join(HERE, "g13_adv_off_fused.npz"), **out)
+
+    if only == "g13":
+        g13()
+        return
     if only == "g12":
         g12()
         return
@@ -538,7 +645,7 @@ def main(ref_root, only=None):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("ref_root", nargs="?", default="/root/reference")
-    ap.add_argument("--only", default=None, help="g7, g8, g9, g10 or g12: regenerate only that "
+    ap.add_argument("--only", default=None, help="g7, g8, g9, g10, g12 or g13: regenerate only that "
                     "fixture; full: g10, g11 and the B=32 g3")
     a = ap.parse_args()
     main(a.ref_root, a.only)

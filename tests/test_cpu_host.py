@@ -25,7 +25,7 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
     assert sorted(_lib.SIGNATURES) == syms  # nothing bound that the header does not declare
-    assert lib.pcadv_abi_version() == 5
+    assert lib.pcadv_abi_version() == 6
 
 
 def test_layout_matches_header_enums():
@@ -182,3 +182,20 @@ def test_image_pool_checks_sample_shape():
         pool.query(torch.ones(2, 40))
     with pytest.raises(ValueError, match="ImagePool"):
         pool.query(torch.ones(2, 7, dtype=torch.float32))
+
+
+def test_shard_order_slices_global_batches():
+    """DeviceCloudLoader's data-parallel sharding (dataset.shard_order): rank r
+    of W takes rows [r B, r B + B) of every whole global batch of W B clouds of
+    the shared epoch order; the ranks' shards tile the whole batches exactly
+    once and the ragged tail is dropped."""
+    import torch
+    from adversarial_learning_on_pointclouds_amd.dataset import shard_order
+    order = torch.randperm(23, generator=torch.Generator().manual_seed(0))
+    B, W = 3, 2
+    shards = [shard_order(order, B, r, W) for r in range(W)]
+    assert all(s.numel() == 3 * B for s in shards)  # 23 // 6 = 3 global batches
+    for k in range(3):
+        glob = order[k * B * W:(k + 1) * B * W]
+        assert torch.equal(torch.cat([s[k * B:(k + 1) * B] for s in shards]), glob)
+    assert torch.equal(shard_order(order, B, 0, 1), order[:21])

@@ -287,7 +287,7 @@ def test_run_training_step_rebuild_keeps_adam_step_count():
         assert float(st["step"]) == iters
 
 
-def _pool_run(pool_size, fused, iters=6):
+def _pool_run(pool_size, fused, iters=6, sizes=(4, 4, 4)):
     """run_training over host batches of 4 + 4 clouds with ImagePool(pool_size)
     on both D inputs; fused=False forces the reference's autograd body (a
     CrossEntropyLoss subclass is off the fused step's configuration)."""
@@ -305,9 +305,9 @@ def _pool_run(pool_size, fused, iters=6):
     G = onp.make_params(onp.cls_spec(40), seed=41)
     Dp = onp.make_params(onp.disc_spec(40, 1), seed=42, init="xavier")
     rng = np.random.default_rng(43)
-    gt = [(torch.from_numpy(rng.uniform(-1, 1, (4, N, 3)).astype(np.float32)),
-           torch.from_numpy(rng.integers(0, 40, 4))) for _ in range(3)]
-    ng = [torch.from_numpy(rng.uniform(-1, 1, (4, N, 3)).astype(np.float32)) for _ in range(3)]
+    gt = [(torch.from_numpy(rng.uniform(-1, 1, (b, N, 3)).astype(np.float32)),
+           torch.from_numpy(rng.integers(0, 40, b))) for b in sizes]
+    ng = [torch.from_numpy(rng.uniform(-1, 1, (b, N, 3)).astype(np.float32)) for b in sizes]
     model, model_D = pc.PointNetCls(k=40), pc.DeepConvDiscNet(40, 1)
     model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
     model_D.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in Dp.items()})
@@ -351,6 +351,20 @@ def test_image_pool_on_fused_step_matches_autograd_body():
     np.testing.assert_allclose(l_f, l_e, rtol=1e-4, atol=1e-6)
     e0 = (d_0 - d_e).norm() / (d_e - D0).norm()
     assert e0 > 0.05, e0
+
+
+def test_image_pool_on_fused_step_ragged_smaller_batches():
+    """the pooled fused step on equal GT / no-GT batches smaller
+    than the step it reuses (4, 4, 2, 4, 4, 2 clouds: the 2-cloud pairs run on
+    the step built for 4, _pooled_d_grads slicing the step's 2B logits) follows
+    the autograd body as the full-batch case does."""
+    g_f, d_f, l_f, _ = _pool_run(3, True, sizes=(4, 4, 2))
+    g_e, d_e, l_e, _ = _pool_run(3, False, sizes=(4, 4, 2))
+    G0, D0 = _pool_run(3, True, iters=0, sizes=(4, 4, 2))[:2]
+    for a, b, a0 in ((g_f, g_e, G0), (d_f, d_e, D0)):
+        e = (a - b).norm() / (b - a0).norm()
+        assert e < 1e-2, e
+    np.testing.assert_allclose(l_f, l_e, rtol=1e-4, atol=1e-6)
 
 
 def _adv_run(tmp_path, use_graph, iters, drop_last, log_every=1):
@@ -523,3 +537,65 @@ def test_graphed_feature_transform_cls_loop_equals_eager(tmp_path, drop_last):
     assert torch.equal(pa, pb)
     assert la == lb and len(la) == 5
     assert all(float(st["step"]) == 5 for st in opt_a.state.values())
+
+
+def _lr_change_run(tmp_path, use_graph, change):
+    """run_training over DeviceCloudLoaders for 6 iterations; the test loader
+    (iterated by run_testing at i_iter 0, 2, 4) raises both optimizers' lr
+    tenfold when it is iterated the second time (a scheduler's effect)."""
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from oracle import pointnet_np as onp
+    lst = _list(tmp_path, ["modelnet_gzip.h5", "modelnet_contig.h5"] * 2)
+    gt_rows = np.array([0, 2, 5, 7, 9, 12])
+    gt = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, gt_rows, npoints=32), 4, seed=11, drop_last=True)
+    ng = D.DeviceCloudLoader(D.ModelNetDataset_noGT(lst, gt_rows, npoints=32), 4, seed=12,
+                             drop_last=True)
+    te = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, None, npoints=32, data_augmentation=False), 4)
+    model, model_D = pc.PointNetCls(k=40), pc.DeepConvDiscNet(40, 1)
+    model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in
+                           onp.make_params(onp.cls_spec(40), seed=31).items()})
+    model_D.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in
+                             onp.make_params(onp.disc_spec(40, 1), seed=32, init="xavier").items()})
+    model.cuda()
+    model_D.cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4)
+
+    class _Test:
+        n = 0
+
+        def __iter__(self):
+            _Test.n += 1
+            if change and _Test.n == 2:
+                for o in (opt, opt_D):
+                    o.param_groups[0]["lr"] = 1e-3
+            return iter(te)
+
+        def __len__(self):
+            return len(te)
+
+    args = argparse.Namespace(device="cuda", total_iterations=6, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=2, exp_dir=str(tmp_path), tensorboard=False,
+                              lambda_cls=1.0, lambda_adv=0.001, batch_size=4, use_graph=use_graph)
+    log = _Log()
+    trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), _Test(), model, model_D,
+                         torch.nn.BCEWithLogitsLoss(),
+                         torch.nn.CrossEntropyLoss(), opt, opt_D, ImagePool(0), ImagePool(0), log,
+                         log, None, args)
+    return torch.cat([p.detach().reshape(-1) for p in list(model.parameters()) +
+                      list(model_D.parameters())]).cpu()
+
+
+def test_graphed_trainer_follows_an_lr_change(tmp_path):
+    """a captured iteration bakes lr / betas / eps in.  When the
+    optimizers' lr changes mid-run, the graphed trainer recaptures (and the
+    fused step re-reads its hyperparameters), so it stays bitwise the eager
+    fused loop, and the change does take effect."""
+    a = _lr_change_run(tmp_path, True, True)
+    b = _lr_change_run(tmp_path, False, True)
+    c = _lr_change_run(tmp_path, True, False)
+    assert torch.equal(a, b)
+    assert not torch.equal(a, c)

@@ -1,0 +1,258 @@
+"""run_training off the fused step against the reference (golden g13, VERDICT
+r04 item 3): three iterations of utils/trainer.py:426-559 captured from the
+reference itself (tests/golden/make_golden.py, g13) in three configurations,
+each driven through THIS package's trainer.run_training:
+
+* ft_pool0: PointNetCls(feature_transform=True) + ImagePool(0) over
+  DeviceCloudLoaders with a capturable Adam: every iteration is the graphed
+  autograd body (trainer._AutogradAdvStep replayed as one HIP graph);
+* plain_pool3: PointNetCls(feature_transform=False) + ImagePool(3): the fused
+  step for G, D's gradient recomputed on the pools' outputs
+  (trainer._pooled_d_grads), then the fused Adam;
+* ft_pool3: both: the eager autograd body (trainer._adv_body).
+
+The reference's dropout masks and soft D labels are injected (the graphed body
+reads them from static device buffers the test refreshes between iterations
+through run_testing's hook; the fused step takes them as its parity-mode
+inputs); the pools draw from Python `random` seeded as in the capture.
+Tolerances: losses 1e-4 absolute (north_star: 1e-3), the last iteration's
+gradients 1e-4 of each tensor's largest entry, the parameters after three Adam
+steps 1e-5.  MI355X only.
+"""
+import argparse
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import check_tensor, check_tensor_rel, load
+
+pytestmark = pytest.mark.gpu
+
+FX = "g13_adv_off_fused.npz"
+
+
+def _models(fx, ft):
+    import adversarial_learning_on_pointclouds_amd as pc
+    from oracle import pointnet_np as onp
+    G = onp.make_params(onp.cls_ft_spec(40) if ft else onp.cls_spec(40), seed=int(fx["g_seed"]))
+    Dp = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
+    m, d = pc.PointNetCls(k=40, feature_transform=ft), pc.DeepConvDiscNet(40, 1)
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    d.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in Dp.items()})
+    return m.cuda(), d.cuda()
+
+
+def _args(fx, **kw):
+    a = dict(device="cuda", total_iterations=int(fx["iters"]), iter_save_epoch=10 ** 9,
+             iter_test_epoch=10 ** 9, exp_dir="/tmp", tensorboard=False,
+             lambda_cls=float(fx["lambda_cls"]), lambda_adv=float(fx["lambda_adv"]),
+             batch_size=int(fx["B"]))
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+class _Log:
+    def __init__(self):
+        self.lines = []
+
+    def info(self, s):
+        self.lines.append(s)
+
+
+def _record_losses(monkeypatch, trainer):
+    """The loss vectors the trainer logs, at full precision (its lines print
+    three decimals): wrap the emit callback of every _LossRing."""
+    raw = []
+    orig = trainer._LossRing.__init__
+
+    def init(self, emit, nl, device, slots=64):
+        def emit2(i_iter, vals, extra):
+            raw.append((i_iter, [float(v) for v in vals[:4]]))
+            emit(i_iter, vals, extra)
+        orig(self, emit2, nl, device, slots)
+    monkeypatch.setattr(trainer._LossRing, "__init__", init)
+    return raw
+
+
+def _check(fx, cfg, raw, model, model_D, grads=True):
+    iters = int(fx["iters"])
+    assert [i for i, _ in raw] == list(range(iters))
+    got = np.array([v for _, v in raw])
+    for j, key in enumerate(("loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt")):
+        np.testing.assert_allclose(got[:, j], fx[f"{cfg}.{key}"], rtol=0, atol=1e-4, err_msg=key)
+    for tag, mod in (("G", model), ("D", model_D)):
+        for nm, p in mod.named_parameters():
+            if grads:
+                check_tensor_rel(fx, f"{cfg}.grad{tag}.{nm}", p.grad.detach().cpu().numpy(), tol=1e-4)
+            check_tensor(fx, f"{cfg}.param{tag}.{nm}", p.detach().cpu().numpy(), tol=1e-5)
+
+
+def _soft_patch(monkeypatch, trainer, source):
+    """make_D_label(random=True) returns source() (GT call first, then no-GT)."""
+    orig = trainer.make_D_label
+
+    def make_D_label(input, value, device, random=False):
+        if not random:
+            return orig(input, value, device, random=False)
+        return source(value).view(input.shape)
+    monkeypatch.setattr(trainer, "make_D_label", make_D_label)
+
+
+def test_g13_graphed_feature_transform_adv_body(monkeypatch, tmp_path):
+    """ft_pool0: the graphed autograd adversarial iteration (the bench
+    --config adv_ft path) held to the reference for three iterations."""
+    from adversarial_learning_on_pointclouds_amd import dataset as D
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    fx = load(FX)
+    cfg, iters, B = "ft_pool0", int(fx["iters"]), int(fx["B"])
+    dev = torch.device("cuda")
+    # the golden batches as a resident split, gathered in order (no shuffle, no jitter)
+    gt_ds = object.__new__(D.ModelNetDatasetGT)
+    gt_ds.select_data = fx["pts_gt"].reshape(iters * B, -1, 3)
+    gt_ds.select_labels = fx["labels"].reshape(-1).astype(np.int32)
+    gt_ds.data_augmentation = False
+    ng_ds = object.__new__(D.ModelNetDataset_noGT)
+    ng_ds.select_data = fx["pts_nogt"].reshape(iters * B, -1, 3)
+    ng_ds.data_augmentation = False
+    gt = D.DeviceCloudLoader(gt_ds, B, shuffle=False, seed=1, drop_last=True)
+    ng = D.DeviceCloudLoader(ng_ds, B, shuffle=False, seed=2, drop_last=True)
+    model, model_D = _models(fx, True)
+    # static device buffers of the current iteration's masks / soft labels
+    mbuf = torch.zeros(2, B, 256, device=dev)
+    sbuf = torch.zeros(2, B, device=dev)
+
+    def load_iter(i):
+        mbuf.copy_(torch.from_numpy(fx["masks"][i]))
+        sbuf.copy_(torch.from_numpy(fx["soft"][i]))
+    load_iter(0)
+    calls = {"m": 0, "s": 0}
+
+    def dropout_mask(B_, device):
+        if not model.training:
+            return None
+        k = calls["m"] % 2  # model(pts) then model(pts_nogt)
+        calls["m"] += 1
+        return mbuf[k]
+    monkeypatch.setattr(model, "_dropout_mask", dropout_mask)
+
+    def soft(value):
+        k = calls["s"] % 2
+        calls["s"] += 1
+        assert value == (1 if k == 0 else 0)
+        return sbuf[k]
+    _soft_patch(monkeypatch, trainer, soft)
+
+    class _Test:  # run_testing iterates it after every iteration: load the next draws
+        n = 0
+
+        def __iter__(self):
+            _Test.n += 1
+            if _Test.n < iters:
+                load_iter(_Test.n)
+            return iter(())
+
+        def __len__(self):
+            return 1
+    raw = _record_losses(monkeypatch, trainer)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), capturable=True)
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999), capturable=True)
+    assert trainer._AutogradAdvStep.graphable(opt, opt_D, (ImagePool(0), ImagePool(0)),
+                                              _args(fx), (gt, ng))
+    graphs = []
+    orig_graph = trainer._GraphedIteration._graph
+
+    def spy(self, semi):
+        g = orig_graph(self, semi)
+        graphs.append(g)
+        return g
+    monkeypatch.setattr(trainer._GraphedIteration, "_graph", spy)
+    trainer.run_training(gt, ng, None, None, _Test(), model, model_D,
+                         torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(), opt, opt_D,
+                         ImagePool(0), ImagePool(0), _Log(), _Log(), None,
+                         _args(fx, iter_test_epoch=1, exp_dir=str(tmp_path)))
+    assert len(graphs) == iters  # every iteration replayed the captured body
+    _check(fx, cfg, raw, model, model_D)
+
+
+def _host_batches(fx):
+    iters = int(fx["iters"])
+    gt = [(torch.from_numpy(fx["pts_gt"][i]), torch.from_numpy(fx["labels"][i])) for i in range(iters)]
+    ng = [torch.from_numpy(fx["pts_nogt"][i]) for i in range(iters)]
+    return gt, ng
+
+
+def _soft_queue(fx):
+    q = [torch.from_numpy(fx["soft"][i, k]).cuda() for i in range(int(fx["iters"])) for k in (0, 1)]
+
+    def soft(value):
+        return q.pop(0)
+    return soft, q
+
+
+def test_g13_pooled_fused_step(monkeypatch, tmp_path):
+    """plain_pool3: run_training with ImagePool(3) pools on the fused step
+    (trainer._pooled_d_grads) held to the reference; the pools end holding the
+    reference's images."""
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+    fx = load(FX)
+    cfg, iters = "plain_pool3", int(fx["iters"])
+    model, model_D = _models(fx, False)
+    mask_list = [torch.from_numpy(fx["masks"][i, k]).cuda() for i in range(iters) for k in (0, 1)]
+    soft_list = [torch.from_numpy(fx["soft"][i, k]).cuda() for i in range(iters) for k in (0, 1)]
+    orig_call = AdvTrainStep.__call__
+    fused_calls = []
+
+    def call(self, pts_gt, labels, pts_nogt, masks=None, soft=None, apply_adam=True, semi=False,
+             part=0):
+        assert masks is None and soft is None
+        fused_calls.append(apply_adam)
+        i = len(fused_calls) - 1  # the reference's draws of this iteration
+        return orig_call(self, pts_gt, labels, pts_nogt, (mask_list[2 * i], mask_list[2 * i + 1]),
+                         (soft_list[2 * i], soft_list[2 * i + 1]), apply_adam, semi, part)
+    monkeypatch.setattr(AdvTrainStep, "__call__", call)
+    soft, q = _soft_queue(fx)
+    _soft_patch(monkeypatch, trainer, soft)
+    raw = _record_losses(monkeypatch, trainer)
+    gt, ng = _host_batches(fx)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    pools = ImagePool(3), ImagePool(3)
+    random.seed(int(fx["random_seed"]))
+    trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), [gt[0]], model, model_D,
+                         torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(), opt, opt_D,
+                         *pools, _Log(), _Log(), None, _args(fx, exp_dir=str(tmp_path)))
+    assert fused_calls == [False] * iters and not q  # every iteration pooled on the fused step
+    _check(fx, cfg, raw, model, model_D)
+    for k, p in (("pool_gt", pools[0]), ("pool_nogt", pools[1])):
+        np.testing.assert_allclose(p._bank[:p.num_imgs].cpu().numpy(), fx[f"{cfg}.{k}"],
+                                   rtol=0, atol=1e-5)
+
+
+def test_g13_eager_feature_transform_pooled_body(monkeypatch, tmp_path):
+    """ft_pool3: the reference's body through autograd over the layer-by-layer
+    kernels with the pools (neither fused nor graphed) held to the reference."""
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    fx = load(FX)
+    cfg, iters = "ft_pool3", int(fx["iters"])
+    model, model_D = _models(fx, True)
+    model.dropout_masks = [torch.from_numpy(fx["masks"][i, k]).cuda()
+                           for i in range(iters) for k in (0, 1)]
+    soft, q = _soft_queue(fx)
+    _soft_patch(monkeypatch, trainer, soft)
+    raw = _record_losses(monkeypatch, trainer)
+    gt, ng = _host_batches(fx)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    random.seed(int(fx["random_seed"]))
+    trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), [gt[0]], model, model_D,
+                         torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(), opt, opt_D,
+                         ImagePool(3), ImagePool(3), _Log(), _Log(), None,
+                         _args(fx, exp_dir=str(tmp_path)))
+    assert not model.dropout_masks and not q
+    _check(fx, cfg, raw, model, model_D)

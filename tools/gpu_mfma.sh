@@ -19,5 +19,5 @@ for cfg in adv cls seg; do
     python bench.py --no-cpu --repeats 1 $args > $d.log 2>&1
   rc=$?; echo "mfma $cfg rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $d.log; exit $rc; fi
-  python tools/pmc_mfma.py $d profiles/${tag}_${cfg}_mfma.json "python bench.py $args" || exit 1
+  python tools/pmc_mfma.py $d gpurun_out/${tag}_${cfg}_mfma.json "python bench.py $args" || exit 1
 done
