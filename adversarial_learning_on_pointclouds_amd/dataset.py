@@ -371,14 +371,17 @@ class DeviceCloudLoader:
         for k in range(len(self)):
             yield order[k * self.B:(k + 1) * self.B]
 
-    def gather_at(self, order, cursor, out, out_lab=None):
+    def gather_at(self, order, cursor, out, out_lab=None, out_seg=None):
         """Batch *cursor (device int32) of the epoch order `order` (int64, on the
-        device) into `out` / `out_lab`: the graph-replayed form of gather (no
-        host copy per batch).  The step counter is NOT advanced here: the
-        caller advances it and the cursor (pcadv_iter_epilogue)."""
+        device) into `out` / `out_lab` (/ `out_seg`, the part ids of a ShapeNet
+        split): the graph-replayed form of gather (no host copy per batch).
+        The step counter is NOT advanced here: the caller advances it and the
+        cursor (pcadv_iter_epilogue)."""
         lw = 0 if self.labels is None else int(self.labels.shape[1])
         if out_lab is None and self.labels is not None:
             raise ValueError("gather_at: out_lab required for a labelled split")
+        if (out_seg is None) != (self.segs is None):
+            raise ValueError("gather_at: out_seg goes with (and only with) a part-labelled split")
         B = self.B
 
         def need(t, name, shape, dtype):
@@ -389,14 +392,16 @@ class DeviceCloudLoader:
         need(out, "out", (B, self.npts, 3), torch.float32)
         if self.labels is not None:
             need(out_lab, "out_lab", (B, lw), torch.int64)
+        if out_seg is not None:
+            need(out_seg, "out_seg", (B, self.npts), torch.int64)
         need(order, "order", (self.order_len,), torch.int64)
         need(cursor, "cursor", (1,), torch.int32)
         P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         check(self.lib.pcadv_gather_clouds_at(P(self.pts), self.n, self.npts, self.npts, P(order),
-                                              P(cursor), self.B, P(self.labels), lw, None,
-                                              self.sigma, self.clip, self.seed, P(self.step),
-                                              P(out), P(out_lab), None, self.rank * self.B,
-                                              stream_ptr()),
+                                              P(cursor), self.B, P(self.labels), lw,
+                                              P(self.segs), self.sigma, self.clip, self.seed,
+                                              P(self.step), P(out), P(out_lab), P(out_seg),
+                                              self.rank * self.B, stream_ptr()),
               "pcadv_gather_clouds_at")
 
     def __iter__(self):

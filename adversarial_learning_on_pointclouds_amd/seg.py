@@ -642,6 +642,23 @@ class SegTrainStep:
             dst.copy_(src)
         return g
 
+    @property
+    def losses(self):
+        """The loss as a 1-vector (the trainers' loss-ring interface)."""
+        return self.loss.view(1)
+
+    def graph_state(self):
+        """What a captured iteration's warm-up changes (restored after it)."""
+        return [self.param, self.m, self.v, self.step_count]
+
+    def sync_hyper(self):
+        """lr / betas / eps as the optimizer holds them now (a graph captured
+        before keeps the old values: the trainer recaptures on a change)."""
+        if self.optimizer is not None:
+            g = self.optimizer.param_groups[0]
+            self.lr, self.betas, self.eps = float(g["lr"]), tuple(float(b) for b in g["betas"]), \
+                float(g["eps"])
+
     def sync_optimizer_state(self):
         t = float(self.step_count.item())
         if self.optimizer is not None:

@@ -357,6 +357,29 @@ class _DPIteration(_GraphedIteration):
         return st.losses
 
 
+class _SegGraphedIteration(_GraphedIteration):
+    """run_training_pointnet_seg's iteration fed by a ShapeNet DeviceCloudLoader
+    as ONE HIP graph: the batch gather (points, class ids, part ids, device
+    jitter) at the device cursor, the one-hot class vector built on the device,
+    SegTrainStep (forward, per-point CE, backward, Adam), and the iteration
+    epilogue (counters += 1, the loss into the ring)."""
+
+    def __init__(self, step, loader, ring, optimizers=()):
+        step.B, step.N = loader.B, loader.npts  # the static batch shape
+        super().__init__(step, (loader,), ring, optimizers)
+        dev = step.device
+        self.seg = torch.zeros(loader.B, loader.npts, dtype=torch.int64, device=dev)
+        self.oh = torch.zeros(loader.B, 1, loader.ds.num_classes, device=dev)
+
+    def _body(self, semi):
+        ld = self.loaders[0]
+        ld.gather_at(self.order[0], self.counters[1:2], self.pts[0], self.lab, out_seg=self.seg)
+        self.oh.zero_()
+        self.oh.scatter_(2, self.lab[:, :1].unsqueeze(1), 1.0)  # one_hot (shapeNetData.py)
+        self.step(self.pts[0], self.oh, self.seg)
+        self.ring.write(self.step.loss.view(1), self.counters, 2)
+
+
 def _dp_world(*loaders):
     """World size of data-parallel (sharded) DeviceCloudLoaders, 1 if none;
     every loader must agree."""
@@ -945,6 +968,7 @@ def run_training_pointnet_seg(trainloader_gt, trainloader_gt_iter, testloader, t
     the HIP device each iteration is one SegTrainStep (forward, per-point CE,
     backward into a flat gradient buffer, one Adam launch); otherwise the
     reference's body runs through autograd over the same kernels."""
+    from .dataset import DeviceCloudLoader
     from .seg import PointNetSeg, SegTrainStep
     max_test_accu = max_test_cat_iou = max_test_all_iou = float("-inf")
     max_train_epoch = max_train_cat_epoch = max_train_all_epoch = 0
@@ -956,35 +980,73 @@ def run_training_pointnet_seg(trainloader_gt, trainloader_gt_iter, testloader, t
              and seg_loss.reduction == "mean" and seg_loss.ignore_index < 0
              and seg_loss.label_smoothing == 0.0 and str(args.device).split(":")[0] == "cuda")
     step = None
+    # fast path: a ShapeNet DeviceCloudLoader (the split resident in HBM) runs
+    # every full batch as one HIP graph (_SegGraphedIteration); the loss lines
+    # are read from the device ring asynchronously (no host sync per iteration)
+    graphed = (fused and bool(getattr(args, "use_graph", True))
+               and isinstance(trainloader_gt, DeviceCloudLoader)
+               and trainloader_gt.kind == "shapenet_gt")
+    gi = None
+    log_every = max(1, int(getattr(args, "log_every", 1)))
+    tb = getattr(args, "tensorboard", False) and writer is not None
+
+    def emit(i_iter, vals, extra):
+        train_logger.info("iter = {0:8d}/{1:8d} loss_seg = {2:.3f} ".format(
+            i_iter, args.total_iterations, vals[0]))
+        if tb:
+            writer.add_scalar("Loss/train_seg", vals[0], i_iter)
+
+    log = _LossRing(emit, 1, args.device)
+
+    def fused_step():
+        nonlocal step
+        if step is None:
+            step = SegTrainStep(model, optimizer=optimizer, lambda_seg=args.lambda_seg,
+                                device=args.device)
+        step.sync_hyper()
+        return step
+
     for i_iter in range(args.total_iterations):
-        model.train()
-        batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
-        pts, cls, seg = batch
-        pts = pts.float().to(args.device).contiguous()
-        cls = cls.float().to(args.device).contiguous()
-        seg = seg.long().to(args.device).contiguous()
-        if fused:
-            if step is None:
-                step = SegTrainStep(model, optimizer=optimizer, lambda_seg=args.lambda_seg,
-                                    device=args.device)
-            loss_seg_value = float(step(pts, cls, seg).item())
+        if i_iter == 0 or not model.training:  # only run_testing_seg's eval() changes it here
+            model.train()
+        loss = None
+        if graphed:
+            if gi is None:
+                gi = _SegGraphedIteration(fused_step(), trainloader_gt, log, optimizers=(optimizer,))
+            bt = gi.next_batches()
+            if bt[0][1] == trainloader_gt.B:
+                loss = gi.replay()
+                fused_step()  # the eager step's hyperparameters follow the optimizer too
+            else:  # a ragged last batch, gathered eagerly from the same epoch order
+                (pts, cls, seg), = gi.eager_batches(bt)
+        else:
+            batch, trainloader_gt_iter = _next(trainloader_gt, trainloader_gt_iter)
+            pts, cls, seg = batch
+        if loss is None:
+            pts = pts.float().to(args.device).contiguous()
+            cls = cls.float().to(args.device).contiguous()
+            seg = seg.long().to(args.device).contiguous()
+            if fused:
+                loss = fused_step()(pts, cls, seg)
+                log.write(loss.view(1))
+        if loss is not None:
+            log.record(i_iter, None, log=i_iter % log_every == 0)
         else:
             optimizer.zero_grad()
             pred, global_gt = model(pts, cls)
             l = seg_loss(pred, seg)
-            loss_seg_value = l.item()
             (args.lambda_seg * l).backward()
             optimizer.step()
-        train_logger.info("iter = {0:8d}/{1:8d} loss_seg = {2:.3f} ".format(
-            i_iter, args.total_iterations, loss_seg_value))
-        if getattr(args, "tensorboard", False) and writer is not None:
-            writer.add_scalar("Loss/train_seg", loss_seg_value, i_iter)
+            if i_iter % log_every == 0:
+                log.emit_now(i_iter, [l.item()])
         if i_iter % args.iter_save_epoch == 0:
+            log.drain()
             if step is not None:
                 step.sync_optimizer_state()
             torch.save(model.state_dict(), os.path.join(
                 args.exp_dir, "model_train_epoch_{}.pth".format(i_iter // len(trainloader_gt))))
         if i_iter % args.iter_test_epoch == 0:
+            log.drain()
             accu, _, cat_iou, all_iou = run_testing_seg(testloader, testdataset, model, seg_loss,
                                                         test_logger, i_iter, writer, args)
             for tag, val in (("accu", accu), ("cat_iou", cat_iou), ("all_iou", all_iou)):
@@ -1000,6 +1062,7 @@ def run_training_pointnet_seg(trainloader_gt, trainloader_gt_iter, testloader, t
                         max_test_all_iou, max_train_all_epoch = val, ep
                     torch.save(model.state_dict(),
                                os.path.join(args.exp_dir, "model_train_best_{}.pth".format(tag)))
+    log.drain()
     if step is not None:
         step.sync_optimizer_state()
     if getattr(args, "tensorboard", False) and writer is not None:

@@ -270,6 +270,87 @@ def cpu_baseline_cls(seconds):
             "sample": f"{steps} numpy-oracle cls steps (B=32, N=1024, fp32) in {dt:.1f}s"}
 
 
+def _time_loop(one, seconds):
+    one()
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        one()
+        steps += 1
+        if time.perf_counter() - t0 >= seconds and steps >= 2:
+            break
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline_ft(seconds, adversarial):
+    """The numpy oracle's feature-transform iterations on the host cores (B=32,
+    N=1024): run_training_pointnet_cls's (oracle.cls_ft_step: forward with the
+    STNkd(64) transform, CE + 0.001 x regulariser, backward; Adam), or for the
+    adversarial iteration two such generator passes (the GT and no-GT batches,
+    as the reference runs model() twice) plus the discriminator's three
+    forward and two backward passes and both Adams."""
+    from oracle import pointnet_np as onp
+    G = onp.make_params(onp.cls_ft_spec(40), seed=3)
+    Dp = onp.make_params(onp.disc_spec(40, 1), seed=4, init="xavier")
+    optG, optD = onp.Adam(G), onp.Adam(Dp)
+    rng = np.random.default_rng(3000)
+    pts = [rng.uniform(-1, 1, (B, N, 3)).astype(np.float32) for _ in range(2)]
+    lab = rng.integers(0, 40, B)
+    m = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+
+    def one():
+        _, _, g, aux = onp.cls_ft_step(G, pts[0], lab, m)
+        if adversarial:
+            _, _, g2, aux2 = onp.cls_ft_step(G, pts[1], lab, m)
+            for k in g:
+                g[k] = g[k] + g2[k]
+            y = np.full((B, 1), 0.9, np.float32)
+            gD = None
+            for logits in (aux2["logits"], aux["logits"], aux2["logits"]):
+                d, acts = onp.disc_forward(Dp, onp.log_softmax(logits))
+                _, dd = onp.bce_with_logits(d, y)
+                gd, _ = onp.disc_backward(Dp, acts, dd)
+                gD = gd if gD is None else {k: gD[k] + gd[k] for k in gD}
+            optD.step(gD)
+        optG.step(g)
+    steps, dt = _time_loop(one, seconds)
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    clouds = (2 if adversarial else 1) * B
+    what = ("adversarial feature-transform iterations (2 x cls_ft_step + 3 D passes, B=32+32)"
+            if adversarial else "cls_ft_step iterations (B=32)")
+    return {"value": round(clouds * steps / dt, 2), "unit": "clouds/s", "cores": cores,
+            "kind": "port", "sample": f"{steps} numpy-oracle {what}, N=1024, fp32, in {dt:.1f}s"}
+
+
+def ft_roofline(C):
+    """The feature-transform steps' dominant kernel: the 1024-channel conv +
+    max over points (k_conv4_max, twice per generator pass: STNkd conv3 and
+    PointNetfeat conv4) on C clouds, timed from a graph of 50 launches on
+    post-ReLU inputs; achieved = algorithmic f32 FLOPs / launch time against
+    the dense bf16 MFMA peak (the pipe its split products run on)."""
+    from adversarial_learning_on_pointclouds_amd import ops
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(9)
+    x = torch.relu(torch.randn(C, N, 128, device=dev, generator=g))
+    w = torch.randn(1024, 128, device=dev, generator=g) * (1.0 / 128 ** 0.5)
+    b = torch.zeros(1024, device=dev)
+    gmax = torch.empty(C, 1024, device=dev)
+    gidx = torch.empty(C, 1024, device=dev, dtype=torch.int32)
+    t = _graph_time(lambda: ops.conv4_max(x, w, b, precision="fp32", out=(gmax, gidx)))
+    f = 2.0 * C * N * 128 * 1024
+    return {"bound": "mfma",
+            "kernel": f"k_conv4_max<3> (1024-channel conv + max over points, {C} clouds x {N} "
+                      "points; STNkd conv3 / PointNetfeat conv4)",
+            "achieved": round(f / t / 1e12, 2), "peak": BF16_PEAK, "unit": "TFLOP/s",
+            "frac": round(f / t / 1e12 / BF16_PEAK, 4),
+            "issued_frac": round(3 * f / t / 1e12 / BF16_PEAK, 4),
+            "traffic": None, "avg_launch_us": round(t * 1e6, 2),
+            "algorithmic_flops_per_launch": f,
+            "algorithmic_bytes_per_launch": C * N * 128 * 4 + 1024 * 128 * 4 + C * 1024 * 8,
+            "peak_basis": "dense bf16 MFMA 2500 TF; achieved = algorithmic f32 FLOPs / HIP-event "
+                          "launch time (graph of 50)"}
+
+
 BF16_PEAK, F32_PEAK = 2500.0, 157.3  # dense TFLOP/s (MI355X_MICROARCH.md)
 
 
@@ -289,6 +370,22 @@ def _pmc_traffic(pattern, prefixes, only_if=True):
     if not all(names):
         return None, None
     return round(sum(kern[n]["traffic_bytes"] for n in names)), os.path.relpath(prof[-1], REPO)
+
+
+def _pmc_mfma(cfg, prefix):
+    """Matrix-pipe utilisation of the named kernel from the newest committed
+    profiles/r*_<cfg>_mfma.json (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES /
+    (1024 SIMDs x GRBM_GUI_ACTIVE / 8), median over the profiled launches), or
+    (None, None)."""
+    prof = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}_mfma.json")))
+    if not prof:
+        return None, None
+    kern = json.load(open(prof[-1]))["kernels"]
+    hits = [v for k, v in kern.items() if k.startswith(prefix)]
+    if not hits:
+        return None, None
+    best = max(hits, key=lambda v: v["SQ_VALU_MFMA_BUSY_CYCLES"])
+    return best["mfma_busy"], os.path.relpath(prof[-1], REPO)
 
 
 def _graph_time(fn, reps=50):
@@ -312,7 +409,7 @@ def _graph_time(fn, reps=50):
     return ev0.elapsed_time(ev1) / 1e3 / reps
 
 
-def feat_roofline(pts_all, fw, prec, traffic_pattern=None):
+def feat_roofline(pts_all, fw, prec, traffic_pattern=None, mfma_cfg=None):
     """The roofline block for the dominant kernel, k_conv4_max (conv4 + max over
     points, models/pointnet.py:128-130), and the same figures for the feature
     forward pair (k_point_mlp + k_conv4_max, conv1..conv4).  achieved = the
@@ -341,6 +438,7 @@ def feat_roofline(pts_all, fw, prec, traffic_pattern=None):
                                    traffic_pattern is not None)
     ach4 = f4 / k2_s / 1e12
     ach_pair = (f12 + f3 + f4) / pair_s / 1e12
+    busy, busy_src = _pmc_mfma(mfma_cfg, f"k_conv4_max<{np4},") if mfma_cfg else (None, None)
     return {
         "bound": "mfma",
         "kernel": f"k_conv4_max<{np4}> (conv4 128->1024 + max over points, {C} clouds x {Np} points)",
@@ -350,6 +448,10 @@ def feat_roofline(pts_all, fw, prec, traffic_pattern=None):
         "traffic": traffic4,
         "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
         "traffic_source": src,
+        "mfma_busy": busy,
+        "mfma_busy_unit": "fraction of SIMD-cycles the matrix pipe is busy (PMC "
+                          "SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8))",
+        "mfma_busy_source": busy_src,
         "avg_launch_us": round(k2_s * 1e6, 2),
         "algorithmic_flops_per_launch": f4,
         "algorithmic_bytes_per_launch": alg_bytes4,
@@ -435,7 +537,8 @@ def bench_cls(args):
           model.feat.conv2.bias, model.feat.conv3.weight, model.feat.conv3.bias,
           model.feat.conv4.weight, model.feat.conv4.bias]
     roof = feat_roofline(pool[(args.steps - 1) % POOL][0], fw, prec,
-                         "r*_cls_pmc_traffic.json" if prec == "bf16" else None)
+                         "r*_cls_pmc_traffic.json" if prec == "bf16" else None,
+                         "cls" if prec == "bf16" else None)
     out = {
         "metric": "point-clouds/sec (cls train step, no discriminator), B=32 N=1024 ModelNet40, 1 GPU",
         "value": round(B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
@@ -544,6 +647,9 @@ def bench_cls_ft(args):
     }
     if why:
         out["graph_capture_error"] = why
+    out["roofline"] = ft_roofline(B)
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_ft(args.cpu_seconds, adversarial=False)
     print(json.dumps(_with_runtime(out)), flush=True)
 
 
@@ -632,6 +738,9 @@ def bench_adv_ft(args):
     }
     if why:
         out["graph_capture_error"] = why
+    out["roofline"] = ft_roofline(B)  # each generator pass runs it on one B-cloud batch
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_ft(args.cpu_seconds, adversarial=True)
     print(json.dumps(_with_runtime(out)), flush=True)
 
 
@@ -822,6 +931,8 @@ def bench_seg(args):
     kern_s = ev0.elapsed_time(ev1) / 1e3 / reps
     kflops = 2.0 * Bs * Ns * 512 * 2048
     kissued = 3 * kflops  # three bf16 MFMA products per f32 product (hi/lo splits)
+    busy, busy_src = _pmc_mfma("seg", "k_gemm_bf2_big<2" if big else "k_gemm_x3<2, 2, 2, 3>") \
+        if precision == "fp32" else (None, None)
     traffic, traffic_src = _pmc_traffic(
         "r*_seg_pmc_traffic.json",
         ("pcadv::k_gemm_bf2_big<2" if big else "pcadv::k_gemm_x3<2, 2, 2, 3>", "pcadv::k_max_combine"))
@@ -850,6 +961,7 @@ def bench_seg(args):
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)",
                      "traffic_source": traffic_src, "avg_launch_us": round(kern_s * 1e6, 2),
+                     "mfma_busy": busy, "mfma_busy_source": busy_src,
                      "algorithmic_flops_per_launch": kflops,
                      "algorithmic_bytes_per_launch": Bs * Ns * 512 * 4 + 2048 * 512 * 4 + Bs * 2048 * 8,
                      "issued_bf16_flops_per_launch": kissued,
@@ -964,7 +1076,8 @@ def main():
           model.feat.conv4.weight, model.feat.conv4.bias]
     # the committed PMC passes ran the default workload (fp32, N = 1024)
     roof = feat_roofline(pts_all, fw, adv_prec,
-                         "r*_pmc_traffic.json" if (N == 1024 and adv_prec == "fp32") else None)
+                         "r*_pmc_traffic.json" if (N == 1024 and adv_prec == "fp32") else None,
+                         "adv" if (N == 1024 and adv_prec == "fp32") else None)
     pair = roof["pair"]
     # algorithmic FLOPs of one B=32 adversarial step (44.53 at N=2048)
     step_gflop = 22.47 if N == 1024 else 22.47 * N / 1024.0

@@ -397,9 +397,26 @@ def main(ref_root, only=None):
             optimizer_D = torch.optim.Adam(model_D.parameters(), lr=1e-4, betas=(0.9, 0.999))
             args = argparse.Namespace(device=torch.device("cpu"), total_iterations=iters,
                                       lambda_cls=1.0, lambda_adv=0.01, iter_save_epoch=10 ** 9,
-                                      iter_test_epoch=10 ** 9,
+                                      iter_test_epoch=1,
                                       exp_dir=tempfile.mkdtemp(prefix="g13_"), tensorboard=False,
                                       batch_size=B)
+            snaps = []
+
+            class SnapTest:
+                """run_testing iterates this after every iteration: the
+                iteration's gradients (p.grad until the next zero_grad)."""
+
+                def __init__(self, batch):
+                    self.batch = batch
+
+                def __iter__(self, _m=model, _d=model_D):
+                    snaps.append({("G", n): p.grad.detach().clone() for n, p in _m.named_parameters()}
+                                 | {("D", n): p.grad.detach().clone()
+                                    for n, p in _d.named_parameters()})
+                    return iter([self.batch])
+
+                def __len__(self):
+                    return 1
             gt_list = [(torch.from_numpy(a), torch.from_numpy(b)) for a, b in batches_gt]
             ng_list = [torch.from_numpy(a) for a in batches_ng]
             logger = logging.getLogger("golden13")
@@ -413,7 +430,7 @@ def main(ref_root, only=None):
                     trainloader_gt=gt_list, trainloader_nogt=ng_list,
                     trainloader_gt_iter=enumerate(list(gt_list)),
                     targetloader_nogt_iter=enumerate(list(ng_list)),
-                    testloader=[gt_list[0]], model=model, model_D=model_D,
+                    testloader=SnapTest(gt_list[0]), model=model, model_D=model_D,
                     gan_loss=Rec(nn.BCEWithLogitsLoss(), "gan"),
                     cls_loss=Rec(nn.CrossEntropyLoss(), "cls"),
                     optimizer=optimizer, optimizer_D=optimizer_D,
@@ -425,18 +442,21 @@ def main(ref_root, only=None):
             gan = np.array(rec["gan"]).reshape(iters, 3)
             out[cfg + ".feature_transform"] = int(ft)
             out[cfg + ".pool_size"] = pool
-            out[cfg + ".loss_cls"] = np.array([rec["cls"][0]] + rec["cls"][2:])
+            out[cfg + ".loss_cls"] = np.array(rec["cls"][0::2])  # train / test alternate
             out[cfg + ".loss_adv"] = gan[:, 0]
             out[cfg + ".loss_D_gt"] = gan[:, 1] * 0.5
             out[cfg + ".loss_D_nogt"] = gan[:, 2] * 0.5
             if pool:
                 out[cfg + ".pool_gt"] = torch.cat(pools[0].images).numpy()
                 out[cfg + ".pool_nogt"] = torch.cat(pools[1].images).numpy()
+            assert len(snaps) == iters
             for name, p in model.named_parameters():
                 summarize(cfg + ".gradG." + name, p.grad.numpy(), out)
+                summarize(cfg + ".grad1G." + name, snaps[0][("G", name)].numpy(), out)
                 summarize(cfg + ".paramG." + name, p.detach().numpy(), out)
             for name, p in model_D.named_parameters():
                 summarize(cfg + ".gradD." + name, p.grad.numpy(), out)
+                summarize(cfg + ".grad1D." + name, snaps[0][("D", name)].numpy(), out)
                 summarize(cfg + ".paramD." + name, p.detach().numpy(), out)
         np.savez_compressed(os.path.join(HERE, "g13_adv_off_fused.npz"), **out)
 

@@ -119,6 +119,53 @@ def test_seg_trainer_end_to_end_on_device_batches(tmp_path):
     assert (tmp_path / "model_train_epoch_0.pth").exists()
 
 
+def _seg_run(tmp_path, use_graph, drop_last, iters=7):
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    torch.manual_seed(0)
+    lst = _list(tmp_path, ["shapenet_latest.h5"])
+    train = D.ShapeNetDatasetGT(np.arange(5), lst, num_classes=16, num_pts=48)
+    test = D.ShapeNetDatasetGT(None, lst, num_classes=16, num_pts=48)
+    tl = D.DeviceCloudLoader(train, batch_size=2, shuffle=True, seed=1, drop_last=drop_last)
+    vl = D.DeviceCloudLoader(test, batch_size=3, shuffle=False)
+    model = pc.PointNetSeg(50).cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    args = argparse.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=4, exp_dir=str(tmp_path), tensorboard=False,
+                              lambda_seg=1.0, input_pts=48, use_graph=use_graph)
+    log = _Log()
+    graphs = []
+    orig = trainer._SegGraphedIteration.replay
+
+    def spy(self, semi=False):
+        graphs.append(1)
+        return orig(self, semi)
+    trainer._SegGraphedIteration.replay = spy
+    try:
+        trainer.run_training_pointnet_seg(tl, enumerate(tl), vl, test, model,
+                                          torch.nn.CrossEntropyLoss(), opt, log, log, None, args)
+    finally:
+        trainer._SegGraphedIteration.replay = orig
+    params = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+    return params, [l for l in log.lines if "loss_seg" in l], len(graphs), opt
+
+
+@pytest.mark.parametrize("drop_last", [True, False])
+def test_graphed_seg_trainer_equals_eager(tmp_path, drop_last):
+    """run_training_pointnet_seg over a ShapeNet DeviceCloudLoader with each
+    full iteration (gather + one-hot + SegTrainStep + epilogue) replayed as one
+    HIP graph, loss lines read from the device ring: bitwise the eager loop
+    (parameters, loss lines, Adam step count), across epoch wrap-arounds and,
+    with drop_last=False, the ragged last batch (run eagerly in between)."""
+    pa, la, na, opt = _seg_run(tmp_path, True, drop_last)
+    pb, lb, nb, _ = _seg_run(tmp_path, False, drop_last)
+    assert na == (7 if drop_last else 5) and nb == 0
+    assert torch.equal(pa, pb)
+    assert la == lb and len(la) == 7
+    assert all(float(st["step"]) == 7 for st in opt.state.values())
+
+
 def test_semi_trainer_end_to_end_on_device_batches(tmp_path):
     """run_training_semi (trainer.py:611-847) fed by DeviceCloudLoader over
     ModelNet-format files with the GT / no-GT split of sample_list."""
