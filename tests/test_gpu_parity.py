@@ -790,8 +790,21 @@ def test_cls_step_bf16_full_size_vs_oracle():
 # (relative L2); conv4 2.6e-2 .. 5.8e-2; conv1..conv3 0.09 .. 0.17 -- the
 # bf16-rounded conv4 operands move the argmax of the channels whose top two
 # points lie within bf16 resolution, and each moved argmax reroutes a whole
-# row of conv1..conv3's gradient.  The bounds below are ~2x those figures.
-BF16_VS_REF = dict(loss=1e-4, logits=2e-3, gmax=1e-2, head=6e-2, conv4=0.12, conv13=0.35)
+# row of conv1..conv3's gradient.  Per quantity, the HIP path measured on
+# MI355X (round 5; the test prints them) -- equal to the oracle's figures to
+# the digits shown: loss 1.19e-6, logits 6.42e-4, gmax 2.58e-3; gradients
+# (relative L2) conv1 0.135 / 0.155, conv2 0.135 / 0.169, conv3 0.0996 /
+# 0.0917, conv4 0.058 / 0.0264, fc1 0.0238 / 0.0272, fc2 3.11e-3 / 0.0176, fc3
+# 1.04e-3 / 9.47e-6 (weight / bias).  The bounds are 1.2x those (2e-5 at
+# least), so a regression that moves any of them by a fifth fails.
+_BF16_MEASURED = {"loss": 1.19e-6, "logits": 6.42e-4, "gmax": 2.58e-3,
+                  "feat.conv1.weight": 0.135, "feat.conv1.bias": 0.155,
+                  "feat.conv2.weight": 0.135, "feat.conv2.bias": 0.169,
+                  "feat.conv3.weight": 0.0996, "feat.conv3.bias": 0.0917,
+                  "feat.conv4.weight": 0.058, "feat.conv4.bias": 0.0264,
+                  "fc1.weight": 0.0238, "fc1.bias": 0.0272, "fc2.weight": 3.11e-3,
+                  "fc2.bias": 0.0176, "fc3.weight": 1.04e-3, "fc3.bias": 9.47e-6}
+BF16_VS_REF = {k: max(1.2 * v, 2e-5) for k, v in _BF16_MEASURED.items()}
 
 
 def test_cls_step_bf16_vs_reference_fp32_capture_g11():
@@ -810,12 +823,15 @@ def test_cls_step_bf16_vs_reference_fp32_capture_g11():
     mask = (rng.random((B, 256)) >= 0.3).astype(np.float32)
     loss = step(_t(pts), _t(lab, torch.int64), mask=_t(mask), apply_adam=False)
     t = BF16_VS_REF
-    assert abs(float(loss[0]) - float(fx["loss"])) < t["loss"]
+    meas = {"loss": abs(float(loss[0]) - float(fx["loss"]))}
     lg = step.logits.cpu().numpy()
-    assert np.abs(lg - fx["logits"]).max() / np.abs(fx["logits"]).max() < t["logits"]
+    meas["logits"] = float(np.abs(lg - fx["logits"]).max() / np.abs(fx["logits"]).max())
     gmax, _, _ = ops.feat_fwd(_t(pts), *_feat_weights(G), precision="bf16")
-    assert np.abs(gmax.cpu().numpy() - fx["gmax"]).max() / np.abs(fx["gmax"]).max() < t["gmax"]
+    meas["gmax"] = float(np.abs(gmax.cpu().numpy() - fx["gmax"]).max() / np.abs(fx["gmax"]).max())
     for nm, p in model.named_parameters():
-        tol = t["head"] if nm.startswith("fc") else t["conv4"] if "conv4" in nm else t["conv13"]
-        check_tensor_l2(fx, "grad." + nm, p.grad.cpu().numpy(), tol=tol)
+        meas[nm] = check_tensor_l2(fx, "grad." + nm, p.grad.cpu().numpy(), tol=1.0)
+    print("bf16 mode vs the reference (g11), measured:",
+          " ".join(f"{k}={v:.3g}" for k, v in meas.items()))
+    for k, v in meas.items():
+        assert v <= t[k], f"{k}: {v:.3e} > bound {t[k]:.3e}"
 
