@@ -44,4 +44,9 @@ if [ "$only" = all ] || [ "$only" = bench ]; then
   step bench_seg 600 python bench.py --config seg --steps 20 --warmup 3
   step bench_n2048 600 python bench.py --points 2048 --no-cpu --steps 100 --warmup 10
   step bench_trainer 600 python bench.py --config trainer --steps 300 --warmup 20
+  step bench_cls_ft 600 python bench.py --config cls_ft --steps 100 --warmup 10
+  step bench_adv_ft 600 python bench.py --config adv_ft --steps 100 --warmup 10
+fi
+if [ "$only" = all ] || [ "$only" = mfma ]; then
+  bash tools/gpu_mfma.sh "$tag" || exit 1
 fi

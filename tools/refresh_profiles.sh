@@ -13,6 +13,14 @@ line "$o/${tag}_bench_seg.log" > "$p/${tag}_seg_bench.json"
 line "$o/${tag}_bench_cls.log" > "$p/${tag}_cls_bench.json"
 line "$o/${tag}_bench_n2048.log" > "$p/${tag}_bench_n2048.json"
 line "$o/${tag}_bench_trainer.log" > "$p/${tag}_trainer_bench.json"
+for f in cls_ft adv_ft; do
+  if [ -f "$o/${tag}_bench_$f.log" ]; then line "$o/${tag}_bench_$f.log" > "$p/${tag}_${f}_bench.json"; fi
+done
+for c in adv cls seg; do
+  if [ -d "$o/${tag}_mfma_$c" ]; then
+    python tools/pmc_mfma.py "$o/${tag}_mfma_$c" "$p/${tag}_${c}_mfma.json" "bench.py ($c)" > /dev/null
+  fi
+done
 for c in "" _cls _seg; do
   cp "$o/${tag}_trace$c/run_kernel_stats.csv" "$p/${tag}${c}_kernel_stats.csv"
   python tools/kstats.py "$o/${tag}_trace$c/run_kernel_trace.csv" > "$p/${tag}${c}_kernel_trace_summary.txt"
