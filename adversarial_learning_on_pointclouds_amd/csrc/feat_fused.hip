@@ -771,7 +771,10 @@ static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, c
   if (rc != PCADV_OK) return rc;
   // two wave groups per 128-channel workgroup when 256-channel workgroups would
   // leave CUs idle (the diagnostic stamps layout assumes the plain form)
-  if (4 * C < 256 && !stamps)
+#ifndef PCADV_C4_G2_MAXC
+#define PCADV_C4_G2_MAXC 63  // A/B builds: the largest cloud count run in the two-group form
+#endif
+  if (C <= PCADV_C4_G2_MAXC && !stamps)
     hipLaunchKernelGGL((k_conv4_max<NP4, true>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
                        sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
   else
