@@ -89,6 +89,20 @@ class AdvArgs(ctypes.Structure):
         ("part", _i),
         ("precision", _i),
         ("rng_rank", _i), ("rng_world", _i),
+        ("epi_counters", _vp), ("epi_ncounters", _i), ("epi_ring", _vp), ("epi_slots", _i),
+        ("epi_nl", _i), ("epi_ring_count", _vp),
+    ]
+
+
+class GatherJob(ctypes.Structure):
+    """Mirror of pcadv_gather_job (include/pcadv.h)."""
+
+    _fields_ = [
+        ("src", _vp), ("n_src", _i64), ("npts", _i), ("src_npts", _i),
+        ("order", _vp), ("cursor", _vp), ("B", _i),
+        ("src_lab", _vp), ("lab_width", _i), ("src_seg", _vp),
+        ("sigma", ctypes.c_double), ("clip", ctypes.c_double), ("seed", _u64), ("step", _vp),
+        ("out", _vp), ("out_lab", _vp), ("out_seg", _vp), ("rng_row0", _i64),
     ]
 
 
@@ -144,6 +158,7 @@ SIGNATURES = {
                                  _vp, _vp, _vp, _i64, _vp]),
     "pcadv_gather_clouds_at": (_i, [_vp, _i64, _i, _i, _vp, _vp, _i, _vp, _i, _vp, ctypes.c_double,
                                     ctypes.c_double, _u64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "pcadv_gather_clouds_multi": (_i, [ctypes.POINTER(GatherJob), _i, _vp]),
     "pcadv_iter_epilogue": (_i, [_vp, _i, _vp, _i, _vp, _i, _vp, _vp]),
     "pcadv_row_ce_workspace_bytes": (_sz, [_i]),
     "pcadv_row_ce": (_i, [_vp, _i64, _vp, _i, _i, _f, _vp, _vp, _vp, _sz, _vp]),

@@ -27,7 +27,8 @@ int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, in
                     const float*, const float*, const float*, const float*, const float*,
                     const float*, const float*, float*, float*, float*, float*, float*, float*,
                     float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr,
-                    const FinAdam* adam = nullptr, const int* sortrec = nullptr);
+                    const FinAdam* adam = nullptr, const int* sortrec = nullptr,
+                    const IterEpi* epi = nullptr);
 size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
@@ -104,6 +105,8 @@ int launch_gather_clouds(const float*, int64_t, int, int, const int64_t*, int, c
                          float*, int64_t*, int64_t*, hipStream_t, const int32_t* cursor = nullptr,
                          int64_t rng_row0 = 0);
 int launch_iter_epilogue(int32_t*, int, const float*, int, float*, int, int32_t*, hipStream_t);
+int check_iter_epi(const IterEpi&);
+int launch_gather_multi(const pcadv_gather_job*, int, hipStream_t);
 size_t row_ce_workspace_bytes(int);
 int launch_row_ce(const float*, long long, const int64_t*, int, int, float, float*, float*, void*,
                   size_t, hipStream_t);
@@ -218,6 +221,17 @@ static int adv_adam(const pcadv_adv_args* a, hipStream_t s) {
 
 static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w, float* logits);
 
+// pcadv_adv_args.epi_*: the iteration epilogue folded into the finishing launch
+static int step_epilogue(const pcadv_adv_args* a, IterEpi* e, bool* on) {
+  *e = IterEpi{a->epi_counters, a->epi_ncounters, a->losses, a->epi_nl, a->epi_ring,
+               a->epi_slots, a->epi_ring_count};
+  *on = a->epi_ncounters > 0 || a->epi_ring;
+  if (!*on) return PCADV_OK;
+  PC_REQUIRE(a->part != 1, "adv_step: the iteration epilogue needs the finishing launch (part 0 or 2)");
+  PC_REQUIRE(!a->epi_ring || a->losses, "adv_step: the loss ring needs losses");
+  return check_iter_epi(*e);
+}
+
 static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(a && a->B > 0 && a->B <= 256 && a->N > 0, "adv_step: bad B/N");
   const int B = a->B, N = a->N, C = 2 * B;
@@ -237,13 +251,17 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v && a->d_param && a->d_m && a->d_v),
              "adv_step: Adam buffers");
   const FinAdam fa = fused_adam(a, true);
+  IterEpi epi;
+  bool epi_on;
+  PC_TRY(step_epilogue(a, &epi, &epi_on));
   return launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
                          G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                          G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec);
+                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec,
+                         epi_on ? &epi : nullptr);
 }
 
 // Part 1 of adv_step: everything before the feature backward.
@@ -435,13 +453,17 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   // feature backward; Adam (generator only) fused into its finishing launch
   PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v), "cls_step: Adam moments");
   const FinAdam fa = fused_adam(a, false);
+  IterEpi epi;
+  bool epi_on;
+  PC_TRY(step_epilogue(a, &epi, &epi_on));
   return launch_feat_bwd(w.dgmax, w.gidx, a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
                          G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                          G + PCADV_G_CONV3_W, G + PCADV_G_CONV4_W, w.x3,
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec);
+                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec,
+                         epi_on ? &epi : nullptr);
 }
 
 }  // namespace pcadv
@@ -451,7 +473,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 6; }
+int pcadv_abi_version(void) { return 7; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -703,6 +725,10 @@ int pcadv_gather_clouds_at(const float* src, int64_t n_src, int npts, int src_np
   return launch_gather_clouds(src, n_src, npts, src_npts, order, B, src_lab, lab_width, src_seg,
                               sigma, clip, nullptr, seed, step, out, out_lab, out_seg, stream,
                               cursor, rng_row0);
+}
+
+int pcadv_gather_clouds_multi(const pcadv_gather_job* jobs, int njobs, hipStream_t stream) {
+  return launch_gather_multi(jobs, njobs, stream);
 }
 
 int pcadv_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl,

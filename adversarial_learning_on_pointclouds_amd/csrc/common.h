@@ -197,6 +197,31 @@ struct FinAdam {
   int step_offset;
 };
 
+// The end of a graph-replayed training iteration (pcadv_iter_epilogue, or
+// folded into the step's last launch through pcadv_adv_args.epi_*): every
+// counter += 1 (the loaders' RNG steps and batch cursors) and, with a ring,
+// losses[0..nl) into slot (*ring_count % slots), *ring_count += 1.  One wave:
+// every lane reads *ring_count in the same instruction, and lane 0's store of
+// the increment depends on its own read.
+struct IterEpi {
+  int32_t* counters;
+  int ncounters;
+  const float* losses;
+  int nl;
+  float* ring;
+  int slots;
+  int32_t* ring_count;
+};
+__device__ __forceinline__ void iter_epi_wave(const IterEpi& e, int lane) {
+  if (e.ring && e.ring_count) {
+    const int32_t cnt = *e.ring_count;
+    const int slot = (int)((uint32_t)cnt % (uint32_t)e.slots);
+    if (lane < e.nl) e.ring[(size_t)slot * e.nl + lane] = e.losses[lane];
+    if (lane == 0) *e.ring_count = cnt + 1;
+  }
+  if (lane < e.ncounters) e.counters[lane] += 1;
+}
+
 // extra weight-gradient job: dw[N][K] (+ db) = sum over rows m < m_w of
 // dz[m][N]^T x[m][K] (dz stored as is: no activation, no dropout)
 struct LinBwdJob {

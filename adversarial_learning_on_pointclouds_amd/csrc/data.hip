@@ -16,14 +16,14 @@ namespace pcadv {
 
 constexpr uint32_t RNG_JITTER = 4;
 
-__global__ void __launch_bounds__(256)
-k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_npts,
-                const int64_t* __restrict__ idx, int B, const int64_t* __restrict__ src_lab,
-                int lab_width, const int64_t* __restrict__ src_seg, double sigma_d, double clip_d,
-                const double* __restrict__ noise, uint64_t seed, const int32_t* __restrict__ step,
-                float* __restrict__ out, int64_t* __restrict__ out_lab,
-                int64_t* __restrict__ out_seg, const int32_t* __restrict__ cursor, int64_t rng_row0) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// One batch point t of a gather (below): batch row b = t / npts, point p.
+__device__ __forceinline__ void gather_point(
+    int64_t t, const float* __restrict__ src, int64_t n_src, int npts, int src_npts,
+    const int64_t* __restrict__ idx, int B, const int64_t* __restrict__ src_lab, int lab_width,
+    const int64_t* __restrict__ src_seg, double sigma_d, double clip_d,
+    const double* __restrict__ noise, uint64_t seed, const int32_t* __restrict__ step,
+    float* __restrict__ out, int64_t* __restrict__ out_lab, int64_t* __restrict__ out_seg,
+    const int32_t* __restrict__ cursor, int64_t rng_row0) {
   if (t >= (int64_t)B * npts) return;
   const int b = (int)(t / npts), p = (int)(t % npts);
   // cursor: batch k = *cursor of an epoch order held in idx (a graph-fed loader)
@@ -69,6 +69,31 @@ k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_
   if (p < lab_width && out_lab && src_lab) out_lab[(size_t)b * lab_width + p] = src_lab[(size_t)c * lab_width + p];
 }
 
+__global__ void __launch_bounds__(256)
+k_gather_clouds(const float* __restrict__ src, int64_t n_src, int npts, int src_npts,
+                const int64_t* __restrict__ idx, int B, const int64_t* __restrict__ src_lab,
+                int lab_width, const int64_t* __restrict__ src_seg, double sigma_d, double clip_d,
+                const double* __restrict__ noise, uint64_t seed, const int32_t* __restrict__ step,
+                float* __restrict__ out, int64_t* __restrict__ out_lab,
+                int64_t* __restrict__ out_seg, const int32_t* __restrict__ cursor, int64_t rng_row0) {
+  gather_point((int64_t)blockIdx.x * 256 + threadIdx.x, src, n_src, npts, src_npts, idx, B, src_lab,
+               lab_width, src_seg, sigma_d, clip_d, noise, seed, step, out, out_lab, out_seg,
+               cursor, rng_row0);
+}
+
+// Several graph-fed loaders' batches in one launch (blockIdx.y = job): the
+// iteration's GT and no-GT gathers without a launch boundary between them.
+constexpr int GATHER_MAXJOBS = 4;
+struct GatherJobs {
+  pcadv_gather_job j[GATHER_MAXJOBS];
+};
+__global__ void __launch_bounds__(256) k_gather_multi(GatherJobs jobs) {
+  const pcadv_gather_job& j = jobs.j[blockIdx.y];
+  gather_point((int64_t)blockIdx.x * 256 + threadIdx.x, j.src, j.n_src, j.npts, j.src_npts,
+               j.order, j.B, j.src_lab, j.lab_width, j.src_seg, j.sigma, j.clip, nullptr, j.seed,
+               j.step, j.out, j.out_lab, j.out_seg, j.cursor, j.rng_row0);
+}
+
 int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts,
                          const int64_t* idx, int B, const int64_t* src_lab, int lab_width,
                          const int64_t* src_seg, double sigma, double clip, const double* noise,
@@ -88,31 +113,50 @@ int launch_gather_clouds(const float* src, int64_t n_src, int npts, int src_npts
   return PCADV_OK;
 }
 
-// The end of a graph-replayed training iteration: every counter += 1 (the
-// loaders' RNG steps and batch cursors) and the step's loss vector into slot
-// (*ring_count % slots) of a loss ring, *ring_count += 1.  One wave.
-__global__ void __launch_bounds__(64)
-k_iter_epilogue(int32_t* __restrict__ counters, int ncounters, const float* __restrict__ losses,
-                int nl, float* __restrict__ ring, int slots, int32_t* __restrict__ ring_count) {
-  const int t = threadIdx.x;
-  if (ring && ring_count) {
-    const int slot = (int)((uint32_t)*ring_count % (uint32_t)slots);
-    if (t < nl) ring[(size_t)slot * nl + t] = losses[t];
-  }
-  if (t < ncounters) counters[t] += 1;
-  __syncthreads();  // every lane has read *ring_count
-  if (t == 0 && ring && ring_count) *ring_count += 1;
+// The end of a graph-replayed training iteration as a launch of its own
+// (iter_epi_wave, common.h).  One wave.
+__global__ void __launch_bounds__(64) k_iter_epilogue(IterEpi e) { iter_epi_wave(e, threadIdx.x); }
+
+int check_iter_epi(const IterEpi& e) {
+  PC_REQUIRE(e.ncounters >= 0 && e.ncounters <= 64 && (e.ncounters == 0 || e.counters),
+             "iter_epilogue: %d counters (at most 64)", e.ncounters);
+  PC_REQUIRE(!e.ring || (e.ring_count && e.losses && e.nl > 0 && e.nl <= 64 && e.slots > 0),
+             "iter_epilogue: bad loss ring (nl=%d slots=%d)", e.nl, e.slots);
+  return PCADV_OK;
 }
 
 int launch_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl, float* ring,
                          int slots, int32_t* ring_count, hipStream_t s) {
-  PC_REQUIRE(ncounters >= 0 && ncounters <= 64 && (ncounters == 0 || counters),
-             "iter_epilogue: %d counters (at most 64)", ncounters);
-  PC_REQUIRE(!ring || (ring_count && losses && nl > 0 && nl <= 64 && slots > 0),
-             "iter_epilogue: bad loss ring (nl=%d slots=%d)", nl, slots);
-  hipLaunchKernelGGL(k_iter_epilogue, dim3(1), dim3(64), 0, s, counters, ncounters, losses, nl,
-                     ring, slots, ring_count);
+  const IterEpi e{counters, ncounters, losses, nl, ring, slots, ring_count};
+  const int rc = check_iter_epi(e);
+  if (rc != PCADV_OK) return rc;
+  hipLaunchKernelGGL(k_iter_epilogue, dim3(1), dim3(64), 0, s, e);
   PC_HIP_CHECK_LAUNCH("k_iter_epilogue");
+  return PCADV_OK;
+}
+
+int launch_gather_multi(const pcadv_gather_job* jobs, int njobs, hipStream_t s) {
+  PC_REQUIRE(jobs && njobs >= 1 && njobs <= GATHER_MAXJOBS, "gather_multi: %d jobs (1..%d)", njobs,
+             GATHER_MAXJOBS);
+  GatherJobs g{};
+  int64_t nmax = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const pcadv_gather_job& j = jobs[k];
+    PC_REQUIRE(j.src && j.order && j.cursor && j.out && j.n_src > 0 && j.B > 0 && j.npts > 0 &&
+                   j.src_npts >= j.npts,
+               "gather_multi: job %d: bad arguments (n_src=%lld B=%d npts=%d src_npts=%d)", k,
+               (long long)j.n_src, j.B, j.npts, j.src_npts);
+    PC_REQUIRE(j.sigma >= 0.0 && (j.sigma == 0.0 || j.clip > 0.0),
+               "gather_multi: job %d: clip must be > 0", k);
+    PC_REQUIRE(!j.src_lab || (j.lab_width > 0 && j.lab_width <= j.npts && j.out_lab),
+               "gather_multi: job %d: labels", k);
+    PC_REQUIRE(!j.src_seg || j.out_seg, "gather_multi: job %d: part ids", k);
+    g.j[k] = j;
+    const int64_t n = (int64_t)j.B * j.npts;
+    if (n > nmax) nmax = n;
+  }
+  hipLaunchKernelGGL(k_gather_multi, dim3((unsigned)((nmax + 255) / 256), njobs), dim3(256), 0, s, g);
+  PC_HIP_CHECK_LAUNCH("k_gather_multi");
   return PCADV_OK;
 }
 

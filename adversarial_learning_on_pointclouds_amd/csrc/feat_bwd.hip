@@ -799,9 +799,13 @@ __device__ void reduce_slabs_block(int blk, float (*part)[64], const float* __re
 constexpr int FIN_NRED = (SLAB + FIN_COLS - 1) / FIN_COLS;
 __global__ void __launch_bounds__(1024)
 k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
-                  float* db2, float* dw3, float* db3, FinAdam fa, int nb4) {
+                  float* db2, float* dw3, float* db3, FinAdam fa, int nb4, IterEpi epi) {
   __shared__ float part[16][64];
   const int blk = (int)blockIdx.x;
+  // the training iteration's epilogue (pcadv_adv_args.epi_*): the step's
+  // losses are final since the launches before this one
+  if (blk == 0 && threadIdx.x < 64 && (epi.ncounters > 0 || epi.ring))
+    iter_epi_wave(epi, (int)threadIdx.x);
   if (blk < FIN_NRED) {
     reduce_slabs_block(blk, part, slabs, nslabs, dw1, db1, dw2, db2, dw3, db3, fa);
   } else {
@@ -821,7 +825,8 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                     const float* b2, const float* w3, const float* w4, const float* x3,
                     float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
                     float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s,
-                    uint64_t* stamps, const FinAdam* adam, const int* sortrec) {
+                    uint64_t* stamps, const FinAdam* adam, const int* sortrec,
+                    const IterEpi* epi) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
@@ -867,7 +872,7 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   const int nb4 = fa.on ? fin_adam_blocks(PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W, 1024, 2) : 0;
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + nb4), dim3(1024), 0, s, slabs, C * nchunk,
-                     dw1, db1, dw2, db2, dw3, db3, fa, nb4);
+                     dw1, db1, dw2, db2, dw3, db3, fa, nb4, epi ? *epi : IterEpi{});
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
   return PCADV_OK;
 }

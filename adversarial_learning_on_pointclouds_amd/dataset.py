@@ -25,7 +25,7 @@ import torch
 import torch.utils.data as data
 
 from . import _lib
-from ._lib import check, stream_ptr
+from ._lib import GatherJob, check, stream_ptr
 
 H5_F32, H5_F64, H5_INT, H5_UINT = 1, 2, 3, 4
 
@@ -377,6 +377,15 @@ class DeviceCloudLoader:
         split): the graph-replayed form of gather (no host copy per batch).
         The step counter is NOT advanced here: the caller advances it and the
         cursor (pcadv_iter_epilogue)."""
+        j = self._gather_job(order, cursor, out, out_lab, out_seg)
+        check(self.lib.pcadv_gather_clouds_at(j.src, j.n_src, j.npts, j.src_npts, j.order,
+                                              j.cursor, j.B, j.src_lab, j.lab_width, j.src_seg,
+                                              j.sigma, j.clip, j.seed, j.step, j.out, j.out_lab,
+                                              j.out_seg, j.rng_row0, stream_ptr()),
+              "pcadv_gather_clouds_at")
+
+    def _gather_job(self, order, cursor, out, out_lab=None, out_seg=None):
+        """The checked arguments of one gather_at as a pcadv_gather_job."""
         lw = 0 if self.labels is None else int(self.labels.shape[1])
         if out_lab is None and self.labels is not None:
             raise ValueError("gather_at: out_lab required for a labelled split")
@@ -396,14 +405,27 @@ class DeviceCloudLoader:
             need(out_seg, "out_seg", (B, self.npts), torch.int64)
         need(order, "order", (self.order_len,), torch.int64)
         need(cursor, "cursor", (1,), torch.int32)
-        P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        check(self.lib.pcadv_gather_clouds_at(P(self.pts), self.n, self.npts, self.npts, P(order),
-                                              P(cursor), self.B, P(self.labels), lw,
-                                              P(self.segs), self.sigma, self.clip, self.seed,
-                                              P(self.step), P(out), P(out_lab), P(out_seg),
-                                              self.rank * self.B, stream_ptr()),
-              "pcadv_gather_clouds_at")
+        P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        return GatherJob(src=P(self.pts), n_src=self.n, npts=self.npts, src_npts=self.npts,
+                         order=P(order), cursor=P(cursor), B=self.B, src_lab=P(self.labels),
+                         lab_width=lw, src_seg=P(self.segs), sigma=self.sigma, clip=self.clip,
+                         seed=self.seed, step=P(self.step), out=P(out), out_lab=P(out_lab),
+                         out_seg=P(out_seg), rng_row0=self.rank * self.B)
 
     def __iter__(self):
         for idx in self.index_batches():
             yield self.gather(idx.contiguous(), _checked=True)
+
+
+def gather_at_multi(items):
+    """Several loaders' gather_at in ONE launch (pcadv_gather_clouds_multi):
+    items = [(loader, order, cursor, out, out_lab, out_seg), ...] (out_lab /
+    out_seg None where the split has none), at most 4; each batch is bitwise
+    what loader.gather_at would write.  The graph-replayed iteration's GT and
+    no-GT batches (trainer._GraphedIteration)."""
+    if not 1 <= len(items) <= 4:
+        raise ValueError(f"gather_at_multi: {len(items)} loaders (1..4)")
+    jobs = (GatherJob * len(items))(*[ld._gather_job(*rest) for ld, *rest in items])
+    lib = items[0][0].lib
+    check(lib.pcadv_gather_clouds_multi(jobs, len(items), stream_ptr()),
+          "pcadv_gather_clouds_multi")

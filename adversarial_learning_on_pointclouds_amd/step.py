@@ -11,6 +11,7 @@ flat too and are handed to a torch Adam optimizer's state as views
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -87,6 +88,18 @@ def _bind_adam_state(optimizer, module, m_flat, v_flat, grad_flat, layout, step_
                                   "exp_avg": mv[name], "exp_avg_sq": vv[name]}
 
 
+def _fill_epilogue(a, epi):
+    """pcadv_adv_args.epi_* from (counters, ncounters, _LossRing) or None."""
+    if epi is None:
+        return
+    counters, n, ring = epi
+    if n:
+        a.epi_counters, a.epi_ncounters = counters.data_ptr(), n
+    if ring is not None:
+        a.epi_ring, a.epi_slots, a.epi_nl = ring.ring.data_ptr(), ring.slots, ring.nl
+        a.epi_ring_count = ring.count.data_ptr()
+
+
 class AdvTrainStep:
     """run_training's iteration body for PointNetCls(k=40) + DeepConvDiscNet(40, 1).
 
@@ -104,6 +117,20 @@ class AdvTrainStep:
     GT and no-GT batches: the device-drawn masks and labels are those of the
     one-process step on the global batch (pcadv_adv_args.rng_rank, ABI 6).
     """
+
+    _epilogue = None  # (counters, ncounters, _LossRing) folded into the last launch
+
+    @contextlib.contextmanager
+    def folded_epilogue(self, counters=None, ncounters=0, ring=None):
+        """Within the block every step call also runs the training iteration's
+        epilogue (counters[:ncounters] += 1, the losses into the loss ring; as
+        pcadv_iter_epilogue) inside its own finishing launch - one launch less
+        per graph-replayed iteration (pcadv_adv_args.epi_*)."""
+        self._epilogue = (counters, int(ncounters), ring)
+        try:
+            yield
+        finally:
+            self._epilogue = None
 
     def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
                  lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
@@ -201,6 +228,8 @@ class AdvTrainStep:
         a.part = int(part)
         a.precision = self.precision
         a.rng_rank, a.rng_world = self.rng_rank, self.rng_world
+        if part != 1:
+            _fill_epilogue(a, self._epilogue)
         return a
 
     def sync_hyper(self):
@@ -371,6 +400,20 @@ class ClsTrainStep:
     precision="bf16": the feature forward's conv3 / conv4 on bf16-rounded
     operands (configs[1] is quoted in bf16); everything else f32."""
 
+    _epilogue = None  # (counters, ncounters, _LossRing) folded into the last launch
+
+    @contextlib.contextmanager
+    def folded_epilogue(self, counters=None, ncounters=0, ring=None):
+        """Within the block every step call also runs the training iteration's
+        epilogue (counters[:ncounters] += 1, the losses into the loss ring; as
+        pcadv_iter_epilogue) inside its own finishing launch - one launch less
+        per graph-replayed iteration (pcadv_adv_args.epi_*)."""
+        self._epilogue = (counters, int(ncounters), ring)
+        try:
+            yield
+        finally:
+            self._epilogue = None
+
     def __init__(self, model, B, N, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
                  lambda_cls=1.0, seed=0, device="cuda", precision="fp32", rng_rank=0, rng_world=1):
         self.lib = _lib.load()
@@ -438,6 +481,7 @@ class ClsTrainStep:
         a.workspace_bytes = self.workspace.numel()
         a.precision = self.precision
         a.rng_rank, a.rng_world = self.rng_rank, self.rng_world
+        _fill_epilogue(a, self._epilogue)
         return a
 
     set_rng_rank = AdvTrainStep.set_rng_rank

@@ -12,6 +12,7 @@ loop body op by op over the same HIP kernels through autograd.
 from __future__ import annotations
 
 import collections
+import contextlib
 import os
 
 import numpy as np
@@ -22,6 +23,7 @@ from .discriminator import DeepConvDiscNet
 from .metric import batch_get_iou, object_names
 from .pointnet import PointNetCls, feature_transform_regularizer
 from ._lib import D_LAYOUT
+from .dataset import gather_at_multi
 from .step import AdvTrainStep, _views
 from .utils import make_D_label
 
@@ -224,16 +226,31 @@ class _GraphedIteration:
         self.counters[self.L:] += 1
         return outs
 
+    def _gathers(self):
+        """Every loader's batch at its device cursor: one launch for all of
+        them (dataset.gather_at_multi)."""
+        L = self.L
+        items = [(ld, self.order[k], self.counters[L + k:L + k + 1], self.pts[k],
+                  self.lab if (k == 0 and ld.labels is not None) else None, None)
+                 for k, ld in enumerate(self.loaders)]
+        if len(items) == 1:
+            ld, *rest = items[0]
+            ld.gather_at(*rest)
+        else:
+            gather_at_multi(items)
+
     def _body(self, semi):
         L = self.L
-        for k, ld in enumerate(self.loaders):
-            ld.gather_at(self.order[k], self.counters[L + k:L + k + 1], self.pts[k],
-                         self.lab if (k == 0 and ld.labels is not None) else None)
-        if L == 2:
-            self.step(self.pts[0], self.lab[:, 0], self.pts[1], semi=semi)
-        else:
-            self.step(self.pts[0], self.lab[:, 0])
-        self.ring.write(self.step.losses, self.counters, 2 * L)
+        self._gathers()
+        # the fused steps run the iteration epilogue in their finishing launch
+        fold = getattr(self.step, "folded_epilogue", None)
+        with (fold(self.counters, 2 * L, self.ring) if fold else contextlib.nullcontext()):
+            if L == 2:
+                self.step(self.pts[0], self.lab[:, 0], self.pts[1], semi=semi)
+            else:
+                self.step(self.pts[0], self.lab[:, 0])
+        if fold is None:
+            self.ring.write(self.step.losses, self.counters, 2 * L)
 
     def _graph(self, semi):
         g = self.graphs.get(semi)
@@ -302,9 +319,7 @@ class _DPIteration(_GraphedIteration):
     def _part(self, k, semi):
         st, L = self.step, self.L
         if k == 1:
-            for i, ld in enumerate(self.loaders):
-                ld.gather_at(self.order[i], self.counters[L + i:L + i + 1], self.pts[i],
-                             self.lab if (i == 0 and ld.labels is not None) else None)
+            self._gathers()
             st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=1)
         elif k == 2:
             st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=2)

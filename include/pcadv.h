@@ -380,6 +380,30 @@ int pcadv_gather_clouds_at(const float* src, int64_t n_src, int npts, int src_np
                            float* out, int64_t* out_lab, int64_t* out_seg, int64_t rng_row0,
                            hipStream_t stream);
 
+/* Several graph-fed loaders' pcadv_gather_clouds_at in ONE launch (the
+ * training iteration's GT and no-GT batches, trainer.py): job k is exactly the
+ * arguments of one pcadv_gather_clouds_at call, and its output is bitwise that
+ * call's.  1 <= njobs <= 4.  ABI version 7. */
+typedef struct pcadv_gather_job {
+  const float* src;
+  int64_t n_src;
+  int npts, src_npts;
+  const int64_t* order;
+  const int32_t* cursor;
+  int B;
+  const int64_t* src_lab;
+  int lab_width;
+  const int64_t* src_seg;
+  double sigma, clip;
+  uint64_t seed;
+  const int32_t* step;
+  float* out;
+  int64_t* out_lab;
+  int64_t* out_seg;
+  int64_t rng_row0;
+} pcadv_gather_job;
+int pcadv_gather_clouds_multi(const pcadv_gather_job* jobs, int njobs, hipStream_t stream);
+
 /* The end of a graph-replayed training iteration (trainer.py): counters[i] += 1
  * for i < ncounters (<= 64: loaders' RNG steps and batch cursors), and, when
  * ring is given, losses[0..nl) into slot (*ring_count % slots) of the [slots][nl]
@@ -455,6 +479,17 @@ typedef struct pcadv_adv_args {
    * one-process step on the global batch (the dropout row of no-GT row j is
    * rng_world B + j, as in the one-process [GT; no-GT] batch). */
   int rng_rank, rng_world;
+  /* The graph-replayed training iteration's epilogue (pcadv_iter_epilogue:
+   * epi_counters[0..epi_ncounters) += 1, losses[0..epi_nl) into slot
+   * (*epi_ring_count % epi_slots) of the [epi_slots][epi_nl] ring, then
+   * *epi_ring_count += 1) run by the step's last launch instead of a launch of
+   * its own; epi_ncounters = 0 and epi_ring = NULL: none.  Not with part = 1.
+   * pcadv_adv_step and pcadv_cls_step.  ABI version 7. */
+  int32_t* epi_counters;
+  int epi_ncounters;
+  float* epi_ring;
+  int epi_slots, epi_nl;
+  int32_t* epi_ring_count;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

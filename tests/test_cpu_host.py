@@ -25,7 +25,7 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
     assert sorted(_lib.SIGNATURES) == syms  # nothing bound that the header does not declare
-    assert lib.pcadv_abi_version() == 6
+    assert lib.pcadv_abi_version() == 7
 
 
 def test_layout_matches_header_enums():
@@ -199,3 +199,38 @@ def test_shard_order_slices_global_batches():
         glob = order[k * B * W:(k + 1) * B * W]
         assert torch.equal(torch.cat([s[k * B:(k + 1) * B] for s in shards]), glob)
     assert torch.equal(shard_order(order, B, 0, 1), order[:21])
+
+
+def _c_layout(struct, fields, tmp_path):
+    """sizeof and offsetof of a C struct of include/pcadv.h, from gcc."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None or not os.path.isdir("/opt/rocm/include"):
+        pytest.skip("gcc or the ROCm headers are absent")
+    body = "".join(f'  printf("%zu\\n", offsetof({struct}, {f}));\n' for f in fields)
+    src = tmp_path / "layout.c"
+    src.write_text(f'#include <stdio.h>\n#include "pcadv.h"\nint main(void) {{\n'
+                   f'  printf("%zu\\n", sizeof({struct}));\n{body}  return 0;\n}}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(REPO, "include"),
+                    "-I", "/opt/rocm/include", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    return int(out[0]), [int(v) for v in out[1:]]
+
+
+@pytest.mark.parametrize("name", ["AdvArgs", "GatherJob"])
+def test_ctypes_structs_match_the_c_layout(name, tmp_path):
+    """The ctypes mirrors of pcadv_adv_args / pcadv_gather_job (the structs
+    the trainer fills) have the C structs' size and field offsets."""
+    from adversarial_learning_on_pointclouds_amd import _lib
+    py = getattr(_lib, name)
+    c = {"AdvArgs": "pcadv_adv_args", "GatherJob": "pcadv_gather_job"}[name]
+    fields = [f for f, _ in py._fields_]
+    size, offs = _c_layout(c, fields, tmp_path)
+    assert ctypes_sizeof(py) == size
+    assert [getattr(py, f).offset for f in fields] == offs
+
+
+def ctypes_sizeof(t):
+    import ctypes
+    return ctypes.sizeof(t)

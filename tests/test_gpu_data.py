@@ -82,6 +82,79 @@ def test_shapenet_batches_with_part_ids(tmp_path):
     assert np.array_equal(oh.cpu().numpy()[:, 0].argmax(1), EXP["shapenet_latest/label"][rows, 0])
 
 
+def test_gather_multi_is_bitwise_the_single_gathers(tmp_path):
+    """dataset.gather_at_multi (pcadv_gather_clouds_multi, one launch) writes
+    exactly what each loader's gather_at writes: a labelled GT split with
+    device jitter, a no-GT split of another batch size, and a ShapeNet split
+    with part ids (different point counts per job)."""
+    lst = _list(tmp_path, ["modelnet_gzip.h5", "modelnet_contig.h5"])
+    gt = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, None, npoints=64), 3, seed=3)
+    ng = D.DeviceCloudLoader(D.ModelNetDataset_noGT(lst, None, npoints=48), 5, seed=4)
+    sn = D.DeviceCloudLoader(D.ShapeNetDatasetGT(None, _list(tmp_path, ["shapenet_latest.h5"]),
+                                                 num_classes=16, num_pts=50), 2, seed=5)
+    dev = torch.device("cuda")
+    jobs = []
+    for ld in (gt, ng, sn):
+        order = ld.epoch_order().to(dev)
+        cursor = torch.ones(1, dtype=torch.int32, device=dev)
+        lab = (torch.zeros(ld.B, int(ld.labels.shape[1]), dtype=torch.int64, device=dev)
+               if ld.labels is not None else None)
+        seg = torch.zeros(ld.B, ld.npts, dtype=torch.int64, device=dev) if ld.segs is not None else None
+        jobs.append((ld, order, cursor, torch.zeros(ld.B, ld.npts, 3, device=dev), lab, seg))
+    D.gather_at_multi(jobs)
+    multi = [[t.clone() for t in j[3:] if t is not None] for j in jobs]
+    for ld, order, cursor, out, lab, seg in jobs:
+        for t in (out, lab, seg):
+            if t is not None:
+                t.fill_(-7)
+        ld.gather_at(order, cursor, out, lab, seg)
+    for j, m in zip(jobs, multi):
+        single = [t for t in j[3:] if t is not None]
+        assert all(torch.equal(a, b) for a, b in zip(single, m))
+    assert not torch.equal(multi[0][0], torch.zeros_like(multi[0][0]))
+
+
+@pytest.mark.parametrize("kind", ["adv", "cls"])
+def test_folded_epilogue_equals_the_epilogue_launch(kind):
+    """The iteration epilogue run inside the step's finishing launch
+    (pcadv_adv_args.epi_*, step.folded_epilogue) against the step followed by
+    pcadv_iter_epilogue: same losses, parameters, loss-ring rows, ring count
+    and counters, over three iterations."""
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep, ClsTrainStep
+    import adversarial_learning_on_pointclouds_amd as pc
+    dev = torch.device("cuda")
+    B, N = 8, 256
+    g = torch.Generator().manual_seed(9)
+    pg, pn = (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dev), (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dev)
+    lab = torch.randint(0, 40, (B,), generator=g).to(dev)
+    out = []
+    for fold in (False, True):
+        torch.manual_seed(0)
+        model = pc.PointNetCls(k=40).to(dev)
+        if kind == "adv":
+            step = AdvTrainStep(model, pc.DeepConvDiscNet(40, 1).to(dev), B, N, seed=5, device=dev)
+            call = lambda: step(pg, lab, pn)  # noqa: E731
+        else:
+            step = ClsTrainStep(model, B, N, seed=5, device=dev)
+            call = lambda: step(pg, lab)  # noqa: E731
+        ring = trainer._LossRing(lambda *a: None, 4 if kind == "adv" else 1, dev, slots=8)
+        counters = torch.arange(4, dtype=torch.int32, device=dev)
+        losses = step.losses if kind == "adv" else step.losses.view(-1)
+        for it in range(3):
+            if fold:
+                with step.folded_epilogue(counters, 4, ring):
+                    call()
+            else:
+                call()
+                ring.write(losses, counters, 4)
+        out.append([losses.clone(), ring.ring.clone(), ring.count.clone(), counters.clone(),
+                    step.g_param.clone()])
+    assert int(out[1][2]) == 3 and out[1][3].tolist() == [3, 4, 5, 6]
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 class _Log:
     def __init__(self):
         self.lines = []
