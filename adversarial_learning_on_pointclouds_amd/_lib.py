@@ -91,6 +91,7 @@ class AdvArgs(ctypes.Structure):
         ("rng_rank", _i), ("rng_world", _i),
         ("epi_counters", _vp), ("epi_ncounters", _i), ("epi_ring", _vp), ("epi_slots", _i),
         ("epi_nl", _i), ("epi_ring_count", _vp),
+        ("gather", _vp), ("ngather", _i),
     ]
 
 

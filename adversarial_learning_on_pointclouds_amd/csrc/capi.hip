@@ -33,7 +33,8 @@ size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
                           const float*, float*, float*, int32_t*, int32_t*, void*, size_t,
-                          hipStream_t, uint64_t* stamps = nullptr, int precision = 0);
+                          hipStream_t, uint64_t* stamps = nullptr, int precision = 0,
+                          const pcadv_gather_job* gather = nullptr, int ngather = 0);
 int launch_conv4_max(const float*, int, int, const float*, const float*, float*, int32_t*,
                      hipStream_t, int);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
@@ -297,7 +298,8 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
                                G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision));
+                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision, a->gather,
+                               a->ngather));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   // fc2 + dropout: a device-drawn mask is stored for the backward
@@ -421,7 +423,8 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
                                G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision));
+                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision, a->gather,
+                               a->ngather));
   PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,

@@ -197,6 +197,38 @@ struct FinAdam {
   int step_offset;
 };
 
+// The device jitter of a gathered batch point (dataset/modelNetData.py:80-91,
+// jitter_point_cloud: clip(sigma * randn, -clip, clip) per coordinate): the
+// point's row tg in the global batch keys a Philox draw whose two uniform
+// pairs give, by Box-Muller, the normals of coordinates 0, 1, 2.  Coordinate d
+// alone costs the same operations as all three do for it, so a thread per
+// coordinate (k_point_mlp's folded gather) and a thread per point
+// (k_gather_clouds) produce the same bits.
+constexpr uint32_t RNG_JITTER = 4;
+__device__ __forceinline__ float jitter_normal(uint64_t seed, uint32_t step, int64_t tg, int d) {
+  const u32x4 r = philox((uint32_t)tg, step, RNG_JITTER, (uint32_t)(tg >> 32), (uint32_t)seed,
+                         (uint32_t)(seed >> 32));
+  // Box-Muller on two uniform pairs -> 4 normals (3 used)
+  if (d < 2) {
+    const float u1 = fmaxf(u01(r.x), 1e-7f), u2 = u01(r.y);
+    const float m1 = sqrtf(-2.f * logf(u1)), a1 = 6.28318530718f * u2;
+    return d == 0 ? m1 * cosf(a1) : m1 * sinf(a1);
+  }
+  const float u3 = fmaxf(u01(r.z), 1e-7f), u4 = u01(r.w);
+  const float m2 = sqrtf(-2.f * logf(u3)), a2 = 6.28318530718f * u4;
+  return m2 * cosf(a2);
+}
+__device__ __forceinline__ float jitter_coord(float x, float sigma, float clip, float z) {
+  return x + fminf(fmaxf(sigma * z, -clip), clip);
+}
+
+// A step's input batches gathered by its first launch (pcadv_adv_args.gather):
+// job 0 the clouds [0, split) of the feature forward, job 1 the rest.
+struct GatherFold {
+  pcadv_gather_job j[2];
+  int n;
+};
+
 // The end of a graph-replayed training iteration (pcadv_iter_epilogue, or
 // folded into the step's last launch through pcadv_adv_args.epi_*): every
 // counter += 1 (the loaders' RNG steps and batch cursors) and, with a ring,

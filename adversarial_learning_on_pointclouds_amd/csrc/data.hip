@@ -14,7 +14,6 @@
 
 namespace pcadv {
 
-constexpr uint32_t RNG_JITTER = 4;
 
 // One batch point t of a gather (below): batch row b = t / npts, point p.
 __device__ __forceinline__ void gather_point(
@@ -48,17 +47,9 @@ __device__ __forceinline__ void gather_point(
       // keyed by the point's row in the global batch (a data-parallel rank's
       // batch rows start at rng_row0), so W ranks jitter as one loader would
       const int64_t tg = t + rng_row0 * npts;
-      const u32x4 r = philox((uint32_t)tg, st, RNG_JITTER, (uint32_t)(tg >> 32), (uint32_t)seed,
-                             (uint32_t)(seed >> 32));
-      // Box-Muller on two uniform pairs -> 4 normals (3 used)
-      const float u1 = fmaxf(u01(r.x), 1e-7f), u2 = u01(r.y);
-      const float u3 = fmaxf(u01(r.z), 1e-7f), u4 = u01(r.w);
-      const float m1 = sqrtf(-2.f * logf(u1)), m2 = sqrtf(-2.f * logf(u3));
-      const float a1 = 6.28318530718f * u2, a2 = 6.28318530718f * u4;
-      const float z0 = m1 * cosf(a1), z1 = m1 * sinf(a1), z2 = m2 * cosf(a2);
-      o[0] = x0 + fminf(fmaxf(sigma * z0, -clip), clip);
-      o[1] = x1 + fminf(fmaxf(sigma * z1, -clip), clip);
-      o[2] = x2 + fminf(fmaxf(sigma * z2, -clip), clip);
+      o[0] = jitter_coord(x0, sigma, clip, jitter_normal(seed, st, tg, 0));
+      o[1] = jitter_coord(x1, sigma, clip, jitter_normal(seed, st, tg, 1));
+      o[2] = jitter_coord(x2, sigma, clip, jitter_normal(seed, st, tg, 2));
     }
   } else {
     o[0] = x0;

@@ -61,13 +61,17 @@ struct MlpLds {
 // |x w|), f32 accumulate: f32-level accuracy at 6/16 of the f32 MFMA cycles.
 // NP3: conv3's bf16 products per f32 product: 6 (f32-level, the default) or 1
 // (bf16 mode: x2 and W3 rounded to bf16, f32 accumulate).
-template <int NP3, int TPW>
+// FOLD: the input batches are gathered here (GatherFold, the trainer's graph)
+// instead of read from pts_a / pts_b; a separate instantiation, so the plain
+// kernel's code is unchanged.
+template <int NP3, int TPW, bool FOLD>
 __global__ void __launch_bounds__(PM_T) __attribute__((amdgpu_waves_per_eu(2)))
 k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split, int N,
             int T, int ntiles, const float* __restrict__ w1, const float* __restrict__ b1,
             const float* __restrict__ w2, const float* __restrict__ b2,
             const float* __restrict__ w3, const float* __restrict__ b3,
-            float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps) {
+            float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps,
+            GatherFold gf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MlpLds& L = *reinterpret_cast<MlpLds*>(smem);
 #ifdef PCADV_STAMPS
@@ -88,11 +92,39 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     const int p = tid / 3;
     return (tid < PM_P * 3 && p0 + p < N) ? pts[(size_t)p0 * 3 + tid] : 0.f;
   };
+  // the same, gathered here from the job's split at its device cursor with the
+  // device jitter (as k_gather_clouds), the value also stored to the step's
+  // input buffer (the backward's recompute reads it) and, in the cloud's first
+  // tile, its label row; an out-of-range index leaves the buffer as it is
+  auto pts_gather = [&](int tile) {
+    const int c = tile / T, p0 = (tile % T) * PM_P;
+    const pcadv_gather_job& j = gf.j[c < split ? 0 : 1];
+    const int b = c < split ? c : c - split, p = p0 + tid / 3, d = tid % 3;
+    if (!(tid < PM_P * 3 && p < N)) return 0.f;
+    const int64_t src = j.order[(int64_t)*j.cursor * j.B + b];
+    float* o = j.out + ((size_t)b * j.npts + p) * 3 + d;
+    if (src < 0 || src >= j.n_src) return *o;
+    const float x = j.src[((size_t)src * j.src_npts + p) * 3 + d];
+    float v = x;
+    if (j.sigma > 0.0) {
+      const uint32_t st = j.step ? (uint32_t)*j.step : 0u;
+      const int64_t tg = (int64_t)b * j.npts + p + j.rng_row0 * j.npts;
+      v = jitter_coord(x, (float)j.sigma, (float)j.clip, jitter_normal(j.seed, st, tg, d));
+    }
+    *o = v;
+    if (p0 == 0 && tid < j.lab_width && j.out_lab && j.src_lab)
+      j.out_lab[(size_t)b * j.lab_width + tid] = j.src_lab[(size_t)src * j.lab_width + tid];
+    return v;
+  };
+  auto pts_next = [&](int tile) {
+    if constexpr (FOLD) return pts_gather(tile);
+    else return pts_load(tile);
+  };
   int tile = blockIdx.x * TPW;
   // loads in the order they are consumed (the memory counter waits in issue
   // order): the first tile's points and conv1's weights, then conv2's B
   // fragments, then W3 (split three ways only after conv1 of the first tile)
-  float pv = tile < ntiles ? pts_load(tile) : 0.f;
+  float pv = tile < ntiles ? pts_next(tile) : 0.f;
   // conv1: thread = (channel tid & 63, 16-point group tid >> 6)
   const int c1 = tid & 63, pg = tid >> 6;
   const float wa = w1[c1 * 3 + 0], wb = w1[c1 * 3 + 1], wc = w1[c1 * 3 + 2], bb1 = b1[c1];
@@ -132,7 +164,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
     if (tid < PM_P * 3) L.pts[(tid / 3) * 4 + tid % 3] = pv;
     __syncthreads();  // (also: every wave is past the previous tile's conv3 reads)
     STAMP(3 + 5 * it);
-    if (it + 1 < TPW && tile + 1 < ntiles) pv = pts_load(tile + 1);  // in flight during this tile
+    if (it + 1 < TPW && tile + 1 < ntiles) pv = pts_next(tile + 1);  // in flight during this tile
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int p = pg * 16 + i;
@@ -748,10 +780,16 @@ static int feat_fwd_attrs() {
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(C4Lds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(MlpLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 1>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 1, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(MlpLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(MlpLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 1, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(MlpLds)) != hipSuccess) {
       set_error("feat_fwd: cannot reserve LDS (%zu / %zu bytes)", sizeof(C4Lds), sizeof(MlpLds));
@@ -789,7 +827,7 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
                               const float* w1, const float* b1, const float* w2, const float* b2,
                               const float* w3, const float* b3, const float* w4, const float* b4,
                               float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter,
-                              hipStream_t s, uint64_t* stamps) {
+                              hipStream_t s, uint64_t* stamps, const GatherFold& gf) {
   const int rc = feat_fwd_attrs<NP3, NP4>();
   if (rc != PCADV_OK) return rc;
   const int T = (N + PM_P - 1) / PM_P;
@@ -797,14 +835,12 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
   uint64_t* mlp_stamps = stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr;
   // one tile per workgroup when two would give fewer than two workgroups per
   // CU (512); the diagnostic stamps layout assumes two
-  if (ntiles < 1024 && !stamps)
-    hipLaunchKernelGGL((k_point_mlp<NP3, 1>), dim3(ntiles), dim3(PM_T), sizeof(MlpLds), s, pts_a,
-                       pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3, inc_counter,
-                       mlp_stamps);
-  else
-    hipLaunchKernelGGL((k_point_mlp<NP3, 2>), dim3((ntiles + 1) / 2), dim3(PM_T), sizeof(MlpLds),
-                       s, pts_a, pts_b, split, N, T, ntiles, w1, b1, w2, b2, w3, b3, x3,
-                       inc_counter, mlp_stamps);
+  const bool one = ntiles < 1024 && !stamps;
+  const dim3 grid(one ? ntiles : (ntiles + 1) / 2);
+  auto kern = one ? (gf.n ? k_point_mlp<NP3, 1, true> : k_point_mlp<NP3, 1, false>)
+                  : (gf.n ? k_point_mlp<NP3, 2, true> : k_point_mlp<NP3, 2, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(PM_T), sizeof(MlpLds), s, pts_a, pts_b, split, N, T, ntiles,
+                     w1, b1, w2, b2, w3, b3, x3, inc_counter, mlp_stamps, gf);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
   return launch_conv4_max_np<NP3, NP4>(x3, C, N, w4, b4, gmax, gidx, s, stamps);
 }
@@ -824,17 +860,40 @@ int launch_feat_fwd_fused(const float* pts_a, const float* pts_b, int split, int
                           const float* w1, const float* b1, const float* w2, const float* b2,
                           const float* w3, const float* b3, const float* w4, const float* b4,
                           float* x3, float* gmax, int32_t* gidx, int32_t* inc_counter, void* ws,
-                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int precision) {
+                          size_t ws_bytes, hipStream_t s, uint64_t* stamps, int precision,
+                          const pcadv_gather_job* gather, int ngather) {
   (void)ws;
   (void)ws_bytes;
   PC_REQUIRE(C > 0 && N > 0, "feat_fwd: bad shape C=%d N=%d", C, N);
   PC_REQUIRE((size_t)C * 4 <= 0x7fffffff / 1, "feat_fwd: too many clouds (%d)", C);
   PC_REQUIRE(precision == 0 || precision == 1, "feat_fwd: precision %d (0 fp32, 1 bf16)", precision);
+  GatherFold gf{};
+  if (ngather) {
+    // job 0 fills clouds [0, split) from pts_a, job 1 clouds [split, C) from pts_b
+    const int want = split < C ? 2 : 1;
+    PC_REQUIRE(gather && ngather == want, "feat_fwd: %d gather jobs for this batch (want %d)",
+               ngather, want);
+    for (int k = 0; k < ngather; ++k) {
+      const pcadv_gather_job& j = gather[k];
+      const float* pts = k == 0 ? pts_a : pts_b;
+      const int rows = k == 0 ? split : C - split;
+      PC_REQUIRE(j.src && j.order && j.cursor && j.out == pts && j.B == rows && j.npts == N &&
+                     j.src_npts >= N && j.n_src > 0,
+                 "feat_fwd: gather job %d does not fill its %d x %d input batch", k, rows, N);
+      PC_REQUIRE(j.sigma >= 0.0 && (j.sigma == 0.0 || j.clip > 0.0),
+                 "feat_fwd: gather job %d: clip must be > 0", k);
+      PC_REQUIRE(!j.src_lab || (j.lab_width > 0 && j.lab_width <= N && j.out_lab),
+                 "feat_fwd: gather job %d: labels", k);
+      PC_REQUIRE(!j.src_seg, "feat_fwd: gather job %d: part ids are not gathered here", k);
+      gf.j[k] = j;
+    }
+    gf.n = ngather;
+  }
   if (precision == 1)
     return launch_feat_fwd_np<1, 1>(pts_a, pts_b, split, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3,
-                                    gmax, gidx, inc_counter, s, stamps);
+                                    gmax, gidx, inc_counter, s, stamps, gf);
   return launch_feat_fwd_np<6, 3>(pts_a, pts_b, split, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3,
-                                  gmax, gidx, inc_counter, s, stamps);
+                                  gmax, gidx, inc_counter, s, stamps, gf);
 }
 
 }  // namespace pcadv

@@ -88,8 +88,11 @@ def _bind_adam_state(optimizer, module, m_flat, v_flat, grad_flat, layout, step_
                                   "exp_avg": mv[name], "exp_avg_sq": vv[name]}
 
 
-def _fill_epilogue(a, epi):
-    """pcadv_adv_args.epi_* from (counters, ncounters, _LossRing) or None."""
+def _fill_epilogue(a, epi, gather=None):
+    """pcadv_adv_args.epi_* from (counters, ncounters, _LossRing) or None, and
+    .gather / .ngather from a ctypes GatherJob array or None."""
+    if gather is not None:
+        a.gather, a.ngather = ctypes.addressof(gather), len(gather)
     if epi is None:
         return
     counters, n, ring = epi
@@ -119,6 +122,7 @@ class AdvTrainStep:
     """
 
     _epilogue = None  # (counters, ncounters, _LossRing) folded into the last launch
+    _gather = None    # ctypes GatherJob array gathered by the first launch
 
     @contextlib.contextmanager
     def folded_epilogue(self, counters=None, ncounters=0, ring=None):
@@ -131,6 +135,18 @@ class AdvTrainStep:
             yield
         finally:
             self._epilogue = None
+
+    @contextlib.contextmanager
+    def folded_gather(self, jobs):
+        """Within the block every step call gathers its own input batches in
+        its first launch (pcadv_adv_args.gather: the loaders' gather_at jobs,
+        DeviceCloudLoader._gather_job, whose outputs are the step's inputs) -
+        the iteration's gather launch disappears."""
+        self._gather = (_lib.GatherJob * len(jobs))(*jobs)
+        try:
+            yield
+        finally:
+            self._gather = None
 
     def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
                  lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
@@ -228,8 +244,8 @@ class AdvTrainStep:
         a.part = int(part)
         a.precision = self.precision
         a.rng_rank, a.rng_world = self.rng_rank, self.rng_world
-        if part != 1:
-            _fill_epilogue(a, self._epilogue)
+        _fill_epilogue(a, self._epilogue if part != 1 else None,
+                       self._gather if part != 2 else None)
         return a
 
     def sync_hyper(self):
@@ -401,6 +417,7 @@ class ClsTrainStep:
     operands (configs[1] is quoted in bf16); everything else f32."""
 
     _epilogue = None  # (counters, ncounters, _LossRing) folded into the last launch
+    _gather = None    # ctypes GatherJob array gathered by the first launch
 
     @contextlib.contextmanager
     def folded_epilogue(self, counters=None, ncounters=0, ring=None):
@@ -413,6 +430,18 @@ class ClsTrainStep:
             yield
         finally:
             self._epilogue = None
+
+    @contextlib.contextmanager
+    def folded_gather(self, jobs):
+        """Within the block every step call gathers its own input batches in
+        its first launch (pcadv_adv_args.gather: the loaders' gather_at jobs,
+        DeviceCloudLoader._gather_job, whose outputs are the step's inputs) -
+        the iteration's gather launch disappears."""
+        self._gather = (_lib.GatherJob * len(jobs))(*jobs)
+        try:
+            yield
+        finally:
+            self._gather = None
 
     def __init__(self, model, B, N, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
                  lambda_cls=1.0, seed=0, device="cuda", precision="fp32", rng_rank=0, rng_world=1):
@@ -481,7 +510,7 @@ class ClsTrainStep:
         a.workspace_bytes = self.workspace.numel()
         a.precision = self.precision
         a.rng_rank, a.rng_world = self.rng_rank, self.rng_world
-        _fill_epilogue(a, self._epilogue)
+        _fill_epilogue(a, self._epilogue, self._gather)
         return a
 
     set_rng_rank = AdvTrainStep.set_rng_rank

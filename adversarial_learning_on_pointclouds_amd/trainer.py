@@ -239,12 +239,30 @@ class _GraphedIteration:
         else:
             gather_at_multi(items)
 
+    def _gather_jobs(self):
+        L = self.L
+        return [ld._gather_job(self.order[k], self.counters[L + k:L + k + 1], self.pts[k],
+                               self.lab if (k == 0 and ld.labels is not None) else None)
+                for k, ld in enumerate(self.loaders)]
+
+    def _folded(self):
+        """The fused steps gather their batches in their first launch and run
+        the iteration epilogue in their last: the graph is the step's launches
+        alone."""
+        st = self.step
+        if not hasattr(st, "folded_gather") or self.lab.shape[1] != 1:
+            return None
+        stack = contextlib.ExitStack()
+        stack.enter_context(st.folded_gather(self._gather_jobs()))
+        stack.enter_context(st.folded_epilogue(self.counters, 2 * self.L, self.ring))
+        return stack
+
     def _body(self, semi):
         L = self.L
-        self._gathers()
-        # the fused steps run the iteration epilogue in their finishing launch
-        fold = getattr(self.step, "folded_epilogue", None)
-        with (fold(self.counters, 2 * L, self.ring) if fold else contextlib.nullcontext()):
+        fold = self._folded()
+        if fold is None:
+            self._gathers()
+        with (fold or contextlib.nullcontext()):
             if L == 2:
                 self.step(self.pts[0], self.lab[:, 0], self.pts[1], semi=semi)
             else:
@@ -319,8 +337,13 @@ class _DPIteration(_GraphedIteration):
     def _part(self, k, semi):
         st, L = self.step, self.L
         if k == 1:
-            self._gathers()
-            st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=1)
+            if hasattr(st, "folded_gather"):
+                with st.folded_gather(self._gather_jobs()):
+                    st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi,
+                       part=1)
+            else:
+                self._gathers()
+                st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=1)
         elif k == 2:
             st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=2)
         elif k == 3:

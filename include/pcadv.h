@@ -490,6 +490,15 @@ typedef struct pcadv_adv_args {
   float* epi_ring;
   int epi_slots, epi_nl;
   int32_t* epi_ring_count;
+  /* The step's input batches gathered by its first launch (the feature
+   * forward's point loads) instead of a pcadv_gather_clouds_multi launch
+   * before the step: job 0 fills pts_gt (and, with src_lab, the label rows
+   * `labels` points into), job 1 pts_nogt (the adversarial step; the cls step
+   * takes job 0 only).  Each job as pcadv_gather_clouds_at (device jitter, no
+   * part ids) with out = the step's input buffer: bitwise that gather's
+   * batch.  ngather = 0: none.  ABI version 7. */
+  const pcadv_gather_job* gather;
+  int ngather;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

@@ -88,15 +88,16 @@ def test_gather_multi_is_bitwise_the_single_gathers(tmp_path):
     device jitter, a no-GT split of another batch size, and a ShapeNet split
     with part ids (different point counts per job)."""
     lst = _list(tmp_path, ["modelnet_gzip.h5", "modelnet_contig.h5"])
-    gt = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, None, npoints=64), 3, seed=3)
-    ng = D.DeviceCloudLoader(D.ModelNetDataset_noGT(lst, None, npoints=48), 5, seed=4)
+    rows = np.array([6, 0, 3, 7, 1])
+    gt = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, rows, npoints=32), 3, seed=3)
+    ng = D.DeviceCloudLoader(D.ModelNetDataset_noGT(lst, rows, npoints=24), 2, seed=4)
     sn = D.DeviceCloudLoader(D.ShapeNetDatasetGT(None, _list(tmp_path, ["shapenet_latest.h5"]),
                                                  num_classes=16, num_pts=50), 2, seed=5)
     dev = torch.device("cuda")
     jobs = []
     for ld in (gt, ng, sn):
         order = ld.epoch_order().to(dev)
-        cursor = torch.ones(1, dtype=torch.int32, device=dev)
+        cursor = torch.zeros(1, dtype=torch.int32, device=dev)  # batch 0: in every order
         lab = (torch.zeros(ld.B, int(ld.labels.shape[1]), dtype=torch.int64, device=dev)
                if ld.labels is not None else None)
         seg = torch.zeros(ld.B, ld.npts, dtype=torch.int64, device=dev) if ld.segs is not None else None
@@ -153,6 +154,67 @@ def test_folded_epilogue_equals_the_epilogue_launch(kind):
     assert int(out[1][2]) == 3 and out[1][3].tolist() == [3, 4, 5, 6]
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kind", ["adv", "cls"])
+def test_folded_gather_equals_the_gather_launch(kind):
+    """The step gathering its own input batches in its first launch
+    (pcadv_adv_args.gather, step.folded_gather) against gather_at + the step:
+    the same jittered points and labels in the input buffers, the same losses
+    and parameters (three iterations, the loaders' RNG steps and cursors
+    advanced between them)."""
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep, ClsTrainStep
+    import adversarial_learning_on_pointclouds_amd as pc
+    dev = torch.device("cuda")
+    B, N = 4, 96
+    rng = np.random.default_rng(77)
+
+    def mem(cls, n):
+        ds = cls.__new__(cls)
+        ds.sample_list, ds.npoints, ds.data_augmentation = None, N, True
+        ds.select_data = rng.uniform(-1, 1, (n, N, 3)).astype(np.float32)
+        if cls is D.ModelNetDatasetGT:
+            ds.select_labels = rng.integers(0, 40, n).astype(np.int32)
+        return ds
+    gds, nds = mem(D.ModelNetDatasetGT, 12), mem(D.ModelNetDataset_noGT, 12)
+    out = []
+    for fold in (False, True):
+        gt = D.DeviceCloudLoader(gds, B, seed=21)
+        ng = D.DeviceCloudLoader(nds, B, seed=22)
+        lds = (gt, ng) if kind == "adv" else (gt,)
+        orders = [ld.epoch_order().to(dev) for ld in lds]
+        cursors = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in lds]
+        pts = [torch.zeros(B, N, 3, device=dev) for _ in lds]
+        lab = torch.zeros(B, 1, dtype=torch.int64, device=dev)
+        torch.manual_seed(0)
+        model = pc.PointNetCls(k=40).to(dev)
+        if kind == "adv":
+            step = AdvTrainStep(model, pc.DeepConvDiscNet(40, 1).to(dev), B, N, seed=3, device=dev)
+            call = lambda: step(pts[0], lab[:, 0], pts[1])  # noqa: E731
+        else:
+            step = ClsTrainStep(model, B, N, seed=3, device=dev)
+            call = lambda: step(pts[0], lab[:, 0])  # noqa: E731
+        rec = []
+        for it in range(3):
+            labs = [lab] + [None] * (len(lds) - 1)
+            if fold:
+                jobs = [ld._gather_job(o, c, p, l)
+                        for ld, o, c, p, l in zip(lds, orders, cursors, pts, labs)]
+                with step.folded_gather(jobs):
+                    call()
+            else:
+                for ld, o, c, p, l in zip(lds, orders, cursors, pts, labs):
+                    ld.gather_at(o, c, p, l)
+                call()
+            rec += [t.clone() for t in pts] + [lab.clone(), step.losses.clone()]
+            for ld, c in zip(lds, cursors):
+                ld.step += 1
+                c += 1
+        rec.append(step.g_param.clone())
+        out.append(rec)
+    for i, (a, b) in enumerate(zip(*out)):
+        assert torch.equal(a, b), i
+    assert not torch.equal(out[0][0], out[0][len(out[0]) // 3])  # fresh batches per iteration
 
 
 class _Log:
