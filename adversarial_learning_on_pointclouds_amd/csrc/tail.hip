@@ -210,6 +210,7 @@ k_head_fwd(const float* __restrict__ h2, const float* __restrict__ w3, const flo
   HeadFwdLds& L = *reinterpret_cast<HeadFwdLds*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   TSTAMP(0, 0);
+  kernarg_prefetch(h2, w3, b3, labels, B, lambda_cls, logits, dlogits, din, dw1, db1, d1, lpart);
   const int rb = blockIdx.x / HF_SPLIT, sp = blockIdx.x % HF_SPLIT, j0 = sp * HF_COLS;
   const int C = 2 * B, r0 = rb * TR, nrows = min(TR, C - r0);
   const int label = wave < nrows && r0 + wave < B ? (int)labels[r0 + wave] : 0;
@@ -319,6 +320,10 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
     return;
   }
   TSTAMP(1, 0);
+  // every argument the row blocks read, in one round of scalar loads (a late
+  // first use costs a dependent kernarg round trip, common.h)
+  kernarg_prefetch(d3, w4, b4, w5, b5, wf, bf, soft_gt, soft_nogt, step, seed, lambda_adv, dd3,
+                   slabs, lpart3, dout, z4g, z5g, a4g, lab_off);
   const int r0 = blockIdx.x * TR, nrows = min(TR, R - r0);
   // per-row label inputs, fetched with the weights (thread t < 16: row r0 + t)
   float ysoft = 0.f;
@@ -531,6 +536,8 @@ k_head_bwd(const float* __restrict__ dz1, const float* __restrict__ h2,
     return;
   }
   TSTAMP(2, 0);
+  kernarg_prefetch(dz1, h2, drop_mask, drop_keep, din, dw1, w3, dlogits, dh2, lpart, nlp, lpart3,
+                   nlp3, losses, semi.on, semi.lambda, semi.th, semi.logits, semi.dout, ddp);
   const int r0 = blockIdx.x * TR, nrows = min(TR, C - r0);
   // this wave's row of log_softmax outputs (noGT) or CE gradient (GT)
   float lsm_or_dl = 0.f;
@@ -728,6 +735,7 @@ k_cls_head(const float* __restrict__ h2, const float* __restrict__ drop_mask, fl
     return;
   }
   ClsHeadLds& L = *reinterpret_cast<ClsHeadLds*>(smem);
+  kernarg_prefetch(h2, drop_mask, keep, w3, b3, labels, lambda_cls, logits, dlogits, dz2, rowloss);
   const int r0 = blockIdx.x * TR, nr = min(TR, B - r0);
   TSTAMP(0, 0);
   {
