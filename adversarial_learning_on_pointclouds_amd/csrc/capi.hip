@@ -223,6 +223,16 @@ static int adv_adam(const pcadv_adv_args* a, hipStream_t s) {
 static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w, float* logits);
 
 // pcadv_adv_args.epi_*: the iteration epilogue folded into the finishing launch
+// pcadv_adv_args.gather: the labels the head reads must be the ones job 0 gathers
+static int check_folded_gather(const pcadv_adv_args* a) {
+  if (!a->ngather) return PCADV_OK;
+  PC_REQUIRE(a->gather, "step: ngather %d without jobs", a->ngather);
+  const pcadv_gather_job& j = a->gather[0];
+  PC_REQUIRE(!j.src_lab || (j.lab_width == 1 && (const int64_t*)j.out_lab == a->labels),
+             "step: the gathered labels (job 0, width %d) are not the step's labels", j.lab_width);
+  return PCADV_OK;
+}
+
 static int step_epilogue(const pcadv_adv_args* a, IterEpi* e, bool* on) {
   *e = IterEpi{a->epi_counters, a->epi_ncounters, a->losses, a->epi_nl, a->epi_ring,
                a->epi_slots, a->epi_ring_count};
@@ -245,7 +255,10 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   PC_REQUIRE(a->part >= 0 && a->part <= 2, "adv_step: part %d (0 whole, 1 head, 2 feature bwd)",
              a->part);
   PC_REQUIRE(!(a->part == 1 && a->apply_adam), "adv_step: part 1 cannot apply Adam");
-  if (a->part != 2) PC_TRY(adv_head_part(a, s, w, logits));
+  if (a->part != 2) {
+    PC_TRY(check_folded_gather(a));
+    PC_TRY(adv_head_part(a, s, w, logits));
+  }
   if (a->part == 1) return PCADV_OK;
   // ---- PointNetfeat backward (sparse max-pool), then optimizer.step();
   //      optimizer_D.step() (:558-559) fused into its finishing launch --------
@@ -419,6 +432,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   const int32_t* rstep = mask ? nullptr : st;
   const int W = a->rng_world > 1 ? a->rng_world : 1, rr = W > 1 ? a->rng_rank : 0;
   PC_REQUIRE(rr >= 0 && rr < W, "cls_step: rng_rank %d not in [0, %d)", a->rng_rank, W);
+  PC_TRY(check_folded_gather(a));
   PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
                                G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
                                G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,

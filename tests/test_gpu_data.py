@@ -215,6 +215,13 @@ def test_folded_gather_equals_the_gather_launch(kind):
     for i, (a, b) in enumerate(zip(*out)):
         assert torch.equal(a, b), i
     assert not torch.equal(out[0][0], out[0][len(out[0]) // 3])  # fresh batches per iteration
+    # the labels the step reads must be the ones job 0 gathers
+    other = torch.zeros_like(lab)
+    jobs = [ld._gather_job(o, c, p, l) for ld, o, c, p, l in
+            zip(lds, orders, cursors, pts, [other] + [None] * (len(lds) - 1))]
+    with pytest.raises(Exception, match="gathered labels"):
+        with step.folded_gather(jobs):
+            call()
 
 
 class _Log:
