@@ -610,6 +610,44 @@ def test_graphed_trainer_equals_eager(tmp_path, drop_last):
     assert torch.equal(pa, pc_) and lc == [la[0], la[3], la[6]]
 
 
+def _cls_run(tmp_path, use_graph, iters, drop_last):
+    import argparse
+    import adversarial_learning_on_pointclouds_amd as pc
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from oracle import pointnet_np as onp
+    torch.manual_seed(0)
+    lst = _list(tmp_path, ["modelnet_gzip.h5", "modelnet_contig.h5"] * 2)
+    gt = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, None, npoints=32), 4, seed=13,
+                             drop_last=drop_last)
+    te = D.DeviceCloudLoader(D.ModelNetDatasetGT(lst, None, npoints=32, data_augmentation=False), 4)
+    G = onp.make_params(onp.cls_spec(40), seed=33)
+    model = pc.PointNetCls(k=40)
+    model.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    model.cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    args = argparse.Namespace(device="cuda", total_iterations=iters, iter_save_epoch=10 ** 9,
+                              iter_test_epoch=10 ** 9, exp_dir=str(tmp_path), lambda_cls=1.0,
+                              use_graph=use_graph, log_every=1, batch_size=4, tensorboard=False)
+    log = _Log()
+    trainer.run_training_pointnet_cls(gt, enumerate(gt), te, model, torch.nn.CrossEntropyLoss(),
+                                      opt, log, log, None, args)
+    params = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+    return params, [l for l in log.lines if l.startswith("iter")]
+
+
+@pytest.mark.parametrize("drop_last", [True, False])
+def test_graphed_cls_trainer_equals_eager(tmp_path, drop_last):
+    """run_training_pointnet_cls over a DeviceCloudLoader on the fused cls step:
+    the graphed iteration (the batch gathered by the step's first launch, the
+    epilogue in its last) equals the eager loop bitwise - parameters and loss
+    lines - across epoch wrap-arounds (10 clouds in batches of 4) and ragged
+    batches."""
+    pa, la = _cls_run(tmp_path, True, 7, drop_last)
+    pb, lb = _cls_run(tmp_path, False, 7, drop_last)
+    assert torch.equal(pa, pb)
+    assert la == lb and len(la) == 7
+
+
 def _ft_cls_run(tmp_path, use_graph, iters, drop_last=True):
     import argparse
     import adversarial_learning_on_pointclouds_amd as pc
