@@ -97,6 +97,27 @@ def test_error_message_roundtrip():
     assert b"bad shape" in lib.pcadv_last_error()
 
 
+def test_gather_multi_and_epilogue_refuse_bad_arguments():
+    """ABI 7's batched gather and iteration epilogue validate on the host before
+    any launch (no GPU needed): job counts outside 1..4, a job without its
+    source, counters beyond 64, a ring without its counter."""
+    import ctypes
+    from adversarial_learning_on_pointclouds_amd import _lib
+    lib = _lib.load()
+    jobs = (_lib.GatherJob * 5)()
+    for n in (0, 5):
+        assert lib.pcadv_gather_clouds_multi(jobs, n, None) == -1
+        assert b"jobs" in lib.pcadv_last_error()
+    assert lib.pcadv_gather_clouds_multi(jobs, 1, None) == -1  # src / order / cursor missing
+    assert b"bad arguments" in lib.pcadv_last_error()
+    x = ctypes.c_int(0)
+    assert lib.pcadv_iter_epilogue(ctypes.byref(x), 65, None, 0, None, 0, None, None) == -1
+    assert b"counters" in lib.pcadv_last_error()
+    f = ctypes.c_float(0)
+    assert lib.pcadv_iter_epilogue(None, 0, ctypes.byref(f), 4, ctypes.byref(f), 8, None, None) == -1
+    assert b"loss ring" in lib.pcadv_last_error()
+
+
 def test_image_pool_history_vs_reference_g10():
     """ImagePool(3) over six queries on a seeded Python RNG returns what the
     reference's utils/image_pool.py:26-55 returned (fixture g10)."""
