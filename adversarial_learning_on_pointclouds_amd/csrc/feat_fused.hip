@@ -123,15 +123,19 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
   int tile = blockIdx.x * TPW;
   // loads in the order they are consumed (the memory counter waits in issue
   // order): the first tile's points and conv1's weights, then conv2's B
-  // fragments, then W3 (split three ways only after conv1 of the first tile)
+  // fragments, then W3 (split three ways beside conv2's MFMAs of the first tile)
   float pv = tile < ntiles ? pts_next(tile) : 0.f;
   // conv1: thread = (channel tid & 63, 16-point group tid >> 6)
   const int c1 = tid & 63, pg = tid >> 6;
   const float wa = w1[c1 * 3 + 0], wb = w1[c1 * 3 + 1], wc = w1[c1 * 3 + 2], bb1 = b1[c1];
+  // (the scheduler otherwise issues conv2's fragments ahead of w1, so conv1
+  // waits for them)
+  __builtin_amdgcn_sched_barrier(0);
   // conv2: wave = (point tile wave >> 1, channel tile wave & 1), f32 B fragments
   f32x4 bf2[8];
   load_bfrag<64>(w2, 32 * (wave & 1), lane, bf2);
   const float bias2 = b2[32 * (wave & 1) + r];
+  __builtin_amdgcn_sched_barrier(0);
   // conv3: wave = channel tile (32 channels), W3 rows split three ways:
   // lane (r, h) holds k = 16 kb + 8 h .. + 8 of channel 32 wave + r
   f32x4 w3raw[8];
@@ -171,13 +175,20 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       const f32x4 q = *reinterpret_cast<const f32x4*>(&L.pts[p * 4]);
       L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
     }
-    if (it == 0) split_w3();  // W3 has landed by now (after conv1 of the first tile)
     __syncthreads();
     STAMP(4 + 5 * it);
     {  // conv2 + ReLU, written to LDS split three ways for conv3
       const int pt = wave >> 1, col = 32 * (wave & 1) + r;
       f32x16 acc = {};
       acc = mfma_rows_x_wt<64>(L.x1 + 32 * pt * S64, S64, bf2, acc, lane);
+      // W3's split beside conv2's MFMAs of the first tile (conv1 does not wait
+      // for W3 to land; the empty asm keeps the compiler from hoisting the
+      // split, and with it the wait for W3, back into conv1)
+      if (it == 0) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(w3raw[q]));
+        split_w3();
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float v = acc[i] + bias2;
