@@ -43,7 +43,9 @@ constexpr int PM_T = 256;   // 4 waves; 2 workgroups per CU (register-bound)
 constexpr int X2S = 72;     // bf16 row stride of the x2 planes (144 B: conflict-free b128 reads)
 
 constexpr int X3S = 136;     // f32 row stride of the x3 store staging (the two half-waves' rows 32 banks apart)
-struct MlpLds {
+// one tile per workgroup: the 64 x 128 conv3 tile staged over x1 / x2 for
+// 512-B row stores
+struct MlpLds1 {
   alignas(16) float pts[PM_P * 4];
   union {
     struct {
@@ -53,6 +55,21 @@ struct MlpLds {
     alignas(16) float x3[PM_P * X3S];  // the tile's conv3 output, staged for 16-B stores
   };
 };
+// two tiles per workgroup: each wave stages its own 64 x 32 slice of conv3's
+// output (x3w[wave], no workgroup barrier), kept until its stores are issued
+// during the next tile; 78.8 KB, two workgroups per CU
+struct MlpLds2 {
+  alignas(16) float pts[PM_P * 4];
+  alignas(16) float x1[PM_P * S64];
+  alignas(16) __bf16 x2[3][PM_P * X2S];
+  alignas(16) float x3w[4][PM_P * 32];  // [wave][point][32 channels]
+};
+// (the folded-gather instantiation keeps the block staging: with the
+// per-wave form it needs more than 256 VGPRs)
+template <int TPW, bool FOLD>
+constexpr bool kMlpWaveStage = TPW == 2 && !FOLD;
+template <int TPW, bool FOLD>
+using MlpLds = std::conditional_t<kMlpWaveStage<TPW, FOLD>, MlpLds2, MlpLds1>;
 
 // conv1 and conv2 run in exact f32 (VALU, then v_mfma_f32_32x32x2_f32 in the k
 // order of mfma_rows_x_wt), bitwise what the backward recomputes.  conv3 runs
@@ -73,7 +90,8 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
             float* __restrict__ x3g, int32_t* inc_counter, uint64_t* __restrict__ stamps,
             GatherFold gf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  MlpLds& L = *reinterpret_cast<MlpLds*>(smem);
+  MlpLds<TPW, FOLD>& L = *reinterpret_cast<MlpLds<TPW, FOLD>*>(smem);
+  constexpr bool WST = kMlpWaveStage<TPW, FOLD>;  // per-wave staging, stores during the next tile
 #ifdef PCADV_STAMPS
   uint64_t* st = stamps + (size_t)blockIdx.x * 16;
 #define STAMP(k) do { if (stamps && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -162,6 +180,22 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       }
   };
   STAMP(1);
+  // pieces [u0, u1) of the wave's staged 64 x 32 slice of tile `stile` as 16-B
+  // nontemporal stores: a tile's stores are issued during the next tile's
+  // conv1 / conv2 (the last tile's at once), so the chip's x3 writes are not
+  // one burst per tile
+  auto store_x3 = [&](int stile, int u0, int u1) {
+    const int sc = stile / T, sp0 = (stile % T) * PM_P;
+    const float* xw = reinterpret_cast<const float*>(smem + offsetof(MlpLds2, x3w)) + wave * PM_P * 32;
+    float* xg = x3g + ((size_t)sc * N + sp0) * 128 + 32 * wave;
+#pragma unroll
+    for (int u = u0; u < u1; ++u) {
+      const int e = lane + 64 * u, row = e >> 3, c4 = e & 7;
+      if (sp0 + row < N)
+        __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&xw[row * 32 + 4 * c4]),
+                                    reinterpret_cast<f32x4*>(xg + (size_t)row * 128 + 4 * c4));
+    }
+  };
 
   for (int it = 0; it < TPW && tile < ntiles; ++it, ++tile) {
     const int c = tile / T, p0 = (tile % T) * PM_P;
@@ -175,6 +209,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       const f32x4 q = *reinterpret_cast<const f32x4*>(&L.pts[p * 4]);
       L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
     }
+    if (WST && it > 0) store_x3(tile - 1, 0, 4);
     __syncthreads();
     STAMP(4 + 5 * it);
     {  // conv2 + ReLU, written to LDS split three ways for conv3
@@ -189,6 +224,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
         for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(w3raw[q]));
         split_w3();
       }
+      if (WST && it > 0) store_x3(tile - 1, 4, 8);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float v = acc[i] + bias2;
@@ -226,6 +262,23 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       asm volatile("s_nop 0" ::"v"(acc[0][0]), "v"(acc[1][15]));
 #endif
       STAMP(6 + 5 * it);
+      if constexpr (WST) {  // the wave's 64 x 32 slice through its own LDS rows, then
+        // 128-B row pieces with 16-B nontemporal stores (as below)
+        float* xw = L.x3w[wave];
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float v = acc[pt][i] + bias3;
+            xw[(32 * pt + acc_row(i, lane)) * 32 + r] = v > 0.f ? v : 0.f;
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the last tile's stores now; the others' during the next tile (whose
+        // conv3 rewrites these rows only after them)
+        if (!(it + 1 < TPW && tile + 1 < ntiles)) store_x3(tile, 0, 8);
+      } else {
       // stage the 64 x 128 tile through LDS (over x1 / x2: every wave is past
       // conv3's reads after the barrier), then write it as the contiguous 32 KB
       // it is in HBM with 16-B stores: a quarter of the store instructions.
@@ -248,6 +301,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
         if (p0 + row < N)
           __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&L.x3[row * X3S + 4 * c4]),
                                       reinterpret_cast<f32x4*>(xg + (size_t)row * 128 + 4 * c4));
+      }
       }
       STAMP(7 + 5 * it);
     }
@@ -793,17 +847,17 @@ static int feat_fwd_attrs() {
                             (int)sizeof(C4Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(MlpLds)) != hipSuccess ||
+                            (int)sizeof(MlpLds<2, false>)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 1, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(MlpLds)) != hipSuccess ||
+                            (int)sizeof(MlpLds<1, false>)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(MlpLds)) != hipSuccess ||
+                            (int)sizeof(MlpLds<2, true>)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 1, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(MlpLds)) != hipSuccess) {
-      set_error("feat_fwd: cannot reserve LDS (%zu / %zu bytes)", sizeof(C4Lds), sizeof(MlpLds));
+                            (int)sizeof(MlpLds<1, true>)) != hipSuccess) {
+      set_error("feat_fwd: cannot reserve LDS (%zu / %zu bytes)", sizeof(C4Lds), sizeof(MlpLds<2, false>));
       return PCADV_EHIP;
     }
     attr_set = true;
@@ -850,7 +904,8 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
   const dim3 grid(one ? ntiles : (ntiles + 1) / 2);
   auto kern = one ? (gf.n ? k_point_mlp<NP3, 1, true> : k_point_mlp<NP3, 1, false>)
                   : (gf.n ? k_point_mlp<NP3, 2, true> : k_point_mlp<NP3, 2, false>);
-  hipLaunchKernelGGL(kern, grid, dim3(PM_T), sizeof(MlpLds), s, pts_a, pts_b, split, N, T, ntiles,
+  const size_t lds = one ? sizeof(MlpLds<1, false>) : gf.n ? sizeof(MlpLds<2, true>) : sizeof(MlpLds<2, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(PM_T), lds, s, pts_a, pts_b, split, N, T, ntiles,
                      w1, b1, w2, b2, w3, b3, x3, inc_counter, mlp_stamps, gf);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
   return launch_conv4_max_np<NP3, NP4>(x3, C, N, w4, b4, gmax, gidx, s, stamps);
