@@ -141,7 +141,8 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
   int tile = blockIdx.x * TPW;
   // loads in the order they are consumed (the memory counter waits in issue
   // order): the first tile's points and conv1's weights, then conv2's B
-  // fragments, then W3 (split three ways beside conv2's MFMAs of the first tile)
+  // fragments; W3 after the first tile's conv1 (split three ways beside conv2's
+  // MFMAs of the first tile)
   float pv = tile < ntiles ? pts_next(tile) : 0.f;
   // conv1: thread = (channel tid & 63, 16-point group tid >> 6)
   const int c1 = tid & 63, pg = tid >> 6;
@@ -157,14 +158,14 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
   // conv3: wave = channel tile (32 channels), W3 rows split three ways:
   // lane (r, h) holds k = 16 kb + 8 h .. + 8 of channel 32 wave + r
   f32x4 w3raw[8];
-  {
+  auto load_w3 = [&]() {
     const float* wrow = w3 + (size_t)(32 * wave + r) * 64 + 8 * h;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       w3raw[2 * kb] = *reinterpret_cast<const f32x4*>(wrow + 16 * kb);
       w3raw[2 * kb + 1] = *reinterpret_cast<const f32x4*>(wrow + 16 * kb + 4);
     }
-  }
+  };
   const float bias3 = b3[32 * wave + r];
   bf16x8 w3h[4], w3m[4], w3l[4];
   auto split_w3 = [&]() {
@@ -208,6 +209,13 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
       const int p = pg * 16 + i;
       const f32x4 q = *reinterpret_cast<const f32x4*>(&L.pts[p * 4]);
       L.x1[p * S64 + c1] = conv1_point(wa, wb, wc, bb1, q.x, q.y, q.z);
+    }
+    // W3 issued only now: the prologue's in-order issue of its eight loads
+    // would hold up conv1 (it lands during the barrier and conv2's MFMAs)
+    if (it == 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_w3();
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (WST && it > 0) store_x3(tile - 1, 0, 4);
     __syncthreads();
