@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 gpurun_out/pw_tests.log
 for i in 1 2 3; do
   for lib in build/abx/lib*.so $tree; do
-    PCADV_LIB=$lib timeout -k 10 200 python bench.py --config cls_ft --steps 200 --warmup 20 > gpurun_out/pw_ab.json 2>/dev/null || { echo "bench failed"; exit 1; }
+    PCADV_LIB=$lib timeout -k 10 200 python bench.py --config cls_ft --steps 200 --warmup 20 --no-cpu > gpurun_out/pw_ab.json 2>/dev/null || { echo "bench failed"; exit 1; }
     python -c "import json,sys; d=json.loads(open('gpurun_out/pw_ab.json').read().strip().splitlines()[-1]); print('AB', sys.argv[1], d['ms_per_step'])" $(basename $lib)
   done
 done
