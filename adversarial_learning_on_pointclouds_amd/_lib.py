@@ -16,6 +16,8 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PCADV_LIB", os.path.join(_HERE, "lib", "libpcadv.so"))
+# the layout of include/pcadv.h these signatures and AdvArgs bind (pcadv_abi_version())
+ABI_VERSION = 7
 
 PCADV_OK = 0
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
@@ -185,6 +187,15 @@ def load():
                 f"libpcadv.so not found at {LIB_PATH}: build it with `make` (hipcc, gfx950). "
                 "There is no CPU fallback for the pcadv ops.")
         lib = ctypes.CDLL(LIB_PATH)
+        lib.pcadv_abi_version.restype = ctypes.c_int
+        lib.pcadv_abi_version.argtypes = []
+        abi = lib.pcadv_abi_version()
+        if abi != ABI_VERSION:
+            # a stale build (or an older PCADV_LIB) would bind silently with shifted
+            # arguments: e.g. ABI 7's rng_row0 would land in an ABI 5 gather's stream
+            raise PcadvError(
+                f"{LIB_PATH} implements pcadv ABI {abi}, this package binds ABI {ABI_VERSION}: "
+                "rebuild it with `make`")
         for name, (res, args) in SIGNATURES.items():
             if os.environ.get("PCADV_LIB") and not hasattr(lib, name):
                 continue  # an older library picked for an A/B timing run

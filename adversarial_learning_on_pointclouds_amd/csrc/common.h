@@ -232,9 +232,12 @@ struct GatherFold {
 // The end of a graph-replayed training iteration (pcadv_iter_epilogue, or
 // folded into the step's last launch through pcadv_adv_args.epi_*): every
 // counter += 1 (the loaders' RNG steps and batch cursors) and, with a ring,
-// losses[0..nl) into slot (*ring_count % slots), *ring_count += 1.  One wave:
-// every lane reads *ring_count in the same instruction, and lane 0's store of
-// the increment depends on its own read.
+// losses[0..nl) into slot (*ring_count % slots), *ring_count += 1.  Called by
+// the threads 0..63 of a workgroup: the count is read once and broadcast from
+// the first lane (readfirstlane), and lane 0 stores the increment after that
+// read, so the slot every writing lane (lane < nl <= 32) uses is the value
+// before the increment also where a workgroup's first 64 threads were split
+// over two wavefronts.
 struct IterEpi {
   int32_t* counters;
   int ncounters;
@@ -246,7 +249,7 @@ struct IterEpi {
 };
 __device__ __forceinline__ void iter_epi_wave(const IterEpi& e, int lane) {
   if (e.ring && e.ring_count) {
-    const int32_t cnt = *e.ring_count;
+    const int32_t cnt = __builtin_amdgcn_readfirstlane(*e.ring_count);
     const int slot = (int)((uint32_t)cnt % (uint32_t)e.slots);
     if (lane < e.nl) e.ring[(size_t)slot * e.nl + lane] = e.losses[lane];
     if (lane == 0) *e.ring_count = cnt + 1;

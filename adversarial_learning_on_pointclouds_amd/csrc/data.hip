@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(64) k_iter_epilogue(IterEpi e) { iter_epi_wave
 int check_iter_epi(const IterEpi& e) {
   PC_REQUIRE(e.ncounters >= 0 && e.ncounters <= 64 && (e.ncounters == 0 || e.counters),
              "iter_epilogue: %d counters (at most 64)", e.ncounters);
-  PC_REQUIRE(!e.ring || (e.ring_count && e.losses && e.nl > 0 && e.nl <= 64 && e.slots > 0),
+  PC_REQUIRE(!e.ring || (e.ring_count && e.losses && e.nl > 0 && e.nl <= 32 && e.slots > 0),
              "iter_epilogue: bad loss ring (nl=%d slots=%d)", e.nl, e.slots);
   return PCADV_OK;
 }

@@ -259,7 +259,17 @@ class AdvTrainStep:
             self.hp.update(lr=float(g["lr"]), betas=tuple(float(b) for b in g["betas"]),
                            eps=float(g["eps"]))
         if opt_d is not None:
-            self.hp["lr_D"] = float(opt_d.param_groups[0]["lr"])
+            gd = opt_d.param_groups[0]
+            if opt is not None and (tuple(float(b) for b in gd["betas"]) != self.hp["betas"]
+                                    or float(gd["eps"]) != self.hp["eps"]
+                                    or float(gd.get("weight_decay", 0) or 0) != 0.0):
+                # the fused Adam applies ONE (betas, eps) pair to G and D (pcadv_adv_args)
+                raise ValueError(
+                    "the fused adversarial step applies the generator optimizer's betas / eps to "
+                    "the discriminator too: optimizer_D now has betas "
+                    f"{tuple(gd['betas'])}, eps {gd['eps']}, weight_decay "
+                    f"{gd.get('weight_decay', 0)} against {self.hp['betas']}, {self.hp['eps']}, 0")
+            self.hp["lr_D"] = float(gd["lr"])
 
     def set_rng_rank(self, rank, world):
         """Key the device draws by the global batch's rows (data parallelism)."""

@@ -604,6 +604,13 @@ def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args):
         g = opt.param_groups[0]
         if g.get("weight_decay", 0) or g.get("amsgrad") or g.get("maximize"):
             return False
+    # the fused Adam applies one (betas, eps) pair to both networks (only the
+    # learning rates are separate): a discriminator optimizer with its own
+    # betas / eps runs the autograd body with the torch optimizers
+    g, gd = optimizer.param_groups[0], optimizer_D.param_groups[0]
+    if tuple(map(float, g["betas"])) != tuple(map(float, gd["betas"])) \
+            or float(g["eps"]) != float(gd["eps"]):
+        return False
     if type(gan_loss) is not torch.nn.BCEWithLogitsLoss or gan_loss.weight is not None \
             or gan_loss.pos_weight is not None or gan_loss.reduction != "mean":
         return False
@@ -707,6 +714,14 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                 "data-parallel run_training runs the fused step graphed over DeviceCloudLoaders: "
                 "PointNetCls(k=40) + DeepConvDiscNet(40, 1), Adam, CE / BCE, ImagePool(0), equal "
                 "GT / no-GT batches (args.use_graph on)")
+        if semi_loss is not None and args.semi_start > 0:
+            # k_head_bwd normalises the pseudo-label CE by this rank's own kept
+            # count (a data-dependent mean), so averaging the ranks' gradients
+            # is not the global batch's mean over all kept clouds
+            raise NotImplementedError(
+                "data-parallel run_training_semi: the pseudo-label CE is a mean over each rank's "
+                "kept clouds, which a gradient average does not turn into the global batch's "
+                "mean; run the semi phase on one process")
         rank = dist.get_rank()
 
     def emit(i_iter, vals, semi_on):

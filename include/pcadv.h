@@ -406,7 +406,7 @@ int pcadv_gather_clouds_multi(const pcadv_gather_job* jobs, int njobs, hipStream
 
 /* The end of a graph-replayed training iteration (trainer.py): counters[i] += 1
  * for i < ncounters (<= 64: loaders' RNG steps and batch cursors), and, when
- * ring is given, losses[0..nl) into slot (*ring_count % slots) of the [slots][nl]
+ * ring is given, losses[0..nl) (nl <= 32) into slot (*ring_count % slots) of the [slots][nl]
  * loss ring, then *ring_count += 1 (the host reads the ring every `slots`
  * iterations instead of copying the losses out every iteration). */
 int pcadv_iter_epilogue(int32_t* counters, int ncounters, const float* losses, int nl,

@@ -25,7 +25,7 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
     assert sorted(_lib.SIGNATURES) == syms  # nothing bound that the header does not declare
-    assert lib.pcadv_abi_version() == 7
+    assert lib.pcadv_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_layout_matches_header_enums():
@@ -255,3 +255,18 @@ def test_ctypes_structs_match_the_c_layout(name, tmp_path):
 def ctypes_sizeof(t):
     import ctypes
     return ctypes.sizeof(t)
+
+
+def test_load_refuses_another_abi(tmp_path, monkeypatch):
+    """a library of another ABI (a stale build, an old PCADV_LIB) is
+    refused at load instead of binding shifted arguments."""
+    import subprocess
+    from adversarial_learning_on_pointclouds_amd import _lib
+    src = tmp_path / "old.c"
+    src.write_text("int pcadv_abi_version(void) { return 5; }\n")
+    so = tmp_path / "libold.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(so))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.PcadvError, match="ABI 5"):
+        _lib.load()

@@ -295,7 +295,7 @@ def test_rccl_bucketed_overlap_path_single_rank(tmp_path):
 H5 = os.path.join(os.path.dirname(__file__), "golden", "h5")
 
 
-def _trainer_run(out, rank, world, B, iters, tmp):
+def _trainer_run(out, rank, world, B, iters, tmp, semi=False):
     import argparse
     import adversarial_learning_on_pointclouds_amd as pc
     from adversarial_learning_on_pointclouds_amd import dataset as D
@@ -334,10 +334,17 @@ def _trainer_run(out, rank, world, B, iters, tmp):
             self.lines.append(s)
 
     log = _Log()
-    trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), te, model, model_D,
-                         torch.nn.BCEWithLogitsLoss(),
-                         torch.nn.CrossEntropyLoss(), opt, opt_D, ImagePool(0), ImagePool(0),
-                         log, log, None, args)
+    if semi:
+        args.semi_start, args.semi_TH, args.lambda_semi = 1, 0.5, 1.0
+        trainer.run_training_semi(gt, ng, enumerate(gt), enumerate(ng), te, model, model_D,
+                                  torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(),
+                                  torch.nn.CrossEntropyLoss(ignore_index=255), opt, opt_D,
+                                  ImagePool(0), ImagePool(0), log, log, None, args)
+    else:
+        trainer.run_training(gt, ng, enumerate(gt), enumerate(ng), te, model, model_D,
+                             torch.nn.BCEWithLogitsLoss(),
+                             torch.nn.CrossEntropyLoss(), opt, opt_D, ImagePool(0), ImagePool(0),
+                             log, log, None, args)
     params = torch.cat([p.detach().reshape(-1) for p in list(model.parameters()) +
                         list(model_D.parameters())]).cpu().numpy()
     loss = np.array([[float(x) for x in re.findall(r"= +([-0-9.]+)", l)[1:]]
@@ -345,13 +352,21 @@ def _trainer_run(out, rank, world, B, iters, tmp):
     np.savez(out, params=params, loss=loss)
 
 
-def _dp_trainer_worker(rank, port, tmp, world, B, iters):
+def _dp_trainer_worker(rank, port, tmp, world, B, iters, semi=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        _trainer_run(os.path.join(tmp, f"dp{rank}.npz"), rank, world, B, iters, tmp)
+        if semi:
+            try:
+                _trainer_run(os.path.join(tmp, f"dp{rank}.npz"), rank, world, B, iters, tmp,
+                             semi=True)
+            except NotImplementedError as e:
+                with open(os.path.join(tmp, f"semi_refused{rank}.txt"), "w") as f:
+                    f.write(str(e))
+        else:
+            _trainer_run(os.path.join(tmp, f"dp{rank}.npz"), rank, world, B, iters, tmp)
     finally:
         dist.destroy_process_group()
 
@@ -380,6 +395,18 @@ def test_dp_trainer_equals_global_batch_trainer(tmp_path):
         np.abs(r0["params"] - one["params"]).max()
     assert r0["loss"].shape == one["loss"].shape == (iters, 3)
     np.testing.assert_allclose(r0["loss"], one["loss"], rtol=2e-3, atol=2e-3)
+
+
+def test_dp_semi_refused(tmp_path):
+    """run_training_semi over sharded loaders is refused loudly:
+    k_head_bwd normalises the pseudo-label CE by each rank's own kept count, so
+    the averaged gradient would not be the global batch's."""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_dp_trainer_worker, args=(_free_port(), str(tmp_path), world, 4, 3, True),
+             nprocs=world, join=True)
+    for r in range(world):
+        assert "pseudo-label" in (tmp_path / f"semi_refused{r}.txt").read_text()
 
 
 def _initial_params():
