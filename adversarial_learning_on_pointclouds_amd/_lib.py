@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PCADV_LIB", os.path.join(_HERE, "lib", "libpcadv.so"))
 # the layout of include/pcadv.h these signatures and AdvArgs bind (pcadv_abi_version())
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 PCADV_OK = 0
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
@@ -94,6 +94,7 @@ class AdvArgs(ctypes.Structure):
         ("epi_counters", _vp), ("epi_ncounters", _i), ("epi_ring", _vp), ("epi_slots", _i),
         ("epi_nl", _i), ("epi_ring_count", _vp),
         ("gather", _vp), ("ngather", _i),
+        ("feat_gmax", _vp), ("feat_dgmax", _vp),
     ]
 
 
@@ -124,6 +125,8 @@ SIGNATURES = {
     "pcadv_linear_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _u64, _f, _vp, _vp, _vp, _vp, _vp,
                               _i, _i, _i, _i, _vp]),
     "pcadv_adam": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _vp]),
+    "pcadv_adam2": (_i, [_vp, _vp, _vp, _vp, _i64, _f, _vp, _vp, _vp, _vp, _i64, _f, _vp, _f, _f,
+                         _f, _vp]),
     "pcadv_pw_fwd": (_i, [_vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "pcadv_pw_bwd_data": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp]),
     "pcadv_pw_bwd_weight_workspace_bytes": (_sz, [_i, _i, _i]),

@@ -252,9 +252,22 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   const float* G = a->g_param;
   float* gG = a->g_grad;
   float* logits = a->logits ? a->logits : w.logits;
-  PC_REQUIRE(a->part >= 0 && a->part <= 2, "adv_step: part %d (0 whole, 1 head, 2 feature bwd)",
-             a->part);
-  PC_REQUIRE(!(a->part == 1 && a->apply_adam), "adv_step: part 1 cannot apply Adam");
+  PC_REQUIRE(a->part >= 0 && a->part <= 3,
+             "adv_step: part %d (0 whole, 1 head, 2 feature bwd, 3 head on given features)", a->part);
+  PC_REQUIRE(!((a->part == 1 || a->part == 3) && a->apply_adam),
+             "adv_step: part %d cannot apply Adam", a->part);
+  if (a->part == 3) {
+    // the caller's feature extractor (the feature-transform generator) ran
+    // outside: no gather, precision or epilogue apply to this part
+    PC_REQUIRE(a->feat_gmax && a->feat_dgmax, "adv_step: part 3 needs feat_gmax and feat_dgmax");
+    PC_REQUIRE(!a->ngather && !a->epi_ncounters && !a->epi_ring,
+               "adv_step: part 3 takes no folded gather or epilogue");
+    PC_REQUIRE(a->step_count, "adv_step: step_count");
+    // the iteration's step number, as the feature forward's first launch
+    // advances it in parts 0 / 1 (the device draws and Adam key on it)
+    PC_TRY(launch_inc(a->step_count, s));
+    return adv_head_part(a, s, w, logits);
+  }
   if (a->part != 2) {
     PC_TRY(check_folded_gather(a));
     PC_TRY(adv_head_part(a, s, w, logits));
@@ -306,14 +319,19 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   const int W = a->rng_world > 1 ? a->rng_world : 1, rr = W > 1 ? a->rng_rank : 0;
   PC_REQUIRE(rr >= 0 && rr < W, "adv_step: rng_rank %d not in [0, %d)", a->rng_rank, W);
 
-  // ---- generator forward, both loaders in one launch (:468, :490) ----------
-  PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
-                               G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
-                               G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
-                               G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision, a->gather,
-                               a->ngather));
-  PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
+  // ---- generator forward, both loaders in one launch (:468, :490); part 3:
+  //      the caller's pooled features (and no hit sort: no sparse chunks) ----
+  const bool ext = a->part == 3;
+  const float* gmax = ext ? a->feat_gmax : w.gmax;
+  float* dgmax = ext ? a->feat_dgmax : w.dgmax;
+  if (!ext)
+    PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_nogt, B, C, N, G + PCADV_G_CONV1_W,
+                                 G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                                 G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
+                                 G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
+                                 w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision, a->gather,
+                                 a->ngather));
+  PC_TRY(launch_linear_fwd(gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   // fc2 + dropout: a device-drawn mask is stored for the backward
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
@@ -334,7 +352,8 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
   PC_TRY(launch_disc_tail(w.d3, B, D + PCADV_D_CONV4_W, D + PCADV_D_CONV4_B, D + PCADV_D_CONV5_W,
                           D + PCADV_D_CONV5_B, D + PCADV_D_FC_W, D + PCADV_D_FC_B, a->soft_gt,
                           a->soft_nogt, st, a->rng_seed, a->lambda_adv, w.dd3, w.dslabs, w.lpart3,
-                          w.dout, s, w.gidx, C, N, w.sortrec, w.z4, w.z5, w.a4, rr * B));
+                          w.dout, s, w.gidx, C, N, ext ? nullptr : w.sortrec, w.z4, w.z5, w.a4,
+                          rr * B));
   // ---- discriminator backward: parameter grads from rows [0,2B) (D loss),
   //      input grads of all rows (rows [2B,3B) feed the generator, D frozen).
   //      Every data gradient is stored as the layer below's dz (its activation
@@ -395,8 +414,8 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,
                              C, 256, 512, s, &ex));
   }
-  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
-                           G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
+  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, gmax,
+                           G + PCADV_G_FC1_W, dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
   return PCADV_OK;
 }
@@ -490,7 +509,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 7; }
+int pcadv_abi_version(void) { return 8; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -626,6 +645,17 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
   PC_TRY(launch_adam2(param, grad, exp_avg, exp_avg_sq, n, lr, nullptr, nullptr, nullptr, nullptr,
                       0, 0.f, step_count, 1, beta1, beta2, eps, stream));
   return launch_inc(step_count, stream);
+}
+
+int pcadv_adam2(float* p0, const float* g0, float* m0, float* v0, int64_t n0, float lr0,
+                float* p1, const float* g1, float* m1, float* v1, int64_t n1, float lr1,
+                const int32_t* step_count, float beta1, float beta2, float eps,
+                hipStream_t stream) {
+  PC_REQUIRE(n0 > 0 && n1 >= 0 && step_count && p0 && g0 && m0 && v0 &&
+                 (n1 == 0 || (p1 && g1 && m1 && v1)),
+             "adam2: bad arguments");
+  return launch_adam2(p0, g0, m0, v0, n0, lr0, p1, g1, m1, v1, n1, lr1, step_count, 0, beta1,
+                      beta2, eps, stream);
 }
 
 // ---- dense point-wise GEMM engine (segmentation net) -----------------------

@@ -123,6 +123,29 @@ class DataParallelAdvStep:
         s._restore(saved)
         return _DPGraph(g_fwd, g_adam, s, self.group)
 
+    def capture_single(self, pts_gt, labels, pts_nogt):
+        """The whole data-parallel iteration as ONE HIP graph: the step's parts,
+        the two all-reduces (captured on RCCL's stream, forked from and joined
+        back to the capturing stream by the collectives' own event waits) and
+        the split Adam, in the order __call__ issues them.  One replay per
+        iteration instead of four graphs around host-issued collectives
+        (VERDICT r05 item 6).  State is left as it was before the capture."""
+        s = self.step
+        saved = s._snapshot()
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=s.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):  # warm-up: communicators and kernels initialised
+            self(pts_gt, labels, pts_nogt)
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self(pts_gt, labels, pts_nogt)
+        torch.cuda.synchronize()
+        s._restore(saved)
+        return g
+
 
 class _DPGraph:
     def __init__(self, g_fwd, g_adam, step, group):

@@ -135,8 +135,19 @@ def conv_max_fwd(x, w, b, relu_before_max=False):
     return gmax, gidx
 
 
-def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True):
-    """Backward of conv_max_fwd: (dx (C, N, K) or None, dw like w, db (O,))."""
+def _out(t, name, like_shape, dev):
+    """A caller-given output buffer (e.g. a view of a flat gradient buffer), checked."""
+    if t is None:
+        return torch.empty(like_shape, device=dev)
+    _req(t, name)
+    if t.numel() != int(torch.Size(like_shape).numel()):
+        raise ValueError(f"{name}: {t.numel()} elements, expected {tuple(like_shape)}")
+    return t
+
+
+def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True, dw_out=None, db_out=None):
+    """Backward of conv_max_fwd: (dx (C, N, K) or None, dw like w, db (O,));
+    dw_out / db_out: write the weight gradients there instead."""
     lib = _lib.load()
     _req(x, "x")
     C, N, K = x.shape
@@ -147,8 +158,8 @@ def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True):
     if gmax_relu is not None:
         _req(gmax_relu, "gmax", (C, O))
     dx = torch.empty(C, N, K, device=x.device) if need_dx else None
-    dw = torch.empty_like(w)
-    db = torch.empty(O, device=x.device)
+    dw = _out(dw_out, "dw", tuple(w.shape), x.device)
+    db = _out(db_out, "db", (O,), x.device)
     check(lib.pcadv_conv_max_bwd(ptr(dgmax), ptr(gidx), ptr(gmax_relu), ptr(x), C, N, K, ptr(wm),
                                  O, ptr(dw), ptr(db), ptr(dx), stream_ptr()), "pcadv_conv_max_bwd")
     return dx, dw, db
@@ -200,8 +211,10 @@ def pw_bwd_data(dy, y, act, w, K, kmajor=False, rows_per_w=0, out=None):
     return dx
 
 
-def pw_bwd_weight(dy, y, act, x, rows_per_group=0, kmajor=False, need_db=True):
-    """(dW, db) of y = act(x W^T + b): dW (groups, O, K) or kmajor (groups, K, O)."""
+def pw_bwd_weight(dy, y, act, x, rows_per_group=0, kmajor=False, need_db=True, dw_out=None,
+                  db_out=None):
+    """(dW, db) of y = act(x W^T + b): dW (groups, O, K) or kmajor (groups, K, O);
+    dw_out / db_out: write them there instead (same element counts)."""
     lib = _lib.load()
     _req(dy, "dy")
     _req(x, "x")
@@ -211,8 +224,8 @@ def pw_bwd_weight(dy, y, act, x, rows_per_group=0, kmajor=False, need_db=True):
         _req(y, "y", tuple(dy.shape))
     G = rows_per_group if rows_per_group else M
     groups = M // G
-    dw = torch.empty(groups, *((K, O) if kmajor else (O, K)), device=dy.device)
-    db = torch.empty(groups, O, device=dy.device) if need_db else None
+    dw = _out(dw_out, "dw", (groups, *((K, O) if kmajor else (O, K))), dy.device)
+    db = _out(db_out, "db", (groups, O), dy.device) if need_db else None
     nb = lib.pcadv_pw_bwd_weight_workspace_bytes(M, O, K)
     ws = torch.empty(nb, device=dy.device, dtype=torch.uint8)
     check(lib.pcadv_pw_bwd_weight(ptr(dy), ptr(y), act, ptr(x), M, O, K, rows_per_group,
@@ -264,7 +277,8 @@ def linear_fwd(x, w, b, act=ACT_NONE, mask=None, p=0.0, add_identity_k=0):
     return y
 
 
-def linear_bwd(dy, y, act, mask, p, x, w, need_dx=True, need_dw=True, m_w=None):
+def linear_bwd(dy, y, act, mask, p, x, w, need_dx=True, need_dw=True, m_w=None, dw_out=None,
+               db_out=None):
     lib = _lib.load()
     M, K = x.shape
     wm = _mat(w)
@@ -277,8 +291,8 @@ def linear_bwd(dy, y, act, mask, p, x, w, need_dx=True, need_dw=True, m_w=None):
         _req(mask, "dropout mask", (M, Nout))
     m_w = M if m_w is None else m_w
     dx = torch.empty(M, K, device=x.device) if need_dx else None
-    dw = torch.empty_like(w) if need_dw else None
-    db = torch.empty(Nout, device=x.device) if need_dw else None
+    dw = _out(dw_out, "weight grad", tuple(w.shape), x.device) if need_dw else None
+    db = _out(db_out, "bias grad", (Nout,), x.device) if need_dw else None
     check(lib.pcadv_linear_bwd(ptr(dy), ptr(y), act, ptr(mask), None, 0, float(p), ptr(x), ptr(wm),
                                ptr(dx), ptr(dw), ptr(db), M, m_w, Nout, K, stream_ptr()),
           "pcadv_linear_bwd")

@@ -417,6 +417,237 @@ class AdvTrainStep:
                 p.grad = gv[name]
 
 
+def ft_layout(model):
+    """Flat layout of a PointNetCls(feature_transform=True): the plain
+    generator's tensors at their include/pcadv.h offsets (so the fused tail's
+    fc1..fc3 offsets hold), then the STNkd(64) parameters in state_dict order,
+    each 256-B aligned.  Returns (layout, numel)."""
+    layout = dict(G_LAYOUT)
+    off = (G_NUMEL + 63) // 64 * 64
+    for name, p in model.named_parameters():
+        if name in layout:
+            continue
+        layout[name] = off
+        off += (p.numel() + 63) // 64 * 64
+    return layout, off
+
+
+class AdvFtTrainStep(AdvTrainStep):
+    """run_training's iteration (utils/trainer.py:426-559) with a
+    PointNetCls(k=40, feature_transform=True) generator + DeepConvDiscNet(40, 1)
+    (VERDICT r05 item 4), without autograd:
+
+    * the generator's feature extractor over BOTH batches as one C = 2B
+      pass on the point-wise kernels: conv1, conv2, STNkd(64) (conv 64->64->128,
+      conv 128->1024 + ReLU + max on k_conv4_max, fc1..fc3 + I), the transform
+      x2 T (models/pointnet.py:118-122), conv3, conv4 + max;
+    * everything from fc1 on - head, dropout, log_softmax / CE, the three D
+      passes and their BCE terms, D's gradients, the head backward - is the
+      fused step's own tail (pcadv_adv_step part 3, the same launches as the
+      plain step), returning dL/dgmax;
+    * the backward of the extractor by hand (sparse max-pool backwards, the
+      transform's dT = x2^T dx2t and dx2 = dx2t T^T, STNkd's backward, its
+      input gradient added into conv2's), weight gradients written straight
+      into the flat gradient buffer;
+    * both Adam updates in one launch (pcadv_adam2).
+
+    The regulariser is not part of run_training's loss (the reference leaves
+    it commented out, utils/trainer.py:473-476, :511-517).  Parameters,
+    gradients, Adam moments and the device draws are laid out and keyed as in
+    AdvTrainStep (ft_layout for the generator), so the trainer's graphed
+    iteration, checkpoints and the torch optimizers' state work unchanged."""
+
+    supports_parts = False
+
+    def __init__(self, model, model_D, B, N, optimizer=None, optimizer_D=None, lr=1e-4,
+                 lr_D=1e-4, betas=(0.9, 0.999), eps=1e-8, lambda_cls=1.0, lambda_adv=0.001,
+                 seed=0, device="cuda", lambda_semi=1.0, semi_th=0.8, rng_rank=0, rng_world=1):
+        self.lib = _lib.load()
+        if not getattr(model, "feature_transform", False):
+            raise ValueError("AdvFtTrainStep: the generator has no feature transform "
+                             "(use AdvTrainStep)")
+        self.set_rng_rank(rng_rank, rng_world)
+        self.model, self.model_D = model, model_D
+        self.precision = 0
+        self.B, self.N = int(B), int(N)
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("AdvFtTrainStep runs on the HIP device only")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        if optimizer is not None:
+            g = optimizer.param_groups[0]
+            lr, betas, eps = g["lr"], tuple(g["betas"]), g["eps"]
+        if optimizer_D is not None:
+            lr_D = optimizer_D.param_groups[0]["lr"]
+        self.hp = dict(lr=float(lr), lr_D=float(lr_D), betas=tuple(float(b) for b in betas),
+                       eps=float(eps), lambda_cls=float(lambda_cls),
+                       lambda_adv=float(lambda_adv), p=float(model.dropout.p),
+                       lambda_semi=float(lambda_semi), semi_th=float(semi_th))
+        self.layout, self.g_numel = ft_layout(model)
+        self.g_param = flatten_params(model, self.layout, self.g_numel, dev)
+        self.d_param = flatten_params(model_D, D_LAYOUT, D_NUMEL, dev)
+        d_off = (self.g_numel + 63) // 64 * 64
+        self.grad_flat = torch.zeros(d_off + D_NUMEL, device=dev)
+        self.g_grad = self.grad_flat[:self.g_numel]
+        self.d_grad = self.grad_flat[d_off:]
+        self.g_m = torch.zeros_like(self.g_param)
+        self.g_v = torch.zeros_like(self.g_param)
+        self.d_m = torch.zeros_like(self.d_param)
+        self.d_v = torch.zeros_like(self.d_param)
+        t0 = max(_adopt_adam_state(optimizer, model, self.g_m, self.g_v, self.layout),
+                 _adopt_adam_state(optimizer_D, model_D, self.d_m, self.d_v, D_LAYOUT))
+        self.step_count = torch.full((1,), t0, device=dev, dtype=torch.int32)
+        self._bind = ((optimizer, model, self.g_m, self.g_v, self.g_grad, self.layout),
+                      (optimizer_D, model_D, self.d_m, self.d_v, self.d_grad, D_LAYOUT))
+        for args_ in self._bind:
+            _bind_adam_state(*args_, t0)
+        self.optimizers = (optimizer, optimizer_D)
+        self.losses = torch.zeros(6, device=dev)
+        self.logits = torch.zeros(2 * self.B, 40, device=dev)
+        nbytes = self.lib.pcadv_adv_step_workspace_bytes(self.B, self.N)
+        self.workspace = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.graph = None
+        self._keep = []
+        C = 2 * self.B
+        self.pts = torch.empty(C, self.N, 3, device=dev)     # [GT; no-GT] clouds
+        self.dgmax = torch.empty(C, 1024, device=dev)
+        self._p = dict(model.named_parameters())
+        self._g = _views(self.g_grad, model, self.layout)
+
+    # the trainer's graphed iteration folds its gathers / epilogue into the
+    # step; here they are this call's first and last launches
+    def _pre(self):
+        if self._gather is not None:
+            check(self.lib.pcadv_gather_clouds_multi(self._gather, len(self._gather),
+                                                     stream_ptr()), "pcadv_gather_clouds_multi")
+
+    def _post(self):
+        if self._epilogue is None:
+            return
+        counters, n, ring = self._epilogue
+        P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        if ring is None:
+            check(self.lib.pcadv_iter_epilogue(P(counters), n, None, 0, None, 0, None,
+                                               stream_ptr()), "pcadv_iter_epilogue")
+        else:
+            check(self.lib.pcadv_iter_epilogue(P(counters), n, P(self.losses), ring.nl,
+                                               P(ring.ring), ring.slots, P(ring.count),
+                                               stream_ptr()), "pcadv_iter_epilogue")
+
+    def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, apply_adam=True,
+                 semi=False, part=0):
+        from . import ops
+        from .ops import ACT_NONE as NONE, ACT_RELU as RELU, _mat
+        if part != 0:
+            raise ValueError("AdvFtTrainStep: no split parts")
+        a = self._args(pts_gt, labels, pts_nogt, masks, soft, False, semi, 3)
+        a.gather, a.ngather = None, 0  # gathered here, not by a fused first launch
+        a.epi_counters, a.epi_ncounters, a.epi_ring = None, 0, None
+        B, N = int(pts_gt.shape[0]), self.N
+        C = 2 * B
+        P, Gr = self._p, self._g
+        self._pre()
+        pts = self.pts[:C]
+        pts[:B].copy_(pts_gt)
+        pts[B:].copy_(pts_nogt)
+        # ---- PointNetfeat with the feature transform (pointnet.py:109-130) ----
+        x1 = ops.pw_fwd(pts, P["feat.conv1.weight"], P["feat.conv1.bias"], RELU)
+        x2 = ops.pw_fwd(x1, P["feat.conv2.weight"], P["feat.conv2.bias"], RELU)
+        s = "feat.fstn."
+        h1 = ops.pw_fwd(x2, P[s + "conv1.weight"], P[s + "conv1.bias"], RELU)
+        h2 = ops.pw_fwd(h1, P[s + "conv2.weight"], P[s + "conv2.bias"], RELU)
+        gs, gis = ops.conv_max_fwd(h2, P[s + "conv3.weight"], P[s + "conv3.bias"], True)
+        f1 = ops.linear_fwd(gs, P[s + "fc1.weight"], P[s + "fc1.bias"], RELU)
+        f2 = ops.linear_fwd(f1, P[s + "fc2.weight"], P[s + "fc2.bias"], RELU)
+        t = ops.linear_fwd(f2, P[s + "fc3.weight"], P[s + "fc3.bias"], NONE, add_identity_k=64)
+        T = t.view(C, 64, 64)
+        x2t = ops.pw_fwd(x2, T, None, NONE, kmajor=True, rows_per_w=N)
+        x3 = ops.pw_fwd(x2t, P["feat.conv3.weight"], P["feat.conv3.bias"], RELU)
+        gmax, gidx = ops.conv_max_fwd(x3, P["feat.conv4.weight"], P["feat.conv4.bias"], False)
+        # ---- fc1 on: the fused step's tail (part 3) -> dL/dgmax ---------------
+        dgmax = self.dgmax[:C]
+        a.feat_gmax, a.feat_dgmax = gmax.data_ptr(), dgmax.data_ptr()
+        self._keep_last = (a, gmax)
+        check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (part 3)")
+        # ---- the extractor's backward ------------------------------------------
+        dx3, _, _ = ops.conv_max_bwd(dgmax, gidx, x3, P["feat.conv4.weight"],
+                                     dw_out=Gr["feat.conv4.weight"], db_out=Gr["feat.conv4.bias"])
+        w3 = _mat(P["feat.conv3.weight"])
+        dx2t = ops.pw_bwd_data(dx3, x3, RELU, w3, 64)
+        ops.pw_bwd_weight(dx3, x3, RELU, x2t, dw_out=Gr["feat.conv3.weight"],
+                          db_out=Gr["feat.conv3.bias"])
+        # x2t = x2 T: dT = x2^T dx2t per cloud, dx2 = dx2t T^T
+        dT, _ = ops.pw_bwd_weight(dx2t, None, NONE, x2, rows_per_group=N, kmajor=True,
+                                  need_db=False)
+        dx2 = ops.pw_bwd_data(dx2t, None, NONE, T, 64, kmajor=True, rows_per_w=N)
+        # STNkd backward (models/pointnet.py:59-79); the identity add has no gradient
+        df2, _, _ = ops.linear_bwd(dT.view(C, 64 * 64), t, NONE, None, 0.0, f2,
+                                   P[s + "fc3.weight"], dw_out=Gr[s + "fc3.weight"],
+                                   db_out=Gr[s + "fc3.bias"])
+        df1, _, _ = ops.linear_bwd(df2, f2, RELU, None, 0.0, f1, P[s + "fc2.weight"],
+                                   dw_out=Gr[s + "fc2.weight"], db_out=Gr[s + "fc2.bias"])
+        dgs, _, _ = ops.linear_bwd(df1, f1, RELU, None, 0.0, gs, P[s + "fc1.weight"],
+                                   dw_out=Gr[s + "fc1.weight"], db_out=Gr[s + "fc1.bias"])
+        dh2, _, _ = ops.conv_max_bwd(dgs, gis, h2, P[s + "conv3.weight"], gmax_relu=gs,
+                                     dw_out=Gr[s + "conv3.weight"], db_out=Gr[s + "conv3.bias"])
+        dh1 = ops.pw_bwd_data(dh2, h2, RELU, _mat(P[s + "conv2.weight"]), 64)
+        ops.pw_bwd_weight(dh2, h2, RELU, h1, dw_out=Gr[s + "conv2.weight"],
+                          db_out=Gr[s + "conv2.bias"])
+        ops.pw_bwd_data(dh1, h1, RELU, _mat(P[s + "conv1.weight"]), 64, out=dx2)
+        ops.pw_bwd_weight(dh1, h1, RELU, x2, dw_out=Gr[s + "conv1.weight"],
+                          db_out=Gr[s + "conv1.bias"])
+        dx1 = ops.pw_bwd_data(dx2, x2, RELU, _mat(P["feat.conv2.weight"]), 64)
+        ops.pw_bwd_weight(dx2, x2, RELU, x1, dw_out=Gr["feat.conv2.weight"],
+                          db_out=Gr["feat.conv2.bias"])
+        ops.pw_bwd_weight(dx1, x1, RELU, pts, dw_out=Gr["feat.conv1.weight"],
+                          db_out=Gr["feat.conv1.bias"])
+        if apply_adam:
+            self.adam()
+        self._post()
+        return self.losses
+
+    def grads(self, pts_gt, labels, pts_nogt, masks=None, soft=None, semi=False):
+        return self(pts_gt, labels, pts_nogt, masks, soft, apply_adam=False, semi=semi)
+
+    def adam(self, part=0):
+        """optimizer.step(); optimizer_D.step() (utils/trainer.py:558-559) at the
+        step number this iteration's tail advanced."""
+        if part != 0:
+            raise ValueError("AdvFtTrainStep: no split Adam")
+        hp = self.hp
+        check(self.lib.pcadv_adam2(self.g_param.data_ptr(), self.g_grad.data_ptr(),
+                                   self.g_m.data_ptr(), self.g_v.data_ptr(), self.g_numel,
+                                   hp["lr"], self.d_param.data_ptr(), self.d_grad.data_ptr(),
+                                   self.d_m.data_ptr(), self.d_v.data_ptr(), D_NUMEL, hp["lr_D"],
+                                   self.step_count.data_ptr(), hp["betas"][0], hp["betas"][1],
+                                   hp["eps"], stream_ptr()), "pcadv_adam2")
+
+    def capture_on(self, pts_gt, labels, pts_nogt, apply_adam=True, semi=False, part=0):
+        """One iteration over resident input buffers as a HIP graph (state left
+        as it was before the capture)."""
+        saved = self._snapshot()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam, semi=semi)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self(pts_gt, labels, pts_nogt, apply_adam=apply_adam, semi=semi)
+        torch.cuda.synchronize()
+        self._restore(saved)
+        return g
+
+    def capture_seq(self, batches, apply_adam=True):
+        raise NotImplementedError("AdvFtTrainStep: one iteration per graph")
+
+    def saved_x3(self):
+        raise NotImplementedError("AdvFtTrainStep keeps no x3 in its workspace")
+
+
 class ClsTrainStep:
     """run_training_pointnet_cls's iteration (utils/trainer.py:222-268) for
     PointNetCls(k=40, feature_transform=False): forward on B labelled clouds,

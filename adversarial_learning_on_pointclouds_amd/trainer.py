@@ -24,7 +24,7 @@ from .metric import batch_get_iou, object_names
 from .pointnet import PointNetCls, feature_transform_regularizer
 from ._lib import D_LAYOUT
 from .dataset import gather_at_multi
-from .step import AdvTrainStep, _views
+from .step import AdvFtTrainStep, AdvTrainStep, _views
 from .utils import make_D_label
 
 
@@ -590,9 +590,14 @@ def _device_loaders(*loaders):
 
 
 def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args):
+    """The configuration the fused steps implement: False, or the step class
+    (AdvTrainStep; AdvFtTrainStep for a feature-transform generator unless
+    args.fused_ft is False)."""
     if not (isinstance(model, PointNetCls) and isinstance(model_D, DeepConvDiscNet)):
         return False
-    if model.feature_transform or model.fc3.out_features != 40:
+    if model.fc3.out_features != 40:
+        return False
+    if model.feature_transform and not getattr(args, "fused_ft", True):
         return False
     if model_D.conv1.in_channels != 40 or model_D.fc.out_features != 1:
         return False
@@ -617,7 +622,7 @@ def _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args):
     if type(cls_loss) is not torch.nn.CrossEntropyLoss or cls_loss.weight is not None \
             or cls_loss.reduction != "mean" or cls_loss.label_smoothing != 0.0:
         return False
-    return True
+    return AdvFtTrainStep if model.feature_transform else AdvTrainStep
 
 
 def _pooled_d_grads(step, model_D, gan_loss, pool_gt, pool_nogt, B, device):
@@ -671,10 +676,13 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
     and the step replay as one HIP graph per iteration (args.use_graph, default
     on), fed by the loaders' own epoch orders.  Loss lines are read
     asynchronously (no host sync per iteration), every args.log_every
-    iterations (default 1, as the reference logs every iteration).  Off the
-    fused step (e.g. a feature-transform generator) the body runs through
-    autograd (_adv_body); with capturable optimizers and DeviceCloudLoaders its
-    full, semi-free iterations are HIP graphs too (_AutogradAdvStep)."""
+    iterations (default 1, as the reference logs every iteration).  A
+    feature-transform generator runs AdvFtTrainStep (the point-wise kernels
+    over both batches + the fused step's tail; args.fused_ft = False keeps the
+    autograd body).  Off the fused steps (other optimizers or losses) the body
+    runs through autograd (_adv_body); with capturable optimizers and
+    DeviceCloudLoaders its full, semi-free iterations are HIP graphs too
+    (_AutogradAdvStep)."""
     max_test_accu = float("-inf")
     max_train_epoch = 0
     fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args)
@@ -709,7 +717,7 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != world:
             raise RuntimeError(f"loaders sharded over {world} ranks: initialise a process group of "
                                "that size first")
-        if not graphed:
+        if not graphed or fused is not AdvTrainStep:
             raise NotImplementedError(
                 "data-parallel run_training runs the fused step graphed over DeviceCloudLoaders: "
                 "PointNetCls(k=40) + DeepConvDiscNet(40, 1), Adam, CE / BCE, ImagePool(0), equal "
@@ -745,14 +753,14 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
         if step is None or step.N != N or step.B < B:
             if step is not None:  # the replacement adopts the Adam state: count included
                 step.sync_optimizer_state()
-            step = AdvTrainStep(model, model_D, B, N,
-                                optimizer=optimizer, optimizer_D=optimizer_D,
-                                lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
-                                seed=int(getattr(args, "seed", 0)) + i_iter,
-                                device=args.device,
-                                lambda_semi=float(getattr(args, "lambda_semi", 1.0)),
-                                semi_th=float(getattr(args, "semi_TH", 0.8)),
-                                rng_rank=rank, rng_world=world)
+            step = fused(model, model_D, B, N,
+                         optimizer=optimizer, optimizer_D=optimizer_D,
+                         lambda_cls=args.lambda_cls, lambda_adv=args.lambda_adv,
+                         seed=int(getattr(args, "seed", 0)) + i_iter,
+                         device=args.device,
+                         lambda_semi=float(getattr(args, "lambda_semi", 1.0)),
+                         semi_th=float(getattr(args, "semi_TH", 0.8)),
+                         rng_rank=rank, rng_world=world)
             if world > 1:  # identical replicas: rank 0's parameters and seed
                 from .distributed import DataParallelAdvStep
                 DataParallelAdvStep(step, broadcast_params=True)

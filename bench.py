@@ -67,17 +67,22 @@ def parse():
     ap.add_argument("--points", type=int, default=1024,
                     help="points per cloud of the adv step (1024: the metric's config; 2048: "
                          "BASELINE configs[4]'s per-rank shape)")
-    ap.add_argument("--config", choices=["adv", "seg", "cls", "cls_ft", "adv_ft", "trainer"], default="adv",
+    ap.add_argument("--config", choices=["adv", "seg", "cls", "cls_ft", "adv_ft", "trainer", "dp1"], default="adv",
                     help="adv: the headline adversarial cls step (default); seg: the "
                          "PointNetSeg training step of BASELINE configs[3]; cls: the "
                          "supervised PointNetCls step of configs[1]; cls_ft: the same with "
                          "feature_transform=True (STNkd(64) + regulariser, layer-by-layer "
                          "kernels through autograd); adv_ft: the adversarial iteration with "
                          "that generator (autograd body, graphed); trainer: run_training end to end over "
-                         "DeviceCloudLoaders")
+                         "DeviceCloudLoaders; dp1: the data-parallel iteration's overhead on a one-rank "
+                         "RCCL group against the plain step graph")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="feature-forward precision (default: bf16 for --config cls, the dtype "
                          "BASELINE configs[1] names; fp32 for adv and seg)")
+    ap.add_argument("--ft-body", action="store_true",
+                    help="--config adv_ft: time the autograd body (trainer._AutogradAdvStep, "
+                         "run_training with args.fused_ft = False) instead of the fused "
+                         "feature-transform step")
     ap.add_argument("--runtime-graph-dispatch", action="store_true",
                     help="leave DEBUG_CLR_GRAPH_PACKET_CAPTURE unset (the HIP runtime's default "
                          "graph dispatch) instead of the stream dispatch path this bench opts in to")
@@ -362,7 +367,7 @@ def _pmc_traffic(pattern, prefixes, only_if=True):
         return None, None
     prof = sorted(p for p in glob.glob(os.path.join(REPO, "profiles", pattern))
                   if pattern != "r*_pmc_traffic.json"
-                  or not any(t in os.path.basename(p) for t in ("_seg_", "_cls_")))
+                  or not any(t in os.path.basename(p) for t in ("_seg_", "_cls_", "_adv_ft_")))
     if not prof:
         return None, None
     kern = json.load(open(prof[-1]))["kernels"]
@@ -655,59 +660,76 @@ def bench_cls_ft(args):
 
 def bench_adv_ft(args):
     """run_training's iteration with PointNetCls(k=40, feature_transform=True) as
-    the generator (off the fused adversarial step): trainer._adv_body, i.e. the
-    reference's body (utils/trainer.py:449-559) through autograd over the
-    layer-by-layer kernels, both torch Adams capturable (fused where available),
-    one HIP graph per resident batch pair as run_training replays it
-    (_AutogradAdvStep); eager when capture fails."""
+    the generator.  Default: the fused feature-transform step run_training uses
+    (step.AdvFtTrainStep: the generator's two batches as one C = 2B pass on the
+    point-wise kernels, the plain step's tail for fc1 on, the hand-written
+    extractor backward, both Adams in one launch), one HIP graph per resident
+    batch pair.  --ft-body: the reference's body through autograd over the
+    same kernels with capturable torch Adams (trainer._AutogradAdvStep, the
+    path before round 6, run_training with args.fused_ft = False)."""
     import argparse
     import adversarial_learning_on_pointclouds_amd as pc
     from adversarial_learning_on_pointclouds_amd import trainer
     from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from adversarial_learning_on_pointclouds_amd.step import AdvFtTrainStep
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = pc.PointNetCls(k=40, feature_transform=True).to(dev).train()
     model_D = pc.DeepConvDiscNet(40, 1).to(dev).train()
-    opts = []
-    for m in (model, model_D):
-        try:
-            opts.append(torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999), fused=True,
-                                         capturable=True))
-            adam = "torch.optim.Adam(fused=True, capturable=True)"
-        except (RuntimeError, ValueError):
-            opts.append(torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999),
-                                         capturable=True))
-            adam = "torch.optim.Adam(capturable=True)"
-    targs = argparse.Namespace(device=str(dev), lambda_cls=1.0, lambda_adv=0.001)
-    step = trainer._AutogradAdvStep(model, model_D, opts[0], opts[1],
-                                    torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(),
-                                    (ImagePool(0), ImagePool(0)), targs, B, N)
     pool = []
     for k in range(POOL):
         rng = np.random.default_rng(3500 + k)
         pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
                      torch.from_numpy(rng.integers(0, 40, B)).to(dev),
                      torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev)))
-    side = torch.cuda.Stream(device=dev)
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):  # autograd / optimizer state created outside any capture
-        for k in range(3):
-            step(*pool[k % POOL])
-    torch.cuda.current_stream().wait_stream(side)
-    torch.cuda.synchronize()
     graphs, why = [], None
-    if not args.no_graph:
-        try:
-            kept = []  # each graph's gradient buffers (the next capture drops p.grad)
-            for k in range(POOL):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    step(*pool[k])
-                graphs.append(g)
-                kept.append([p.grad for p in list(model.parameters()) + list(model_D.parameters())])
-        except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
-            graphs, why = [], f"{type(e).__name__}: {e}"[:200]
-            torch.cuda.synchronize()
+    if not args.ft_body:
+        opts = [torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999))
+                for m in (model, model_D)]
+        adam = "fused (pcadv_adam2: both networks in one launch)"
+        step = AdvFtTrainStep(model, model_D, B, N, optimizer=opts[0], optimizer_D=opts[1],
+                              seed=1234, device=dev)
+        if not args.no_graph:
+            graphs = [step.capture_on(*p) for p in pool]
+        workload = ("run_training iteration with PointNetCls(k=40, feature_transform=True) + "
+                    "DeepConvDiscNet(40, 1): fused feature-transform step (AdvFtTrainStep)")
+    else:
+        opts = []
+        for m in (model, model_D):
+            try:
+                opts.append(torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999),
+                                             fused=True, capturable=True))
+                adam = "torch.optim.Adam(fused=True, capturable=True)"
+            except (RuntimeError, ValueError):
+                opts.append(torch.optim.Adam(m.parameters(), lr=1e-4, betas=(0.9, 0.999),
+                                             capturable=True))
+                adam = "torch.optim.Adam(capturable=True)"
+        targs = argparse.Namespace(device=str(dev), lambda_cls=1.0, lambda_adv=0.001)
+        step = trainer._AutogradAdvStep(model, model_D, opts[0], opts[1],
+                                        torch.nn.BCEWithLogitsLoss(), torch.nn.CrossEntropyLoss(),
+                                        (ImagePool(0), ImagePool(0)), targs, B, N)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # autograd / optimizer state created outside any capture
+            for k in range(3):
+                step(*pool[k % POOL])
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        if not args.no_graph:
+            try:
+                kept = []  # each graph's gradient buffers (the next capture drops p.grad)
+                for k in range(POOL):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        step(*pool[k])
+                    graphs.append(g)
+                    kept.append([p.grad for p in list(model.parameters()) +
+                                 list(model_D.parameters())])
+            except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
+                graphs, why = [], f"{type(e).__name__}: {e}"[:200]
+                torch.cuda.synchronize()
+        workload = ("run_training iteration with PointNetCls(k=40, feature_transform=True) + "
+                    "DeepConvDiscNet(40, 1): autograd body over the pcadv ops, two Adams")
 
     def one(k):
         if graphs:
@@ -725,12 +747,10 @@ def bench_adv_ft(args):
         "value": round(2 * B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32 (layer-by-layer kernels: exact-f32 MFMA point-wise layers, split-product "
-                 "conv4 + exact max re-evaluation)",
+        "dtype": "fp32 (point-wise layers exact-f32 MFMA, 1024-channel conv + max as split "
+                 "products with the exact max re-evaluated, head / D f32)",
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
-        "config": {"workload": "run_training iteration with PointNetCls(k=40, feature_transform="
-                               "True) + DeepConvDiscNet(40, 1): autograd body over the pcadv ops, "
-                               "two Adams", "global_batch": 2 * B, "points": N,
+        "config": {"workload": workload, "global_batch": 2 * B, "points": N,
                    "parallelism": "dp1", "hip_graph": bool(graphs), "optimizer": adam},
         "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
         "losses_last_step": [round(v, 5) for v in vals],
@@ -738,7 +758,16 @@ def bench_adv_ft(args):
     }
     if why:
         out["graph_capture_error"] = why
-    out["roofline"] = ft_roofline(B)  # each generator pass runs it on one B-cloud batch
+    # the dominant kernel: the 1024-channel conv + max, twice per generator pass
+    # (over the 2B clouds of both batches in the fused step, B in the body)
+    C = B if args.ft_body else 2 * B
+    roof = ft_roofline(C)
+    if not args.ft_body:
+        roof["traffic"], roof["traffic_source"] = _pmc_traffic(
+            "r*_adv_ft_pmc_traffic.json", ["k_conv4_max"])
+        roof["traffic_unit"] = "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)"
+        roof["mfma_busy"], roof["mfma_busy_source"] = _pmc_mfma("adv_ft", "k_conv4_max")
+    out["roofline"] = roof
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_ft(args.cpu_seconds, adversarial=True)
     print(json.dumps(_with_runtime(out)), flush=True)
@@ -977,6 +1006,75 @@ def bench_seg(args):
     print(json.dumps(_with_runtime(out)), flush=True)
 
 
+def bench_dp1(args):
+    """what the data-parallel iteration costs beyond the
+    step itself, on the one GPU there is.  A one-rank RCCL group (the
+    all-reduce's average is then the identity, so every form computes the
+    plain step bitwise, tests/test_gpu_distributed.py) times, over the same
+    resident batches and alternating in one process:
+      plain   the step's HIP graph (bench.py's headline form);
+      dp4     DataParallelAdvStep.capture: four graphs (step part 1 | part 2 |
+              Adam of the early bucket | Adam of conv1..conv4) around the two
+              host-issued RCCL all-reduces (bench --gpus N, trainer _DPIteration);
+      dp1g    DataParallelAdvStep.capture_single: the same iteration as ONE graph
+              with both all-reduces captured on RCCL's stream.
+    overhead = form - plain per iteration (the communication itself is ~0 on
+    one rank; the multi-rank exchange is the driver's scaling runs)."""
+    import torch.distributed as tdist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    tdist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
+    from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
+    model, model_D = make_models(dev, seed=0)
+    step = AdvTrainStep(model, model_D, B, N, seed=1234, device=dev, precision="fp32")
+    runner = DataParallelAdvStep(step, overlap=True)
+    pool = []
+    for k in range(POOL):
+        rng = np.random.default_rng(1000 + k * 64)
+        pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
+                     torch.from_numpy(rng.integers(0, 40, B)).to(dev),
+                     torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev)))
+    forms = {"plain": [step.capture_on(*p) for p in pool],
+             "dp4": [runner.capture(*p) for p in pool]}
+    try:
+        forms["dp1g"] = [runner.capture_single(*p) for p in pool]
+        single_err = None
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        single_err = f"{type(e).__name__}: {e}"[:300]
+    host = {}
+    times = {k: [] for k in forms}
+    for _ in range(args.repeats):
+        for name, gs in forms.items():
+            for k in range(args.warmup):
+                gs[k % POOL].replay()
+            t_enq = []
+            def one(k, gs=gs):
+                t0 = time.perf_counter()
+                gs[k % POOL].replay()
+                t_enq.append(time.perf_counter() - t0)
+            times[name] += timed_regions(one, args.steps, 1)
+            host[name] = float(np.median(t_enq)) * 1e6
+    ms = {k: float(np.median(v)) / args.steps * 1e3 for k, v in times.items()}
+    out = {
+        "metric": "data-parallel iteration overhead on a one-rank RCCL group (adv step, B=32+32, N=1024)",
+        "value": round((ms["dp4"] - ms["plain"]) * 1e3, 2), "unit": "us/iteration (dp4 - plain)",
+        "higher_is_better": False, "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": {k: round(v, 4) for k, v in ms.items()},
+        "overhead_us": {k: round((v - ms["plain"]) * 1e3, 2) for k, v in ms.items() if k != "plain"},
+        "host_enqueue_us_per_iteration": {k: round(v, 1) for k, v in host.items()},
+        "regions_s": {k: [round(r, 6) for r in v] for k, v in times.items()},
+        "single_graph_capture_error": single_err,
+        "note": "forms alternated per repeat in one process; one rank: the all-reduce averages "
+                "nothing, so this is the iteration's structure cost (graph splits, host-issued "
+                "collectives, stream waits), not xGMI time",
+    }
+    print(json.dumps(_with_runtime(out)), flush=True)
+    tdist.destroy_process_group()
+
+
 def main():
     global N
     args = parse()
@@ -1005,6 +1103,8 @@ def main():
         return bench_adv_ft(args)
     if args.config == "trainer":
         return bench_trainer(args)
+    if args.config == "dp1":
+        return bench_dp1(args)
     if _backend() != "nccl":  # rehearsal: ranks may share a GPU
         local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)

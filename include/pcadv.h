@@ -425,6 +425,16 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
                int64_t n, int32_t* step_count, float lr, float beta1, float beta2,
                float eps, hipStream_t stream);
 
+/* Two Adam updates of one iteration in one launch (segment 1 may be empty,
+ * n1 = 0), each with its own learning rate, at the step number *step_count
+ * that the iteration already advanced (pcadv_adv_step part 3): t =
+ * *step_count, not incremented.  The feature-transform step's optimizer.step()
+ * + optimizer_D.step() (utils/trainer.py:558-559).  ABI version 8. */
+int pcadv_adam2(float* p0, const float* g0, float* m0, float* v0, int64_t n0, float lr0,
+                float* p1, const float* g1, float* m1, float* v1, int64_t n1, float lr1,
+                const int32_t* step_count, float beta1, float beta2, float eps,
+                hipStream_t stream);
+
 /* ---- the fused adversarial step (utils/trainer.py:426-559) -------------------
  * B clouds of N points per loader.  Stochastic inputs: when drop_mask_gt /
  * drop_mask_nogt ([B][256] {0,1}) or soft_gt / soft_nogt ([B]) are NULL they are
@@ -465,7 +475,8 @@ typedef struct pcadv_adv_args {
    * 1 = forward, losses, discriminator and head backward (every gradient
    *     except the generator's conv1..conv4, g_grad[0, PCADV_G_FC1_W));
    * 2 = the feature backward (those conv1..conv4 gradients; and both Adam
-   *     updates when apply_adam) on the state part 1 left in the workspace. */
+   *     updates when apply_adam) on the state part 1 left in the workspace;
+   * 3 = part 1 from fc1 on, over the caller's features (feat_* below). */
   int part;
   /* feature forward precision: 0 = f32-level (default), 1 = bf16 (as
    * pcadv_feat_fwd_bf16; the head, the discriminator and every backward stay
@@ -499,6 +510,17 @@ typedef struct pcadv_adv_args {
    * batch.  ngather = 0: none.  ABI version 7. */
   const pcadv_gather_job* gather;
   int ngather;
+  /* A generator whose feature extractor runs outside the step (the
+   * feature-transform generator, PointNetCls(feature_transform=True), built
+   * from the point-wise kernels): part = 3 runs part 1's work from fc1 on
+   * (fc1..fc3 + dropout, log_softmax / CE, the three discriminator passes with
+   * their BCE terms, D's gradients, the head backward) on the caller's pooled
+   * features feat_gmax [2B][1024] (GT clouds first) and writes dL/dgmax to
+   * feat_dgmax [2B][1024].  No gather, epilogue or Adam: the caller
+   * backpropagates through its extractor and runs Adam (pcadv_adam).  NULL for
+   * parts 0-2.  ABI version 8. */
+  const float* feat_gmax;
+  float* feat_dgmax;
 } pcadv_adv_args;
 
 size_t pcadv_adv_step_workspace_bytes(int B, int N);

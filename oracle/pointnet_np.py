@@ -564,25 +564,60 @@ def regularizer_bwd(trans):
     return (np.matmul(a, trans) * (2.0 / (B * n))[:, None, None]).astype(F32)
 
 
-def cls_ft_step(p, pts, labels, mask, lambda_cls=1.0, lambda_regu=0.001):
-    """One run_training_pointnet_cls iteration body (utils/trainer.py:254-268) for
-    PointNetCls(feature_transform=True): loss = lambda_cls * CE + lambda_regu *
-    feature_transform_regularizer(trans_feat).  Returns (loss_cls, reg, grads)."""
+def conv_max_at(x, w, b, am, relu_before_max=False):
+    """conv_max_fwd's pooled values at GIVEN argmax points (a "same activation"
+    check feeds the device's own max-pool decisions back into the oracle, so a
+    near-tie resolved differently by two f32 summation orders cannot reroute a
+    gradient): gmax[b, o] = relu?(x[b, am[b, o]] . w[o] + b[o])."""
+    B = x.shape[0]
+    rows = x[np.arange(B)[:, None], am]                      # (B, O, K)
+    g = (np.einsum("bok,ok->bo", rows, w) + b[None, :]).astype(F32)
+    return (np.maximum(g, F32(0)) if relu_before_max else g).astype(F32)
+
+
+def cls_ft_forward_train(p, pts, mask, am_stn=None, am=None):
+    """PointNetCls(feature_transform=True).forward in train mode
+    (models/pointnet.py:59-79,109-137,197-203) keeping what cls_ft_backward
+    needs.  am_stn / am: the STNkd's conv3 and the feature conv4 max-pool
+    argmax to use instead of the oracle's own (same-activation checks)."""
     pts = np.ascontiguousarray(pts, F32)
     x1 = relu(pts @ _w(p, "feat.conv1.weight").T + p["feat.conv1.bias"]).astype(F32)
     x2 = relu(x1 @ _w(p, "feat.conv2.weight").T + p["feat.conv2.bias"]).astype(F32)
     trans, sc = stn_forward_train(p, x2, "feat.fstn.", 64)
+    if am_stn is not None:
+        pre = "feat.fstn."
+        g = conv_max_at(sc["h2"], _w(p, pre + "conv3.weight"), p[pre + "conv3.bias"],
+                        am_stn, relu_before_max=True)
+        f1 = relu(g @ p[pre + "fc1.weight"].T + p[pre + "fc1.bias"]).astype(F32)
+        f2 = relu(f1 @ p[pre + "fc2.weight"].T + p[pre + "fc2.bias"]).astype(F32)
+        t = (f2 @ p[pre + "fc3.weight"].T + p[pre + "fc3.bias"]).astype(F32)
+        t = t + np.eye(64, dtype=F32).reshape(1, 64 * 64)
+        trans = t.reshape(-1, 64, 64).astype(F32)
+        sc.update(g=g, am=np.asarray(am_stn, np.int64), f1=f1, f2=f2)
     x2t = np.matmul(x2, trans).astype(F32)
     x3 = relu(x2t @ _w(p, "feat.conv3.weight").T + p["feat.conv3.bias"]).astype(F32)
     W4 = _w(p, "feat.conv4.weight")
-    gmax, am = conv_max_fwd(x3, W4, p["feat.conv4.bias"])
+    if am is None:
+        gmax, am = conv_max_fwd(x3, W4, p["feat.conv4.bias"])
+    else:
+        am = np.asarray(am, np.int64)
+        gmax = conv_max_at(x3, W4, p["feat.conv4.bias"], am)
     logits, hc = head_fwd(gmax, p, mask)
-    l, dce = cross_entropy(logits, labels)
-    reg = feature_transform_regularizer(trans)
-    # head (reuse cls_backward's head part through a cache without the conv stack)
-    h1, h2, scale = hc
+    cache = dict(pts=pts, x1=x1, x2=x2, trans=trans, sc=sc, x2t=x2t, x3=x3, gmax=gmax, am=am,
+                 head=hc)
+    return logits, cache
+
+
+def cls_ft_backward(p, cache, dlogits, lambda_regu=0.0):
+    """Autograd of cls_ft_forward_train given dL/dlogits, plus lambda_regu x
+    feature_transform_regularizer(trans) (run_training_pointnet_cls adds it,
+    utils/trainer.py:257-267; run_training does not, :472-519).  Grads keyed
+    and shaped like the state_dict."""
+    pts, x1, x2, trans, sc = (cache[n] for n in ("pts", "x1", "x2", "trans", "sc"))
+    x2t, x3, gmax, am = cache["x2t"], cache["x3"], cache["gmax"], cache["am"]
+    h1, h2, scale = cache["head"]
     g = OrderedDict()
-    dl = (F32(lambda_cls) * dce).astype(F32)
+    dl = np.asarray(dlogits, F32)
     g["fc3.weight"] = dl.T @ h2
     g["fc3.bias"] = dl.sum(0)
     dz2 = (dl @ p["fc3.weight"]) * (h2 > 0)
@@ -594,13 +629,15 @@ def cls_ft_step(p, pts, labels, mask, lambda_cls=1.0, lambda_regu=0.001):
     g["fc1.weight"] = dz1.T @ gmax
     g["fc1.bias"] = dz1.sum(0)
     dgl = (dz1 @ p["fc1.weight"]).astype(F32)
+    W4 = _w(p, "feat.conv4.weight")
     dW4, db4, dX3 = conv_max_bwd(dgl, am, x3, W4)
     g["feat.conv4.weight"], g["feat.conv4.bias"] = dW4[:, :, None], db4
     dW3, db3, dx2t = _layer_bwd(dX3, x2t, x3, _w(p, "feat.conv3.weight"))
     g["feat.conv3.weight"], g["feat.conv3.bias"] = dW3[:, :, None], db3
     # x2t = x2 @ T (models/pointnet.py:120-121)
     dT = np.matmul(x2.transpose(0, 2, 1), dx2t).astype(F32)
-    dT = dT + F32(lambda_regu) * regularizer_bwd(trans)
+    if lambda_regu:
+        dT = dT + F32(lambda_regu) * regularizer_bwd(trans)
     dx2 = np.matmul(dx2t, trans.transpose(0, 2, 1)).astype(F32)
     gs, dx2s = stn_backward(p, sc, dT, "feat.fstn.")
     g.update(gs)
@@ -609,9 +646,51 @@ def cls_ft_step(p, pts, labels, mask, lambda_cls=1.0, lambda_regu=0.001):
     g["feat.conv2.weight"], g["feat.conv2.bias"] = dW2[:, :, None], db2
     dW1, db1, _ = _layer_bwd(dx1, pts, x1, _w(p, "feat.conv1.weight"))
     g["feat.conv1.weight"], g["feat.conv1.bias"] = dW1[:, :, None], db1
-    grads = OrderedDict((k, g[k].astype(F32).reshape(p[k].shape)) for k in p)
-    aux = dict(logits=logits, gmax=gmax, am=am, trans=trans, am_stn=sc["am"], x2t=x2t, x3=x3)
+    return OrderedDict((k, g[k].astype(F32).reshape(p[k].shape)) for k in p)
+
+
+def cls_ft_step(p, pts, labels, mask, lambda_cls=1.0, lambda_regu=0.001):
+    """One run_training_pointnet_cls iteration body (utils/trainer.py:254-268) for
+    PointNetCls(feature_transform=True): loss = lambda_cls * CE + lambda_regu *
+    feature_transform_regularizer(trans_feat).  Returns (loss_cls, reg, grads)."""
+    logits, c = cls_ft_forward_train(p, pts, mask)
+    l, dce = cross_entropy(logits, labels)
+    reg = feature_transform_regularizer(c["trans"])
+    grads = cls_ft_backward(p, c, (F32(lambda_cls) * dce).astype(F32), lambda_regu)
+    aux = dict(logits=logits, gmax=c["gmax"], am=c["am"], trans=c["trans"], am_stn=c["sc"]["am"],
+               x2t=c["x2t"], x3=c["x3"])
     return l, reg, grads, aux
+
+
+def adv_ft_grads(G, D, pts_gt, labels, pts_nogt, mask_gt, mask_nogt, y_gt, y_nogt,
+                 lambda_cls=1.0, lambda_adv=0.001, am=None):
+    """run_training's iteration body (utils/trainer.py:468-556, ImagePool(0))
+    with a feature-transform generator: G's and D's gradients before the Adam
+    steps.  No regulariser: run_training leaves it commented out (:473-476,
+    :511-517).  am: optional (am_stn_gt, am_gt, am_stn_nogt, am_nogt) device
+    argmax decisions (same-activation checks)."""
+    am = am or (None, None, None, None)
+    lg, cg = cls_ft_forward_train(G, pts_gt, mask_gt, am[0], am[1])          # :467
+    l, dce = cross_entropy(lg, labels)                                      # :468
+    lsm_gt = log_softmax(lg)                                                # :471
+    ln, cn = cls_ft_forward_train(G, pts_nogt, mask_nogt, am[2], am[3])      # :490
+    lsm_ng = log_softmax(ln)                                                # :492
+    d_ng, acts_ng = disc_forward(D, lsm_ng)                                 # :498
+    loss_adv, dadv = bce_with_logits(d_ng, np.ones_like(d_ng))              # :499-506
+    _, dlsm = disc_backward(D, acts_ng, F32(lambda_adv) * dadv, need_params=False)
+    dlog_ng = log_softmax_bwd(lsm_ng, dlsm)
+    ga = cls_ft_backward(G, cg, (F32(lambda_cls) * dce).astype(F32))
+    gb = cls_ft_backward(G, cn, dlog_ng)
+    gG = OrderedDict((k, (ga[k] + gb[k]).astype(F32)) for k in G)
+    d_gt, acts_gt = disc_forward(D, lsm_gt)                                 # :526-540
+    lD1, d1 = bce_with_logits(d_gt, y_gt)
+    lD2, d2 = bce_with_logits(d_ng, y_nogt)                                 # :544-556
+    g1, _ = disc_backward(D, acts_gt, F32(0.5) * d1, need_input=False)
+    g2, _ = disc_backward(D, acts_ng, F32(0.5) * d2, need_input=False)
+    gD = OrderedDict((k, (g1[k] + g2[k]).astype(F32)) for k in D)
+    losses = dict(loss_cls=l, loss_adv=loss_adv, loss_D_gt=0.5 * lD1, loss_D_nogt=0.5 * lD2)
+    aux = dict(am=(cg["sc"]["am"], cg["am"], cn["sc"]["am"], cn["am"]))
+    return losses, gG, gD, aux
 
 
 # --------------------------------------------------------------------------

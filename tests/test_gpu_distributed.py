@@ -245,7 +245,7 @@ def _rccl_worker(rank, port, out_dir):
         from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
         from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
         res = {}
-        for mode in ("plain", "dp_eager", "dp_graph"):
+        for mode in ("plain", "dp_eager", "dp_graph", "dp_single"):
             m, d = _models(dev)
             st = AdvTrainStep(m, d, B, N, seed=7, device=dev)
             if mode == "plain":
@@ -259,7 +259,7 @@ def _rccl_worker(rank, port, out_dir):
                         dp(*_batch(dev, 60 + k))
                 else:
                     bufs = _batch(dev, 60)
-                    graph = dp.capture(*bufs)
+                    graph = dp.capture(*bufs) if mode == "dp_graph" else dp.capture_single(*bufs)
                     for k in range(3):
                         for dst, src in zip(bufs, _batch(dev, 60 + k)):
                             dst.copy_(src)
@@ -284,6 +284,8 @@ def test_rccl_bucketed_overlap_path_single_rank(tmp_path):
     r = dict(np.load(tmp_path / "rccl.npz"))
     assert np.array_equal(r["plain"], r["dp_eager"])
     assert np.array_equal(r["plain"], r["dp_graph"])
+    # the whole iteration as one graph with both all-reduces captured
+    assert np.array_equal(r["plain"], r["dp_single"])
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,173 @@
+"""The fused feature-transform adversarial step (step.AdvFtTrainStep, SURVEY
+row a7): run_training's iteration with
+PointNetCls(k=40, feature_transform=True) + DeepConvDiscNet(40, 1), the
+generator's two batches as one C = 2B pass on the point-wise kernels and the
+plain step's own tail (pcadv_adv_step part 3), against the numpy oracle
+(oracle.adv_ft_grads, pinned to the reference's own g13 capture by
+tests/test_oracle_golden.py).
+
+Gradients: against the oracle's backward on the device's own max-pool argmax
+(same-activation), per tensor 1e-4 of the largest entry and 1e-5 relative L2
+at B = 4; at B = 32 the default per-tensor bound (1e-3 / 1e-4): two f32
+computations there can route a gradient differently at a pre-activation
+within rounding of a ReLU (the ReLU-flip policy).  Losses 1e-4.
+Graph replay equals eager bitwise.  MI355X only."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import grad_err
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def _models(g_seed, d_seed):
+    import adversarial_learning_on_pointclouds_amd as pc
+    from oracle import pointnet_np as onp
+    G = onp.make_params(onp.cls_ft_spec(40), seed=g_seed)
+    D = onp.make_params(onp.disc_spec(40, 1), seed=d_seed, init="xavier")
+    m, d = pc.PointNetCls(k=40, feature_transform=True), pc.DeepConvDiscNet(40, 1)
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in G.items()})
+    d.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in D.items()})
+    return m.to(DEV), d.to(DEV), G, D
+
+
+def _inputs(seed, B, N):
+    rng = np.random.default_rng(seed)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, B).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, B).astype(np.float32)
+    return pg, lab, pn, m1, m2, y1, y2
+
+
+def _record_conv_max(monkeypatch):
+    from adversarial_learning_on_pointclouds_amd import ops
+    rec = []
+    orig = ops.conv_max_fwd
+
+    def conv_max_fwd(*a, **k):
+        gmax, gidx = orig(*a, **k)
+        rec.append(gidx)
+        return gmax, gidx
+    monkeypatch.setattr(ops, "conv_max_fwd", conv_max_fwd)
+    return rec
+
+
+@pytest.mark.parametrize("B,N,strict", [(4, 1024, True), (5, 300, True), (32, 1024, False)])
+def test_ft_step_vs_oracle_same_activation(monkeypatch, B, N, strict):
+    from adversarial_learning_on_pointclouds_amd.step import AdvFtTrainStep
+    from oracle import pointnet_np as onp
+    model, model_D, G, D = _models(21, 22)
+    st = AdvFtTrainStep(model, model_D, B, N, seed=5)
+    pg, lab, pn, m1, m2, y1, y2 = _inputs(100 + B, B, N)
+    rec = _record_conv_max(monkeypatch)
+    losses = st(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
+                soft=(_t(y1), _t(y2)), apply_adam=False).cpu().numpy()
+    s3, c4 = (r.cpu().numpy() for r in rec[-2:])
+    am = (s3[:B], c4[:B], s3[B:], c4[B:])
+    args = (G, D, pg, lab, pn, m1, m2, y1[:, None], y2[:, None], 1.0, 0.001)
+    ref_l, _, _, own = onp.adv_ft_grads(*args)
+    moved = [int((a != o).sum()) for a, o in zip(am, own["am"])]
+    print(f"B={B}: argmax the oracle's own forward moves: {moved}")
+    lr, gG, gD, _ = onp.adv_ft_grads(*args, am=am)
+    for i, k in enumerate(("loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt")):
+        assert abs(losses[i] - lr[k]) < 1e-4, (k, losses[i], lr[k])
+        assert abs(lr[k] - ref_l[k]) < 1e-4, k
+    tol = (1e-4, 1e-5) if strict else (1e-3, 1e-4)
+    bad = []
+    for tag, mod, ref in (("G", model, gG), ("D", model_D, gD)):
+        for nm, p in mod.named_parameters():
+            e = grad_err(p.grad.detach().cpu().numpy(), ref[nm])
+            print(f"{tag}.{nm}: max {e[0]:.2e} l2 {e[1]:.2e}")
+            if not (e[0] <= tol[0] and e[1] <= tol[1]):
+                bad.append((tag, nm, e))
+    assert not bad, bad
+
+
+def test_ft_step_graph_replay_equals_eager():
+    """Three iterations with device-drawn masks / labels and Adam: eager calls
+    and replays of one captured graph leave bitwise the same parameters,
+    moments, step count and losses."""
+    from adversarial_learning_on_pointclouds_amd.step import AdvFtTrainStep
+    B, N = 8, 512
+    outs = []
+    for graphed in (False, True):
+        model, model_D, _, _ = _models(31, 32)
+        st = AdvFtTrainStep(model, model_D, B, N, seed=9)
+        bufs = [_t(a) if a.dtype != np.int64 else _t(a, torch.int64)
+                for a in _inputs(7, B, N)[:3]]
+        g = st.capture_on(*bufs) if graphed else None
+        for k in range(3):
+            new = _inputs(40 + k, B, N)[:3]
+            for dst, src in zip(bufs, new):
+                dst.copy_(_t(src) if src.dtype != np.int64 else _t(src, torch.int64))
+            if graphed:
+                g.replay()
+            else:
+                st(*bufs)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (st.g_param, st.d_param, st.g_m, st.g_v, st.d_m, st.d_v,
+                                         st.step_count, st.losses)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_ft_step_matches_autograd_body():
+    """AdvFtTrainStep's gradients against the trainer's autograd body (_adv_body
+    over the layer-by-layer kernels, as run_training ran a feature-transform
+    generator before) on the same batch, masks and soft labels: the two differ
+    in batching (one C = 2B pass against two B-cloud model calls) and the
+    weight-gradient summation order only.  The body's torch Adam runs at lr 0,
+    so p.grad keeps its gradients."""
+    from adversarial_learning_on_pointclouds_amd import trainer
+    from adversarial_learning_on_pointclouds_amd.image_pool import ImagePool
+    from adversarial_learning_on_pointclouds_amd.step import AdvFtTrainStep
+    import argparse
+    B, N = 4, 512
+    pg, lab, pn, m1, m2, y1, y2 = _inputs(70, B, N)
+    model, model_D, _, _ = _models(41, 42)
+    st = AdvFtTrainStep(model, model_D, B, N)
+    st(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)), soft=(_t(y1), _t(y2)),
+       apply_adam=False)
+    fused = {n: p.grad.detach().cpu().numpy().copy() for m in (model, model_D)
+             for n, p in m.named_parameters()}
+    lf = st.losses[:4].cpu().numpy()
+    model, model_D, _, _ = _models(41, 42)
+    opt = torch.optim.Adam(model.parameters(), lr=0.0)
+    opt_D = torch.optim.Adam(model_D.parameters(), lr=0.0)
+    args = argparse.Namespace(lambda_cls=1.0, lambda_adv=0.001, device=DEV)
+    soft_q = [_t(y1), _t(y2)]
+    orig = trainer.make_D_label
+
+    def make_D_label(input, value, device, random=False):
+        if not random:
+            return orig(input, value, device, random=False)
+        return soft_q.pop(0).view(input.shape)
+    trainer.make_D_label = make_D_label
+    try:
+        model.dropout_masks = [_t(m1), _t(m2)]
+        out = trainer._adv_body(model, model_D, opt, opt_D, torch.nn.BCEWithLogitsLoss(),
+                                torch.nn.CrossEntropyLoss(), _t(pg), _t(lab, torch.int64), _t(pn),
+                                ImagePool(0), ImagePool(0), args)
+    finally:
+        trainer.make_D_label = orig
+    lb = np.array([float(t) for t in out[:4]])
+    np.testing.assert_allclose(lf, lb, rtol=0, atol=1e-5)
+    bad = []
+    for m in (model, model_D):
+        for n, p in m.named_parameters():
+            e = grad_err(fused[n], p.grad.detach().cpu().numpy())
+            print(f"{n}: max {e[0]:.2e} l2 {e[1]:.2e}")
+            if not (e[0] <= 1e-4 and e[1] <= 1e-5):
+                bad.append((n, e))
+    assert not bad, bad

@@ -265,3 +265,23 @@ def test_adam_update_check_is_sensitive():
         # feature layers' small gradients
         if k.startswith("feat.") and k.endswith("weight"):
             assert adam_update_err(bad_eps[k], old[k], ref[k], old[k], gG[k])[0] > 2e-3, k
+
+
+def test_g13_adv_ft_grads_first_iteration():
+    """oracle.adv_ft_grads (run_training's body with a feature-transform
+    generator, utils/trainer.py:467-556) against the reference's own first
+    iteration of g13 ft_pool0 (same parameters, batches, dropout masks and soft
+    labels): losses and every G / D gradient.  It is the checker of the GPU's
+    same-activation test at iteration 3 (test_gpu_g13.py)."""
+    fx = load("g13_adv_off_fused.npz")
+    G = onp.make_params(onp.cls_ft_spec(40), seed=int(fx["g_seed"]))
+    D = onp.make_params(onp.disc_spec(40, 1), seed=int(fx["d_seed"]), init="xavier")
+    m, y = fx["masks"][0], fx["soft"][0]
+    losses, gG, gD, _ = onp.adv_ft_grads(G, D, fx["pts_gt"][0], fx["labels"][0], fx["pts_nogt"][0],
+                                         m[0], m[1], y[0][:, None], y[1][:, None],
+                                         float(fx["lambda_cls"]), float(fx["lambda_adv"]))
+    for k in ("loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt"):
+        assert abs(losses[k] - float(fx[f"ft_pool0.{k}"][0])) < 1e-5, k
+    for tag, grads in (("G", gG), ("D", gD)):
+        for name, g in grads.items():
+            check_tensor_rel(fx, f"ft_pool0.grad1{tag}.{name}", g, tol=1e-4)
