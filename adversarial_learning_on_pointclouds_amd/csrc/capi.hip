@@ -67,6 +67,9 @@ int launch_disc_tail(const float*, int, const float*, const float*, const float*
                      const int32_t* gidx, int C, int N, int* sortrec, float* z4g, float* z5g,
                      float* a4g, int lab_off = 0);
 size_t feat_sort_record_ints(int C, int N);
+#if defined(PCADV_C4_CERT) && PCADV_C4_CERT
+int c4_cert_read(unsigned* host);
+#endif
 #ifdef PCADV_STAMPS
 int tail_stamps_read(uint64_t* host);
 int chunk_stamps_read(uint64_t* host);
@@ -548,6 +551,12 @@ int pcadv_feat_fwd_stamped(const float* pts, int C, int N, const float* w1, cons
 
 size_t pcadv_feat_bwd_workspace_bytes(int C, int N) { return feat_bwd_workspace_bytes(C, N); }
 
+#if defined(PCADV_C4_CERT) && PCADV_C4_CERT
+// diagnostic build only (tools/cert_diag.py): k_conv4_max's certification
+// counters since the last read: [flagged at the rigorous bound, channels,
+// flagged at 2^-17 x the bound, launches]
+int pcadv_c4_cert_read(unsigned* host) { return c4_cert_read(host); }
+#endif
 #ifdef PCADV_STAMPS
 int pcadv_tail_stamps(uint64_t* host) { return tail_stamps_read(host); }
 int pcadv_chunk_stamps(uint64_t* host) { return chunk_stamps_read(host); }

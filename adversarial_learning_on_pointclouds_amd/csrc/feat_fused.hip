@@ -321,6 +321,19 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
 // ============================================================================
 // k_conv4_max: conv4 (128 -> 1024) + max over points
 // ============================================================================
+#ifndef PCADV_C4_CERT
+// diagnostic builds only (make ab ABDEFS=-DPCADV_C4_CERT=1): every lane also
+// tracks the largest screened key it DROPS (the channel's third candidate),
+// and after the exact re-evaluation a channel is counted when that third value
+// plus a rigorous screening-error bound reaches the winner's exact value -
+// what certifying the argmax would have to re-check (tools/cert_diag.py)
+#define PCADV_C4_CERT 0
+#endif
+#if PCADV_C4_CERT
+// [0] channels counted, [1] channels seen, [2] channels whose third screened
+// value lies within 2^-16 x the bound (an empirical band), [3] launches
+__device__ unsigned int g_c4_cert[4];
+#endif
 #ifndef PCADV_C4_DIAG
 #define PCADV_C4_DIAG 0  // diagnostic builds only: 1 = no screening, 2 = no staging
 #endif
@@ -375,15 +388,16 @@ __device__ __forceinline__ int screen_key_asm(float v, int m_ord, int m_hi) {
 // top-2 (TOP2) or top-1 (bf16 mode, whose result is the screened winner itself)
 template <int I, bool TOP2>
 __device__ __forceinline__ void screen_one(const f32x16& acc, int m_ord, int m_hi, int& k1,
-                                           int& k2) {
+                                           int& k2, int& k3) {
   const int key = screen_key_asm<31 - ((I & 3) + 8 * (I >> 2))>(acc[I], m_ord, m_hi);
+  if constexpr (PCADV_C4_CERT && TOP2) k3 = max(min(key, k2), k3);  // the key k2 / key drops
   if constexpr (TOP2) k2 = max(min(key, k1), k2);  // median(key, k1, k2) for k2 <= k1: v_med3_i32
   k1 = max(k1, key);
 }
 template <int I0, bool TOP2, int... J>
 __device__ __forceinline__ void screen_seq(const f32x16& acc, int m_ord, int m_hi, int& k1,
-                                           int& k2, std::integer_sequence<int, J...>) {
-  (screen_one<I0 + J, TOP2>(acc, m_ord, m_hi, k1, k2), ...);
+                                           int& k2, int& k3, std::integer_sequence<int, J...>) {
+  (screen_one<I0 + J, TOP2>(acc, m_ord, m_hi, k1, k2, k3), ...);
 }
 __device__ __forceinline__ int key_row(int k) { return 31 - (k & 63); }
 __device__ __forceinline__ float key_value(int k) {
@@ -497,11 +511,19 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
 #pragma unroll
     for (int j = 0; j < 4; ++j) stg[j] = src[j];
   };
+  float cert_ss = 0.f, cert_xn2 = 0.f;  // PCADV_C4_CERT >= 2: max_p ||x_p||^2 of the cloud
+  auto cert_row_done = [&]() {
+    if constexpr (PCADV_C4_CERT >= 2) {
+      cert_xn2 = fmaxf(cert_xn2, octet_sum(cert_ss));
+      cert_ss = 0.f;
+    }
+  };
   auto stage_write = [&](int buf) {  // split the staged f32 rows into bf16 hi / lo
     bf16x8 hi[2], lo[2];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const float v = stg[j >> 2][j & 3];
+      if constexpr (PCADV_C4_CERT >= 2) cert_ss = fmaf(v, v, cert_ss);
       const __bf16 hb = (__bf16)v;
       hi[j >> 3][j & 7] = hb;
       lo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
@@ -548,6 +570,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   }
   __syncthreads();  // every wave holds its fragments before tile 0 overwrites the staging rows
   stage_write(0);
+  cert_row_done();
   stage_load(1);
   __syncthreads();
   STAMP(1);
@@ -558,22 +581,32 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   // lane's own h (keys are only compared within a lane).
   int r1 = KEY_NONE, r2 = KEY_NONE;
   int t1 = -1, t2 = -1;
+  int r3 = KEY_NONE;  // PCADV_C4_CERT: the largest truncated key this lane dropped
   auto screen_unit = [&](const f32x16& acc, int u, auto MASKED, int kb_lo, int kb_hi, int& k1,
-                         int& k2) {
+                         int& k2, int& k3) {
 #pragma unroll
     for (int i = 2 * kb_lo; i < 2 * kb_hi; ++i) {
       if constexpr (decltype(MASKED)::value)
         if (u * 32 + acc_row(i, lane) >= N) continue;
       const int key = screen_key(acc[i], 31 - acc_row(i, 0));
+      if constexpr (PCADV_C4_CERT && NP4 == 3) k3 = max(min(key, k2), k3);
       if constexpr (NP4 == 3) k2 = max(min(key, k1), k2);  // median(key, k1, k2): v_med3_i32
       k1 = max(k1, key);
     }
   };
   // unmasked screening of acc elements [I, I + CNT) with the asm keys
   const int m_ord = 0x7fffffc0, m_hi = ~63;
-  auto screen_fast = [&](const f32x16& acc, auto I, auto CNT, int& k1, int& k2) {
-    screen_seq<decltype(I)::value, NP4 == 3>(acc, m_ord, m_hi, k1, k2,
+  auto screen_fast = [&](const f32x16& acc, auto I, auto CNT, int& k1, int& k2, int& k3) {
+    screen_seq<decltype(I)::value, NP4 == 3>(acc, m_ord, m_hi, k1, k2, k3,
                                              std::make_integer_sequence<int, decltype(CNT)::value>{});
+  };
+  // PCADV_C4_CERT: a unit's top-2 (n1 >= n2) and dropped max n3 merged into the
+  // running r1, r2, r3: the third largest of {n1, n2, r1, r2} is dropped too
+  auto cert_merge = [&](int n1, int n2, int n3) {
+    if constexpr (PCADV_C4_CERT && NP4 == 3) {
+      const int m1 = n1 & ~63, m2 = n2 & ~63, q1 = r1 & ~63, q2 = r2 & ~63;
+      r3 = max(r3, max(n3 & ~63, max(min(m1, q2), min(m2, q1))));
+    }
   };
 
   // Software pipeline over 32-point units (step s, half pt): the 24 MFMAs of a
@@ -586,7 +619,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     const __bf16* xh = &L.x[buf][0][(32 * pt + r) * C4_SB + 8 * h];
     const __bf16* xl = &L.x[buf][1][(32 * pt + r) * C4_SB + 8 * h];
     const int uprev = G2 ? 2 * s + pt - 2 : 2 * s + pt - 1;
-    int k1 = KEY_NONE, k2 = KEY_NONE;
+    int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
     bf16x8 fa[3][2];  // A fragments, a 3-deep register ring: [k-block % 3][hi, lo]
     auto frag = [&](int kb) {
       fa[kb % 3][0] = *reinterpret_cast<const bf16x8*>(xh + 16 * kb);
@@ -608,19 +641,19 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       }
       cur = mfma_bf16(ah, bh[kb], cur);
       if constexpr (decltype(SCREEN)::value && decltype(MASKED)::value) {
-        screen_unit(prev, uprev, MASKED, kb, kb + 1, k1, k2);
+        screen_unit(prev, uprev, MASKED, kb, kb + 1, k1, k2, k3);
         asm volatile("" ::"v"(k1), "v"(k2));
       } else if constexpr (decltype(SCREEN)::value && !(PCADV_C4_DIAG & 1)) {
         // 16 values over k-blocks 1..7 (2,2,2,2,2,3,3); none in k-block 0, so the
         // previous unit's MFMAs have retired before the asm reads them
         using IC = std::integral_constant<int, 0>;
-        if (kb == 1) screen_fast(prev, IC{}, std::integral_constant<int, 2>{}, k1, k2);
-        if (kb == 2) screen_fast(prev, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, k1, k2);
-        if (kb == 3) screen_fast(prev, std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{}, k1, k2);
-        if (kb == 4) screen_fast(prev, std::integral_constant<int, 6>{}, std::integral_constant<int, 2>{}, k1, k2);
-        if (kb == 5) screen_fast(prev, std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{}, k1, k2);
-        if (kb == 6) screen_fast(prev, std::integral_constant<int, 10>{}, std::integral_constant<int, 3>{}, k1, k2);
-        if (kb == 7) screen_fast(prev, std::integral_constant<int, 13>{}, std::integral_constant<int, 3>{}, k1, k2);
+        if (kb == 1) screen_fast(prev, IC{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+        if (kb == 2) screen_fast(prev, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+        if (kb == 3) screen_fast(prev, std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+        if (kb == 4) screen_fast(prev, std::integral_constant<int, 6>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+        if (kb == 5) screen_fast(prev, std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+        if (kb == 6) screen_fast(prev, std::integral_constant<int, 10>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+        if (kb == 7) screen_fast(prev, std::integral_constant<int, 13>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
         // pin the keys to this region (otherwise the IR passes sink the whole
         // screening below the MFMAs, next to its only use)
         asm volatile("" ::"v"(k1), "v"(k2));
@@ -629,10 +662,12 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
 #pragma unroll
         for (int j = 4 * kb; j < 4 * kb + 4; ++j) {
           const float v = stg[j >> 2][j & 3];
+          if constexpr (PCADV_C4_CERT >= 2) cert_ss = fmaf(v, v, cert_ss);
           const __bf16 hb = (__bf16)v;
           shi[j >> 3][j & 7] = hb;
           if constexpr (NP4 == 3) slo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
         }
+        if (kb == 3) cert_row_done();
         if constexpr (NP4 == 3) asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
         else asm volatile("" ::"v"(shi[kb >> 1]));
       }
@@ -651,7 +686,10 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) stage_load(s + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (decltype(SCREEN)::value) pair_merge<NP4 == 3>(k1, uprev, k2, uprev, r1, t1, r2, t2);
+    if constexpr (decltype(SCREEN)::value) {
+      cert_merge(k1, k2, k3);
+      pair_merge<NP4 == 3>(k1, uprev, k2, uprev, r1, t1, r2, t2);
+    }
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -694,21 +732,39 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         wv[G][u] = *reinterpret_cast<const f32x4*>(wbase + (size_t)(8 * G + oc) * 128 + 4 * u);
   }
   if constexpr (G2) {  // this wave's last unit
-    int k1 = KEY_NONE, k2 = KEY_NONE;
+    int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
     const int ul = 2 * (S - 1) + grp;
-    if ((S - 1) & 1) screen_unit(accB, ul, T_{}, 0, 8, k1, k2);
-    else screen_unit(accA, ul, T_{}, 0, 8, k1, k2);
+    if ((S - 1) & 1) screen_unit(accB, ul, T_{}, 0, 8, k1, k2, k3);
+    else screen_unit(accA, ul, T_{}, 0, 8, k1, k2, k3);
+    cert_merge(k1, k2, k3);
     pair_merge<NP4 == 3>(k1, ul, k2, ul, r1, t1, r2, t2);
   } else {  // the last unit
-    int k1 = KEY_NONE, k2 = KEY_NONE;
-    screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2);
+    int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
+    screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2, k3);
+    cert_merge(k1, k2, k3);
     pair_merge<NP4 == 3>(k1, 2 * S - 1, k2, 2 * S - 1, r1, t1, r2, t2);
   }
   STAMP(2);
 
+#if PCADV_C4_CERT >= 2
+  __shared__ unsigned cert_xn2_wg;  // max over the workgroup's rows (non-negative: uint order)
+  if (tid == 0) cert_xn2_wg = 0u;
+  __syncthreads();
+  atomicMax(&cert_xn2_wg, __float_as_uint(cert_xn2));
+  __syncthreads();
+  const float cert_xn = sqrtf(__uint_as_float(cert_xn2_wg));
+#endif
   // lanes l and l + 32 hold the same channel over interleaved rows
   {
     const int o1 = __shfl_xor(r1, 32), o2 = __shfl_xor(r2, 32);
+    // PCADV_C4_CERT: the channel's third screened value = the largest of both
+    // lanes' dropped keys and the third of the four candidates merged here
+    float cert_v3 = -INFINITY;
+    if constexpr (PCADV_C4_CERT && NP4 == 3) {
+      const int q3 = max(max(r3, __shfl_xor(r3, 32)),
+                         max(min(r1 & ~63, o2 & ~63), min(r2 & ~63, o1 & ~63)));
+      cert_v3 = q3 == KEY_NONE ? -INFINITY : key_value(q3);
+    }
     const int u1 = __shfl_xor(t1, 32), u2 = __shfl_xor(t2, 32);
     // order by (value, global index): decode both pairs first
     const int hm = 4 * h, ho = 4 - hm;  // row offsets of this lane half and the other
@@ -744,14 +800,20 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       float* xv = L.w[0];  // free: the point loop's last barrier has passed
       int* xi = reinterpret_cast<int*>(L.w[1]);
       const int slot = 32 * wblk + r;  // lanes r and r + 32 hold the same pair
+      float* x3v = L.w[2];
       if (grp == 1 && h == 0) {
         xv[2 * slot] = v1;
         xv[2 * slot + 1] = v2;
         xi[2 * slot] = a1;
         xi[2 * slot + 1] = a2;
+        if constexpr (PCADV_C4_CERT && NP4 == 3) x3v[slot] = cert_v3;
       }
       __syncthreads();
       if (grp == 1) return;
+      if constexpr (PCADV_C4_CERT && NP4 == 3) {
+        const float g1 = xv[2 * slot], g2 = xv[2 * slot + 1];
+        cert_v3 = fmaxf(fmaxf(cert_v3, x3v[slot]), fmaxf(fminf(v1, g2), fminf(v2, g1)));
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const float v = xv[2 * slot + q];
@@ -832,10 +894,39 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       gmax[(size_t)c * C4_O + o] = second ? e2 : e1;
       gidx[(size_t)c * C4_O + o] = second ? a2 : a1;
     }
+#if PCADV_C4_CERT == 1
+    asm volatile("" ::"v"(cert_v3));  // tracking cost only
+#elif PCADV_C4_CERT >= 2
+    {
+      // a dropped point p has exact value <= s_p + err_p <= v3 + err, with the
+      // screening error err <= 2^-14.3 sum_k |x_pk w_ok| (three dropped split
+      // terms <= 3 2^-18, up to 384 f32 accumulation roundings <= 2^-15.4, the
+      // 2^-17 key truncation) <= 2^-14 ||x_p|| ||w_o|| (Cauchy-Schwarz)
+      float wn2 = 0.f;
+      for (int k = 0; k < 128; ++k) wn2 = fmaf(w4[(size_t)o * 128 + k], w4[(size_t)o * 128 + k], wn2);
+      const float bound = cert_xn * sqrtf(wn2);
+      const float ew = second ? res2 : res1;  // the winner's exact value, no bias
+      if (h == 0) {
+        atomicAdd(&g_c4_cert[0], cert_v3 + 0x1p-14f * bound >= ew ? 1u : 0u);
+        atomicAdd(&g_c4_cert[1], 1u);
+        atomicAdd(&g_c4_cert[2], cert_v3 + 0x1p-17f * bound >= ew ? 1u : 0u);
+      }
+      if (blockIdx.x == 0 && tid == 0) atomicAdd(&g_c4_cert[3], 1u);
+    }
+#endif
   }
   STAMP(3);
 #undef STAMP
 }
+
+#if PCADV_C4_CERT
+// diagnostic builds only: read (and reset) the certification counters
+int c4_cert_read(unsigned* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_c4_cert), sizeof(g_c4_cert)) != hipSuccess) return -1;
+  const unsigned z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_c4_cert), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t feat_fwd_workspace_bytes(int C, int N) {
   (void)C;

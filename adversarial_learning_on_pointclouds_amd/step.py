@@ -470,6 +470,9 @@ class AdvFtTrainStep(AdvTrainStep):
         self.model, self.model_D = model, model_D
         self.precision = 0
         self.B, self.N = int(B), int(N)
+        if self.N % 64:
+            # the per-cloud transform x2 T runs on 64-row tiles (pcadv_pw_fwd rows_per_w)
+            raise ValueError(f"AdvFtTrainStep: N = {self.N} points, a multiple of 64 is required")
         dev = torch.device(device)
         if dev.type != "cuda":
             raise ValueError("AdvFtTrainStep runs on the HIP device only")
