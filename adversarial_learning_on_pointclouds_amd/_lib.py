@@ -125,6 +125,7 @@ SIGNATURES = {
     "pcadv_linear_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _u64, _f, _vp, _vp, _vp, _vp, _vp,
                               _i, _i, _i, _i, _vp]),
     "pcadv_adam": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _vp]),
+    "pcadv_concat2": (_i, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "pcadv_adam2": (_i, [_vp, _vp, _vp, _vp, _i64, _f, _vp, _vp, _vp, _vp, _i64, _f, _vp, _f, _f,
                          _f, _vp]),
     "pcadv_pw_fwd": (_i, [_vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),

@@ -36,7 +36,7 @@ int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float
                           hipStream_t, uint64_t* stamps = nullptr, int precision = 0,
                           const pcadv_gather_job* gather = nullptr, int ngather = 0);
 int launch_conv4_max(const float*, int, int, const float*, const float*, float*, int32_t*,
-                     hipStream_t, int);
+                     hipStream_t, int, int relu = 0);
 int launch_linear_fwd(const float*, const float*, const float*, float*, int, int, int, int,
                       const float*, const int32_t*, uint64_t, float, hipStream_t,
                       int add_identity_k = 0, float* mask_out = nullptr, int row_split = 0,
@@ -55,6 +55,7 @@ int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, c
                  float*, float*, int64_t, float, const int32_t*, int, float, float, float,
                  hipStream_t);
 int launch_inc(int32_t*, hipStream_t);
+int launch_concat2(const float*, int64_t, const float*, int64_t, float*, int32_t*, hipStream_t);
 size_t disc_tail_slab_floats();
 int disc_tail_slab_n();
 int head_rowblocks(int B);
@@ -266,9 +267,8 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
     PC_REQUIRE(!a->ngather && !a->epi_ncounters && !a->epi_ring,
                "adv_step: part 3 takes no folded gather or epilogue");
     PC_REQUIRE(a->step_count, "adv_step: step_count");
-    // the iteration's step number, as the feature forward's first launch
-    // advances it in parts 0 / 1 (the device draws and Adam key on it)
-    PC_TRY(launch_inc(a->step_count, s));
+    // *step_count was advanced by the caller's first launch (pcadv_concat2),
+    // as the feature forward's first launch advances it in parts 0 / 1
     return adv_head_part(a, s, w, logits);
   }
   if (a->part != 2) {
@@ -654,6 +654,11 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
   PC_TRY(launch_adam2(param, grad, exp_avg, exp_avg_sq, n, lr, nullptr, nullptr, nullptr, nullptr,
                       0, 0.f, step_count, 1, beta1, beta2, eps, stream));
   return launch_inc(step_count, stream);
+}
+
+int pcadv_concat2(const float* a, int64_t na, const float* b, int64_t nb, float* out,
+                  int32_t* inc_counter, hipStream_t stream) {
+  return launch_concat2(a, na, b, nb, out, inc_counter, stream);
 }
 
 int pcadv_adam2(float* p0, const float* g0, float* m0, float* v0, int64_t n0, float lr0,

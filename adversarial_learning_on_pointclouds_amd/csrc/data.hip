@@ -126,6 +126,37 @@ int launch_iter_epilogue(int32_t* counters, int ncounters, const float* losses, 
   return PCADV_OK;
 }
 
+// out = [a; b] (f32 elements; 16-B pieces where both halves are 16-B aligned)
+// and, with inc, *inc += 1 by one thread: the feature-transform step's first
+// launch (its GT and no-GT batches as one 2B-cloud input, the iteration's step
+// number advanced for the device draws and Adam).
+__global__ void __launch_bounds__(256)
+k_concat2(const float* __restrict__ a, int64_t na, const float* __restrict__ b, int64_t nb,
+          float* __restrict__ out, int32_t* __restrict__ inc, int vec) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (inc && t == 0) *inc += 1;
+  if (vec) {
+    const int64_t qa = na / 4, q = qa + nb / 4;
+    if (t < q)
+      reinterpret_cast<f32x4*>(out)[t] =
+          t < qa ? reinterpret_cast<const f32x4*>(a)[t] : reinterpret_cast<const f32x4*>(b)[t - qa];
+    return;
+  }
+  if (t < na + nb) out[t] = t < na ? a[t] : b[t - na];
+}
+
+int launch_concat2(const float* a, int64_t na, const float* b, int64_t nb, float* out,
+                   int32_t* inc, hipStream_t s) {
+  PC_REQUIRE(a && b && out && na >= 0 && nb >= 0 && na + nb > 0, "concat2: bad arguments");
+  const bool vec = na % 4 == 0 && nb % 4 == 0 && ((uintptr_t)a & 15) == 0 &&
+                   ((uintptr_t)b & 15) == 0 && ((uintptr_t)out & 15) == 0;
+  const int64_t n = vec ? (na + nb) / 4 : na + nb;
+  hipLaunchKernelGGL(k_concat2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, na, b, nb,
+                     out, inc, vec ? 1 : 0);
+  PC_HIP_CHECK_LAUNCH("k_concat2");
+  return PCADV_OK;
+}
+
 int launch_gather_multi(const pcadv_gather_job* jobs, int njobs, hipStream_t s) {
   PC_REQUIRE(jobs && njobs >= 1 && njobs <= GATHER_MAXJOBS, "gather_multi: %d jobs (1..%d)", njobs,
              GATHER_MAXJOBS);

@@ -475,7 +475,7 @@ template <int NP4, bool G2>
 __global__ void __launch_bounds__(C4_T)
 k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
             const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
-            uint64_t* __restrict__ stamps) {
+            uint64_t* __restrict__ stamps, int relu) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   C4Lds& L = *reinterpret_cast<C4Lds*>(smem);
   // XCD-aware order: consecutive workgroup ids run on different XCDs, so the
@@ -838,8 +838,11 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     // DESIGN.md, Numerics.)
     if constexpr (NP4 == 1) {  // bf16 mode: the screened winner and its value
       if (h == 0) {
-        gmax[(size_t)c * C4_O + o] = v1 + b4[o];
-        gidx[(size_t)c * C4_O + o] = a1;
+        float gv = v1 + b4[o];
+        int gi = a1;
+        if (relu && gv <= 0.f) gv = 0.f, gi = 0;  // see below
+        gmax[(size_t)c * C4_O + o] = gv;
+        gidx[(size_t)c * C4_O + o] = gi;
       }
       return;
     }
@@ -891,8 +894,14 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     const float e1 = res1 + bias, e2 = res2 + bias;
     const bool second = near && ranks_before(e2, a2, e1, a1);
     if (h == 0) {
-      gmax[(size_t)c * C4_O + o] = second ? e2 : e1;
-      gidx[(size_t)c * C4_O + o] = second ? a2 : a1;
+      float gv = second ? e2 : e1;
+      int gi = second ? a2 : a1;
+      // relu (the T-Nets' ReLU before the max, pointnet.py:30-31,63-64):
+      // max_n relu(v) = relu(max_n v), and where every v <= 0 the ReLU'd row
+      // is all zeros, whose first index (torch.max) is point 0
+      if (relu && gv <= 0.f) gv = 0.f, gi = 0;
+      gmax[(size_t)c * C4_O + o] = gv;
+      gidx[(size_t)c * C4_O + o] = gi;
     }
 #if PCADV_C4_CERT == 1
     asm volatile("" ::"v"(cert_v3));  // tracking cost only
@@ -968,7 +977,8 @@ static int feat_fwd_attrs() {
 // feature forward
 template <int NP3, int NP4>
 static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, const float* b4,
-                               float* gmax, int32_t* gidx, hipStream_t s, uint64_t* stamps) {
+                               float* gmax, int32_t* gidx, hipStream_t s, uint64_t* stamps,
+                               int relu = 0) {
   const int rc = feat_fwd_attrs<NP3, NP4>();
   if (rc != PCADV_OK) return rc;
   // two wave groups per 128-channel workgroup when 256-channel workgroups would
@@ -978,10 +988,10 @@ static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, c
 #endif
   if (C <= PCADV_C4_G2_MAXC && !stamps)
     hipLaunchKernelGGL((k_conv4_max<NP4, true>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
-                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
   else
     hipLaunchKernelGGL((k_conv4_max<NP4, false>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
-                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps);
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
   PC_HIP_CHECK_LAUNCH("k_conv4_max");
   return PCADV_OK;
 }
@@ -1011,12 +1021,13 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
 }
 
 int launch_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4, float* gmax,
-                     int32_t* gidx, hipStream_t s, int precision) {
+                     int32_t* gidx, hipStream_t s, int precision, int relu) {
   PC_REQUIRE(C > 0 && N > 0, "conv4_max: bad shape C=%d N=%d", C, N);
   PC_REQUIRE(precision == 0 || precision == 1, "conv4_max: precision %d (0 fp32, 1 bf16)",
              precision);
-  if (precision == 1) return launch_conv4_max_np<1, 1>(x3, C, N, w4, b4, gmax, gidx, s, nullptr);
-  return launch_conv4_max_np<6, 3>(x3, C, N, w4, b4, gmax, gidx, s, nullptr);
+  if (precision == 1)
+    return launch_conv4_max_np<1, 1>(x3, C, N, w4, b4, gmax, gidx, s, nullptr, relu);
+  return launch_conv4_max_np<6, 3>(x3, C, N, w4, b4, gmax, gidx, s, nullptr, relu);
 }
 
 // precision 0: f32-level (conv3 six bf16 products, conv4 three + the exact

@@ -204,17 +204,7 @@ int launch_point_mlp3(const float* pts_a, const float* pts_b, int split, int C, 
 }
 
 int launch_conv4_max(const float*, int, int, const float*, const float*, float*, int32_t*,
-                     hipStream_t, int);
-
-// ReLU before the max: max_n relu(v) = relu(max_n v), and where every v <= 0
-// the ReLU'd row is all zeros, whose first index (torch.max) is point 0
-__global__ void k_relu_max_fix(float* __restrict__ gmax, int32_t* __restrict__ gidx, int n) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n && gmax[i] <= 0.f) {
-    gmax[i] = 0.f;
-    gidx[i] = 0;
-  }
-}
+                     hipStream_t, int, int relu = 0);
 
 int launch_conv_max128(const float* x, int C, int N, const float* w, const float* b, int O,
                        bool relu, float* gmax, int32_t* gidx, hipStream_t s) {
@@ -222,12 +212,8 @@ int launch_conv_max128(const float* x, int C, int N, const float* w, const float
     // the 1024-channel layers (feature conv4, the T-Nets' conv3) on the fused
     // forward's k_conv4_max: split-product screening + exact f32 re-evaluation
     // of every winner, ~4x this file's f32 kernel
-    const int rc = launch_conv4_max(x, C, N, w, b, gmax, gidx, s, 0);
-    if (rc != PCADV_OK || !relu) return rc;
-    const int n = C * O;
-    hipLaunchKernelGGL(k_relu_max_fix, dim3((n + 255) / 256), dim3(256), 0, s, gmax, gidx, n);
-    PC_HIP_CHECK_LAUNCH("k_relu_max_fix");
-    return PCADV_OK;
+    // (the ReLU before the max applied in its epilogue)
+    return launch_conv4_max(x, C, N, w, b, gmax, gidx, s, 0, relu ? 1 : 0);
   }
   dim3 grid(O / 128, C);
   if (relu)

@@ -470,9 +470,10 @@ class AdvFtTrainStep(AdvTrainStep):
         self.model, self.model_D = model, model_D
         self.precision = 0
         self.B, self.N = int(B), int(N)
-        if self.N % 64:
-            # the per-cloud transform x2 T runs on 64-row tiles (pcadv_pw_fwd rows_per_w)
-            raise ValueError(f"AdvFtTrainStep: N = {self.N} points, a multiple of 64 is required")
+        if self.N % 128:
+            # the per-cloud transform x2 T and its dT = x2^T dx2t run on 64- / 128-row
+            # tiles (pcadv_pw_fwd rows_per_w, pcadv_pw_bwd_weight rows_per_group)
+            raise ValueError(f"AdvFtTrainStep: N = {self.N} points, a multiple of 128 is required")
         dev = torch.device(device)
         if dev.type != "cuda":
             raise ValueError("AdvFtTrainStep runs on the HIP device only")
@@ -554,8 +555,11 @@ class AdvFtTrainStep(AdvTrainStep):
         P, Gr = self._p, self._g
         self._pre()
         pts = self.pts[:C]
-        pts[:B].copy_(pts_gt)
-        pts[B:].copy_(pts_nogt)
+        # [GT; no-GT] as one input and the step number advanced, in one launch
+        # (two memcpy graph nodes and a counter launch cost ~24 us)
+        n = B * N * 3
+        check(self.lib.pcadv_concat2(pts_gt.data_ptr(), n, pts_nogt.data_ptr(), n, pts.data_ptr(),
+                                     self.step_count.data_ptr(), stream_ptr()), "pcadv_concat2")
         # ---- PointNetfeat with the feature transform (pointnet.py:109-130) ----
         x1 = ops.pw_fwd(pts, P["feat.conv1.weight"], P["feat.conv1.bias"], RELU)
         x2 = ops.pw_fwd(x1, P["feat.conv2.weight"], P["feat.conv2.bias"], RELU)

@@ -699,7 +699,7 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
                and trainloader_gt.B == trainloader_nogt.B
                and trainloader_gt.npts == trainloader_nogt.npts
                and trainloader_gt.B <= MAX_FUSED_B
-               and (fused is not AdvFtTrainStep or trainloader_gt.npts % 64 == 0))
+               and (fused is not AdvFtTrainStep or trainloader_gt.npts % 128 == 0))
     # off the fused step, with capturable optimizers over DeviceCloudLoaders:
     # each full, semi-free iteration's gathers + autograd body as one HIP graph
     ag_graphed = (not fused) and _AutogradAdvStep.graphable(
@@ -800,7 +800,7 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
             cls = cls.long().to(args.device).contiguous()
             pts_nogt = pts_nogt.float().to(args.device).contiguous()
             if (fused and pts.shape == pts_nogt.shape and pts.shape[0] <= MAX_FUSED_B
-                    and (fused is not AdvFtTrainStep or pts.shape[1] % 64 == 0)):
+                    and (fused is not AdvFtTrainStep or pts.shape[1] % 128 == 0)):
                 st = fused_step(pts.shape[0], pts.shape[1])
                 if pooled:
                     losses = st(pts, cls, pts_nogt, apply_adam=False, semi=semi_on)

@@ -425,6 +425,14 @@ int pcadv_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_s
                int64_t n, int32_t* step_count, float lr, float beta1, float beta2,
                float eps, hipStream_t stream);
 
+/* out = [a; b] (na + nb floats) and, when inc_counter is not NULL,
+ * *inc_counter += 1: the feature-transform step's first launch, its GT and
+ * no-GT batches as one 2B-cloud input (PointNetCls runs on each,
+ * utils/trainer.py:467,490) and the iteration's step number advanced for the
+ * device draws and pcadv_adam2.  ABI version 8. */
+int pcadv_concat2(const float* a, int64_t na, const float* b, int64_t nb, float* out,
+                  int32_t* inc_counter, hipStream_t stream);
+
 /* Two Adam updates of one iteration in one launch (segment 1 may be empty,
  * n1 = 0), each with its own learning rate, at the step number *step_count
  * that the iteration already advanced (pcadv_adv_step part 3): t =
@@ -516,9 +524,10 @@ typedef struct pcadv_adv_args {
    * (fc1..fc3 + dropout, log_softmax / CE, the three discriminator passes with
    * their BCE terms, D's gradients, the head backward) on the caller's pooled
    * features feat_gmax [2B][1024] (GT clouds first) and writes dL/dgmax to
-   * feat_dgmax [2B][1024].  No gather, epilogue or Adam: the caller
-   * backpropagates through its extractor and runs Adam (pcadv_adam).  NULL for
-   * parts 0-2.  ABI version 8. */
+   * feat_dgmax [2B][1024].  No gather, epilogue or Adam, and *step_count is
+   * NOT advanced: the caller's first launch advances it (pcadv_concat2), its
+   * extractor's backward and Adam (pcadv_adam2) follow.  NULL for parts 0-2.
+   * ABI version 8. */
   const float* feat_gmax;
   float* feat_dgmax;
 } pcadv_adv_args;

@@ -63,7 +63,7 @@ def _record_conv_max(monkeypatch):
     return rec
 
 
-@pytest.mark.parametrize("B,N,strict", [(4, 1024, True), (5, 320, True), (32, 1024, False)])
+@pytest.mark.parametrize("B,N,strict", [(4, 1024, True), (5, 384, True), (32, 1024, False)])
 def test_ft_step_vs_oracle_same_activation(monkeypatch, B, N, strict):
     from adversarial_learning_on_pointclouds_amd.step import AdvFtTrainStep
     from oracle import pointnet_np as onp
