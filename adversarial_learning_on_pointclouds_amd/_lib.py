@@ -98,6 +98,12 @@ class AdvArgs(ctypes.Structure):
     ]
 
 
+class PwWgradJob(ctypes.Structure):
+    """Mirror of pcadv_pw_wgrad_job (include/pcadv.h)."""
+
+    _fields_ = [("slabs", _vp), ("M", _i), ("O", _i), ("K", _i), ("dw", _vp), ("db", _vp)]
+
+
 class GatherJob(ctypes.Structure):
     """Mirror of pcadv_gather_job (include/pcadv.h)."""
 
@@ -133,6 +139,7 @@ SIGNATURES = {
     "pcadv_pw_bwd_weight_workspace_bytes": (_sz, [_i, _i, _i]),
     "pcadv_pw_bwd_weight": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _sz,
                                  _vp]),
+    "pcadv_pw_wgrad_finish": (_i, [ctypes.POINTER(PwWgradJob), _i, _vp]),
     "pcadv_conv_max_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "pcadv_tnet_reg_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_tnet_reg_bwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),

@@ -55,6 +55,7 @@ int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, c
                  float*, float*, int64_t, float, const int32_t*, int, float, float, float,
                  hipStream_t);
 int launch_inc(int32_t*, hipStream_t);
+int launch_pw_wgrad_finish(const pcadv_pw_wgrad_job*, int, hipStream_t);
 int launch_concat2(const float*, int64_t, const float*, int64_t, float*, int32_t*, hipStream_t);
 size_t disc_tail_slab_floats();
 int disc_tail_slab_n();
@@ -619,6 +620,10 @@ int pcadv_pw_bwd_weight(const float* dy, const float* y, int act, const float* x
                         void* workspace, size_t workspace_bytes, hipStream_t stream) {
   return launch_pw_bwd_weight(dy, y, act, x, M, O, K, rows_per_group, dw_kmajor, dw, db,
                               workspace, workspace_bytes, stream);
+}
+
+int pcadv_pw_wgrad_finish(const pcadv_pw_wgrad_job* jobs, int njobs, hipStream_t stream) {
+  return launch_pw_wgrad_finish(jobs, njobs, stream);
 }
 
 int pcadv_conv_max_bwd(const float* dgmax, const int32_t* gidx, const float* gmax_relu,

@@ -417,6 +417,47 @@ k_pw_reduce(const float* __restrict__ slabs, int per, int width, int wsize,
   }
 }
 
+// Several weight gradients' slab sums in ONE launch (blockIdx.y = job), each
+// job summed exactly as k_pw_reduce sums it (same slabs, order and waves), so
+// the results are bitwise the per-gradient launches'.
+constexpr int PWR_MAXJOBS = 8;
+struct PwReduceJobs {
+  const float* slabs[PWR_MAXJOBS];
+  float* dw[PWR_MAXJOBS];
+  float* db[PWR_MAXJOBS];
+  int per[PWR_MAXJOBS], width[PWR_MAXJOBS], wsize[PWR_MAXJOBS];
+};
+__global__ void __launch_bounds__(64 * PWR_W) k_pw_reduce_batch(PwReduceJobs jb) {
+  __shared__ float part[PWR_W][64];
+  const int q = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = jb.per[q], width = jb.width[q];
+  const int j = blockIdx.x * 64 + lane;
+  if ((int)blockIdx.x * 64 >= width) return;  // block-uniform
+  const int s0 = wave * per / PWR_W, s1 = (wave + 1) * per / PWR_W;
+  float acc = 0.f;
+  if (j < width) {
+    const float* s = jb.slabs[q] + j;
+    int i = s0;
+    for (; i + 8 <= s1; i += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(i + u) * width];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; i < s1; ++i) acc += s[(size_t)i * width];
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && j < width) {
+    float x = part[0][lane];
+    for (int w = 1; w < PWR_W; ++w) x += part[w][lane];
+    if (j < jb.wsize[q]) jb.dw[q][j] = x;
+    else if (jb.db[q]) jb.db[q][j - jb.wsize[q]] = x;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // conv + max over points, backward (sparse; optional ReLU before the max)
 // ---------------------------------------------------------------------------
@@ -753,6 +794,8 @@ int launch_pw_bwd_weight(const float* dy, const float* y, int act, const float* 
   PC_REQUIRE(K != 3 || (!dw_kmajor && O <= 64), "pw_bwd_weight: K=3 needs O <= 64, [o][k]");
   PC_REQUIRE(ws && ws_bytes >= pw_bwd_weight_workspace_bytes(M, O, K),
              "pw_bwd_weight: workspace too small");
+  PC_REQUIRE(dw || (!db && rows_per_group == 0 && !dw_kmajor),
+             "pw_bwd_weight: the deferred form (dw = db = NULL) takes rows_per_group 0, [o][k]");
   float* slabs = static_cast<float*>(ws);
   const int nslab = (M + PWW_ROWS - 1) / PWW_ROWS;
   if (K == 3) {
@@ -768,12 +811,36 @@ int launch_pw_bwd_weight(const float* dy, const float* y, int act, const float* 
 #undef PW_CASE
   }
   PC_HIP_CHECK_LAUNCH("k_pw_bwd_weight");
+  if (!dw) return PCADV_OK;  // slabs only: summed later by launch_pw_wgrad_finish
   const int width = O * K + O;
   const int groups = rows_per_group ? M / rows_per_group : 1;
   const int per = rows_per_group ? rows_per_group / PWW_ROWS : nslab;
   hipLaunchKernelGGL(k_pw_reduce, dim3((width + 63) / 64, groups), dim3(64 * PWR_W), 0, s, slabs,
                      per, width, O * K, dw, db);
   PC_HIP_CHECK_LAUNCH("k_pw_reduce");
+  return PCADV_OK;
+}
+
+int launch_pw_wgrad_finish(const pcadv_pw_wgrad_job* jobs, int njobs, hipStream_t s) {
+  PC_REQUIRE(jobs && njobs >= 1 && njobs <= PWR_MAXJOBS, "pw_wgrad_finish: %d jobs (1..%d)", njobs,
+             PWR_MAXJOBS);
+  PwReduceJobs jb{};
+  int maxw = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const pcadv_pw_wgrad_job& j = jobs[k];
+    PC_REQUIRE(j.slabs && j.dw && j.M > 0 && (j.O == 64 || j.O == 128) &&
+                   (j.K == 3 || j.K == 64 || j.K == 128),
+               "pw_wgrad_finish: job %d: bad arguments (M=%d O=%d K=%d)", k, j.M, j.O, j.K);
+    jb.slabs[k] = static_cast<const float*>(j.slabs);
+    jb.dw[k] = j.dw;
+    jb.db[k] = j.db;
+    jb.per[k] = (j.M + PWW_ROWS - 1) / PWW_ROWS;
+    jb.width[k] = j.O * j.K + j.O;
+    jb.wsize[k] = j.O * j.K;
+    if (jb.width[k] > maxw) maxw = jb.width[k];
+  }
+  hipLaunchKernelGGL(k_pw_reduce_batch, dim3((maxw + 63) / 64, njobs), dim3(64 * PWR_W), 0, s, jb);
+  PC_HIP_CHECK_LAUNCH("k_pw_reduce_batch");
   return PCADV_OK;
 }
 

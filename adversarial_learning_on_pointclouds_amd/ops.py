@@ -13,7 +13,7 @@ from ._lib import ACT_LRELU, ACT_NONE, ACT_RELU, check, ptr, stream_ptr
 
 __all__ = ["ACT_NONE", "ACT_RELU", "ACT_LRELU", "feat_fwd", "feat_bwd", "conv_max_fwd",
            "conv_max_bwd", "linear_fwd", "linear_bwd", "adam_", "pw_fwd", "pw_bwd_data",
-           "pw_bwd_weight", "tnet_reg_fwd", "tnet_reg_bwd", "PointFeatFunction",
+           "pw_bwd_weight", "pw_wgrad_finish", "tnet_reg_fwd", "tnet_reg_bwd", "PointFeatFunction",
            "LinearFunction", "PointwiseFunction", "TransformFunction", "ConvMaxFunction",
            "RegularizerFunction"]
 
@@ -212,9 +212,12 @@ def pw_bwd_data(dy, y, act, w, K, kmajor=False, rows_per_w=0, out=None):
 
 
 def pw_bwd_weight(dy, y, act, x, rows_per_group=0, kmajor=False, need_db=True, dw_out=None,
-                  db_out=None):
+                  db_out=None, defer=None):
     """(dW, db) of y = act(x W^T + b): dW (groups, O, K) or kmajor (groups, K, O);
-    dw_out / db_out: write them there instead (same element counts)."""
+    dw_out / db_out: write them there instead (same element counts).  defer: a
+    list; the slab partial sums are left in a workspace and a job appended to
+    it, for one pw_wgrad_finish(defer) launch later (dw_out / db_out required,
+    rows_per_group 0, [o][k]); returns (dw_out, db_out) unwritten until then."""
     lib = _lib.load()
     _req(dy, "dy")
     _req(x, "x")
@@ -228,10 +231,27 @@ def pw_bwd_weight(dy, y, act, x, rows_per_group=0, kmajor=False, need_db=True, d
     db = _out(db_out, "db", (groups, O), dy.device) if need_db else None
     nb = lib.pcadv_pw_bwd_weight_workspace_bytes(M, O, K)
     ws = torch.empty(nb, device=dy.device, dtype=torch.uint8)
+    if defer is not None:
+        if dw_out is None or rows_per_group or kmajor:
+            raise ValueError("pw_bwd_weight(defer=...): dw_out, rows_per_group 0, [o][k]")
+        check(lib.pcadv_pw_bwd_weight(ptr(dy), ptr(y), act, ptr(x), M, O, K, 0, 0, None, None,
+                                      ptr(ws), nb, stream_ptr()), "pcadv_pw_bwd_weight (slabs)")
+        defer.append((_lib.PwWgradJob(ws.data_ptr(), M, O, K, dw.data_ptr(),
+                                      db.data_ptr() if db is not None else None), ws))
+        return dw, db
     check(lib.pcadv_pw_bwd_weight(ptr(dy), ptr(y), act, ptr(x), M, O, K, rows_per_group,
                                   int(bool(kmajor)), ptr(dw), ptr(db), ptr(ws), nb, stream_ptr()),
           "pcadv_pw_bwd_weight")
     return dw, db
+
+
+def pw_wgrad_finish(jobs):
+    """The slab sums of the weight gradients pw_bwd_weight(defer=jobs) left, in
+    one launch (bitwise the per-gradient sums); the workspaces stay alive
+    through the list until then."""
+    lib = _lib.load()
+    arr = (_lib.PwWgradJob * len(jobs))(*[j for j, _ in jobs])
+    check(lib.pcadv_pw_wgrad_finish(arr, len(jobs), stream_ptr()), "pcadv_pw_wgrad_finish")
 
 
 def tnet_reg_fwd(T):

@@ -579,13 +579,15 @@ class AdvFtTrainStep(AdvTrainStep):
         a.feat_gmax, a.feat_dgmax = gmax.data_ptr(), dgmax.data_ptr()
         self._keep_last = (a, gmax)
         check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (part 3)")
-        # ---- the extractor's backward ------------------------------------------
+        # ---- the extractor's backward (the five point-wise weight gradients'
+        #      slab sums deferred to one launch at the end) -----------------------
+        jobs = []
         dx3, _, _ = ops.conv_max_bwd(dgmax, gidx, x3, P["feat.conv4.weight"],
                                      dw_out=Gr["feat.conv4.weight"], db_out=Gr["feat.conv4.bias"])
         w3 = _mat(P["feat.conv3.weight"])
         dx2t = ops.pw_bwd_data(dx3, x3, RELU, w3, 64)
         ops.pw_bwd_weight(dx3, x3, RELU, x2t, dw_out=Gr["feat.conv3.weight"],
-                          db_out=Gr["feat.conv3.bias"])
+                          db_out=Gr["feat.conv3.bias"], defer=jobs)
         # x2t = x2 T: dT = x2^T dx2t per cloud, dx2 = dx2t T^T
         dT, _ = ops.pw_bwd_weight(dx2t, None, NONE, x2, rows_per_group=N, kmajor=True,
                                   need_db=False)
@@ -602,15 +604,16 @@ class AdvFtTrainStep(AdvTrainStep):
                                      dw_out=Gr[s + "conv3.weight"], db_out=Gr[s + "conv3.bias"])
         dh1 = ops.pw_bwd_data(dh2, h2, RELU, _mat(P[s + "conv2.weight"]), 64)
         ops.pw_bwd_weight(dh2, h2, RELU, h1, dw_out=Gr[s + "conv2.weight"],
-                          db_out=Gr[s + "conv2.bias"])
+                          db_out=Gr[s + "conv2.bias"], defer=jobs)
         ops.pw_bwd_data(dh1, h1, RELU, _mat(P[s + "conv1.weight"]), 64, out=dx2)
         ops.pw_bwd_weight(dh1, h1, RELU, x2, dw_out=Gr[s + "conv1.weight"],
-                          db_out=Gr[s + "conv1.bias"])
+                          db_out=Gr[s + "conv1.bias"], defer=jobs)
         dx1 = ops.pw_bwd_data(dx2, x2, RELU, _mat(P["feat.conv2.weight"]), 64)
         ops.pw_bwd_weight(dx2, x2, RELU, x1, dw_out=Gr["feat.conv2.weight"],
-                          db_out=Gr["feat.conv2.bias"])
+                          db_out=Gr["feat.conv2.bias"], defer=jobs)
         ops.pw_bwd_weight(dx1, x1, RELU, pts, dw_out=Gr["feat.conv1.weight"],
-                          db_out=Gr["feat.conv1.bias"])
+                          db_out=Gr["feat.conv1.bias"], defer=jobs)
+        ops.pw_wgrad_finish(jobs)
         if apply_adam:
             self.adam()
         self._post()

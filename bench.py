@@ -1017,7 +1017,10 @@ def bench_dp1(args):
               Adam of the early bucket | Adam of conv1..conv4) around the two
               host-issued RCCL all-reduces (bench --gpus N, trainer _DPIteration);
       dp1g    DataParallelAdvStep.capture_single: the same iteration as ONE graph
-              with both all-reduces captured on RCCL's stream.
+              with both all-reduces captured on RCCL's stream;
+      dp2     overlap=False: the step without Adam | ONE all-reduce of the 4.2 MB
+              gradient buffer | both Adams (two graphs around one collective);
+      dp2g    the same as ONE graph with the all-reduce captured.
     overhead = form - plain per iteration (the communication itself is ~0 on
     one rank; the multi-rank exchange is the driver's scaling runs)."""
     import torch.distributed as tdist
@@ -1031,6 +1034,7 @@ def bench_dp1(args):
     model, model_D = make_models(dev, seed=0)
     step = AdvTrainStep(model, model_D, B, N, seed=1234, device=dev, precision="fp32")
     runner = DataParallelAdvStep(step, overlap=True)
+    flat = DataParallelAdvStep(step, broadcast_params=False, overlap=False)
     pool = []
     for k in range(POOL):
         rng = np.random.default_rng(1000 + k * 64)
@@ -1038,12 +1042,14 @@ def bench_dp1(args):
                      torch.from_numpy(rng.integers(0, 40, B)).to(dev),
                      torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev)))
     forms = {"plain": [step.capture_on(*p) for p in pool],
-             "dp4": [runner.capture(*p) for p in pool]}
-    try:
-        forms["dp1g"] = [runner.capture_single(*p) for p in pool]
-        single_err = None
-    except Exception as e:  # noqa: BLE001 - reported in the line
-        single_err = f"{type(e).__name__}: {e}"[:300]
+             "dp4": [runner.capture(*p) for p in pool],
+             "dp2": [flat.capture(*p) for p in pool]}
+    single_err = None
+    for name, r in (("dp1g", runner), ("dp2g", flat)):
+        try:
+            forms[name] = [r.capture_single(*p) for p in pool]
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            single_err = f"{name}: {type(e).__name__}: {e}"[:300]
     host = {}
     times = {k: [] for k in forms}
     for _ in range(args.repeats):

@@ -175,6 +175,21 @@ int pcadv_pw_bwd_weight(const float* dy, const float* y, int act, const float* x
                         int K, int rows_per_group, int dw_kmajor, float* dw, float* db,
                         void* workspace, size_t workspace_bytes, hipStream_t stream);
 
+/* The deferred form of pcadv_pw_bwd_weight (rows_per_group = 0, dw [O][K]):
+ * pcadv_pw_bwd_weight with dw = db = NULL writes only the per-slab partial sums
+ * into its workspace; pcadv_pw_wgrad_finish then sums the slabs of up to 8
+ * such weight gradients (each job: that call's workspace, M, O, K, and the
+ * dw / db to write) in ONE launch, bitwise the per-call sums.  The
+ * feature-transform step's backward finishes its five parameter gradients
+ * this way.  ABI version 8. */
+typedef struct pcadv_pw_wgrad_job {
+  const void* slabs;
+  int M, O, K;
+  float* dw;
+  float* db;
+} pcadv_pw_wgrad_job;
+int pcadv_pw_wgrad_finish(const pcadv_pw_wgrad_job* jobs, int njobs, hipStream_t stream);
+
 /* Backward of pcadv_conv_max_fwd: each channel's gradient goes to its argmax
  * point (times [gmax > 0] when gmax_relu is given: the ReLU before the max of
  * the T-Nets, pointnet.py:30-31,63-64).  dw [O][K], db [O] (may be NULL), dx

@@ -515,10 +515,14 @@ def _layer_bwd(dy, x, y, w):
     return (dz2.T @ x2).astype(F32), dz2.sum(0).astype(F32), (dz @ w).astype(F32)
 
 
-def stn_forward_train(p, x, prefix, k):
-    """STNkd forward keeping what its backward needs (models/pointnet.py:59-79)."""
-    h1 = relu(x @ _w(p, prefix + "conv1.weight").T + p[prefix + "conv1.bias"]).astype(F32)
-    h2 = relu(h1 @ _w(p, prefix + "conv2.weight").T + p[prefix + "conv2.bias"]).astype(F32)
+def stn_forward_train(p, x, prefix, k, h1=None, h2=None):
+    """STNkd forward keeping what its backward needs (models/pointnet.py:59-79).
+    h1 / h2: conv1's / conv2's activations to use instead of recomputing them
+    (same-activation checks)."""
+    if h1 is None:
+        h1 = relu(x @ _w(p, prefix + "conv1.weight").T + p[prefix + "conv1.bias"]).astype(F32)
+    if h2 is None:
+        h2 = relu(h1 @ _w(p, prefix + "conv2.weight").T + p[prefix + "conv2.bias"]).astype(F32)
     g, am = conv_max_fwd(h2, _w(p, prefix + "conv3.weight"), p[prefix + "conv3.bias"],
                          relu_before_max=True)
     f1 = relu(g @ p[prefix + "fc1.weight"].T + p[prefix + "fc1.bias"]).astype(F32)
@@ -575,15 +579,23 @@ def conv_max_at(x, w, b, am, relu_before_max=False):
     return (np.maximum(g, F32(0)) if relu_before_max else g).astype(F32)
 
 
-def cls_ft_forward_train(p, pts, mask, am_stn=None, am=None):
+def cls_ft_forward_train(p, pts, mask, am_stn=None, am=None, acts=None):
     """PointNetCls(feature_transform=True).forward in train mode
     (models/pointnet.py:59-79,109-137,197-203) keeping what cls_ft_backward
     needs.  am_stn / am: the STNkd's conv3 and the feature conv4 max-pool
-    argmax to use instead of the oracle's own (same-activation checks)."""
+    argmax to use instead of the oracle's own; acts: {"x1", "x2", "h1", "h2",
+    "x3"} point-wise activations to use instead of recomputing them (both for
+    same-activation checks: a pre-activation within rounding of a ReLU or max
+    decision then routes the gradient as the device did)."""
+    acts = acts or {}
     pts = np.ascontiguousarray(pts, F32)
-    x1 = relu(pts @ _w(p, "feat.conv1.weight").T + p["feat.conv1.bias"]).astype(F32)
-    x2 = relu(x1 @ _w(p, "feat.conv2.weight").T + p["feat.conv2.bias"]).astype(F32)
-    trans, sc = stn_forward_train(p, x2, "feat.fstn.", 64)
+    x1 = acts.get("x1")
+    if x1 is None:
+        x1 = relu(pts @ _w(p, "feat.conv1.weight").T + p["feat.conv1.bias"]).astype(F32)
+    x2 = acts.get("x2")
+    if x2 is None:
+        x2 = relu(x1 @ _w(p, "feat.conv2.weight").T + p["feat.conv2.bias"]).astype(F32)
+    trans, sc = stn_forward_train(p, x2, "feat.fstn.", 64, acts.get("h1"), acts.get("h2"))
     if am_stn is not None:
         pre = "feat.fstn."
         g = conv_max_at(sc["h2"], _w(p, pre + "conv3.weight"), p[pre + "conv3.bias"],
@@ -595,7 +607,9 @@ def cls_ft_forward_train(p, pts, mask, am_stn=None, am=None):
         trans = t.reshape(-1, 64, 64).astype(F32)
         sc.update(g=g, am=np.asarray(am_stn, np.int64), f1=f1, f2=f2)
     x2t = np.matmul(x2, trans).astype(F32)
-    x3 = relu(x2t @ _w(p, "feat.conv3.weight").T + p["feat.conv3.bias"]).astype(F32)
+    x3 = acts.get("x3")
+    if x3 is None:
+        x3 = relu(x2t @ _w(p, "feat.conv3.weight").T + p["feat.conv3.bias"]).astype(F32)
     W4 = _w(p, "feat.conv4.weight")
     if am is None:
         gmax, am = conv_max_fwd(x3, W4, p["feat.conv4.bias"])
@@ -663,17 +677,19 @@ def cls_ft_step(p, pts, labels, mask, lambda_cls=1.0, lambda_regu=0.001):
 
 
 def adv_ft_grads(G, D, pts_gt, labels, pts_nogt, mask_gt, mask_nogt, y_gt, y_nogt,
-                 lambda_cls=1.0, lambda_adv=0.001, am=None):
+                 lambda_cls=1.0, lambda_adv=0.001, am=None, acts=None):
     """run_training's iteration body (utils/trainer.py:468-556, ImagePool(0))
     with a feature-transform generator: G's and D's gradients before the Adam
     steps.  No regulariser: run_training leaves it commented out (:473-476,
     :511-517).  am: optional (am_stn_gt, am_gt, am_stn_nogt, am_nogt) device
-    argmax decisions (same-activation checks)."""
+    argmax decisions, acts: (GT, no-GT) activation dicts of cls_ft_forward_train
+    (same-activation checks)."""
     am = am or (None, None, None, None)
-    lg, cg = cls_ft_forward_train(G, pts_gt, mask_gt, am[0], am[1])          # :467
+    acts = acts or (None, None)
+    lg, cg = cls_ft_forward_train(G, pts_gt, mask_gt, am[0], am[1], acts[0])  # :467
     l, dce = cross_entropy(lg, labels)                                      # :468
     lsm_gt = log_softmax(lg)                                                # :471
-    ln, cn = cls_ft_forward_train(G, pts_nogt, mask_nogt, am[2], am[3])      # :490
+    ln, cn = cls_ft_forward_train(G, pts_nogt, mask_nogt, am[2], am[3], acts[1])  # :490
     lsm_ng = log_softmax(ln)                                                # :492
     d_ng, acts_ng = disc_forward(D, lsm_ng)                                 # :498
     loss_adv, dadv = bce_with_logits(d_ng, np.ones_like(d_ng))              # :499-506

@@ -6,11 +6,9 @@ plain step's own tail (pcadv_adv_step part 3), against the numpy oracle
 (oracle.adv_ft_grads, pinned to the reference's own g13 capture by
 tests/test_oracle_golden.py).
 
-Gradients: against the oracle's backward on the device's own max-pool argmax
-(same-activation), per tensor 1e-4 of the largest entry and 1e-5 relative L2
-at B = 4; at B = 32 the default per-tensor bound (1e-3 / 1e-4): two f32
-computations there can route a gradient differently at a pre-activation
-within rounding of a ReLU (the ReLU-flip policy).  Losses 1e-4.
+Gradients: against the oracle's backward on the device's own activations and
+max-pool argmax (same-activation), per tensor 1e-4 of the largest entry and
+1e-5 relative L2 (the ReLU-flip policy).  Losses 1e-4.
 Graph replay equals eager bitwise.  MI355X only."""
 import numpy as np
 import pytest
@@ -50,40 +48,54 @@ def _inputs(seed, B, N):
     return pg, lab, pn, m1, m2, y1, y2
 
 
-def _record_conv_max(monkeypatch):
+def _record(monkeypatch, name, pick):
+    """Every ops.<name> call's pick(output), in call order."""
     from adversarial_learning_on_pointclouds_amd import ops
     rec = []
-    orig = ops.conv_max_fwd
+    orig = getattr(ops, name)
 
-    def conv_max_fwd(*a, **k):
-        gmax, gidx = orig(*a, **k)
-        rec.append(gidx)
-        return gmax, gidx
-    monkeypatch.setattr(ops, "conv_max_fwd", conv_max_fwd)
+    def wrapped(*a, **k):
+        out = orig(*a, **k)
+        rec.append(pick(out))
+        return out
+    monkeypatch.setattr(ops, name, wrapped)
     return rec
 
 
-@pytest.mark.parametrize("B,N,strict", [(4, 1024, True), (5, 384, True), (32, 1024, False)])
-def test_ft_step_vs_oracle_same_activation(monkeypatch, B, N, strict):
+@pytest.mark.parametrize("B,N", [(4, 1024), (5, 384), (32, 1024)])
+def test_ft_step_vs_oracle_same_activation(monkeypatch, B, N):
+    """The oracle's backward on the device's own point-wise activations (x1,
+    x2, STNkd h1 / h2, x3) and max-pool argmax: per tensor 1e-4 of the
+    largest entry and 1e-5 relative L2, at B = 32 too (end to end, a
+    pre-activation within rounding of 0 in the STNkd's 65 536 x 128 conv
+    outputs flips and moves fstn conv1 / conv2's gradients by ~2e-3 L2,
+    printed below: the ReLU-flip policy of DESIGN.md)."""
     from adversarial_learning_on_pointclouds_amd.step import AdvFtTrainStep
     from oracle import pointnet_np as onp
     model, model_D, G, D = _models(21, 22)
     st = AdvFtTrainStep(model, model_D, B, N, seed=5)
     pg, lab, pn, m1, m2, y1, y2 = _inputs(100 + B, B, N)
-    rec = _record_conv_max(monkeypatch)
+    rec = _record(monkeypatch, "conv_max_fwd", lambda out: out[1])
+    pw = _record(monkeypatch, "pw_fwd", lambda out: out)
     losses = st(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
                 soft=(_t(y1), _t(y2)), apply_adam=False).cpu().numpy()
     s3, c4 = (r.cpu().numpy() for r in rec[-2:])
     am = (s3[:B], c4[:B], s3[B:], c4[B:])
+    x1, x2, h1, h2, _, x3 = (a.cpu().numpy() for a in pw[-6:])
+    acts = tuple(dict(x1=x1[sl], x2=x2[sl], h1=h1[sl], h2=h2[sl], x3=x3[sl])
+                 for sl in (slice(0, B), slice(B, 2 * B)))
     args = (G, D, pg, lab, pn, m1, m2, y1[:, None], y2[:, None], 1.0, 0.001)
-    ref_l, _, _, own = onp.adv_ft_grads(*args)
+    ref_l, gG0, _, own = onp.adv_ft_grads(*args)
     moved = [int((a != o).sum()) for a, o in zip(am, own["am"])]
     print(f"B={B}: argmax the oracle's own forward moves: {moved}")
-    lr, gG, gD, _ = onp.adv_ft_grads(*args, am=am)
+    for nm in ("feat.fstn.conv1.weight", "feat.fstn.conv2.weight", "feat.conv1.weight"):
+        e = grad_err(dict(model.named_parameters())[nm].grad.detach().cpu().numpy(), gG0[nm])
+        print(f"end to end {nm}: max {e[0]:.2e} l2 {e[1]:.2e}")
+    lr, gG, gD, _ = onp.adv_ft_grads(*args, am=am, acts=acts)
     for i, k in enumerate(("loss_cls", "loss_adv", "loss_D_gt", "loss_D_nogt")):
         assert abs(losses[i] - lr[k]) < 1e-4, (k, losses[i], lr[k])
         assert abs(lr[k] - ref_l[k]) < 1e-4, k
-    tol = (1e-4, 1e-5) if strict else (1e-3, 1e-4)
+    tol = (1e-4, 1e-5)
     bad = []
     for tag, mod, ref in (("G", model, gG), ("D", model_D, gD)):
         for nm, p in mod.named_parameters():
@@ -171,3 +183,24 @@ def test_ft_step_matches_autograd_body():
             if not (e[0] <= 1e-4 and e[1] <= 1e-5):
                 bad.append((n, e))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("K,O,act", [(3, 64, 1), (64, 64, 1), (64, 128, 1), (64, 64, 0)])
+def test_deferred_weight_gradients_are_bitwise_the_immediate_ones(K, O, act):
+    """pw_bwd_weight(defer=...) + ONE pw_wgrad_finish over several gradients
+    (the FT step's backward) equals the per-gradient launches bitwise."""
+    from adversarial_learning_on_pointclouds_amd import ops
+    rng = np.random.default_rng(K * 7 + O)
+    M = 4096
+    # the same three (dy, y, x) both ways
+    data = [(rng.normal(size=(M, O)).astype(np.float32), np.maximum(rng.normal(size=(M, O)), 0)
+             .astype(np.float32), rng.normal(size=(M, K)).astype(np.float32)) for _ in range(3)]
+    imm = [ops.pw_bwd_weight(_t(dy), _t(y), act, _t(x)) for dy, y, x in data]
+    jobs = []
+    dws = [torch.empty(O, K, device=DEV) for _ in data]
+    dbs = [torch.empty(O, device=DEV) for _ in data]
+    for (dy, y, x), dw, db in zip(data, dws, dbs):
+        ops.pw_bwd_weight(_t(dy), _t(y), act, _t(x), dw_out=dw, db_out=db, defer=jobs)
+    ops.pw_wgrad_finish(jobs)
+    for (dw0, db0), dw, db in zip(imm, dws, dbs):
+        assert torch.equal(dw0.reshape(O, K), dw) and torch.equal(db0.reshape(O), db)

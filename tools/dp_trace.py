@@ -1,6 +1,6 @@
 """One data-parallel form of the adversarial iteration on a one-rank RCCL
 group, replayed K times for a kernel trace (bench.py --config dp1 alternates
-the forms; a trace needs one): plain | dp4 | dp1g (see bench.bench_dp1).
+the forms; a trace needs one): plain | dp4 | dp1g | dp2 | dp2g (see bench.bench_dp1).
 
     rocprofv3 --kernel-trace ... -- python tools/dp_trace.py dp4 [K]
 """
@@ -31,12 +31,14 @@ def main():
     B, N = bench.B, bench.N
     step = AdvTrainStep(model, model_D, B, N, seed=1234, device=dev)
     runner = DataParallelAdvStep(step, overlap=True)
+    flat = DataParallelAdvStep(step, broadcast_params=False, overlap=False)
     rng = np.random.default_rng(1000)
     p = (torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
          torch.from_numpy(rng.integers(0, 40, B)).to(dev),
          torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev))
     g = {"plain": lambda: step.capture_on(*p), "dp4": lambda: runner.capture(*p),
-         "dp1g": lambda: runner.capture_single(*p)}[form]()
+         "dp1g": lambda: runner.capture_single(*p), "dp2": lambda: flat.capture(*p),
+         "dp2g": lambda: flat.capture_single(*p)}[form]()
     for _ in range(K):
         g.replay()
     torch.cuda.synchronize()
