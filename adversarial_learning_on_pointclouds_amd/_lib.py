@@ -140,7 +140,7 @@ SIGNATURES = {
     "pcadv_pw_bwd_weight": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _sz,
                                  _vp]),
     "pcadv_pw_wgrad_finish": (_i, [ctypes.POINTER(PwWgradJob), _i, _vp]),
-    "pcadv_conv_max_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "pcadv_conv_max_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _i, _vp]),
     "pcadv_tnet_reg_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_tnet_reg_bwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_gemm": (_i, [_vp, _i64, _i, _vp, _i64, _i, _vp, _i64, _i, _i, _i, _vp, _vp, _i, _i, _i,

@@ -49,7 +49,7 @@ size_t pw_bwd_weight_workspace_bytes(int M, int O, int K);
 int launch_pw_bwd_weight(const float*, const float*, int, const float*, int, int, int, int, int,
                          float*, float*, void*, size_t, hipStream_t);
 int launch_convmax_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
-                       const float*, int, float*, float*, float*, hipStream_t);
+                       const float*, int, float*, float*, float*, hipStream_t, int);
 int launch_tnet_reg(const float*, int, int, float*, float*, const float*, float*, hipStream_t);
 int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, const float*,
                  float*, float*, int64_t, float, const int32_t*, int, float, float, float,
@@ -628,8 +628,9 @@ int pcadv_pw_wgrad_finish(const pcadv_pw_wgrad_job* jobs, int njobs, hipStream_t
 
 int pcadv_conv_max_bwd(const float* dgmax, const int32_t* gidx, const float* gmax_relu,
                        const float* x, int C, int N, int K, const float* w, int O, float* dw,
-                       float* db, float* dx, hipStream_t stream) {
-  return launch_convmax_bwd(dgmax, gidx, gmax_relu, x, C, N, K, w, O, dw, db, dx, stream);
+                       float* db, float* dx, int dx_relu, hipStream_t stream) {
+  return launch_convmax_bwd(dgmax, gidx, gmax_relu, x, C, N, K, w, O, dw, db, dx, stream,
+                            dx_relu);
 }
 
 int pcadv_tnet_reg_fwd(const float* T, int B, int k, float* norms, float* reg,

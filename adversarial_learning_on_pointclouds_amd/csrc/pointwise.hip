@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(CMB_T)
 k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
               const float* __restrict__ gmax, const float* __restrict__ x, int C, int N, int K,
               const float* __restrict__ w, int O, float* __restrict__ dw, float* __restrict__ db,
-              float* __restrict__ dx, int nchunk) {
+              float* __restrict__ dx, int nchunk, int dx_relu) {
   __shared__ CmbLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nxb = dx ? C * nchunk : 0;
@@ -591,6 +591,13 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   if (r1 <= r0) return;
   const int j1 = L.roff[r1 - 1] + L.rcnt[r1 - 1];
   float* drow = dx + ((size_t)c * N + p0) * K + k;
+  // dx_relu: dx stored as the layer below's dz = dx * [x > 0] (x = relu(z) is
+  // this conv's input), so its consumers read no activations for the mask
+  const float* xrow = x + ((size_t)c * N + p0) * K + k;
+  auto put = [&](int rr, float v) {
+    if (dx_relu && v != 0.f && !(xrow[(size_t)rr * K] > 0.f)) v = 0.f;
+    drow[(size_t)rr * K] = v;
+  };
   int row = r0, rend = L.roff[r0] + L.rcnt[r0];
   float acc = 0.f;
   for (int j = L.roff[r0]; j < j1; j += HD) {
@@ -602,7 +609,7 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     for (int u = 0; u < HD; ++u) {
       if (j + u < j1) {
         while (j + u >= rend) {  // row done: store it, move to the next
-          drow[(size_t)row * K] = acc;
+          put(row, acc);
           acc = 0.f;
           ++row;
           rend = L.roff[row] + L.rcnt[row];
@@ -612,7 +619,7 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     }
   }
   for (; row < r1; ++row) {  // the last row with hits, then the rows after it
-    drow[(size_t)row * K] = acc;
+    put(row, acc);
     acc = 0.f;
   }
 }
@@ -846,13 +853,13 @@ int launch_pw_wgrad_finish(const pcadv_pw_wgrad_job* jobs, int njobs, hipStream_
 
 int launch_convmax_bwd(const float* dg, const int32_t* gidx, const float* gmax, const float* x,
                        int C, int N, int K, const float* w, int O, float* dw, float* db,
-                       float* dx, hipStream_t s) {
+                       float* dx, hipStream_t s, int dx_relu) {
   PC_REQUIRE(C > 0 && N > 0 && K > 0 && K <= 128 && O > 0 && O <= CMB_MAXO && dw,
              "convmax_bwd: unsupported shape C=%d N=%d K=%d O=%d", C, N, K, O);
   const int nchunk = (N + CMB_PCH - 1) / CMB_PCH;
   const int nxb = dx ? C * nchunk : 0;
   hipLaunchKernelGGL(k_convmax_bwd, dim3(nxb + (O + 7) / 8), dim3(CMB_T), 0, s, dg, gidx, gmax, x,
-                     C, N, K, w, O, dw, db, dx, nchunk);
+                     C, N, K, w, O, dw, db, dx, nchunk, dx_relu);
   PC_HIP_CHECK_LAUNCH("k_convmax_bwd");
   return PCADV_OK;
 }

@@ -8,13 +8,17 @@ buffer (811 240 + 238 785 fp32 = 4.2 MB) between backward and the replicated
 Adam updates.  With equal shards this equals the single-process step on the
 global batch, since CE/BCE are batch means (mean of per-rank means).
 
-The buffer goes in two buckets, overlapped with backward: the head and
-discriminator gradients (3.6 MB, final before the feature backward) are
-all-reduced on RCCL's stream while the feature backward runs (step part 2);
-the generator's conv1..conv4 gradients (0.58 MB) follow it, and while that
-small all-reduce is in flight the parameters of the first bucket take their
-Adam update (Adam is elementwise: the split update equals the whole one
-bitwise), so only conv1..conv4's update waits for the last collective.
+By default (round 6) the iteration is the whole step without Adam, ONE
+all-reduce of the buffer, then both Adams, and over RCCL the three are
+captured as ONE HIP graph (capture_single).  The round-5 default - two
+buckets overlapped with the backward (the head and discriminator gradients,
+3.6 MB, all-reduced on RCCL's stream while the feature backward runs; the
+conv1..conv4 bucket, 0.58 MB, beside the first bucket's Adam) - stays
+available as overlap=True: on a one-rank RCCL group it cost 62 us per
+iteration over the plain step against 11 us for the captured single
+all-reduce, and its kernel trace shows the feature backward waiting for the
+RCCL kernel, so the overlap it was built for does not happen (bench.py
+--config dp1).
 """
 from __future__ import annotations
 
@@ -53,8 +57,8 @@ class DataParallelAdvStep:
     SAME masks for its local rows unless the seeds differ)."""
 
     def __init__(self, step, group=None, broadcast_params=True, overlap=None, global_rng=True):
-        """overlap: bucket the all-reduce around the feature backward (default:
-        when the step supports parts and the backend is RCCL)."""
+        """overlap=True: bucket the all-reduce around the feature backward (the
+        round-5 form; needs a step with parts); default: one all-reduce."""
         self.step, self.group = step, group
         self.overlap = overlap
         if broadcast_params:  # identical initial weights on every rank
@@ -70,9 +74,7 @@ class DataParallelAdvStep:
             step.seed = int(seed.item())
 
     def _split(self):
-        if self.overlap is not None:
-            return bool(self.overlap)
-        return getattr(self.step, "supports_parts", False) and dist.get_backend(self.group) == "nccl"
+        return bool(self.overlap) and getattr(self.step, "supports_parts", False)
 
     def __call__(self, pts_gt, labels, pts_nogt, masks=None, soft=None, semi=False):
         # semi: each rank's pseudo-label CE is the mean over its own kept clouds,
@@ -96,6 +98,14 @@ class DataParallelAdvStep:
             _avg_(s.grad_flat, self.group)
         s.adam()
         return s.losses
+
+    def graphed(self, pts_gt, labels, pts_nogt):
+        """The iteration over resident buffers as replayable graphs: ONE graph
+        with the collectives captured over RCCL (capture_single), graphs around
+        eager collectives otherwise (gloo cannot be captured)."""
+        if dist.get_backend(self.group) == "nccl":
+            return self.capture_single(pts_gt, labels, pts_nogt)
+        return self.capture(pts_gt, labels, pts_nogt)
 
     def capture(self, pts_gt, labels, pts_nogt):
         """HIP graphs for the compute halves around the (eager) all-reduce."""

@@ -145,9 +145,12 @@ def _out(t, name, like_shape, dev):
     return t
 
 
-def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True, dw_out=None, db_out=None):
+def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True, dw_out=None, db_out=None,
+                 dx_relu=False):
     """Backward of conv_max_fwd: (dx (C, N, K) or None, dw like w, db (O,));
-    dw_out / db_out: write the weight gradients there instead."""
+    dw_out / db_out: write the weight gradients there instead; dx_relu: x is a
+    ReLU output and dx is returned as dx * [x > 0] (the pre-activation gradient
+    of the layer below)."""
     lib = _lib.load()
     _req(x, "x")
     C, N, K = x.shape
@@ -161,7 +164,8 @@ def conv_max_bwd(dgmax, gidx, x, w, gmax_relu=None, need_dx=True, dw_out=None, d
     dw = _out(dw_out, "dw", tuple(w.shape), x.device)
     db = _out(db_out, "db", (O,), x.device)
     check(lib.pcadv_conv_max_bwd(ptr(dgmax), ptr(gidx), ptr(gmax_relu), ptr(x), C, N, K, ptr(wm),
-                                 O, ptr(dw), ptr(db), ptr(dx), stream_ptr()), "pcadv_conv_max_bwd")
+                                 O, ptr(dw), ptr(db), ptr(dx), int(bool(dx_relu)), stream_ptr()),
+          "pcadv_conv_max_bwd")
     return dx, dw, db
 
 

@@ -582,11 +582,14 @@ class AdvFtTrainStep(AdvTrainStep):
         # ---- the extractor's backward (the five point-wise weight gradients'
         #      slab sums deferred to one launch at the end) -----------------------
         jobs = []
-        dx3, _, _ = ops.conv_max_bwd(dgmax, gidx, x3, P["feat.conv4.weight"],
-                                     dw_out=Gr["feat.conv4.weight"], db_out=Gr["feat.conv4.bias"])
+        # dz3 = dx3 [x3 > 0] straight from the max-pool backward (its dx rows
+        # already carry conv3's ReLU mask: conv3's backward reads no x3)
+        dz3, _, _ = ops.conv_max_bwd(dgmax, gidx, x3, P["feat.conv4.weight"],
+                                     dw_out=Gr["feat.conv4.weight"], db_out=Gr["feat.conv4.bias"],
+                                     dx_relu=True)
         w3 = _mat(P["feat.conv3.weight"])
-        dx2t = ops.pw_bwd_data(dx3, x3, RELU, w3, 64)
-        ops.pw_bwd_weight(dx3, x3, RELU, x2t, dw_out=Gr["feat.conv3.weight"],
+        dx2t = ops.pw_bwd_data(dz3, None, NONE, w3, 64)
+        ops.pw_bwd_weight(dz3, None, NONE, x2t, dw_out=Gr["feat.conv3.weight"],
                           db_out=Gr["feat.conv3.bias"], defer=jobs)
         # x2t = x2 T: dT = x2^T dx2t per cloud, dx2 = dx2t T^T
         dT, _ = ops.pw_bwd_weight(dx2t, None, NONE, x2, rows_per_group=N, kmajor=True,
@@ -600,10 +603,11 @@ class AdvFtTrainStep(AdvTrainStep):
                                    dw_out=Gr[s + "fc2.weight"], db_out=Gr[s + "fc2.bias"])
         dgs, _, _ = ops.linear_bwd(df1, f1, RELU, None, 0.0, gs, P[s + "fc1.weight"],
                                    dw_out=Gr[s + "fc1.weight"], db_out=Gr[s + "fc1.bias"])
-        dh2, _, _ = ops.conv_max_bwd(dgs, gis, h2, P[s + "conv3.weight"], gmax_relu=gs,
-                                     dw_out=Gr[s + "conv3.weight"], db_out=Gr[s + "conv3.bias"])
-        dh1 = ops.pw_bwd_data(dh2, h2, RELU, _mat(P[s + "conv2.weight"]), 64)
-        ops.pw_bwd_weight(dh2, h2, RELU, h1, dw_out=Gr[s + "conv2.weight"],
+        dzh2, _, _ = ops.conv_max_bwd(dgs, gis, h2, P[s + "conv3.weight"], gmax_relu=gs,
+                                      dw_out=Gr[s + "conv3.weight"], db_out=Gr[s + "conv3.bias"],
+                                      dx_relu=True)
+        dh1 = ops.pw_bwd_data(dzh2, None, NONE, _mat(P[s + "conv2.weight"]), 64)
+        ops.pw_bwd_weight(dzh2, None, NONE, h1, dw_out=Gr[s + "conv2.weight"],
                           db_out=Gr[s + "conv2.bias"], defer=jobs)
         ops.pw_bwd_data(dh1, h1, RELU, _mat(P[s + "conv1.weight"]), 64, out=dx2)
         ops.pw_bwd_weight(dh1, h1, RELU, x2, dw_out=Gr[s + "conv1.weight"],

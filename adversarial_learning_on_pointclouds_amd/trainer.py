@@ -321,36 +321,49 @@ class _GraphedIteration:
 class _DPIteration(_GraphedIteration):
     """_GraphedIteration for a data-parallel rank (DeviceCloudLoaders sharded
     over the process group, AdvTrainStep keyed to this rank's global rows):
-    the iteration runs as four HIP graphs around the eager RCCL all-reduces of
-    DataParallelAdvStep (bucketed, overlapped with the feature backward):
-    [gathers + step part 1] | all-reduce(AVG) of the early gradient bucket and
-    of the loss vector | [step part 2] | all-reduce of the late bucket beside
-    [Adam of the early bucket's parameters] | [Adam of conv1..conv4 + the
-    iteration epilogue].  With equal shards the replicas take exactly the
-    one-process step on the global batch (CE / BCE are batch means; the
-    logged losses are the ranks' average, i.e. the global batch's)."""
+    [gathers + the whole step without Adam] | all-reduce(AVG) of the 4.2 MB
+    G + D gradient buffer and of the loss vector | [both Adams + the iteration
+    epilogue].  Over RCCL the collectives are captured with the rest: the
+    iteration is ONE HIP graph (measured on a one-rank RCCL group, bench.py
+    --config dp1: 11 us per iteration over the plain step, against 62 us for
+    the round-5 form - four graphs around bucketed, overlapped host-issued
+    all-reduces, whose overlap never materialised: the trace shows the
+    feature backward waiting for the RCCL kernel).  Over gloo
+    (CPU collectives, not capturable) two graphs around eager all-reduces.
+    With equal shards the replicas take exactly the one-process step on the
+    global batch (CE / BCE are batch means; the logged losses are the ranks'
+    average, i.e. the global batch's)."""
 
     def __init__(self, step, loaders, ring, group=None, optimizers=()):
         super().__init__(step, loaders, ring, optimizers)
         self.group = group
+        import torch.distributed as dist
+        self.captured = dist.get_backend(group) == "nccl"
 
     def _part(self, k, semi):
         st, L = self.step, self.L
         if k == 1:
             if hasattr(st, "folded_gather"):
                 with st.folded_gather(self._gather_jobs()):
-                    st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi,
-                       part=1)
+                    st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi)
             else:
                 self._gathers()
-                st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=1)
-        elif k == 2:
-            st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi, part=2)
-        elif k == 3:
-            st.adam(part=1)
+                st(self.pts[0], self.lab[:, 0], self.pts[1], apply_adam=False, semi=semi)
         else:
-            st.adam(part=2)
+            st.adam()
             self.ring.write(st.losses, self.counters, 2 * L)
+
+    def _average(self):
+        from .distributed import _avg_async
+        done = _avg_async(self.step.grad_flat, self.group)
+        done_loss = _avg_async(self.step.losses, self.group)
+        done()
+        done_loss()
+
+    def _whole(self, semi):
+        self._part(1, semi)
+        self._average()
+        self._part(2, semi)
 
     def _graph(self, semi):
         gs = self.graphs.get(semi)
@@ -360,16 +373,22 @@ class _DPIteration(_GraphedIteration):
             cur = torch.cuda.current_stream()
             side = torch.cuda.Stream(device=self.step.device)
             side.wait_stream(cur)
-            with torch.cuda.stream(side):  # warm-up outside the capture (no collectives)
-                for k in (1, 2, 3, 4):
-                    self._part(k, semi)
+            with torch.cuda.stream(side):  # warm-up outside the capture (every rank alike)
+                self._whole(semi)
             cur.wait_stream(side)
-            gs = []
-            for k in (1, 2, 3, 4):
+            torch.cuda.synchronize()
+            if self.captured:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._part(k, semi)
-                gs.append(g)
+                    self._whole(semi)
+                gs = [g]
+            else:
+                gs = []
+                for k in (1, 2):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self._part(k, semi)
+                    gs.append(g)
             torch.cuda.synchronize()
             with torch.no_grad():
                 for dst, src in zip(state, saved):
@@ -378,21 +397,15 @@ class _DPIteration(_GraphedIteration):
         return gs
 
     def replay(self, semi=False):
-        from .distributed import _avg_async
         self._check_hyper()
-        g1, g2, g3, g4 = self._graph(semi)
-        st = self.step
-        g1.replay()
-        done = _avg_async(st.early_grads(), self.group)
-        done_loss = _avg_async(st.losses, self.group)
-        g2.replay()
-        done()
-        done_late = _avg_async(st.late_grads(), self.group)
-        g3.replay()  # the early bucket's Adam beside the late all-reduce
-        done_late()
-        done_loss()
-        g4.replay()
-        return st.losses
+        gs = self._graph(semi)
+        if len(gs) == 1:
+            gs[0].replay()
+        else:
+            gs[0].replay()
+            self._average()
+            gs[1].replay()
+        return self.step.losses
 
 
 class _SegGraphedIteration(_GraphedIteration):
@@ -686,8 +699,8 @@ def _adv_loop(trainloader_gt, trainloader_nogt, trainloader_gt_iter, targetloade
     max_test_accu = float("-inf")
     max_train_epoch = 0
     fused = _fusable(model, model_D, optimizer, optimizer_D, gan_loss, cls_loss, args)
-    if semi_loss is not None:
-        fused = fused and _semi_fusable(semi_loss)
+    if semi_loss is not None and not _semi_fusable(semi_loss):
+        fused = False
     # ImagePool(pool_size > 0): the fused step's G half stands, D's gradient is
     # recomputed on the pools' outputs (_pooled_d_grads); the pools draw from
     # the host's `random`, so these iterations are not graphed

@@ -1134,8 +1134,8 @@ def main():
     adv_prec = args.precision or "fp32"
     # DataParallelAdvStep keys the device draws by global rows (rank 0's seed)
     step = AdvTrainStep(model, model_D, B, N, seed=1234, device=dev, precision=adv_prec)
-    # PCADV_BENCH_OVERLAP=1 forces the bucketed all-reduce (the RCCL default) in a gloo rehearsal
-    overlap = {"1": True, "0": False}.get(os.environ.get("PCADV_BENCH_OVERLAP", ""))
+    # PCADV_BENCH_OVERLAP=1 selects the round-5 bucketed, overlapped all-reduce
+    overlap = os.environ.get("PCADV_BENCH_OVERLAP", "") == "1"
     runner = DataParallelAdvStep(step, overlap=overlap) if dist is not None else None
 
     # resident synthetic inputs: rank-specific shards of the global batch
@@ -1150,8 +1150,8 @@ def main():
     G = 1
     seq = None
     if use_graph:
-        if runner is not None:
-            graphs = [runner.capture(*pool[k]) for k in range(POOL)]
+        if runner is not None:  # over RCCL one graph per iteration, all-reduce captured
+            graphs = [runner.graphed(*pool[k]) for k in range(POOL)]
         else:
             graphs = [step.capture_on(*pool[k]) for k in range(POOL)]
             G = max(1, min(args.graph_steps, POOL))

@@ -193,10 +193,13 @@ int pcadv_pw_wgrad_finish(const pcadv_pw_wgrad_job* jobs, int njobs, hipStream_t
 /* Backward of pcadv_conv_max_fwd: each channel's gradient goes to its argmax
  * point (times [gmax > 0] when gmax_relu is given: the ReLU before the max of
  * the T-Nets, pointnet.py:30-31,63-64).  dw [O][K], db [O] (may be NULL), dx
- * [C][N][K] (NULL: skipped; rows of points without hits are written as 0). */
+ * [C][N][K] (NULL: skipped; rows of points without hits are written as 0).
+ * dx_relu (ABI 8): x is the ReLU output of the layer below and dx is stored
+ * as that layer's pre-activation gradient, dx * [x > 0], so the layer's
+ * backward reads no activations for its mask. */
 int pcadv_conv_max_bwd(const float* dgmax, const int32_t* gidx, const float* gmax_relu,
                        const float* x, int C, int N, int K, const float* w, int O, float* dw,
-                       float* db, float* dx, hipStream_t stream);
+                       float* db, float* dx, int dx_relu, hipStream_t stream);
 
 /* feature_transform_regularizer (pointnet.py:345-353): norms[b] =
  * ||T_b T_b^T - I||_F and *reg = mean_b norms[b]; backward dT = *grad_reg *

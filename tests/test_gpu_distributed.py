@@ -245,21 +245,21 @@ def _rccl_worker(rank, port, out_dir):
         from adversarial_learning_on_pointclouds_amd.distributed import DataParallelAdvStep
         from adversarial_learning_on_pointclouds_amd.step import AdvTrainStep
         res = {}
-        for mode in ("plain", "dp_eager", "dp_graph", "dp_single"):
+        for mode in ("plain", "eager", "graphs", "single", "b_eager", "b_graphs", "b_single"):
             m, d = _models(dev)
             st = AdvTrainStep(m, d, B, N, seed=7, device=dev)
             if mode == "plain":
                 for k in range(3):
                     st(*_batch(dev, 60 + k))
             else:
-                dp = DataParallelAdvStep(st)  # RCCL: bucketed + overlapped by default
-                assert dp._split()
-                if mode == "dp_eager":
+                dp = DataParallelAdvStep(st, overlap=mode.startswith("b_"))
+                assert dp._split() == mode.startswith("b_")
+                if mode.endswith("eager"):
                     for k in range(3):
                         dp(*_batch(dev, 60 + k))
                 else:
                     bufs = _batch(dev, 60)
-                    graph = dp.capture(*bufs) if mode == "dp_graph" else dp.capture_single(*bufs)
+                    graph = dp.capture(*bufs) if mode.endswith("graphs") else dp.capture_single(*bufs)
                     for k in range(3):
                         for dst, src in zip(bufs, _batch(dev, 60 + k)):
                             dst.copy_(src)
@@ -272,20 +272,20 @@ def _rccl_worker(rank, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_rccl_bucketed_overlap_path_single_rank(tmp_path):
-    """The RCCL code path of DataParallelAdvStep (ReduceOp.AVG with async_op on
-    RCCL's stream, bucketed around the feature backward, graphs replayed
-    between the collectives) executed on a one-rank RCCL group: with one rank
-    the average is the identity, so three steps must equal the plain step
-    bitwise, eager and captured.  Checks the stream ordering of the overlap
-    (a missed wait shows as a race on the gradient buffer)."""
+def test_rccl_data_parallel_paths_single_rank(tmp_path):
+    """Every RCCL code path of DataParallelAdvStep on a one-rank RCCL group,
+    where the average is the identity, so three steps must equal the plain
+    step bitwise: the default single all-reduce (eager; as graphs around the
+    collective; as ONE graph with the collective captured, the bench's and the
+    trainer's form) and the round-5 bucketed, overlapped all-reduce
+    (b_*: ReduceOp.AVG with async_op on RCCL's stream, the two buckets around
+    the feature backward).  Checks the stream ordering of every form (a missed
+    wait shows as a race on the gradient buffer)."""
     import torch.multiprocessing as mp
     mp.spawn(_rccl_worker, args=(_free_port(), str(tmp_path)), nprocs=1, join=True)
     r = dict(np.load(tmp_path / "rccl.npz"))
-    assert np.array_equal(r["plain"], r["dp_eager"])
-    assert np.array_equal(r["plain"], r["dp_graph"])
-    # the whole iteration as one graph with both all-reduces captured
-    assert np.array_equal(r["plain"], r["dp_single"])
+    for mode in ("eager", "graphs", "single", "b_eager", "b_graphs", "b_single"):
+        assert np.array_equal(r["plain"], r[mode]), mode
 
 
 # ---------------------------------------------------------------------------
