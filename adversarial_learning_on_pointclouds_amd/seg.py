@@ -38,6 +38,7 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import check, stream_ptr
+from .step import _step_tensor, set_optimizer_step
 
 __all__ = ["PointNetSeg", "SegTrainStep", "seg_cross_entropy", "seg_forward", "seg_backward"]
 
@@ -581,7 +582,7 @@ class SegTrainStep:
         if optimizer is not None:
             for (name, p), o in zip(named, offs):
                 k = p.numel()
-                optimizer.state[p] = {"step": torch.tensor(float(t0)),
+                optimizer.state[p] = {"step": _step_tensor(optimizer, p, t0),
                                       "exp_avg": self.m[o:o + k].view_as(p),
                                       "exp_avg_sq": self.v[o:o + k].view_as(p)}
         self.step_count = torch.full((1,), t0, device=dev, dtype=torch.int32)
@@ -660,7 +661,5 @@ class SegTrainStep:
                 float(g["eps"])
 
     def sync_optimizer_state(self):
-        t = float(self.step_count.item())
         if self.optimizer is not None:
-            for st in self.optimizer.state.values():
-                st["step"] = torch.tensor(t)
+            set_optimizer_step(self.optimizer, float(self.step_count.item()))

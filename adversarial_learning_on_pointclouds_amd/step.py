@@ -76,6 +76,27 @@ def _adopt_adam_state(optimizer, module, m_flat, v_flat, layout):
     return steps
 
 
+def _step_tensor(optimizer, p, t):
+    """'step' as torch.optim.Adam keeps it for p: an f32 scalar on p's device
+    when its group is capturable or fused (the step then runs on the device,
+    and Adam refuses a CPU count), a CPU f32 scalar otherwise."""
+    for g in optimizer.param_groups:
+        if any(q is p for q in g["params"]):
+            if g.get("capturable", False) or g.get("fused", False):
+                return torch.tensor(float(t), dtype=torch.float32, device=p.device)
+            break
+    return torch.tensor(float(t), dtype=torch.float32)
+
+
+def set_optimizer_step(optimizer, t):
+    """Every state entry's 'step' = t (the device step counter's value)."""
+    if optimizer is None:
+        return
+    for p, st in optimizer.state.items():
+        if st:
+            st["step"] = _step_tensor(optimizer, p, t)
+
+
 def _bind_adam_state(optimizer, module, m_flat, v_flat, grad_flat, layout, step_t):
     """p.grad and the optimizer's exp_avg / exp_avg_sq become views of the flat
     buffers; 'step' holds the completed-step count."""
@@ -84,7 +105,7 @@ def _bind_adam_state(optimizer, module, m_flat, v_flat, grad_flat, layout, step_
     for name, p in module.named_parameters():
         p.grad = gv[name]
         if optimizer is not None:
-            optimizer.state[p] = {"step": torch.tensor(float(step_t)),
+            optimizer.state[p] = {"step": _step_tensor(optimizer, p, step_t),
                                   "exp_avg": mv[name], "exp_avg_sq": vv[name]}
 
 
@@ -396,9 +417,7 @@ class AdvTrainStep:
         """Copy the device step counter into the torch optimizers' 'step'."""
         t = float(self.step_count.item())
         for opt in self.optimizers:
-            if opt is not None:
-                for st in opt.state.values():
-                    st["step"] = torch.tensor(t)
+            set_optimizer_step(opt, t)
 
     def after_torch_step(self):
         """After an iteration the trainer ran through autograd and the torch
@@ -816,8 +835,6 @@ class ClsTrainStep:
 
     def sync_optimizer_state(self):
         if self.optimizer is not None:
-            t = float(self.step_count.item())
-            for st in self.optimizer.state.values():
-                st["step"] = torch.tensor(t)
+            set_optimizer_step(self.optimizer, float(self.step_count.item()))
 
     after_torch_step = AdvTrainStep.after_torch_step
