@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PCADV_LIB", os.path.join(_HERE, "lib", "libpcadv.so"))
 # the layout of include/pcadv.h these signatures and AdvArgs bind (pcadv_abi_version())
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 PCADV_OK = 0
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
@@ -104,6 +104,13 @@ class PwWgradJob(ctypes.Structure):
     _fields_ = [("slabs", _vp), ("M", _i), ("O", _i), ("K", _i), ("dw", _vp), ("db", _vp)]
 
 
+class PwLayer(ctypes.Structure):
+    """Mirror of pcadv_pw_layer (include/pcadv.h)."""
+
+    _fields_ = [("w", _vp), ("b", _vp), ("y", _vp), ("O", _i), ("act", _i), ("w_kmajor", _i),
+                ("rows_per_w", _i)]
+
+
 class GatherJob(ctypes.Structure):
     """Mirror of pcadv_gather_job (include/pcadv.h)."""
 
@@ -135,6 +142,7 @@ SIGNATURES = {
     "pcadv_adam2": (_i, [_vp, _vp, _vp, _vp, _i64, _f, _vp, _vp, _vp, _vp, _i64, _f, _vp, _f, _f,
                          _f, _vp]),
     "pcadv_pw_fwd": (_i, [_vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "pcadv_pw_chain": (_i, [_vp, _i, _i, ctypes.POINTER(PwLayer), _i, _vp]),
     "pcadv_pw_bwd_data": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp]),
     "pcadv_pw_bwd_weight_workspace_bytes": (_sz, [_i, _i, _i]),
     "pcadv_pw_bwd_weight": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _sz,

@@ -43,6 +43,7 @@ int launch_linear_fwd(const float*, const float*, const float*, float*, int, int
                       int row_off_lo = 0, int row_off_hi = 0);
 int launch_pw_fwd(const float*, int, int, const float*, const float*, int, int, int, int, float*,
                   hipStream_t);
+int launch_pw_chain(const float*, int, int, const pcadv_pw_layer*, int, hipStream_t);
 int launch_pw_bwd_data(const float*, const float*, int, int, int, const float*, int, int, int,
                        float*, int, hipStream_t);
 size_t pw_bwd_weight_workspace_bytes(int M, int O, int K);
@@ -513,7 +514,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 8; }
+int pcadv_abi_version(void) { return 9; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -603,6 +604,11 @@ int pcadv_linear_fwd(const float* x, const float* w, const float* b, float* y, i
 int pcadv_pw_fwd(const float* x, int M, int K, const float* w, const float* b, int O, int act,
                  int w_kmajor, int rows_per_w, float* y, hipStream_t stream) {
   return launch_pw_fwd(x, M, K, w, b, O, act, w_kmajor, rows_per_w, y, stream);
+}
+
+int pcadv_pw_chain(const float* x, int M, int K, const pcadv_pw_layer* layers, int n,
+                   hipStream_t stream) {
+  return launch_pw_chain(x, M, K, layers, n, stream);
 }
 
 int pcadv_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,

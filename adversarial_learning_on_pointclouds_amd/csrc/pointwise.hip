@@ -130,6 +130,237 @@ k_pw_fwd3(const float* __restrict__ x, int M, WView wv, const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// forward chains: consecutive point-wise layers of a 64-row tile in ONE launch
+// (the feature-transform extractor's conv1 -> conv2 -> STNkd conv1 -> STNkd
+// conv2, and x2 T -> conv3).  Every layer's output is stored (the backward
+// reads them all) and kept in LDS as the next layer's input, so no layer
+// re-reads its input from HBM or waits out a launch boundary.  Per layer the
+// same operations in the same order as k_pw_fwd3 / k_pw_fwd (conv1's fma
+// chain; the k-permuted f32 MFMA chain, then + bias, then the activation), so
+// every output is bitwise what the per-layer launches write.  Persistent:
+// 2 workgroups per CU stride over the tiles, each keeping the shared weights'
+// fragments in registers; a per-cloud weight (rows_per_w, the transform T) is
+// re-fetched for the next tile right after its layer, in flight meanwhile.
+// ---------------------------------------------------------------------------
+// LDS row strides (floats, = 4 mod 64 banks): buffer 0 holds up to 128
+// columns, buffer 1 up to 64 (52.2 KB in all: three workgroups per CU)
+constexpr int PC_S0 = 132, PC_S1 = 68;
+constexpr int PC_GRID = 768;
+__host__ __device__ constexpr int pc_stride(int k) { return k ? PC_S1 : PC_S0; }
+
+struct PwChainLayer {
+  WView wv;
+  const float* b;
+  float* y;
+  int act;
+};
+struct PwChainArgs {
+  PwChainLayer l[PCADV_PW_CHAIN_MAX];
+};
+struct PwChainLds {
+  alignas(16) float pts[PW_ROWS * 4];
+  alignas(16) float buf0[PW_ROWS * PC_S0];
+  alignas(16) float buf1[PW_ROWS * PC_S1];
+  __device__ float* buf(int k) { return k ? buf1 : buf0; }
+};
+
+// B fragments of one K = 64 layer for this wave's 32-column tile (k_pw_fwd's
+// loads; O = 64: columns 32 (wave & 1), O = 128: columns 32 wave).  KMAJ: the
+// weight is a [K][O] matrix (coalesced 4-B loads across the lanes), else a
+// 16-B aligned [O][K] one (the launcher checks the alignment)
+template <int O, bool KMAJ>
+__device__ __forceinline__ void chain_frags(const WView& wv, int r0, int wave, int lane,
+                                            f32x4 (&bf)[8]) {
+  const int r = lane & 31, h = lane >> 5;
+  const int oc = O == 64 ? 32 * (wave & 1) : 32 * wave;
+  const float* w = wv.base(r0);
+  if constexpr (!KMAJ) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+      bf[g] = *reinterpret_cast<const f32x4*>(w + (size_t)(oc + r) * 64 + 8 * g + 4 * h);
+  } else {
+    const float* c = w + (size_t)(4 * h) * O + oc + r;
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[g][j] = c[(size_t)(8 * g + j) * O];
+  }
+}
+
+// one K = 64 layer of the tile on the f32 MFMA (k_pw_fwd's chain per output):
+// in -> out, LDS [64][SI] -> [64][SO]
+template <int O, int ACT, int SI, int SO>
+__device__ __forceinline__ void chain_mfma(const float* in, float* out, const f32x4 (&bf)[8],
+                                           float bias, int wave, int lane) {
+  const int r = lane & 31;
+  const int oc = O == 64 ? 32 * (wave & 1) : 32 * wave;
+  const int rt0 = O == 64 ? (wave >> 1) : 0;
+  constexpr int NRT = O == 64 ? 1 : 2;
+#pragma unroll
+  for (int t = 0; t < NRT; ++t) {
+    const int rt = rt0 + t;
+    f32x16 acc = {};
+    acc = mfma_rows_x_wt<64>(in + 32 * rt * SI, SI, bf, acc, lane);
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      out[(32 * rt + acc_row(e, lane)) * SO + oc + r] = act_fwd(acc[e] + bias, ACT);
+  }
+}
+
+// a layer's output tile (LDS) to HBM as 16-B row pieces
+template <int O, int S>
+__device__ __forceinline__ void chain_store(const float* src, float* __restrict__ y, int r0, int M,
+                                            int tid) {
+  constexpr int V = O / 4;
+#pragma unroll
+  for (int q = 0; q < PW_ROWS * V / PW_T; ++q) {
+    const int e = tid + PW_T * q, row = e / V, c4 = e % V;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(src + row * S + 4 * c4);
+    if (r0 + row < M) *reinterpret_cast<f32x4*>(y + (size_t)(r0 + row) * O + 4 * c4) = v;
+  }
+}
+
+// RELU: bit i set = layer i applies the ReLU (else no activation), KMAJ: bit
+// i set = layer i's weight is [K][O] (compile-time masks: no per-element
+// branches in the epilogues, one load form per weight).  Layer i
+// reads its input buffer (pts / buf[0] for i = 0, else buf[i & 1]) and writes
+// buf[(i + 1) & 1].  The K = 64 layers' B fragments alternate between two
+// register sets: layer i's set is loaded while layer i - 1 runs (the next
+// tile's first MFMA layer's during this tile's last layer).
+template <int K0, int O1, int O2, int O3, int O4, int RELU, int KMAJ>
+__global__ void __launch_bounds__(PW_T, 2)
+k_pw_chain(const float* __restrict__ x, int M, int ntiles, PwChainArgs a) {
+  constexpr int Os[5] = {K0, O1, O2, O3, O4};
+  constexpr int NL = O4 ? 4 : O3 ? 3 : O2 ? 2 : 1;
+  static_assert(K0 == 3 || K0 == 64, "chain input: 3 or 64 channels");
+  static_assert(K0 != 3 || O1 == 64, "a K = 3 first layer has 64 outputs");
+  static_assert(NL % 2 == 0, "the fragment sets alternate by layer parity");
+  static_assert(O2 == 0 || O1 == 64, "MFMA layers take K = 64");
+  static_assert(O3 == 0 || O2 == 64, "MFMA layers take K = 64");
+  static_assert(O4 == 0 || O3 == 64, "MFMA layers take K = 64");
+  static_assert(O1 <= 64 && O3 <= 64, "buffer 1 (the even layers' outputs) holds 64 columns");
+  constexpr int F = K0 == 3 ? 1 : 0;  // first MFMA layer
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  PwChainLds& L = *reinterpret_cast<PwChainLds*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31;
+  const int t0 = blockIdx.x, stride = gridDim.x;
+
+  // every kernel argument the loop reads, named once (kernarg loads up front)
+  WView wv[NL];
+  const float* bp[NL];
+  float* yp[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    wv[i] = a.l[i].wv;
+    bp[i] = a.l[i].b;
+    yp[i] = a.l[i].y;
+  }
+  float bias[NL];
+#pragma unroll
+  for (int i = F; i < NL; ++i) {
+    const int oc = Os[i + 1] == 64 ? 32 * (wave & 1) : 32 * wave;
+    bias[i] = bp[i] ? bp[i][oc + r] : 0.f;
+  }
+  float c1[4] = {0.f, 0.f, 0.f, 0.f};  // K0 = 3: conv1's w[o][0..2], b[o] of column tid & 63
+  if constexpr (K0 == 3) {
+    const int o = tid & 63;
+    const float* w = wv[0].base(t0 * PW_ROWS);
+    c1[0] = wv[0].get(w, o, 0);
+    c1[1] = wv[0].get(w, o, 1);
+    c1[2] = wv[0].get(w, o, 2);
+    c1[3] = bp[0] ? bp[0][o] : 0.f;
+  }
+  f32x4 fs[2][8];  // the two fragment sets
+  constexpr bool kLastShares = ((NL - 1) & 1) == (F & 1);
+  // layer i's fragments (i a constant once the layer loop is unrolled)
+  auto frags = [&](int i, int rr, f32x4 (&bf)[8]) __attribute__((always_inline)) {
+    const bool km = (KMAJ >> i) & 1;
+    if (Os[i + 1] == 64 && km) chain_frags<64, true>(wv[i], rr, wave, lane, bf);
+    if (Os[i + 1] == 64 && !km) chain_frags<64, false>(wv[i], rr, wave, lane, bf);
+    if (Os[i + 1] == 128 && km) chain_frags<128, true>(wv[i], rr, wave, lane, bf);
+    if (Os[i + 1] == 128 && !km) chain_frags<128, false>(wv[i], rr, wave, lane, bf);
+  };
+  frags(F, t0 * PW_ROWS, fs[F & 1]);
+
+  // input tile: K0 = 3, thread < 192 holds one coordinate; K0 = 64, 16 floats
+  // per thread as four 16-B pieces; rows past M read zeros
+  f32x4 xin[K0 == 64 ? 4 : 1];
+  auto load_in = [&](int tile) __attribute__((always_inline)) {
+    const int r0 = tile * PW_ROWS;
+    if constexpr (K0 == 3) {
+      const int row = tid / 3;
+      xin[0][0] = (tid < PW_ROWS * 3 && r0 + row < M) ? x[(size_t)r0 * 3 + tid] : 0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = tid + PW_T * j, row = e >> 4, c4 = e & 15;
+        xin[j] = r0 + row < M ? *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + row) * 64 + 4 * c4)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  load_in(t0);
+  for (int tile = t0; tile < ntiles; tile += stride) {
+    const int r0 = tile * PW_ROWS, nt = tile + stride;
+    if constexpr (K0 == 3) {
+      if (tid < PW_ROWS * 3) L.pts[(tid / 3) * 4 + tid % 3] = xin[0][0];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = tid + PW_T * j, row = e >> 4, c4 = e & 15;
+        *reinterpret_cast<f32x4*>(&L.buf0[row * PC_S0 + 4 * c4]) = xin[j];
+      }
+    }
+    __syncthreads();
+    if (nt < ntiles) load_in(nt);  // in flight during this tile's layers
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      // the next MFMA layer's fragments (or the next tile's first) into the
+      // other set: in flight while this layer runs
+      if (i + 1 < NL) {
+        if (i + 1 >= F) frags(i + 1, r0, fs[(i + 1) & 1]);
+      } else if (nt < ntiles && !kLastShares) {
+        frags(F, nt * PW_ROWS, fs[F & 1]);
+      }
+      float* out = L.buf((i + 1) & 1);
+      const int so = pc_stride((i + 1) & 1), si = pc_stride(i == 0 ? 0 : i & 1);
+      if (K0 == 3 && i == 0) {  // k_pw_fwd3's fma chain: thread = (column, 16 rows)
+        const int o = tid & 63, rg = tid >> 6;
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+          const int row = 16 * rg + q;
+          const float* p = &L.pts[row * 4];
+          const float v = fmaf(c1[2], p[2], fmaf(c1[1], p[1], fmaf(c1[0], p[0], c1[3])));
+          out[row * so + o] = act_fwd(v, (RELU & 1) ? ACT_RELU : ACT_NONE);
+        }
+      } else {
+        const float* in = i == 0 ? L.buf0 : L.buf(i & 1);
+        const int O = Os[i + 1];
+        const bool relu = (RELU >> i) & 1;
+        // buffer 1 (64 columns) is written by the even layers, read by the odd ones
+        constexpr int A = ACT_RELU, N_ = ACT_NONE;
+        const bool odd = i & 1;
+        if (O == 64 && relu && !odd) chain_mfma<64, A, PC_S0, PC_S1>(in, out, fs[0], bias[i], wave, lane);
+        if (O == 64 && !relu && !odd) chain_mfma<64, N_, PC_S0, PC_S1>(in, out, fs[0], bias[i], wave, lane);
+        if (O == 64 && relu && odd) chain_mfma<64, A, PC_S1, PC_S0>(in, out, fs[1], bias[i], wave, lane);
+        if (O == 64 && !relu && odd) chain_mfma<64, N_, PC_S1, PC_S0>(in, out, fs[1], bias[i], wave, lane);
+        if (O == 128 && relu && odd) chain_mfma<128, A, PC_S1, PC_S0>(in, out, fs[1], bias[i], wave, lane);
+        if (O == 128 && !relu && odd) chain_mfma<128, N_, PC_S1, PC_S0>(in, out, fs[1], bias[i], wave, lane);
+      }
+      // the last layer shares its set with the next tile's first MFMA layer:
+      // that load goes out once this layer's MFMAs have read the set
+      if (kLastShares && i + 1 == NL && nt < ntiles) frags(F, nt * PW_ROWS, fs[F & 1]);
+      __syncthreads();
+      if (Os[i + 1] == 64 && (i & 1)) chain_store<64, PC_S0>(out, yp[i], r0, M, tid);
+      if (Os[i + 1] == 64 && !(i & 1)) chain_store<64, PC_S1>(out, yp[i], r0, M, tid);
+      if (Os[i + 1] == 128) chain_store<128, PC_S0>(out, yp[i], r0, M, tid);
+    }
+    __syncthreads();  // the last copy-out and the input buffer's readers are done
+  }
+}
+
+// ---------------------------------------------------------------------------
 // backward, input gradient: dx[m][k] (+)= sum_o dz[m][o] w[o][k], dz = dy act'(y)
 // ---------------------------------------------------------------------------
 template <int R, int ACT>
@@ -751,6 +982,62 @@ int launch_pw_fwd(const float* x, int M, int K, const float* w, const float* b, 
 #undef PW_CASE
   PC_HIP_CHECK_LAUNCH("k_pw_fwd");
   return PCADV_OK;
+}
+
+// the chain shapes instantiated: the feature-transform extractor's two runs
+template <int K0, int O1, int O2, int O3, int O4, int RELU, int KMAJ>
+static int launch_chain(const float* x, int M, const PwChainArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_pw_chain<K0, O1, O2, O3, O4, RELU, KMAJ>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(PwChainLds)) != hipSuccess) {
+      set_error("pw_chain: cannot reserve %zu bytes of LDS", sizeof(PwChainLds));
+      return PCADV_EHIP;
+    }
+    attr = true;
+  }
+  const int ntiles = (M + PW_ROWS - 1) / PW_ROWS;
+  hipLaunchKernelGGL((k_pw_chain<K0, O1, O2, O3, O4, RELU, KMAJ>), dim3(ntiles < PC_GRID ? ntiles : PC_GRID), dim3(PW_T),
+                     sizeof(PwChainLds), s, x, M, ntiles, a);
+  PC_HIP_CHECK_LAUNCH("k_pw_chain");
+  return PCADV_OK;
+}
+
+int launch_pw_chain(const float* x, int M, int K, const pcadv_pw_layer* layers, int n,
+                    hipStream_t s) {
+  PC_REQUIRE(x && layers && M > 0 && n >= 1 && n <= PCADV_PW_CHAIN_MAX,
+             "pw_chain: bad arguments (M=%d, %d layers)", M, n);
+  PwChainArgs a{};
+  int k = K;
+  int O[PCADV_PW_CHAIN_MAX] = {0, 0, 0, 0};
+  int relu = 0, kmaj = 0;
+  for (int i = 0; i < n; ++i) {
+    const pcadv_pw_layer& l = layers[i];
+    PC_REQUIRE(l.w && l.y && l.O > 0, "pw_chain: layer %d: weight, output and O are required", i);
+    PC_REQUIRE(l.act == ACT_NONE || l.act == ACT_RELU, "pw_chain: layer %d: act %d", i, l.act);
+    PC_REQUIRE(l.rows_per_w == 0 || l.rows_per_w % PW_ROWS == 0,
+               "pw_chain: layer %d: rows per weight matrix (%d) must be a multiple of %d", i,
+               l.rows_per_w, PW_ROWS);
+    a.l[i] = PwChainLayer{make_view(l.w, l.O, k, l.w_kmajor, l.rows_per_w), l.b, l.y, l.act};
+    O[i] = l.O;
+    relu |= (l.act == ACT_RELU) << i;
+    kmaj |= (l.w_kmajor != 0) << i;
+    // [O][K] weights are read as 16-B pieces (each matrix of a stack too)
+    PC_REQUIRE(l.w_kmajor || ((reinterpret_cast<uintptr_t>(l.w) & 15) == 0 &&
+                              (l.rows_per_w == 0 || (l.O * k) % 4 == 0)),
+               "pw_chain: layer %d: an [O][K] weight must be 16-byte aligned", i);
+    k = l.O;
+  }
+  if (K == 3 && n == 4 && O[0] == 64 && O[1] == 64 && O[2] == 64 && O[3] == 128 && relu == 15 &&
+      kmaj == 0)
+    return launch_chain<3, 64, 64, 64, 128, 15, 0>(x, M, a, s);
+  if (K == 64 && n == 2 && O[0] == 64 && O[1] == 128 && relu == 2 && kmaj == 1)
+    return launch_chain<64, 64, 128, 0, 0, 2, 1>(x, M, a, s);
+  set_error("pw_chain: shape K=%d -> %d layers (%d, %d, %d, %d; ReLU mask %d, [K][O] mask %d) is "
+            "not instantiated (3 -> 64, 64, 64, 128 all ReLU [O][K], and 64 -> 64 [K][O], 128 ReLU "
+            "[O][K] are)", K, n, O[0], O[1], O[2], O[3], relu, kmaj);
+  return PCADV_EINVAL;
 }
 
 int launch_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,

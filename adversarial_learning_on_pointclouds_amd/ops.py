@@ -199,6 +199,33 @@ def pw_fwd(x, w, b, act, kmajor=False, rows_per_w=0):
     return y
 
 
+def pw_chain(x, layers):
+    """Consecutive pw_fwd layers in one launch: layers = [(w, b, act, kmajor,
+    rows_per_w), ...], layer i's input the output of layer i-1.  Returns every
+    layer's output, bitwise what the per-layer pw_fwd calls return.  Shapes:
+    K = 3 -> 64, 64, 64, 128 and K = 64 -> 64, 128 (the feature-transform
+    extractor's two runs, include/pcadv.h pcadv_pw_chain)."""
+    lib = _lib.load()
+    _req(x, "x")
+    K = x.shape[-1]
+    M = x.numel() // K
+    arr = (_lib.PwLayer * len(layers))()
+    outs = []
+    for i, (w, b, act, kmajor, rows_per_w) in enumerate(layers):
+        if kmajor:
+            _req(w, "w")
+            O = w.shape[-1]
+        else:
+            O = _req(_mat(w), "w").shape[0]
+        if b is not None:
+            _req(b, "b", (O,))
+        y = torch.empty(*x.shape[:-1], O, device=x.device)
+        arr[i] = _lib.PwLayer(ptr(w), ptr(b), ptr(y), O, act, int(bool(kmajor)), rows_per_w)
+        outs.append(y)
+    check(lib.pcadv_pw_chain(ptr(x), M, K, arr, len(layers), stream_ptr()), "pcadv_pw_chain")
+    return outs
+
+
 def pw_bwd_data(dy, y, act, w, K, kmajor=False, rows_per_w=0, out=None):
     """dx = (dy * act'(y)) W; accumulated into `out` when given."""
     lib = _lib.load()

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import torch
 
@@ -50,6 +51,12 @@ def _precision(name):
     if name not in codes:
         raise ValueError(f"precision {name!r}: one of {sorted(codes)}")
     return codes[name]
+
+
+# the feature-transform step's point-wise forward as two chained launches
+# (pcadv_pw_chain, bitwise the per-layer pcadv_pw_fwd launches); PCADV_FT_CHAIN=0
+# keeps the six per-layer launches (A/B)
+_FT_CHAIN = os.environ.get("PCADV_FT_CHAIN", "1") == "1"
 
 
 def _align(nbytes):
@@ -580,18 +587,30 @@ class AdvFtTrainStep(AdvTrainStep):
         check(self.lib.pcadv_concat2(pts_gt.data_ptr(), n, pts_nogt.data_ptr(), n, pts.data_ptr(),
                                      self.step_count.data_ptr(), stream_ptr()), "pcadv_concat2")
         # ---- PointNetfeat with the feature transform (pointnet.py:109-130) ----
-        x1 = ops.pw_fwd(pts, P["feat.conv1.weight"], P["feat.conv1.bias"], RELU)
-        x2 = ops.pw_fwd(x1, P["feat.conv2.weight"], P["feat.conv2.bias"], RELU)
         s = "feat.fstn."
-        h1 = ops.pw_fwd(x2, P[s + "conv1.weight"], P[s + "conv1.bias"], RELU)
-        h2 = ops.pw_fwd(h1, P[s + "conv2.weight"], P[s + "conv2.bias"], RELU)
+        if _FT_CHAIN:  # conv1 -> conv2 -> STNkd conv1 -> conv2 in one launch
+            x1, x2, h1, h2 = ops.pw_chain(pts, [
+                (P["feat.conv1.weight"], P["feat.conv1.bias"], RELU, False, 0),
+                (P["feat.conv2.weight"], P["feat.conv2.bias"], RELU, False, 0),
+                (P[s + "conv1.weight"], P[s + "conv1.bias"], RELU, False, 0),
+                (P[s + "conv2.weight"], P[s + "conv2.bias"], RELU, False, 0)])
+        else:
+            x1 = ops.pw_fwd(pts, P["feat.conv1.weight"], P["feat.conv1.bias"], RELU)
+            x2 = ops.pw_fwd(x1, P["feat.conv2.weight"], P["feat.conv2.bias"], RELU)
+            h1 = ops.pw_fwd(x2, P[s + "conv1.weight"], P[s + "conv1.bias"], RELU)
+            h2 = ops.pw_fwd(h1, P[s + "conv2.weight"], P[s + "conv2.bias"], RELU)
         gs, gis = ops.conv_max_fwd(h2, P[s + "conv3.weight"], P[s + "conv3.bias"], True)
         f1 = ops.linear_fwd(gs, P[s + "fc1.weight"], P[s + "fc1.bias"], RELU)
         f2 = ops.linear_fwd(f1, P[s + "fc2.weight"], P[s + "fc2.bias"], RELU)
         t = ops.linear_fwd(f2, P[s + "fc3.weight"], P[s + "fc3.bias"], NONE, add_identity_k=64)
         T = t.view(C, 64, 64)
-        x2t = ops.pw_fwd(x2, T, None, NONE, kmajor=True, rows_per_w=N)
-        x3 = ops.pw_fwd(x2t, P["feat.conv3.weight"], P["feat.conv3.bias"], RELU)
+        if _FT_CHAIN:  # the transform x2 T and conv3 in one launch
+            x2t, x3 = ops.pw_chain(x2, [(T, None, NONE, True, N),
+                                        (P["feat.conv3.weight"], P["feat.conv3.bias"], RELU,
+                                         False, 0)])
+        else:
+            x2t = ops.pw_fwd(x2, T, None, NONE, kmajor=True, rows_per_w=N)
+            x3 = ops.pw_fwd(x2t, P["feat.conv3.weight"], P["feat.conv3.bias"], RELU)
         gmax, gidx = ops.conv_max_fwd(x3, P["feat.conv4.weight"], P["feat.conv4.bias"], False)
         # ---- fc1 on: the fused step's tail (part 3) -> dL/dgmax ---------------
         dgmax = self.dgmax[:C]

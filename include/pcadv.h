@@ -159,6 +159,25 @@ int pcadv_conv_max_fwd(const float* x, int C, int N, int K, const float* w, cons
 int pcadv_pw_fwd(const float* x, int M, int K, const float* w, const float* b, int O, int act,
                  int w_kmajor, int rows_per_w, float* y, hipStream_t stream);
 
+/* pcadv_pw_chain: n consecutive pcadv_pw_fwd layers in ONE launch (layer i's
+ * input is layer i-1's output, layer 0's is x[M][K]); every layer's y is
+ * written, bitwise what the per-layer pcadv_pw_fwd calls write.  Instantiated
+ * for the feature-transform extractor (models/pointnet.py:115-122, :57-60):
+ * K = 3 -> 64, 64, 64, 128 (conv1, conv2, STNkd conv1, STNkd conv2) and
+ * K = 64 -> 64, 128 (x2 T, conv3); other shapes return PCADV_EINVAL. ABI 9. */
+#define PCADV_PW_CHAIN_MAX 4
+typedef struct pcadv_pw_layer {
+  const float* w; /* [O][K] Conv1d weight, or [K][O] with w_kmajor = 1 */
+  const float* b; /* bias [O] or NULL */
+  float* y;       /* output [M][O] */
+  int O;
+  int act;        /* PCADV_ACT_NONE / PCADV_ACT_RELU */
+  int w_kmajor;
+  int rows_per_w; /* 0, or a multiple of 64: one matrix per rows_per_w rows */
+} pcadv_pw_layer;
+int pcadv_pw_chain(const float* x, int M, int K, const pcadv_pw_layer* layers, int n,
+                   hipStream_t stream);
+
 /* dx[M][K] (+)= (dy * act'(y)) W  (y = that layer's output; O in {64, 128},
  * K % 32 == 0); accumulate=1 adds into dx. */
 int pcadv_pw_bwd_data(const float* dy, const float* y, int act, int M, int O, const float* w,

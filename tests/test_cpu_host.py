@@ -25,7 +25,7 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
     assert sorted(_lib.SIGNATURES) == syms  # nothing bound that the header does not declare
-    assert lib.pcadv_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.pcadv_abi_version() == _lib.ABI_VERSION == 9
 
 
 def test_layout_matches_header_enums():
@@ -239,14 +239,14 @@ def _c_layout(struct, fields, tmp_path):
     return int(out[0]), [int(v) for v in out[1:]]
 
 
-@pytest.mark.parametrize("name", ["AdvArgs", "GatherJob", "PwWgradJob"])
+@pytest.mark.parametrize("name", ["AdvArgs", "GatherJob", "PwWgradJob", "PwLayer"])
 def test_ctypes_structs_match_the_c_layout(name, tmp_path):
     """The ctypes mirrors of pcadv_adv_args / pcadv_gather_job (the structs
     the trainer fills) have the C structs' size and field offsets."""
     from adversarial_learning_on_pointclouds_amd import _lib
     py = getattr(_lib, name)
     c = {"AdvArgs": "pcadv_adv_args", "GatherJob": "pcadv_gather_job",
-         "PwWgradJob": "pcadv_pw_wgrad_job"}[name]
+         "PwWgradJob": "pcadv_pw_wgrad_job", "PwLayer": "pcadv_pw_layer"}[name]
     fields = [f for f, _ in py._fields_]
     size, offs = _c_layout(c, fields, tmp_path)
     assert ctypes_sizeof(py) == size

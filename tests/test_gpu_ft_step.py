@@ -48,15 +48,19 @@ def _inputs(seed, B, N):
     return pg, lab, pn, m1, m2, y1, y2
 
 
-def _record(monkeypatch, name, pick):
-    """Every ops.<name> call's pick(output), in call order."""
+def _record(monkeypatch, name, pick, rec=None, many=False):
+    """Every ops.<name> call's pick(output), in call order (many: the call
+    returns a list, each element recorded; rec: append to that list)."""
     from adversarial_learning_on_pointclouds_amd import ops
-    rec = []
+    rec = [] if rec is None else rec
     orig = getattr(ops, name)
 
     def wrapped(*a, **k):
         out = orig(*a, **k)
-        rec.append(pick(out))
+        if many:
+            rec.extend(pick(o) for o in out)
+        else:
+            rec.append(pick(out))
         return out
     monkeypatch.setattr(ops, name, wrapped)
     return rec
@@ -77,6 +81,7 @@ def test_ft_step_vs_oracle_same_activation(monkeypatch, B, N):
     pg, lab, pn, m1, m2, y1, y2 = _inputs(100 + B, B, N)
     rec = _record(monkeypatch, "conv_max_fwd", lambda out: out[1])
     pw = _record(monkeypatch, "pw_fwd", lambda out: out)
+    _record(monkeypatch, "pw_chain", lambda out: out, rec=pw, many=True)  # the chained form
     losses = st(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)),
                 soft=(_t(y1), _t(y2)), apply_adam=False).cpu().numpy()
     s3, c4 = (r.cpu().numpy() for r in rec[-2:])
