@@ -156,6 +156,9 @@ SIGNATURES = {
     "pcadv_gemm_bf2": (_i, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i, _i, _i,
                             _vp, _vp, _i, _i, _i, _vp, _i64, _vp]),
     "pcadv_split_bf2": (_i, [_vp, _i64, _i, _i, _vp, _vp, _i64, _vp]),
+    "pcadv_split_bf3": (_i, [_vp, _i64, _i, _i, _vp, _vp, _vp, _i64, _vp]),
+    "pcadv_gemm_b3": (_i, [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _i, _i, _i, _vp, _vp, _i, _i,
+                           _i, _vp]),
     "pcadv_conv_max_bf2": (_i, [_vp, _i64, _vp, _vp, _i64, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i,
                                 _vp, _vp, _vp, _sz, _vp]),
     "pcadv_gemm_wgrad_workspace_bytes": (_sz, [_i, _i, _i, _i]),

@@ -89,6 +89,9 @@ int launch_gemm_bf2(const void*, const void*, long long, const void*, const void
                     long long, void*, void*, long long, int, int, int, const float*, const float*,
                     int, int, int, const float*, long long, hipStream_t);
 int launch_split_bf2(const float*, long long, int, int, void*, void*, long long, hipStream_t);
+int launch_split_bf3(const float*, long long, int, int, void*, void*, void*, long long, hipStream_t);
+int launch_gemm_b3(const float*, long long, const void*, const void*, const void*, long long, float*,
+                   long long, int, int, int, const float*, const float*, int, int, int, hipStream_t);
 size_t gemm_wgrad_workspace_bytes(int, int, int, int);
 int launch_gemm_wgrad(const float*, long long, const float*, long long, int, int, int, float*,
                       long long, float*, float*, int, int, void*, size_t, hipStream_t);
@@ -706,6 +709,19 @@ int pcadv_gemm_bf2(const void* a_hi, const void* a_lo, int64_t lda, const void* 
 int pcadv_split_bf2(const float* x, int64_t ld, int rows, int cols, void* hi, void* lo,
                     int64_t ldo, hipStream_t stream) {
   return launch_split_bf2(x, ld, rows, cols, hi, lo, ldo, stream);
+}
+
+int pcadv_split_bf3(const float* x, int64_t ld, int rows, int cols, void* hi, void* mid, void* lo,
+                    int64_t ldo, hipStream_t stream) {
+  return launch_split_bf3(x, ld, rows, cols, hi, mid, lo, ldo, stream);
+}
+
+int pcadv_gemm_b3(const float* a, int64_t lda, const void* b_hi, const void* b_mid,
+                  const void* b_lo, int64_t ldb, float* c, int64_t ldc, int M, int N, int K,
+                  const float* bias, const float* bias_rows, int rows_per_group, int relu,
+                  int accumulate, hipStream_t stream) {
+  return launch_gemm_b3(a, lda, b_hi, b_mid, b_lo, ldb, c, ldc, M, N, K, bias, bias_rows,
+                        rows_per_group, relu, accumulate, stream);
 }
 
 size_t pcadv_gemm_wgrad_workspace_bytes(int rows, int O, int Kin, int rows_per_group) {

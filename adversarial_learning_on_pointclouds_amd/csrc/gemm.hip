@@ -76,7 +76,7 @@ struct GemmP {
   // row stride in elements), split once by its producer: staged as plain
   // copies (no VALU split per tile)
   const __bf16* ap[2]; long long ldap;
-  const __bf16* bp[2]; long long ldbp;
+  const __bf16* bp[3]; long long ldbp;  // TB = 3: hi, mid, lo (the three-way split)
   __bf16* cp[2]; long long ldcp;    // nullable: the epilogue also writes C's hi / lo planes
   // max-over-points screening epilogue (mode 2): per (row tile, column) top-2
   int2* part;                      // [M / BM][N] screening keys
@@ -335,8 +335,12 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
   // (planes: hi and lo resources, A's at this cloud's rows in mode 2)
   const __amdgpu_buffer_rsrc_t ars = rsrc(TA == 2 ? (const void*)(p.ap[0] + aoff2) : (const void*)Ab);
   const __amdgpu_buffer_rsrc_t arsl = rsrc(TA == 2 ? (const void*)(p.ap[1] + aoff2) : (const void*)Ab);
-  const __amdgpu_buffer_rsrc_t brs = rsrc(TB == 2 ? (const void*)p.bp[0] : (const void*)p.b);
-  const __amdgpu_buffer_rsrc_t brsl = rsrc(TB == 2 ? (const void*)p.bp[1] : (const void*)p.b);
+  const __amdgpu_buffer_rsrc_t brs = rsrc(TB >= 2 ? (const void*)p.bp[0] : (const void*)p.b);
+  const __amdgpu_buffer_rsrc_t brsl = rsrc(TB >= 2 ? (const void*)p.bp[1] : (const void*)p.b);
+  // TB = 3: B as the hi / mid / lo planes of its three-way split (split once per
+  // step by pcadv_split_bf3, bitwise split_planes<3> of the f32 value), staged
+  // as plain copies; same LDS image, so the same MFMAs on the same values
+  const __amdgpu_buffer_rsrc_t brs3 = rsrc(TB == 3 ? (const void*)p.bp[2] : (const void*)p.b);
   constexpr bool vecA = (VEC & 1) != 0, vecB = (VEC & 2) != 0;
   auto load_rows = [&](f32x4 (&v)[4], const __amdgpu_buffer_rsrc_t& rs, long long ld, int row0,
                        int rlim, int k0, auto VECT) {
@@ -426,6 +430,26 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
     v[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, o, 0, 0));
     v[3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, o + 16u, 0, 0));
   };
+  // three planes: v[0..1] = hi, v[2..3] = mid, v[4..5] = lo
+  auto load_planes3 = [&](f32x4 (&v)[6], long long ld, int row0, int rlim, int k0) {
+    const int row = row0 + (tid >> 1), k = k0 + 16 * (tid & 1);
+    const bool ok = row < rlim && k >= kz0 && k < kz1;
+    const uint32_t o = opq(ok ? (uint32_t)((long long)row * ld + k) * 2u : OOB);
+    v[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brs, o, 0, 0));
+    v[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brs, o + 16u, 0, 0));
+    v[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brsl, o, 0, 0));
+    v[3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brsl, o + 16u, 0, 0));
+    v[4] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brs3, o, 0, 0));
+    v[5] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brs3, o + 16u, 0, 0));
+  };
+  auto store_planes3 = [&](const f32x4 (&v)[6], __bf16 (*planes)[GM_BM * GM_S]) {
+    const int row = tid >> 1, kk = 16 * (tid & 1);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk]) = v[2 * q];
+      *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk + 8]) = v[2 * q + 1];
+    }
+  };
   auto store_planes = [&](const f32x4 (&v)[4], __bf16 (*planes)[GM_BM * GM_S]) {
     const int row = tid >> 1, kk = 16 * (tid & 1);
 #pragma unroll
@@ -435,15 +459,16 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
     }
   };
   float cs[4] = {0.f, 0.f, 0.f, 0.f};  // TA = 1: this thread's column sums of A
-  auto load_tile = [&](f32x4 (&ra)[4], f32x4 (&rb)[4], int k0) {
+  auto load_tile = [&](f32x4 (&ra)[4], auto& rb, int k0) {
     if (TA == 2) load_planes(ra, ars, arsl, p.ldap, m0, Mlim, k0);
     else if (TA == 0) load_rows(ra, ars, p.lda, m0, Mlim, k0, std::integral_constant<bool, vecA>{});
     else load_cols(ra, ars, p.lda, m0, Mlim, k0, std::integral_constant<bool, vecA>{});
-    if (TB == 2) load_planes(rb, brs, brsl, p.ldbp, n0, p.N, k0);
-    else if (TB == 0) load_rows(rb, brs, p.ldb, n0, p.N, k0, std::integral_constant<bool, vecB>{});
+    if constexpr (TB == 3) load_planes3(rb, p.ldbp, n0, p.N, k0);
+    else if constexpr (TB == 2) load_planes(rb, brs, brsl, p.ldbp, n0, p.N, k0);
+    else if constexpr (TB == 0) load_rows(rb, brs, p.ldb, n0, p.N, k0, std::integral_constant<bool, vecB>{});
     else load_cols(rb, brs, p.ldb, n0, p.N, k0, std::integral_constant<bool, vecB>{});
   };
-  auto store_tile = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
+  auto store_tile = [&](const f32x4 (&ra)[4], const auto& rb) {
     if (TA == 2) store_planes(ra, L.a);
     else if (TA == 0) store_rows(ra, L.a);
     else {
@@ -453,8 +478,9 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
         for (int i = 0; i < 4; ++i) cs[i] += ((ra[0][i] + ra[1][i]) + ra[2][i]) + ra[3][i];
       }
     }
-    if (TB == 2) store_planes(rb, L.b);
-    else if (TB == 0) store_rows(rb, L.b);
+    if constexpr (TB == 3) store_planes3(rb, L.b);
+    else if constexpr (TB == 2) store_planes(rb, L.b);
+    else if constexpr (TB == 0) store_rows(rb, L.b);
     else store_cols(rb, L.b);
   };
 
@@ -574,7 +600,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmP& p, int lin, int gx, in
   // one register set: tile t + 1 is loaded right after tile t is stored; the
   // sched_barrier keeps those loads ahead of tile t's MFMAs (as
   // k_gemm_bf2_big), so one tile's MFMAs cover the next tile's loads
-  f32x4 ra[4], rb[4];
+  f32x4 ra[4], rb[TB == 3 ? 6 : 4];
   load_tile(ra, rb, kz0);
   for (int k0 = kz0; k0 < kz1; k0 += GM_BK) {
     __syncthreads();  // every wave is done reading the previous tile
@@ -795,7 +821,7 @@ k_gemm_bf2_big(GemmP p) {
       *reinterpret_cast<f32x4*>(&planes[q][row * GM_S + kk + 8]) = v[2 * q + 1];
     }
   };
-  auto load_tile = [&](f32x4 (&ra)[4], f32x4 (&rb)[4], int k0) {
+  auto load_tile = [&](f32x4 (&ra)[4], auto& rb, int k0) {
     load_planes(ra, arsc, abase, arow_ok, k0);
     load_planes(rb, brsc, bbase, brow_ok, k0);
   };
@@ -1637,7 +1663,7 @@ template <int TA, int TB>
 static int gemm_vec_flags(const GemmP& p) {
   const bool kq = p.K % 4 == 0 && p.grp % 4 == 0 && (p.zpg == 1 || p.ksplit_len % 4 == 0);
   const bool va = TA == 2 || (p.avec && (TA == 0 ? kq : p.M % 4 == 0 && p.rows_per_group % 4 == 0));
-  const bool vb = TB == 2 || (p.bvec && (TB == 0 ? kq : p.N % 4 == 0));
+  const bool vb = TB >= 2 || (p.bvec && (TB == 0 ? kq : p.N % 4 == 0));
   return (va ? 1 : 0) | (vb ? 2 : 0);
 }
 
@@ -1789,6 +1815,69 @@ int launch_split_bf2(const float* x, long long ld, int rows, int cols, void* hi,
                      cols, static_cast<__bf16*>(hi), static_cast<__bf16*>(lo), ldo);
   PC_HIP_CHECK_LAUNCH("k_split_bf2");
   return PCADV_OK;
+}
+
+// f32 [rows][cols] -> bf16 hi / mid / lo planes (split_planes<3>: bitwise the
+// three-way split the six-product GEMMs make of an f32 operand per tile); hi and
+// mid are also the two-way split's hi / lo (split_planes<2>)
+__global__ void __launch_bounds__(256)
+k_split_bf3(const float* __restrict__ x, long long ld, int rows, int cols, __bf16* __restrict__ hi,
+            __bf16* __restrict__ mid, __bf16* __restrict__ lo, long long ldo) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)rows * cols) return;
+  const int r = (int)(e / cols), c = (int)(e % cols);
+  __bf16 o[3];
+  split_planes<3>(x[(size_t)r * ld + c], o);
+  const size_t d = (size_t)r * ldo + c;
+  hi[d] = o[0];
+  mid[d] = o[1];
+  lo[d] = o[2];
+}
+
+int launch_split_bf3(const float* x, long long ld, int rows, int cols, void* hi, void* mid,
+                     void* lo, long long ldo, hipStream_t s) {
+  PC_REQUIRE(x && hi && mid && lo && rows > 0 && cols > 0 && ld >= cols && ldo >= cols,
+             "split_bf3: bad arguments");
+  const long long n = (long long)rows * cols;
+  hipLaunchKernelGGL(k_split_bf3, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ld, rows,
+                     cols, static_cast<__bf16*>(hi), static_cast<__bf16*>(mid),
+                     static_cast<__bf16*>(lo), ldo);
+  PC_HIP_CHECK_LAUNCH("k_split_bf3");
+  return PCADV_OK;
+}
+
+// The six-product GEMM C[M][N] (+)= A B^T with A f32 [m][k] (split three ways
+// per tile, as launch_gemm with precise = 1, ta = tb = 0) and B given as the
+// hi / mid / lo planes of its three-way split ([n][k], made once by
+// pcadv_split_bf3): the same MFMAs on the same values, so C is bitwise
+// launch_gemm's, without B's per-tile VALU split.
+int launch_gemm_b3(const float* a, long long lda, const void* b_hi, const void* b_mid,
+                   const void* b_lo, long long ldb, float* c, long long ldc, int M, int N, int K,
+                   const float* bias, const float* bias_rows, int rows_per_group, int relu,
+                   int accumulate, hipStream_t s) {
+  PC_REQUIRE(a && b_hi && b_mid && b_lo && c && M > 32 && N > 0 && K > 0,
+             "gemm_b3: bad shape M=%d N=%d K=%d (M > 32)", M, N, K);
+  PC_REQUIRE(K % 16 == 0 && ldb % 8 == 0 && ldb >= K && lda >= K,
+             "gemm_b3: K %% 16 and ldb %% 8 required (K=%d ldb=%lld)", K, ldb);
+  PC_REQUIRE((((uintptr_t)b_hi | (uintptr_t)b_mid | (uintptr_t)b_lo) & 15) == 0,
+             "gemm_b3: planes must be 16-B aligned");
+  PC_REQUIRE(((uintptr_t)a & 3) == 0 && ((uintptr_t)c & 3) == 0, "gemm_b3: float alignment");
+  PC_REQUIRE(ldc >= N && (!bias_rows || rows_per_group > 0), "gemm_b3: bad ldc / bias_rows");
+  PC_REQUIRE(fits31(M, lda, 4) && fits31(N, ldb, 2) && fits31(M, ldc, 4),
+             "gemm_b3: operands must span < 2 GB");
+  GemmP p{};
+  p.a = a; p.lda = lda;
+  p.bp[0] = static_cast<const __bf16*>(b_hi); p.bp[1] = static_cast<const __bf16*>(b_mid);
+  p.bp[2] = static_cast<const __bf16*>(b_lo); p.ldbp = ldb;
+  p.c = c; p.ldc = ldc;
+  p.bias = bias; p.bias_rows = bias_rows; p.rows_per_group = rows_per_group;
+  p.M = M; p.N = N; p.K = K; p.relu = relu; p.accumulate = accumulate;
+  p.avec = lda % 4 == 0 && ((uintptr_t)a & 15) == 0;
+  p.bvec = 1;
+  p.cvec = ldc % 4 == 0 && ((uintptr_t)c & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0) &&
+           (!bias_rows || (N % 4 == 0 && ((uintptr_t)bias_rows & 15) == 0));
+  p.grp = K; p.zpg = 1; p.ksplit_len = K;
+  return accumulate ? gemm_launch<0, 3, 1, 6>(p, 1, s) : gemm_launch<0, 3, 0, 6>(p, 1, s);
 }
 
 // weight gradient dW[O][Kin] (+)= sum over the rows of dZ[row][o] X[row][k]:

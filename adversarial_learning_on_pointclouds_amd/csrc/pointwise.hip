@@ -324,7 +324,7 @@ k_pw_chain(const float* __restrict__ x, int M, int ntiles, PwChainArgs a) {
         frags(F, nt * PW_ROWS, fs[F & 1]);
       }
       float* out = L.buf((i + 1) & 1);
-      const int so = pc_stride((i + 1) & 1), si = pc_stride(i == 0 ? 0 : i & 1);
+      const int so = pc_stride((i + 1) & 1);
       if (K0 == 3 && i == 0) {  // k_pw_fwd3's fma chain: thread = (column, 16 rows)
         const int o = tid & 63, rg = tid >> 6;
 #pragma unroll 4

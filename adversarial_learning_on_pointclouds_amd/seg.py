@@ -48,6 +48,12 @@ PRECISIONS = ("fp32", "bf16x3")
 # their producers (pcadv_gemm_bf2; bitwise the f32-staged result);
 # PCADV_SEG_PLANES=0 stages f32
 _PLANES = os.environ.get("PCADV_SEG_PLANES", "1") == "1"
+# fp32 mode: the forward GEMMs' weights as hi / mid / lo planes split once per
+# step (pcadv_split_bf3 + pcadv_gemm_b3, bitwise the per-tile split).  Measured
+# slower (seg 1.183 -> 1.200 ms, profiles/r06_seg_b3_ab.txt: the plane copies
+# move 1.5x the f32 bytes per B tile, and the per-tile split they replace was
+# hidden under the MFMAs), so off unless PCADV_SEG_B3=1
+_B3 = os.environ.get("PCADV_SEG_B3", "0") == "1"
 
 
 def _check_precision(precision):
@@ -100,6 +106,21 @@ class _Engine:
                                       None if bias_rows is None else _p(bias_rows),
                                       rows_per_group, int(relu), 0, None, 0, stream_ptr()),
               "pcadv_gemm_bf2")
+
+    def gemm_b3(self, a, lda, bp, ldb, c, ldc, M, N, K, *, bias=None, bias_rows=None,
+                rows_per_group=0, relu=False, a_off=0, c_off=0):
+        """The six-product (fp32-mode) GEMM with B as its (hi, mid, lo) planes."""
+        check(self.lib.pcadv_gemm_b3(_p(a, a_off), lda, _pb(bp[0]), _pb(bp[1]), _pb(bp[2]), ldb,
+                                     _p(c, c_off), ldc, M, N, K,
+                                     None if bias is None else _p(bias),
+                                     None if bias_rows is None else _p(bias_rows), rows_per_group,
+                                     int(relu), 0, stream_ptr()), "pcadv_gemm_b3")
+
+    def split3(self, x, hi, mid, lo):
+        """x f32 contiguous -> its hi, mid, lo bf16 planes (hi / mid = split's hi / lo)."""
+        r, c = (1, x.numel()) if x.dim() == 1 else (x.shape[0], x.shape[1])
+        check(self.lib.pcadv_split_bf3(_p(x), c, r, c, _pb(hi), _pb(mid), _pb(lo), c, stream_ptr()),
+              "pcadv_split_bf3")
 
     def split(self, x, hi, lo):
         """x (rows, cols) f32 contiguous -> hi, lo bf16 of the same shape."""
@@ -232,7 +253,7 @@ def _weight_planes(W, Wf, wplanes=None):
     return [None] + out[:5], out[5:]
 
 
-def seg_forward(pts, cls, params, wplanes=None, precision="fp32"):
+def seg_forward(pts, cls, params, wplanes=None, precision="fp32", wplanes3=None):
     """PointNetSeg forward (pointnet.py:282-317) on the engine.  Returns a dict
     with logits (B*N, C) point-major, gmax (B, 2048), gidx (B, 2048) and every
     activation the backward needs.  Each layer's epilogue also writes its
@@ -255,6 +276,12 @@ def seg_forward(pts, cls, params, wplanes=None, precision="fp32"):
     # conv6's screen is three products in both modes (its winners are re-evaluated
     # in exact f32), staged from x5's planes: conv5's epilogue writes them
     c6p = _PLANES
+    # fp32 mode with the caller's three-way weight planes (list of 20 (hi, mid,
+    # lo) in state_dict order): the forward GEMMs stage B as plain copies
+    b3 = fp32 and wplanes3 is not None
+    if b3:
+        W3p = [None] + [tuple(t.view(W[i].shape) for t in wplanes3[2 * i]) for i in range(1, 5)]
+        Wf3p = [tuple(t.view(Wf[i].shape) for t in wplanes3[12 + 2 * i]) for i in range(4)]
     xloc = torch.empty(M, _LOC, device=dev)
     pl = lambda rows, cols: (torch.empty(rows, cols, device=dev, dtype=torch.bfloat16),  # noqa: E731
                              torch.empty(rows, cols, device=dev, dtype=torch.bfloat16))
@@ -273,6 +300,9 @@ def seg_forward(pts, cls, params, wplanes=None, precision="fp32"):
         if planes:
             E.gemm_bf2(xp, _LOC, Wp[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
                        a_off=_OFF[i - 1], c_off=_OFF[i], cp=xp, ldcp=_LOC, cp_off=_OFF[i])
+        elif b3 and not (i == 4 and c6p):
+            E.gemm_b3(xloc, _LOC, W3p[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
+                      a_off=_OFF[i - 1], c_off=_OFF[i])
         else:
             last = i == 4 and c6p  # conv5 also writes x5's planes for conv6's screen
             E.gemm(xloc, _LOC, W[i], K, xloc, _LOC, M, O, K, bias=bc[i], relu=True,
@@ -313,6 +343,12 @@ def seg_forward(pts, cls, params, wplanes=None, precision="fp32"):
         E.gemm_bf2(h2p, 256, Wfp[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True, cp=h3p,
                    ldcp=128)
         E.gemm_bf2(h3p, 128, Wfp[3], 128, logits, ncls, M, ncls, 128, bias=bf[3])
+    elif b3:
+        E.gemm_b3(xloc, _LOC, Wf3p[0], 3024, h1, 256, M, 256, _LOC, bias_rows=cb,
+                  rows_per_group=N, relu=True)
+        E.gemm_b3(h1, 256, Wf3p[1], 256, h2, 256, M, 256, 256, bias=bf[1], relu=True)
+        E.gemm_b3(h2, 256, Wf3p[2], 256, h3, 128, M, 128, 256, bias=bf[2], relu=True)
+        E.gemm_b3(h3, 128, Wf3p[3], 128, logits, ncls, M, ncls, 128, bias=bf[3])
     else:
         E.gemm(xloc, _LOC, W1, 3024, h1, 256, M, 256, _LOC, bias_rows=cb, rows_per_group=N,
                relu=True, precise=pf)
@@ -593,6 +629,12 @@ class SegTrainStep:
         self.wpl = torch.empty(n, device=dev, dtype=torch.bfloat16)
         self.wplanes = [(self.wph[o:o + p.numel()], self.wpl[o:o + p.numel()])
                         for (_, p), o in zip(named, offs)]
+        # fp32 mode: the three-way split (hi, mid = wph, wpl, and lo), one launch
+        # per step, for the forward GEMMs' weight operands
+        self.wpl3 = torch.empty(n, device=dev, dtype=torch.bfloat16) if _B3 else None
+        self.wplanes3 = ([(self.wph[o:o + p.numel()], self.wpl[o:o + p.numel()],
+                           self.wpl3[o:o + p.numel()]) for (_, p), o in zip(named, offs)]
+                         if _B3 else None)
         self.optimizer = optimizer
         self.loss = torch.zeros((), device=dev)
         self.graph = None
@@ -602,12 +644,15 @@ class SegTrainStep:
         _check_dev(pts, "pts")
         if seg.shape != (B, N) or seg.dtype != torch.int64 or not seg.is_contiguous():
             raise ValueError("seg: expected contiguous int64 (B, N)")
-        wpl = None
-        if _PLANES:  # every weight's planes (fp32 mode reads conv6's only)
+        wpl = wpl3 = None
+        if _B3 and self.precision == "fp32":  # hi / mid / lo: conv6 reads hi / mid
+            _engine().split3(self.param, self.wph, self.wpl, self.wpl3)
+            wpl, wpl3 = (self.wplanes if _PLANES else None), self.wplanes3
+        elif _PLANES:  # every weight's planes (fp32 mode reads conv6's only)
             _engine().split(self.param, self.wph, self.wpl)
             wpl = self.wplanes
         fw = seg_forward(pts, cls.float().reshape(B, 1, 16), self.params, wplanes=wpl,
-                         precision=self.precision)
+                         precision=self.precision, wplanes3=wpl3)
         if self.keep_activations:
             self.fw = fw  # the last step's activations (logits, x_global, argmax, ...)
         M, ncls = B * N, fw["dims"][2]

@@ -285,6 +285,21 @@ int pcadv_gemm_bf2(const void* a_hi, const void* a_lo, int64_t lda, const void* 
 /* f32 [rows][cols] (stride ld) -> its bf16 hi / lo planes (stride ldo). */
 int pcadv_split_bf2(const float* x, int64_t ld, int rows, int cols, void* hi, void* lo,
                     int64_t ldo, hipStream_t stream);
+/* f32 [rows][cols] (stride ld) -> its bf16 hi / mid / lo planes (stride ldo),
+ * the three-way split whose six products give pcadv_gemm's precise (f32-level)
+ * GEMMs; hi / mid are pcadv_split_bf2's hi / lo.  ABI 9. */
+int pcadv_split_bf3(const float* x, int64_t ld, int rows, int cols, void* hi, void* mid, void* lo,
+                    int64_t ldo, hipStream_t stream);
+/* pcadv_gemm with precise = 1, ta = tb = 0 (C[M][N] (+)= act(A B^T + bias)),
+ * B given as the hi / mid / lo planes of its three-way split ([N][K], stride
+ * ldb, K % 16 == 0, 16-B aligned; pcadv_split_bf3 once per step for a weight):
+ * bitwise pcadv_gemm's result without the per-tile split of B.  M > 32.
+ * ABI 9 (the segmentation forward's weight operands, models/pointnet.py:
+ * 282-317). */
+int pcadv_gemm_b3(const float* a, int64_t lda, const void* b_hi, const void* b_mid,
+                  const void* b_lo, int64_t ldb, float* c, int64_t ldc, int M, int N, int K,
+                  const float* bias, const float* bias_rows, int rows_per_group, int relu,
+                  int accumulate, hipStream_t stream);
 
 /* Weight gradient dw[o][k] (row stride ldo) (+)= sum over `rows` points of
  * dz[p][o] x[p][k]: six-product (f32-level) GEMM over fixed-order slabs of the

@@ -937,3 +937,62 @@ def test_seg_train_step_full_size_configs3_vs_oracle(precision, e2e):
     step.adam()
     for name, p in m.named_parameters():
         assert np.abs(p.detach().cpu().numpy() - S[name]).max() < 1e-6, name
+
+
+@pytest.mark.parametrize("M,N,K,ldb,rows", [(700, 128, 64, 64, 0), (2048, 256, 960, 3024, 1024),
+                                            (4096, 50, 128, 128, 0), (333, 512, 128, 128, 0)])
+def test_gemm_b3_is_bitwise_the_precise_gemm(M, N, K, ldb, rows):
+    """pcadv_gemm_b3 (B as the hi / mid / lo planes pcadv_split_bf3 makes once)
+    against pcadv_gemm with precise = 1 (B split three ways per tile): the same
+    planes in LDS, the same MFMAs, so C is bitwise equal; ragged M and N, fc1's
+    960 local columns of a 3024-wide weight, and a per-cloud bias."""
+    from adversarial_learning_on_pointclouds_amd import seg as segmod
+    E = segmod._engine()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, ldb, generator=g) * 0.1).to(DEV)
+    bias = None if rows else torch.randn(N, generator=g).to(DEV)
+    brow = torch.randn((M + rows - 1) // rows, N, generator=g).to(DEV) if rows else None
+    hi, mid, lo = (torch.empty(N, ldb, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    E.split3(w, hi, mid, lo)
+    c1 = torch.empty(M, N, device=DEV)
+    c2 = torch.empty(M, N, device=DEV)
+    E.gemm(a, K, w, ldb, c1, N, M, N, K, bias=bias, bias_rows=brow, rows_per_group=rows,
+           relu=True, precise=True)
+    E.gemm_b3(a, K, (hi, mid, lo), ldb, c2, N, M, N, K, bias=bias, bias_rows=brow,
+              rows_per_group=rows, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(c1, c2)
+    # the planes: hi / mid are the two-way split's hi / lo, and hi + mid + lo = w
+    h2, l2 = torch.empty_like(hi), torch.empty_like(hi)
+    E.split(w, h2, l2)
+    assert torch.equal(hi, h2) and torch.equal(mid, l2)
+    assert torch.equal(hi.float() + mid.float() + lo.float(), w)
+
+
+def test_seg_step_weight_planes_path_is_bitwise():
+    """SegTrainStep in fp32 mode with the forward GEMMs' weights split once per
+    step (PCADV_SEG_B3, the default) against the per-tile split: two steps give
+    bitwise the same loss, parameters and gradients."""
+    from adversarial_learning_on_pointclouds_amd import seg as segmod
+    torch.manual_seed(6)
+    res = []
+    saved = segmod._B3
+    try:
+        for b3 in (True, False):
+            segmod._B3 = b3
+            m = PointNetSeg(50).to(DEV)
+            torch.manual_seed(7)
+            m.load_state_dict({k: torch.randn_like(v) * 0.1 for k, v in m.state_dict().items()})
+            st = segmod.SegTrainStep(m, lr=1e-3)
+            pts = torch.rand(4, 2048, 3, device=DEV) * 2 - 1
+            cls = torch.zeros(4, 1, 16, device=DEV)
+            cls[:, 0, 5] = 1
+            lab = torch.randint(0, 50, (4, 2048), device=DEV)
+            losses = [st(pts, cls, lab).clone() for _ in range(2)]
+            res.append((losses, st.param.clone(), st.grad.clone()))
+    finally:
+        segmod._B3 = saved
+    (la, pa, ga), (lb, pb, gb) = res
+    assert all(torch.equal(x, y) for x, y in zip(la, lb))
+    assert torch.equal(pa, pb) and torch.equal(ga, gb)
