@@ -61,6 +61,7 @@ class DataParallelAdvStep:
         round-5 form; needs a step with parts); default: one all-reduce."""
         self.step, self.group = step, group
         self.overlap = overlap
+        self.graph_form = None  # set by graphed()
         if broadcast_params:  # identical initial weights on every rank
             dist.broadcast(step.g_param, src=0, group=group)
             dist.broadcast(step.d_param, src=0, group=group)
@@ -102,9 +103,22 @@ class DataParallelAdvStep:
     def graphed(self, pts_gt, labels, pts_nogt):
         """The iteration over resident buffers as replayable graphs: ONE graph
         with the collectives captured over RCCL (capture_single), graphs around
-        eager collectives otherwise (gloo cannot be captured)."""
+        eager collectives otherwise (gloo cannot be captured).  If the RCCL
+        capture itself fails (a runtime that refuses to capture the collective:
+        every rank takes the same branch, so the ranks stay in step), the
+        iteration falls back to the graphs around eager all-reduces and
+        self.graph_form says so."""
         if dist.get_backend(self.group) == "nccl":
-            return self.capture_single(pts_gt, labels, pts_nogt)
+            try:
+                g = self.capture_single(pts_gt, labels, pts_nogt)
+                self.graph_form = "one graph, all-reduce captured"
+                return g
+            except RuntimeError as e:  # torch reports capture failures as RuntimeError
+                torch.cuda.synchronize()
+                self.graph_form = f"graphs around eager all-reduces (capture failed: {e})"[:300]
+                dist.barrier(group=self.group)
+        else:
+            self.graph_form = "graphs around eager all-reduces (gloo)"
         return self.capture(pts_gt, labels, pts_nogt)
 
     def capture(self, pts_gt, labels, pts_nogt):

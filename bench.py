@@ -1210,7 +1210,8 @@ def main():
         "config": {"workload": "adversarial cls step: PointNetCls(k=40)+DeepConvDiscNet(40,1), "
                                f"B=32 GT + 32 noGT clouds/GPU, N={N}, Adam x2",
                    "global_batch": 2 * B * world, "points": N,
-                   "parallelism": f"dp{world}", "hip_graph": use_graph, "steps_per_graph": G},
+                   "parallelism": f"dp{world}", "hip_graph": use_graph, "steps_per_graph": G,
+                   **({"dp_iteration": runner.graph_form} if runner is not None else {})},
         "world_size": world,
         "backend": ((_backend() if _backend() != "nccl" else "nccl (RCCL)") if world > 1 else None),
         "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median",
