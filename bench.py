@@ -764,7 +764,7 @@ def bench_adv_ft(args):
     roof = ft_roofline(C)
     if not args.ft_body:
         roof["traffic"], roof["traffic_source"] = _pmc_traffic(
-            "r*_adv_ft_pmc_traffic.json", ["k_conv4_max"])
+            "r*_adv_ft_pmc_traffic.json", ["pcadv::k_conv4_max"])
         roof["traffic_unit"] = "bytes/launch (L2->memory, PMC FETCH_SIZEx2+WRITE_SIZE)"
         roof["mfma_busy"], roof["mfma_busy_source"] = _pmc_mfma("adv_ft", "k_conv4_max")
     out["roofline"] = roof
