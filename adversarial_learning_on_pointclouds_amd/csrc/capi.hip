@@ -447,6 +447,17 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   float* gG = a->g_grad;
   const int32_t* st = a->step_count;
   float* logits = a->logits ? a->logits : w.logits;
+  // part 3 (ABI 9): the head on a caller's pooled features (the feature-
+  // transform generator's extractor runs outside, as adv_step's part 3):
+  // fc1 .. the CE and back to dL/dgmax, no feature launches, no Adam
+  PC_REQUIRE(a->part == 0 || a->part == 3, "cls_step: part %d (0 whole, 3 head on given features)",
+             a->part);
+  const bool ext = a->part == 3;
+  PC_REQUIRE(!ext || (a->feat_gmax && a->feat_dgmax && !a->apply_adam && !a->ngather &&
+                      !a->epi_ncounters && !a->epi_ring),
+             "cls_step: part 3 needs feat_gmax / feat_dgmax and takes no Adam, gather or epilogue");
+  const float* gmax = ext ? a->feat_gmax : w.gmax;
+  float* dgmax = ext ? a->feat_dgmax : w.dgmax;
   const float* mask = nullptr;
   if (a->drop_mask_gt) {
     if (hipMemcpyAsync(w.mask, a->drop_mask_gt, sizeof(float) * B * 256, hipMemcpyDeviceToDevice,
@@ -460,13 +471,14 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   const int W = a->rng_world > 1 ? a->rng_world : 1, rr = W > 1 ? a->rng_rank : 0;
   PC_REQUIRE(rr >= 0 && rr < W, "cls_step: rng_rank %d not in [0, %d)", a->rng_rank, W);
   PC_TRY(check_folded_gather(a));
-  PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
-                               G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
-                               G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
-                               G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
-                               w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision, a->gather,
-                               a->ngather));
-  PC_TRY(launch_linear_fwd(w.gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
+  if (!ext)
+    PC_TRY(launch_feat_fwd_fused(a->pts_gt, a->pts_gt, B, C, N, G + PCADV_G_CONV1_W,
+                                 G + PCADV_G_CONV1_B, G + PCADV_G_CONV2_W, G + PCADV_G_CONV2_B,
+                                 G + PCADV_G_CONV3_W, G + PCADV_G_CONV3_B, G + PCADV_G_CONV4_W,
+                                 G + PCADV_G_CONV4_B, w.x3, w.gmax, w.gidx, a->step_count,
+                                 w.feat_ws, w.feat_ws_bytes, s, nullptr, a->precision, a->gather,
+                                 a->ngather));
+  PC_TRY(launch_linear_fwd(gmax, G + PCADV_G_FC1_W, G + PCADV_G_FC1_B, w.h1, C, 512, 1024,
                            PCADV_ACT_RELU, nullptr, nullptr, 0, 0.f, s));
   PC_TRY(launch_linear_fwd(w.h1, G + PCADV_G_FC2_W, G + PCADV_G_FC2_B, w.h2, C, 256, 512,
                            PCADV_ACT_RELU, mask, rstep, a->rng_seed, a->drop_p, s, 0,
@@ -474,8 +486,8 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   // fc3, CrossEntropyLoss (train_classification.py:199), lambda_cls * dCE/dlogits
   // and fc3's input gradient, stored as fc2's dz (k_cls_head)
   PC_TRY(launch_cls_head(w.h2, w.mask, a->drop_p, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, a->labels,
-                         B, a->lambda_cls, logits, w.dlogits, w.dh2, w.rowloss, s, w.gidx, C, N,
-                         w.sortrec));
+                         B, a->lambda_cls, logits, w.dlogits, w.dh2, w.rowloss, s,
+                         ext ? nullptr : w.gidx, C, N, ext ? nullptr : w.sortrec));
   {
     // fc2's backward; fc3's weight gradient and the CE batch mean ride along
     LinBwdExtra ex{};
@@ -491,9 +503,10 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,
                              C, 256, 512, s, &ex));
   }
-  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, w.gmax,
-                           G + PCADV_G_FC1_W, w.dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
+  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, gmax,
+                           G + PCADV_G_FC1_W, dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
                            C, 512, 1024, s));
+  if (ext) return PCADV_OK;
   // feature backward; Adam (generator only) fused into its finishing launch
   PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v), "cls_step: Adam moments");
   const FinAdam fa = fused_adam(a, false);

@@ -458,6 +458,96 @@ def ft_layout(model):
     return layout, off
 
 
+def _ft_extractor_forward(P, pts, N):
+    """PointNetfeat(feature_transform=True) forward (models/pointnet.py:109-130)
+    on the point-wise kernels over C clouds of N points: conv1 -> conv2 ->
+    STNkd(64) (conv 64 -> 64 -> 128, conv 128 -> 1024 + ReLU + max, fc1 .. fc3
+    + I) -> x2 T -> conv3 -> conv4 + max.  P: the generator's parameters by
+    name.  Returns every activation the backward reads."""
+    from . import ops
+    from .ops import ACT_NONE as NONE, ACT_RELU as RELU
+    C = pts.shape[0]
+    s = "feat.fstn."
+    if _FT_CHAIN:  # conv1 -> conv2 -> STNkd conv1 -> conv2 in one launch
+        x1, x2, h1, h2 = ops.pw_chain(pts, [
+            (P["feat.conv1.weight"], P["feat.conv1.bias"], RELU, False, 0),
+            (P["feat.conv2.weight"], P["feat.conv2.bias"], RELU, False, 0),
+            (P[s + "conv1.weight"], P[s + "conv1.bias"], RELU, False, 0),
+            (P[s + "conv2.weight"], P[s + "conv2.bias"], RELU, False, 0)])
+    else:
+        x1 = ops.pw_fwd(pts, P["feat.conv1.weight"], P["feat.conv1.bias"], RELU)
+        x2 = ops.pw_fwd(x1, P["feat.conv2.weight"], P["feat.conv2.bias"], RELU)
+        h1 = ops.pw_fwd(x2, P[s + "conv1.weight"], P[s + "conv1.bias"], RELU)
+        h2 = ops.pw_fwd(h1, P[s + "conv2.weight"], P[s + "conv2.bias"], RELU)
+    gs, gis = ops.conv_max_fwd(h2, P[s + "conv3.weight"], P[s + "conv3.bias"], True)
+    f1 = ops.linear_fwd(gs, P[s + "fc1.weight"], P[s + "fc1.bias"], RELU)
+    f2 = ops.linear_fwd(f1, P[s + "fc2.weight"], P[s + "fc2.bias"], RELU)
+    t = ops.linear_fwd(f2, P[s + "fc3.weight"], P[s + "fc3.bias"], NONE, add_identity_k=64)
+    T = t.view(C, 64, 64)
+    if _FT_CHAIN:  # the transform x2 T and conv3 in one launch
+        x2t, x3 = ops.pw_chain(x2, [(T, None, NONE, True, N),
+                                    (P["feat.conv3.weight"], P["feat.conv3.bias"], RELU,
+                                     False, 0)])
+    else:
+        x2t = ops.pw_fwd(x2, T, None, NONE, kmajor=True, rows_per_w=N)
+        x3 = ops.pw_fwd(x2t, P["feat.conv3.weight"], P["feat.conv3.bias"], RELU)
+    gmax, gidx = ops.conv_max_fwd(x3, P["feat.conv4.weight"], P["feat.conv4.bias"], False)
+    return dict(x1=x1, x2=x2, h1=h1, h2=h2, gs=gs, gis=gis, f1=f1, f2=f2, t=t, T=T, x2t=x2t,
+                x3=x3, gmax=gmax, gidx=gidx)
+
+
+def _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_extra=None):
+    """The extractor's backward by hand from dL/dgmax: sparse max-pool
+    backwards, dT = x2^T dx2t and dx2 = dx2t T^T per cloud (+ dT_extra, the
+    regulariser's gradient when it joins the loss), STNkd's backward, its input
+    gradient added into conv2's; weight gradients written into the flat
+    gradient views Gr, the five point-wise ones' slab sums in one launch."""
+    from . import ops
+    from .ops import ACT_NONE as NONE, ACT_RELU as RELU, _mat
+    C = pts.shape[0]
+    s = "feat.fstn."
+    x1, x2, h1, h2, gs, gis = act["x1"], act["x2"], act["h1"], act["h2"], act["gs"], act["gis"]
+    f1, f2, t, T, x2t, x3, gidx = (act["f1"], act["f2"], act["t"], act["T"], act["x2t"], act["x3"],
+                                   act["gidx"])
+    jobs = []
+    # dz3 = dx3 [x3 > 0] straight from the max-pool backward (its dx rows
+    # already carry conv3's ReLU mask: conv3's backward reads no x3)
+    dz3, _, _ = ops.conv_max_bwd(dgmax, gidx, x3, P["feat.conv4.weight"],
+                                 dw_out=Gr["feat.conv4.weight"], db_out=Gr["feat.conv4.bias"],
+                                 dx_relu=True)
+    w3 = _mat(P["feat.conv3.weight"])
+    dx2t = ops.pw_bwd_data(dz3, None, NONE, w3, 64)
+    ops.pw_bwd_weight(dz3, None, NONE, x2t, dw_out=Gr["feat.conv3.weight"],
+                      db_out=Gr["feat.conv3.bias"], defer=jobs)
+    # x2t = x2 T: dT = x2^T dx2t per cloud, dx2 = dx2t T^T
+    dT, _ = ops.pw_bwd_weight(dx2t, None, NONE, x2, rows_per_group=N, kmajor=True, need_db=False)
+    if dT_extra is not None:
+        dT.add_(dT_extra)
+    dx2 = ops.pw_bwd_data(dx2t, None, NONE, T, 64, kmajor=True, rows_per_w=N)
+    # STNkd backward (models/pointnet.py:59-79); the identity add has no gradient
+    df2, _, _ = ops.linear_bwd(dT.view(C, 64 * 64), t, NONE, None, 0.0, f2, P[s + "fc3.weight"],
+                               dw_out=Gr[s + "fc3.weight"], db_out=Gr[s + "fc3.bias"])
+    df1, _, _ = ops.linear_bwd(df2, f2, RELU, None, 0.0, f1, P[s + "fc2.weight"],
+                               dw_out=Gr[s + "fc2.weight"], db_out=Gr[s + "fc2.bias"])
+    dgs, _, _ = ops.linear_bwd(df1, f1, RELU, None, 0.0, gs, P[s + "fc1.weight"],
+                               dw_out=Gr[s + "fc1.weight"], db_out=Gr[s + "fc1.bias"])
+    dzh2, _, _ = ops.conv_max_bwd(dgs, gis, h2, P[s + "conv3.weight"], gmax_relu=gs,
+                                  dw_out=Gr[s + "conv3.weight"], db_out=Gr[s + "conv3.bias"],
+                                  dx_relu=True)
+    dh1 = ops.pw_bwd_data(dzh2, None, NONE, _mat(P[s + "conv2.weight"]), 64)
+    ops.pw_bwd_weight(dzh2, None, NONE, h1, dw_out=Gr[s + "conv2.weight"],
+                      db_out=Gr[s + "conv2.bias"], defer=jobs)
+    ops.pw_bwd_data(dh1, h1, RELU, _mat(P[s + "conv1.weight"]), 64, out=dx2)
+    ops.pw_bwd_weight(dh1, h1, RELU, x2, dw_out=Gr[s + "conv1.weight"],
+                      db_out=Gr[s + "conv1.bias"], defer=jobs)
+    dx1 = ops.pw_bwd_data(dx2, x2, RELU, _mat(P["feat.conv2.weight"]), 64)
+    ops.pw_bwd_weight(dx2, x2, RELU, x1, dw_out=Gr["feat.conv2.weight"],
+                      db_out=Gr["feat.conv2.bias"], defer=jobs)
+    ops.pw_bwd_weight(dx1, x1, RELU, pts, dw_out=Gr["feat.conv1.weight"],
+                      db_out=Gr["feat.conv1.bias"], defer=jobs)
+    ops.pw_wgrad_finish(jobs)
+
+
 class AdvFtTrainStep(AdvTrainStep):
     """run_training's iteration (utils/trainer.py:426-559) with a
     PointNetCls(k=40, feature_transform=True) generator + DeepConvDiscNet(40, 1)
@@ -587,75 +677,15 @@ class AdvFtTrainStep(AdvTrainStep):
         check(self.lib.pcadv_concat2(pts_gt.data_ptr(), n, pts_nogt.data_ptr(), n, pts.data_ptr(),
                                      self.step_count.data_ptr(), stream_ptr()), "pcadv_concat2")
         # ---- PointNetfeat with the feature transform (pointnet.py:109-130) ----
-        s = "feat.fstn."
-        if _FT_CHAIN:  # conv1 -> conv2 -> STNkd conv1 -> conv2 in one launch
-            x1, x2, h1, h2 = ops.pw_chain(pts, [
-                (P["feat.conv1.weight"], P["feat.conv1.bias"], RELU, False, 0),
-                (P["feat.conv2.weight"], P["feat.conv2.bias"], RELU, False, 0),
-                (P[s + "conv1.weight"], P[s + "conv1.bias"], RELU, False, 0),
-                (P[s + "conv2.weight"], P[s + "conv2.bias"], RELU, False, 0)])
-        else:
-            x1 = ops.pw_fwd(pts, P["feat.conv1.weight"], P["feat.conv1.bias"], RELU)
-            x2 = ops.pw_fwd(x1, P["feat.conv2.weight"], P["feat.conv2.bias"], RELU)
-            h1 = ops.pw_fwd(x2, P[s + "conv1.weight"], P[s + "conv1.bias"], RELU)
-            h2 = ops.pw_fwd(h1, P[s + "conv2.weight"], P[s + "conv2.bias"], RELU)
-        gs, gis = ops.conv_max_fwd(h2, P[s + "conv3.weight"], P[s + "conv3.bias"], True)
-        f1 = ops.linear_fwd(gs, P[s + "fc1.weight"], P[s + "fc1.bias"], RELU)
-        f2 = ops.linear_fwd(f1, P[s + "fc2.weight"], P[s + "fc2.bias"], RELU)
-        t = ops.linear_fwd(f2, P[s + "fc3.weight"], P[s + "fc3.bias"], NONE, add_identity_k=64)
-        T = t.view(C, 64, 64)
-        if _FT_CHAIN:  # the transform x2 T and conv3 in one launch
-            x2t, x3 = ops.pw_chain(x2, [(T, None, NONE, True, N),
-                                        (P["feat.conv3.weight"], P["feat.conv3.bias"], RELU,
-                                         False, 0)])
-        else:
-            x2t = ops.pw_fwd(x2, T, None, NONE, kmajor=True, rows_per_w=N)
-            x3 = ops.pw_fwd(x2t, P["feat.conv3.weight"], P["feat.conv3.bias"], RELU)
-        gmax, gidx = ops.conv_max_fwd(x3, P["feat.conv4.weight"], P["feat.conv4.bias"], False)
+        act = _ft_extractor_forward(P, pts, N)
+        gmax = act["gmax"]
         # ---- fc1 on: the fused step's tail (part 3) -> dL/dgmax ---------------
         dgmax = self.dgmax[:C]
         a.feat_gmax, a.feat_dgmax = gmax.data_ptr(), dgmax.data_ptr()
         self._keep_last = (a, gmax)
         check(self.lib.pcadv_adv_step(ctypes.byref(a), stream_ptr()), "pcadv_adv_step (part 3)")
-        # ---- the extractor's backward (the five point-wise weight gradients'
-        #      slab sums deferred to one launch at the end) -----------------------
-        jobs = []
-        # dz3 = dx3 [x3 > 0] straight from the max-pool backward (its dx rows
-        # already carry conv3's ReLU mask: conv3's backward reads no x3)
-        dz3, _, _ = ops.conv_max_bwd(dgmax, gidx, x3, P["feat.conv4.weight"],
-                                     dw_out=Gr["feat.conv4.weight"], db_out=Gr["feat.conv4.bias"],
-                                     dx_relu=True)
-        w3 = _mat(P["feat.conv3.weight"])
-        dx2t = ops.pw_bwd_data(dz3, None, NONE, w3, 64)
-        ops.pw_bwd_weight(dz3, None, NONE, x2t, dw_out=Gr["feat.conv3.weight"],
-                          db_out=Gr["feat.conv3.bias"], defer=jobs)
-        # x2t = x2 T: dT = x2^T dx2t per cloud, dx2 = dx2t T^T
-        dT, _ = ops.pw_bwd_weight(dx2t, None, NONE, x2, rows_per_group=N, kmajor=True,
-                                  need_db=False)
-        dx2 = ops.pw_bwd_data(dx2t, None, NONE, T, 64, kmajor=True, rows_per_w=N)
-        # STNkd backward (models/pointnet.py:59-79); the identity add has no gradient
-        df2, _, _ = ops.linear_bwd(dT.view(C, 64 * 64), t, NONE, None, 0.0, f2,
-                                   P[s + "fc3.weight"], dw_out=Gr[s + "fc3.weight"],
-                                   db_out=Gr[s + "fc3.bias"])
-        df1, _, _ = ops.linear_bwd(df2, f2, RELU, None, 0.0, f1, P[s + "fc2.weight"],
-                                   dw_out=Gr[s + "fc2.weight"], db_out=Gr[s + "fc2.bias"])
-        dgs, _, _ = ops.linear_bwd(df1, f1, RELU, None, 0.0, gs, P[s + "fc1.weight"],
-                                   dw_out=Gr[s + "fc1.weight"], db_out=Gr[s + "fc1.bias"])
-        dzh2, _, _ = ops.conv_max_bwd(dgs, gis, h2, P[s + "conv3.weight"], gmax_relu=gs,
-                                      dw_out=Gr[s + "conv3.weight"], db_out=Gr[s + "conv3.bias"],
-                                      dx_relu=True)
-        dh1 = ops.pw_bwd_data(dzh2, None, NONE, _mat(P[s + "conv2.weight"]), 64)
-        ops.pw_bwd_weight(dzh2, None, NONE, h1, dw_out=Gr[s + "conv2.weight"],
-                          db_out=Gr[s + "conv2.bias"], defer=jobs)
-        ops.pw_bwd_data(dh1, h1, RELU, _mat(P[s + "conv1.weight"]), 64, out=dx2)
-        ops.pw_bwd_weight(dh1, h1, RELU, x2, dw_out=Gr[s + "conv1.weight"],
-                          db_out=Gr[s + "conv1.bias"], defer=jobs)
-        dx1 = ops.pw_bwd_data(dx2, x2, RELU, _mat(P["feat.conv2.weight"]), 64)
-        ops.pw_bwd_weight(dx2, x2, RELU, x1, dw_out=Gr["feat.conv2.weight"],
-                          db_out=Gr["feat.conv2.bias"], defer=jobs)
-        ops.pw_bwd_weight(dx1, x1, RELU, pts, dw_out=Gr["feat.conv1.weight"],
-                          db_out=Gr["feat.conv1.bias"], defer=jobs)
-        ops.pw_wgrad_finish(jobs)
+        # ---- the extractor's backward -------------------------------------------
+        _ft_extractor_backward(P, Gr, act, pts, dgmax, N)
         if apply_adam:
             self.adam()
         self._post()
@@ -857,3 +887,122 @@ class ClsTrainStep:
             set_optimizer_step(self.optimizer, float(self.step_count.item()))
 
     after_torch_step = AdvTrainStep.after_torch_step
+
+
+class ClsFtTrainStep(ClsTrainStep):
+    """run_training_pointnet_cls's iteration (utils/trainer.py:222-268) with
+    PointNetCls(k=40, feature_transform=True), without autograd: the
+    extractor's forward on the point-wise kernels (_ft_extractor_forward: two
+    chained launches, STNkd, the transform), the cls step's head on those
+    pooled features (pcadv_cls_step part 3: fc1, fc2 + dropout, fc3 + CE and
+    lambda_cls dCE back to dL/dgmax), feature_transform_regularizer(T) and
+    lambda_regu times its gradient (models/pointnet.py:345-353, trainer.py:
+    259-266), the extractor's backward by hand, one Adam launch.  losses =
+    [loss_cls, loss_regu] (the two values the reference logs).  Parameters,
+    gradients and Adam moments are flat buffers in ft_layout order bound to
+    the model and optimizer as ClsTrainStep's."""
+
+    def __init__(self, model, B, N, optimizer=None, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
+                 lambda_cls=1.0, lambda_regu=0.001, seed=0, device="cuda", rng_rank=0,
+                 rng_world=1):
+        self.lib = _lib.load()
+        self.set_rng_rank(rng_rank, rng_world)
+        if not getattr(model, "feature_transform", False):
+            raise ValueError("ClsFtTrainStep: the model has no feature transform (use ClsTrainStep)")
+        self.model = model
+        self.precision = 0
+        self.B, self.N = int(B), int(N)
+        if self.N % 128:
+            raise ValueError(f"ClsFtTrainStep: N = {self.N} points, a multiple of 128 is required")
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("ClsFtTrainStep runs on the HIP device only")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        if optimizer is not None:
+            g = optimizer.param_groups[0]
+            lr, betas, eps = g["lr"], tuple(g["betas"]), g["eps"]
+        self.hp = dict(lr=float(lr), betas=tuple(float(b) for b in betas), eps=float(eps),
+                       lambda_cls=float(lambda_cls), p=float(model.dropout.p))
+        self.layout, self.g_numel = ft_layout(model)
+        self.g_param = flatten_params(model, self.layout, self.g_numel, dev)
+        self.g_grad = torch.zeros(self.g_numel, device=dev)
+        self.g_m = torch.zeros_like(self.g_param)
+        self.g_v = torch.zeros_like(self.g_param)
+        t0 = _adopt_adam_state(optimizer, model, self.g_m, self.g_v, self.layout)
+        self.step_count = torch.full((1,), t0, device=dev, dtype=torch.int32)
+        _bind_adam_state(optimizer, model, self.g_m, self.g_v, self.g_grad, self.layout, t0)
+        self._bind = ((optimizer, model, self.g_m, self.g_v, self.g_grad, self.layout),)
+        self.optimizer = optimizer
+        self.losses = torch.zeros(2, device=dev)  # [loss_cls, loss_regu]
+        self.logits = torch.zeros(self.B, 40, device=dev)
+        nbytes = self.lib.pcadv_adv_step_workspace_bytes(self.B, self.N)
+        self.workspace = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._keep = []
+        self.dgmax = torch.empty(self.B, 1024, device=dev)
+        self._norms = torch.empty(self.B, device=dev)
+        self._lregu = torch.full((1,), float(lambda_regu), device=dev)
+        self._p = dict(model.named_parameters())
+        self._g = _views(self.g_grad, model, self.layout)
+
+    @property
+    def lambda_regu(self):
+        return float(self._lregu.item())
+
+    # gathers / epilogue as this call's own first and last launches
+    _pre = AdvFtTrainStep._pre
+    _post = AdvFtTrainStep._post
+
+    def __call__(self, pts, labels, mask=None, apply_adam=True):
+        from . import ops
+        a = self._args(pts, labels, mask, False)
+        a.part = 3
+        a.gather, a.ngather = None, 0
+        a.epi_counters, a.epi_ncounters, a.epi_ring = None, 0, None
+        B, N = int(pts.shape[0]), self.N
+        P, Gr = self._p, self._g
+        self._pre()
+        act = _ft_extractor_forward(P, pts, N)
+        # fc1 .. CE and back to dL/dgmax: the cls step's head (part 3); its
+        # dropout draws read the step count of the completed steps
+        dgmax = self.dgmax[:B]
+        a.feat_gmax, a.feat_dgmax = act["gmax"].data_ptr(), dgmax.data_ptr()
+        self._keep_last = (a, act["gmax"])
+        check(self.lib.pcadv_cls_step(ctypes.byref(a), stream_ptr()), "pcadv_cls_step (part 3)")
+        # loss += lambda_regu * ||T T^T - I||_F mean (trainer.py:259-266): its
+        # value into losses[1], lambda_regu times its gradient into dT
+        T = act["T"]
+        check(self.lib.pcadv_tnet_reg_fwd(T.data_ptr(), B, 64, self._norms.data_ptr(),
+                                          self.losses.data_ptr() + 4, stream_ptr()),
+              "pcadv_tnet_reg_fwd")
+        dT_reg = ops.tnet_reg_bwd(T, self._lregu)
+        _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_extra=dT_reg)
+        if apply_adam:  # advances the step count, then optimizer.step()
+            hp = self.hp
+            check(self.lib.pcadv_adam(self.g_param.data_ptr(), self.g_grad.data_ptr(),
+                                      self.g_m.data_ptr(), self.g_v.data_ptr(), self.g_numel,
+                                      self.step_count.data_ptr(), hp["lr"], hp["betas"][0],
+                                      hp["betas"][1], hp["eps"], stream_ptr()), "pcadv_adam")
+        self._post()
+        return self.losses
+
+    def capture_on(self, pts, labels):
+        """One iteration over resident buffers as a HIP graph (state restored)."""
+        saved = [t.clone() for t in (self.g_param, self.g_m, self.g_v, self.step_count)]
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self(pts, labels)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self(pts, labels)
+        torch.cuda.synchronize()
+        for dst, src in zip((self.g_param, self.g_m, self.g_v, self.step_count), saved):
+            dst.copy_(src)
+        return g
+
+    def capture_seq(self, batches):
+        raise NotImplementedError("ClsFtTrainStep: one iteration per graph")

@@ -899,43 +899,57 @@ def run_training_semi(trainloader_gt, trainloader_nogt, trainloader_gt_iter,
 def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, model, cls_loss,
                               optimizer, train_logger, test_logger, writer, args):
     """utils/trainer.py:222-308 (supervised baseline, no discriminator).  With
-    PointNetCls(k=40, feature_transform=False), CrossEntropyLoss and Adam on the
-    HIP device each iteration is one ClsTrainStep (pcadv_cls_step); otherwise
-    (e.g. feature_transform=True, whose regulariser joins the loss) the
-    reference's body runs through autograd over the same kernels."""
-    from .step import ClsTrainStep
+    PointNetCls(k=40), CrossEntropyLoss and Adam on the HIP device each
+    iteration is one ClsTrainStep (pcadv_cls_step), or with
+    feature_transform=True one ClsFtTrainStep (its regulariser in the loss);
+    otherwise the reference's body runs through autograd over the same
+    kernels."""
+    from .step import ClsFtTrainStep, ClsTrainStep
     max_test_accu = float("-inf")
     max_train_epoch = 0
-    fused = (isinstance(model, PointNetCls) and not model.feature_transform
-             and model.fc3.out_features == 40 and type(optimizer) is torch.optim.Adam
-             and len(optimizer.param_groups) == 1
-             and not optimizer.param_groups[0].get("weight_decay", 0)
-             and not optimizer.param_groups[0].get("amsgrad")
-             and type(cls_loss) is torch.nn.CrossEntropyLoss and cls_loss.weight is None
-             and cls_loss.reduction == "mean" and cls_loss.label_smoothing == 0.0
-             and str(args.device).split(":")[0] == "cuda")
+    fusable = (isinstance(model, PointNetCls)
+               and model.fc3.out_features == 40 and type(optimizer) is torch.optim.Adam
+               and len(optimizer.param_groups) == 1
+               and not optimizer.param_groups[0].get("weight_decay", 0)
+               and not optimizer.param_groups[0].get("amsgrad")
+               and type(cls_loss) is torch.nn.CrossEntropyLoss and cls_loss.weight is None
+               and cls_loss.reduction == "mean" and cls_loss.label_smoothing == 0.0
+               and str(args.device).split(":")[0] == "cuda")
+    fused = fusable and not model.feature_transform
+    # feature_transform=True: the fused FT cls step (step.ClsFtTrainStep: the
+    # regulariser joins the loss there); args.fused_ft = False keeps the
+    # autograd body
+    fused_ft = fusable and model.feature_transform and bool(getattr(args, "fused_ft", True))
     step = None
-    graphed = (fused and bool(getattr(args, "use_graph", True)) and _device_loaders(trainloader_gt)
-               and trainloader_gt.B <= MAX_FUSED_B)
+    graphed = ((fused or fused_ft) and bool(getattr(args, "use_graph", True))
+               and _device_loaders(trainloader_gt) and trainloader_gt.B <= MAX_FUSED_B
+               and (not fused_ft or trainloader_gt.npts % 128 == 0))
     gi = None
     log_every = max(1, int(getattr(args, "log_every", 1)))
-    # feature_transform=True with a capturable optimizer over a DeviceCloudLoader:
-    # each full batch's gather + autograd body replayed as one HIP graph
-    ft_graphed = (not fused) and _AutogradClsStep.graphable(model, optimizer, args, trainloader_gt)
+    # feature_transform=True off the fused step, with a capturable optimizer over
+    # a DeviceCloudLoader: each full batch's gather + autograd body replayed as
+    # one HIP graph
+    ft_graphed = (not fused and not fused_ft) and _AutogradClsStep.graphable(
+        model, optimizer, args, trainloader_gt)
 
     def emit(i_iter, vals, regu):
         train_logger.info("iter = {0:8d}/{1:8d} loss_cls = {2:.3f} loss regu = {3:.3f} ".format(
             i_iter, args.total_iterations, vals[0], vals[1] if regu is None else regu))
 
-    log = _LossRing(emit, 2 if ft_graphed else 1, args.device)
+    two = ft_graphed or fused_ft  # [loss_cls, loss_regu] in the ring
+    log = _LossRing(emit, 2 if two else 1, args.device)
 
     def fused_step(B, N):
         nonlocal step
         if step is None or step.N != N or step.B < B:
             if step is not None:
                 step.sync_optimizer_state()
-            step = ClsTrainStep(model, B, N, optimizer=optimizer, lambda_cls=args.lambda_cls,
-                                seed=int(getattr(args, "seed", 0)) + i_iter, device=args.device)
+            seed = int(getattr(args, "seed", 0)) + i_iter
+            step = (ClsFtTrainStep(model, B, N, optimizer=optimizer, lambda_cls=args.lambda_cls,
+                                   lambda_regu=args.lambda_regu, seed=seed, device=args.device)
+                    if fused_ft else
+                    ClsTrainStep(model, B, N, optimizer=optimizer, lambda_cls=args.lambda_cls,
+                                 seed=seed, device=args.device))
         step.sync_hyper()
         return step
 
@@ -961,11 +975,12 @@ def run_training_pointnet_cls(trainloader_gt, trainloader_gt_iter, testloader, m
             pts, cls = batch
         if losses is None:
             pts, cls = pts.float().to(args.device).contiguous(), cls.long().to(args.device).contiguous()
-            if fused and pts.shape[0] <= MAX_FUSED_B:
+            if ((fused or fused_ft) and pts.shape[0] <= MAX_FUSED_B
+                    and (not fused_ft or pts.shape[1] % 128 == 0)):
                 losses = fused_step(pts.shape[0], pts.shape[1])(pts, cls)
                 log.write(losses)
         if losses is not None:
-            log.record(i_iter, None if ft_graphed else 0.0, log=i_iter % log_every == 0)
+            log.record(i_iter, None if two else 0.0, log=i_iter % log_every == 0)
         else:
             if step is not None:
                 step.sync_optimizer_state()

@@ -570,82 +570,107 @@ def bench_cls(args):
 
 def bench_cls_ft(args):
     """run_training_pointnet_cls with PointNetCls(k=40, feature_transform=True)
-    (utils/trainer.py:254-268: CE + 0.001 x the regulariser, Adam): the fused
-    cls step does not cover the feature transform, so this is the autograd body
-    over the layer-by-layer kernels (point-wise conv1..conv3, the STNkd(64) and
-    transform kernels, conv4 + max, the head), fp32 throughout, with torch's
-    Adam (fused where available, else capturable); one HIP graph per resident
-    batch when capture works, else eager."""
+    (utils/trainer.py:254-268: CE + 0.001 x the regulariser, Adam).  Default:
+    the fused feature-transform cls step run_training_pointnet_cls uses
+    (step.ClsFtTrainStep: the extractor's forward in chained point-wise
+    launches, the cls step's head on its pooled features, the regulariser and
+    the extractor backward by hand, one Adam launch), one HIP graph per
+    resident batch.  --ft-body: the reference's body through autograd over the
+    same kernels with torch's Adam (fused where available, else capturable),
+    the path before round 6."""
     import adversarial_learning_on_pointclouds_amd as pc
     from adversarial_learning_on_pointclouds_amd.pointnet import feature_transform_regularizer
+    from adversarial_learning_on_pointclouds_amd.step import ClsFtTrainStep
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = pc.PointNetCls(k=40, feature_transform=True).to(dev).train()
-    try:  # one fused multi-tensor kernel per step where this torch build has it
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), fused=True,
-                               capturable=True)
-        adam = "torch.optim.Adam(fused=True, capturable=True)"
-    except (RuntimeError, ValueError):
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), capturable=True)
-        adam = "torch.optim.Adam(capturable=True)"
     pool = []
     for k in range(POOL):
         rng = np.random.default_rng(3000 + k)
         pool.append((torch.from_numpy(rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)).to(dev),
                      torch.from_numpy(rng.integers(0, 40, B)).to(dev)))
-    losses = torch.zeros(POOL, device=dev)
-
-    def body(pts, lab, k):
-        opt.zero_grad()  # captured: backward's gradients become p.grad, no accumulate adds
-        logits, _, trans = model(pts)
-        loss = torch.nn.functional.cross_entropy(logits, lab) + 0.001 * feature_transform_regularizer(trans)
-        loss.backward()
-        opt.step()
-        losses[k].copy_(loss.detach())
-
-    side = torch.cuda.Stream(device=dev)
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):  # autograd / optimizer state created outside any capture
-        for k in range(3):
-            body(*pool[k % POOL], k % POOL)
-    torch.cuda.current_stream().wait_stream(side)
-    torch.cuda.synchronize()
     graphs, why = [], None
-    if not args.no_graph:
-        try:
-            kept = []  # each graph's gradient buffers (the next capture drops p.grad)
-            for k in range(POOL):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    body(*pool[k], k)
-                graphs.append(g)
-                kept.append([p.grad for p in model.parameters()])
-        except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
-            graphs, why = [], f"{type(e).__name__}: {e}"[:200]
-            torch.cuda.synchronize()
+    if not args.ft_body:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999))
+        adam = "fused (pcadv_adam over the flat generator buffer)"
+        step = ClsFtTrainStep(model, B, N, optimizer=opt, lambda_regu=0.001, seed=1234, device=dev)
+        if not args.no_graph:
+            graphs = [step.capture_on(*p) for p in pool]
+        workload = ("run_training_pointnet_cls with PointNetCls(k=40, feature_transform=True): "
+                    "CE + 0.001 regulariser, Adam; fused feature-transform cls step (ClsFtTrainStep)")
+
+        def loss_now(k):
+            return float(step.losses[0].item()) + 0.001 * float(step.losses[1].item())
+
+        def run(k):
+            step(*pool[k % POOL])
+    else:
+        try:  # one fused multi-tensor kernel per step where this torch build has it
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), fused=True,
+                                   capturable=True)
+            adam = "torch.optim.Adam(fused=True, capturable=True)"
+        except (RuntimeError, ValueError):
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999), capturable=True)
+            adam = "torch.optim.Adam(capturable=True)"
+        losses = torch.zeros(POOL, device=dev)
+
+        def body(pts, lab, k):
+            opt.zero_grad()  # captured: backward's gradients become p.grad, no accumulate adds
+            logits, _, trans = model(pts)
+            loss = (torch.nn.functional.cross_entropy(logits, lab)
+                    + 0.001 * feature_transform_regularizer(trans))
+            loss.backward()
+            opt.step()
+            losses[k].copy_(loss.detach())
+
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # autograd / optimizer state created outside any capture
+            for k in range(3):
+                body(*pool[k % POOL], k % POOL)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        if not args.no_graph:
+            try:
+                kept = []  # each graph's gradient buffers (the next capture drops p.grad)
+                for k in range(POOL):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        body(*pool[k], k)
+                    graphs.append(g)
+                    kept.append([p.grad for p in model.parameters()])
+            except Exception as e:  # noqa: BLE001 - reported in the line, eager timing instead
+                graphs, why = [], f"{type(e).__name__}: {e}"[:200]
+                torch.cuda.synchronize()
+        workload = ("run_training_pointnet_cls with PointNetCls(k=40, feature_transform=True): "
+                    "CE + 0.001 regulariser, Adam, autograd over the pcadv ops")
+
+        def loss_now(k):
+            return float(losses[k % POOL].item())
+
+        def run(k):
+            body(*pool[k % POOL], k % POOL)
 
     def one(k):
         if graphs:
             graphs[k % POOL].replay()
         else:
-            body(*pool[k % POOL], k % POOL)
+            run(k)
     for k in range(args.warmup):
         one(k)
     regions = timed_regions(one, args.steps, args.repeats)
     dt = float(np.median(regions))
-    loss = float(losses[(args.steps - 1) % POOL].item())
+    loss = loss_now(args.steps - 1)
     out = {
         "metric": "point-clouds/sec (cls train step with feature_transform=True), B=32 N=1024 "
                   "ModelNet40, 1 GPU",
         "value": round(B * args.steps / dt, 1), "unit": "clouds/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32 (layer-by-layer kernels: exact-f32 MFMA point-wise layers, split-product "
-                 "conv4 + exact max re-evaluation)",
+        "dtype": "fp32 (exact-f32 MFMA point-wise layers, split-product 1024-channel conv + max "
+                 "with the exact max re-evaluated, head f32)",
         "data": "synthetic (seeded U(-1,1) clouds, labels in [0,40); resident in HBM)",
-        "config": {"workload": "run_training_pointnet_cls with PointNetCls(k=40, "
-                               "feature_transform=True): CE + 0.001 regulariser, Adam, autograd "
-                               "over the pcadv ops", "global_batch": B, "points": N,
+        "config": {"workload": workload, "global_batch": B, "points": N,
                    "parallelism": "dp1", "hip_graph": bool(graphs), "optimizer": adam},
         "timing": {"regions_s": [round(r, 6) for r in regions], "reported": "median"},
         "loss_last_step": round(loss, 5), "finite": bool(np.isfinite(loss)),

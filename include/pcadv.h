@@ -536,7 +536,8 @@ typedef struct pcadv_adv_args {
    *     except the generator's conv1..conv4, g_grad[0, PCADV_G_FC1_W));
    * 2 = the feature backward (those conv1..conv4 gradients; and both Adam
    *     updates when apply_adam) on the state part 1 left in the workspace;
-   * 3 = part 1 from fc1 on, over the caller's features (feat_* below). */
+   * 3 = part 1 from fc1 on, over the caller's features (feat_* below);
+   *     pcadv_cls_step takes 0 or 3 (ABI 9: its head on given features). */
   int part;
   /* feature forward precision: 0 = f32-level (default), 1 = bf16 (as
    * pcadv_feat_fwd_bf16; the head, the discriminator and every backward stay
@@ -604,7 +605,11 @@ int pcadv_adv_step_adam(const pcadv_adv_args* args, hipStream_t stream);
  * and (apply_adam) the generator's Adam step.  Uses the generator fields of
  * pcadv_adv_args (pts_nogt, d_*, soft_*, lambda_adv, semi ignored);
  * drop_mask_gt optional (else device-drawn); losses[0] = CE; workspace as
- * pcadv_adv_step_workspace_bytes(B, N). */
+ * pcadv_adv_step_workspace_bytes(B, N).  part = 3 (ABI 9): the head alone on
+ * the caller's pooled features feat_gmax [B][1024] (fc1 .. the CE, and back to
+ * feat_dgmax = dL/dgmax and the head's gradients), for the feature-transform
+ * generator's step whose extractor runs outside; the caller advances
+ * *step_count first (the dropout draws read it) and runs Adam. */
 int pcadv_cls_step(const pcadv_adv_args* args, hipStream_t stream);
 
 #ifdef __cplusplus
