@@ -151,6 +151,7 @@ SIGNATURES = {
     "pcadv_conv_max_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _i, _vp]),
     "pcadv_tnet_reg_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pcadv_tnet_reg_bwd": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "pcadv_tnet_reg_step": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "pcadv_gemm": (_i, [_vp, _i64, _i, _vp, _i64, _i, _vp, _i64, _i, _i, _i, _vp, _vp, _i, _i, _i,
                         _vp, _i64, _i, _vp, _vp, _i64, _vp]),
     "pcadv_gemm_bf2": (_i, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i, _i, _i,

@@ -51,7 +51,8 @@ int launch_pw_bwd_weight(const float*, const float*, int, const float*, int, int
                          float*, float*, void*, size_t, hipStream_t);
 int launch_convmax_bwd(const float*, const int32_t*, const float*, const float*, int, int, int,
                        const float*, int, float*, float*, float*, hipStream_t, int);
-int launch_tnet_reg(const float*, int, int, float*, float*, const float*, float*, hipStream_t);
+int launch_tnet_reg(const float*, int, int, float*, float*, const float*, float*, hipStream_t,
+                    int accumulate = 0, int32_t* step_inc = nullptr);
 int launch_adam2(float*, const float*, float*, float*, int64_t, float, float*, const float*,
                  float*, float*, int64_t, float, const int32_t*, int, float, float, float,
                  hipStream_t);
@@ -665,6 +666,13 @@ int pcadv_tnet_reg_bwd(const float* T, int B, int k, const float* grad_reg, floa
                        hipStream_t stream) {
   PC_REQUIRE(grad_reg && dT, "tnet_reg_bwd: grad_reg and dT are required");
   return launch_tnet_reg(T, B, k, nullptr, nullptr, grad_reg, dT, stream);
+}
+
+int pcadv_tnet_reg_step(const float* T, int B, int k, float* norms, float* reg,
+                        const float* grad_reg, float* dT, int32_t* step_count,
+                        hipStream_t stream) {
+  PC_REQUIRE(norms && reg && grad_reg && dT, "tnet_reg_step: norms, reg, grad_reg and dT are required");
+  return launch_tnet_reg(T, B, k, norms, reg, grad_reg, dT, stream, 1, step_count);
 }
 
 int pcadv_linear_bwd(const float* dy, const float* y, int act, const float* drop_mask,

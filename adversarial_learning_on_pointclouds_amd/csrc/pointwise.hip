@@ -857,11 +857,14 @@ k_convmax_bwd(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 
 // ---------------------------------------------------------------------------
 // feature_transform_regularizer: ||T T^T - I||_F per cloud and its gradient
-// (2 * gscale / (B n_b)) (T T^T - I) T
+// (2 * gscale / (B n_b)) (T T^T - I) T, stored or (accumulate) added into dT;
+// norms (nullable) written in either mode; step_inc (nullable): block 0 also
+// advances the step counter (the fused cls FT step's, ahead of its Adam)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 k_tnet_reg(const float* __restrict__ T, int B, int k, float* __restrict__ norms,
-           const float* __restrict__ gscale, float* __restrict__ dT) {
+           const float* __restrict__ gscale, float* __restrict__ dT, int accumulate,
+           int32_t* __restrict__ step_inc) {
   extern __shared__ float sm[];
   const int ks = k + 1;       // LDS row stride: row j's element l for 32 consecutive j
   float* t = sm;              //   hits 32 banks (stride k = 64 was one bank)
@@ -913,10 +916,9 @@ k_tnet_reg(const float* __restrict__ T, int B, int k, float* __restrict__ norms,
     __syncthreads();
   }
   const float n = (float)sqrt(part[0]);
-  if (!dT) {
-    if (tid == 0) norms[b] = n;
-    return;
-  }
+  if (norms && tid == 0) norms[b] = n;
+  if (step_inc && b == 0 && tid == 0) *step_inc += 1;
+  if (!dT) return;
   const float scale = 2.f * (*gscale) / ((float)B * n);
   if (k == 64) {  // (T T^T - I) T in 4 x 4 blocks
     const int i0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);
@@ -936,13 +938,16 @@ k_tnet_reg(const float* __restrict__ T, int B, int k, float* __restrict__ norms,
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dT[(size_t)b * k * k + (i0 + u) * k + j0 + q] = scale * v[u][q];
+      for (int q = 0; q < 4; ++q) {
+        float* d = &dT[(size_t)b * k * k + (i0 + u) * k + j0 + q];
+        *d = accumulate ? *d + scale * v[u][q] : scale * v[u][q];
+      }
   } else {
     for (int e = tid; e < k * k; e += 256) {
       const int i = e / k, j = e % k;
       float v = 0.f;
       for (int l = 0; l < k; ++l) v = fmaf(a[i * ks + l], t[l * ks + j], v);
-      dT[(size_t)b * k * k + e] = scale * v;
+      dT[(size_t)b * k * k + e] = accumulate ? dT[(size_t)b * k * k + e] + scale * v : scale * v;
     }
   }
 }
@@ -1152,21 +1157,19 @@ int launch_convmax_bwd(const float* dg, const int32_t* gidx, const float* gmax, 
 }
 
 int launch_tnet_reg(const float* T, int B, int k, float* norms, float* reg,
-                    const float* gscale, float* dT, hipStream_t s) {
+                    const float* gscale, float* dT, hipStream_t s, int accumulate,
+                    int32_t* step_inc) {
   PC_REQUIRE(B > 0 && k > 0 && k <= 64, "tnet_reg: unsupported B=%d k=%d", B, k);
+  PC_REQUIRE(!dT || gscale, "tnet_reg: the gradient needs the upstream gradient");
+  PC_REQUIRE(!reg || norms, "tnet_reg: the mean needs the per-cloud norms");
   const size_t lds = 2 * (size_t)k * (k + 1) * sizeof(float);
-  if (!dT) {
-    hipLaunchKernelGGL(k_tnet_reg, dim3(B), dim3(256), lds, s, T, B, k, norms, nullptr, nullptr);
-    PC_HIP_CHECK_LAUNCH("k_tnet_reg");
-    if (reg) {
-      hipLaunchKernelGGL(k_mean, dim3(1), dim3(64), 0, s, norms, B, reg);
-      PC_HIP_CHECK_LAUNCH("k_mean");
-    }
-    return PCADV_OK;
-  }
-  PC_REQUIRE(gscale, "tnet_reg: backward needs the upstream gradient");
-  hipLaunchKernelGGL(k_tnet_reg, dim3(B), dim3(256), lds, s, T, B, k, norms, gscale, dT);
+  hipLaunchKernelGGL(k_tnet_reg, dim3(B), dim3(256), lds, s, T, B, k, norms, dT ? gscale : nullptr,
+                     dT, accumulate, step_inc);
   PC_HIP_CHECK_LAUNCH("k_tnet_reg");
+  if (reg) {
+    hipLaunchKernelGGL(k_mean, dim3(1), dim3(64), 0, s, norms, B, reg);
+    PC_HIP_CHECK_LAUNCH("k_mean");
+  }
   return PCADV_OK;
 }
 

@@ -496,12 +496,13 @@ def _ft_extractor_forward(P, pts, N):
                 x3=x3, gmax=gmax, gidx=gidx)
 
 
-def _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_extra=None):
+def _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_hook=None):
     """The extractor's backward by hand from dL/dgmax: sparse max-pool
-    backwards, dT = x2^T dx2t and dx2 = dx2t T^T per cloud (+ dT_extra, the
-    regulariser's gradient when it joins the loss), STNkd's backward, its input
-    gradient added into conv2's; weight gradients written into the flat
-    gradient views Gr, the five point-wise ones' slab sums in one launch."""
+    backwards, dT = x2^T dx2t and dx2 = dx2t T^T per cloud (dT_hook(dT) then
+    adds the regulariser's gradient in place when it joins the loss), STNkd's
+    backward, its input gradient added into conv2's; weight gradients written
+    into the flat gradient views Gr, the five point-wise ones' slab sums in
+    one launch."""
     from . import ops
     from .ops import ACT_NONE as NONE, ACT_RELU as RELU, _mat
     C = pts.shape[0]
@@ -521,8 +522,8 @@ def _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_extra=None):
                       db_out=Gr["feat.conv3.bias"], defer=jobs)
     # x2t = x2 T: dT = x2^T dx2t per cloud, dx2 = dx2t T^T
     dT, _ = ops.pw_bwd_weight(dx2t, None, NONE, x2, rows_per_group=N, kmajor=True, need_db=False)
-    if dT_extra is not None:
-        dT.add_(dT_extra)
+    if dT_hook is not None:
+        dT_hook(dT)
     dx2 = ops.pw_bwd_data(dx2t, None, NONE, T, 64, kmajor=True, rows_per_w=N)
     # STNkd backward (models/pointnet.py:59-79); the identity add has no gradient
     df2, _, _ = ops.linear_bwd(dT.view(C, 64 * 64), t, NONE, None, 0.0, f2, P[s + "fc3.weight"],
@@ -956,7 +957,6 @@ class ClsFtTrainStep(ClsTrainStep):
     _post = AdvFtTrainStep._post
 
     def __call__(self, pts, labels, mask=None, apply_adam=True):
-        from . import ops
         a = self._args(pts, labels, mask, False)
         a.part = 3
         a.gather, a.ngather = None, 0
@@ -972,19 +972,24 @@ class ClsFtTrainStep(ClsTrainStep):
         self._keep_last = (a, act["gmax"])
         check(self.lib.pcadv_cls_step(ctypes.byref(a), stream_ptr()), "pcadv_cls_step (part 3)")
         # loss += lambda_regu * ||T T^T - I||_F mean (trainer.py:259-266): its
-        # value into losses[1], lambda_regu times its gradient into dT
+        # value into losses[1], lambda_regu times its gradient added into the
+        # bmm's dT, and (with Adam) the step count advanced, in one launch + the mean
         T = act["T"]
-        check(self.lib.pcadv_tnet_reg_fwd(T.data_ptr(), B, 64, self._norms.data_ptr(),
-                                          self.losses.data_ptr() + 4, stream_ptr()),
-              "pcadv_tnet_reg_fwd")
-        dT_reg = ops.tnet_reg_bwd(T, self._lregu)
-        _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_extra=dT_reg)
-        if apply_adam:  # advances the step count, then optimizer.step()
+
+        def regulariser(dT):
+            check(self.lib.pcadv_tnet_reg_step(
+                T.data_ptr(), B, 64, self._norms.data_ptr(), self.losses.data_ptr() + 4,
+                self._lregu.data_ptr(), dT.data_ptr(),
+                self.step_count.data_ptr() if apply_adam else None, stream_ptr()),
+                "pcadv_tnet_reg_step")
+        _ft_extractor_backward(P, Gr, act, pts, dgmax, N, dT_hook=regulariser)
+        if apply_adam:  # optimizer.step() at the count advanced above
             hp = self.hp
-            check(self.lib.pcadv_adam(self.g_param.data_ptr(), self.g_grad.data_ptr(),
-                                      self.g_m.data_ptr(), self.g_v.data_ptr(), self.g_numel,
-                                      self.step_count.data_ptr(), hp["lr"], hp["betas"][0],
-                                      hp["betas"][1], hp["eps"], stream_ptr()), "pcadv_adam")
+            check(self.lib.pcadv_adam2(self.g_param.data_ptr(), self.g_grad.data_ptr(),
+                                       self.g_m.data_ptr(), self.g_v.data_ptr(), self.g_numel,
+                                       hp["lr"], None, None, None, None, 0, 0.0,
+                                       self.step_count.data_ptr(), hp["betas"][0],
+                                       hp["betas"][1], hp["eps"], stream_ptr()), "pcadv_adam2")
         self._post()
         return self.losses
 

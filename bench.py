@@ -592,7 +592,7 @@ def bench_cls_ft(args):
     graphs, why = [], None
     if not args.ft_body:
         opt = torch.optim.Adam(model.parameters(), lr=1e-3, betas=(0.9, 0.999))
-        adam = "fused (pcadv_adam over the flat generator buffer)"
+        adam = "fused (pcadv_adam2 over the flat generator buffer)"
         step = ClsFtTrainStep(model, B, N, optimizer=opt, lambda_regu=0.001, seed=1234, device=dev)
         if not args.no_graph:
             graphs = [step.capture_on(*p) for p in pool]

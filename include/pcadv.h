@@ -227,6 +227,13 @@ int pcadv_tnet_reg_fwd(const float* T, int B, int k, float* norms, float* reg,
                        hipStream_t stream);
 int pcadv_tnet_reg_bwd(const float* T, int B, int k, const float* grad_reg, float* dT,
                        hipStream_t stream);
+/* The regulariser of a training step in two launches (ABI 9): norms and
+ * *reg as pcadv_tnet_reg_fwd, dT += pcadv_tnet_reg_bwd's gradient (the bmm's
+ * dT accumulated in place), and *step_count += 1 when given (the fused
+ * feature-transform cls step advances its count there, ahead of its Adam). */
+int pcadv_tnet_reg_step(const float* T, int B, int k, float* norms, float* reg,
+                        const float* grad_reg, float* dT, int32_t* step_count,
+                        hipStream_t stream);
 
 /* ---- linear / 1x1 conv on B x C x 1 ----------------------------------------
  * y[M][Nout] = act(s * (x[M][K] w[Nout][K]^T + b)), where s is the dropout

@@ -177,6 +177,12 @@ def test_cls_ft_trainer_uses_fused_step_and_matches_autograd(tmp_path, monkeypat
     assert built == [1]  # the fused run built the step once, the autograd run none
     (pa, la), (pb, lb) = res
     p0 = torch.cat([torch.from_numpy(v).reshape(-1) for v in G.values()])
-    move = (pb - p0).abs().max().item()
-    assert (pa - pb).abs().max().item() <= 1e-3 * move + 1e-7
+    # Adam moves every element by about lr whatever its gradient's size, so an
+    # element whose gradient sits at rounding level can move either way in the
+    # two paths: the movements are compared as vectors (relative L2)
+    da, db = (pa - p0).double(), (pb - p0).double()
+    rel = ((da - db).norm() / db.norm()).item()
+    print(f"fused vs autograd parameter movement after 3 iterations: relative L2 {rel:.2e}, "
+          f"max |diff| {(pa - pb).abs().max().item():.2e} of max movement {db.abs().max().item():.2e}")
+    assert rel <= 1e-3
     assert len(la) == len(lb) == 3
