@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PCADV_LIB", os.path.join(_HERE, "lib", "libpcadv.so"))
 # the layout of include/pcadv.h these signatures and AdvArgs bind (pcadv_abi_version())
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 PCADV_OK = 0
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2

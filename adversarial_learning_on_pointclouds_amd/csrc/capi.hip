@@ -28,7 +28,7 @@ int launch_feat_bwd(const float*, const int32_t*, const float*, const float*, in
                     const float*, const float*, float*, float*, float*, float*, float*, float*,
                     float*, float*, void*, size_t, hipStream_t, uint64_t* stamps = nullptr,
                     const FinAdam* adam = nullptr, const int* sortrec = nullptr,
-                    const IterEpi* epi = nullptr);
+                    const IterEpi* epi = nullptr, int x3_bf16 = 0);
 size_t feat_fwd_workspace_bytes(int C, int N);
 int launch_feat_fwd_fused(const float*, const float*, int, int, int, const float*, const float*,
                           const float*, const float*, const float*, const float*, const float*,
@@ -297,7 +297,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
                          s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec,
-                         epi_on ? &epi : nullptr);
+                         epi_on ? &epi : nullptr, a->precision == 1);
 }
 
 // Part 1 of adv_step: everything before the feature backward.
@@ -521,7 +521,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
                          s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec,
-                         epi_on ? &epi : nullptr);
+                         epi_on ? &epi : nullptr, a->precision == 1);
 }
 
 }  // namespace pcadv
@@ -531,7 +531,7 @@ using namespace pcadv;
 extern "C" {
 
 const char* pcadv_last_error(void) { return g_err; }
-int pcadv_abi_version(void) { return 9; }
+int pcadv_abi_version(void) { return 10; }
 
 size_t pcadv_feat_fwd_workspace_bytes(int C, int N) { return feat_fwd_workspace_bytes(C, N); }
 
@@ -543,17 +543,20 @@ int pcadv_feat_fwd(const float* pts, int C, int N, const float* w1, const float*
                                nullptr, workspace, workspace_bytes, stream);
 }
 
-int pcadv_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4, float* gmax,
+int pcadv_conv4_max(const void* x3, int C, int N, const float* w4, const float* b4, float* gmax,
                     int32_t* gidx, int precision, hipStream_t stream) {
-  return launch_conv4_max(x3, C, N, w4, b4, gmax, gidx, stream, precision);
+  return launch_conv4_max(static_cast<const float*>(x3), C, N, w4, b4, gmax, gidx, stream,
+                          precision);
 }
 
 int pcadv_feat_fwd_bf16(const float* pts, int C, int N, const float* w1, const float* b1,
                         const float* w2, const float* b2, const float* w3, const float* b3,
-                        const float* w4, const float* b4, float* x3, float* gmax, int32_t* gidx,
+                        const float* w4, const float* b4, void* x3, float* gmax, int32_t* gidx,
                         void* workspace, size_t workspace_bytes, hipStream_t stream) {
-  return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4, x3, gmax, gidx,
-                               nullptr, workspace, workspace_bytes, stream, nullptr, 1);
+  // x3: bf16 [C][N][128] (k_point_mlp<1>'s store)
+  return launch_feat_fwd_fused(pts, pts, C, C, N, w1, b1, w2, b2, w3, b3, w4, b4,
+                               static_cast<float*>(x3), gmax, gidx, nullptr, workspace,
+                               workspace_bytes, stream, nullptr, 1);
 }
 
 #ifdef PCADV_STAMPS

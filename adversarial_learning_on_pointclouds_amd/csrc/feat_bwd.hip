@@ -140,7 +140,8 @@ static int fin_adam_blocks(int64_t n, int nt, int v4) {
 // v_readlane (scalar base + lane offset), so the row loads are all in flight
 // together: two memory round trips per wave.
 constexpr int DW4_WPC = 2;  // waves per channel
-template <int NW>
+// XB: x3 is bf16 (bf16 mode's forward store), two columns in one 4-B load
+template <int NW, bool XB>
 __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__ dg,
                           const int32_t* __restrict__ gidx, int C, int N, int O,
                           const float* __restrict__ x3, float* __restrict__ dw4,
@@ -162,7 +163,13 @@ __device__ void dw4_block(int blk, float4 (*part)[64], const float* __restrict__
         for (int u = 0; u < U; ++u) {
           const int cu = min(u0 + u, cnt - 1);  // clamped: loads past cnt are discarded
           const int n = __builtin_amdgcn_readlane(nl, cu);
-          v[u] = *reinterpret_cast<const float2*>(x3 + ((size_t)(c0 + cu) * N + n) * 128 + 2 * lane);
+          const size_t off = ((size_t)(c0 + cu) * N + n) * 128 + 2 * lane;
+          if constexpr (XB) {
+            const uint32_t b = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const __bf16*>(x3) + off);
+            v[u] = make_float2(__uint_as_float(b << 16), __uint_as_float(b & 0xffff0000u));
+          } else {
+            v[u] = *reinterpret_cast<const float2*>(x3 + off);
+          }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -208,7 +215,8 @@ int chunk_stamps_read(uint64_t* host) {
 
 // PRE: phases 1-3 (the hit sort) were done ahead of this launch (feat_sort.h,
 // records at sortrec): load them and gather the hits' gradients instead.
-template <bool PRE>
+// XB: x3 is bf16 (bf16 mode): the conv3 ReLU mask and the dW4 gather read it so
+template <bool PRE, bool XB>
 __global__ void __launch_bounds__(BW_T, 4)
 k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx, int O,
                  const float* __restrict__ pts_a, const float* __restrict__ pts_b, int split,
@@ -235,7 +243,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
     const bool is_dw4 = PCADV_TRAIL_ADAM_FIRST ? (b >= nad && b - nad < NDW4) : b < NDW4;
     const int bd = PCADV_TRAIL_ADAM_FIRST ? b - nad : b, ba = PCADV_TRAIL_ADAM_FIRST ? b : b - NDW4;
     if (is_dw4)
-      dw4_block<BW_T / 64>(bd, reinterpret_cast<float4(*)[64]>(smem), dg, gidx, nclouds, N, O, x3,
+      dw4_block<BW_T / 64, XB>(bd, reinterpret_cast<float4(*)[64]>(smem), dg, gidx, nclouds, N, O, x3,
                            dw4, db4);
     else if (ba >= 0 && ba < nad)
       adam_block<BW_T, FIN_ADAM_V4>(ba, nb_adam0, nb_adam1, fa);
@@ -280,8 +288,10 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   const __amdgpu_buffer_rsrc_t w4r =
       __builtin_amdgcn_make_buffer_rsrc((void*)w4, (short)0, BW_MAXO * 128 * 4, 0x00020000);
   // this cloud's x3 rows (C x N x 128 f32 < 4 GB: 32-bit offsets from the cloud base)
+  constexpr int XE = XB ? 2 : 4;  // bytes per x3 element
   const __amdgpu_buffer_rsrc_t x3r = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(x3 + (size_t)c * N * 128), (short)0, N * 128 * 4, 0x00020000);
+      (void*)(reinterpret_cast<const char*>(x3) + (size_t)c * N * 128 * XE), (short)0, N * 128 * XE,
+      0x00020000);
   // conv1 weights, fetched up front so they land during the hit sort
   const int ch1 = tid & 63;
   const float w1a = w1[ch1 * 3 + 0], w1b = w1[ch1 * 3 + 1], w1c = w1[ch1 * 3 + 2], b1v = b1[ch1];
@@ -503,8 +513,17 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
         const int rr = grp + BW_G * u;
         if (rr < nb) {
           const int p = p0 + L.rows_list[b0 + rr];
-          const f32x4 xv = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(x3r, (p * 128 + 4 * cq) * 4, 0, 0));
+          f32x4 xv;
+          if constexpr (XB) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 b = __builtin_bit_cast(
+                u32x2, __builtin_amdgcn_raw_buffer_load_b64(x3r, (p * 128 + 4 * cq) * 2, 0, 0));
+            xv = f32x4{__uint_as_float(b.x << 16), __uint_as_float(b.x & 0xffff0000u),
+                       __uint_as_float(b.y << 16), __uint_as_float(b.y & 0xffff0000u)};
+          } else {
+            xv = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(x3r, (p * 128 + 4 * cq) * 4, 0, 0));
+          }
           mask |= ((xv.x > 0.f ? 1u : 0u) | (xv.y > 0.f ? 2u : 0u) | (xv.z > 0.f ? 4u : 0u) |
                    (xv.w > 0.f ? 8u : 0u)) << (4 * u);
         }
@@ -826,17 +845,23 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                     float* dw1, float* db1, float* dw2, float* db2, float* dw3, float* db3,
                     float* dw4, float* db4, void* ws, size_t ws_bytes, hipStream_t s,
                     uint64_t* stamps, const FinAdam* adam, const int* sortrec,
-                    const IterEpi* epi) {
+                    const IterEpi* epi, int x3_bf16) {
   const int O = PCADV_C4;
   PC_REQUIRE(ws_bytes >= feat_bwd_workspace_bytes(C, N), "feat_bwd: workspace too small");
   const int nchunk = (N + BW_PCH - 1) / BW_PCH;
   float* slabs = static_cast<float*>(ws);
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<false>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<false, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(BwdLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<true>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<true, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(BwdLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<false, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(BwdLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_feat_bwd_chunk<true, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(BwdLds)) != hipSuccess) {
       set_error("feat_bwd: cannot reserve %zu bytes of LDS", sizeof(BwdLds));
@@ -861,14 +886,11 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
   PC_REQUIRE(O == BW_MAXO, "feat_bwd: %d pooled channels (expects %d)", O, BW_MAXO);
   constexpr int NDW4 = BW_MAXO / (BW_T / 64 / DW4_WPC);
   const int arows = (NDW4 + nba0 + nba1 + nchunk - 1) / nchunk;
-  if (sortrec)
-    hipLaunchKernelGGL(k_feat_bwd_chunk<true>, dim3(nchunk, C + arows), dim3(BW_T), sizeof(BwdLds),
-                       s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs,
-                       stamps, sortrec, C, dw4, db4, fa, nba0, nba1);
-  else
-    hipLaunchKernelGGL(k_feat_bwd_chunk<false>, dim3(nchunk, C + arows), dim3(BW_T),
-                       sizeof(BwdLds), s, dg, gidx, O, pts_a, pts_b, split, N, w1, b1, w2, b2, w3,
-                       w4, x3, slabs, stamps, sortrec, C, dw4, db4, fa, nba0, nba1);
+  auto kern = sortrec ? (x3_bf16 ? k_feat_bwd_chunk<true, true> : k_feat_bwd_chunk<true, false>)
+                      : (x3_bf16 ? k_feat_bwd_chunk<false, true> : k_feat_bwd_chunk<false, false>);
+  hipLaunchKernelGGL(kern, dim3(nchunk, C + arows), dim3(BW_T), sizeof(BwdLds), s, dg, gidx, O,
+                     pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps, sortrec, C,
+                     dw4, db4, fa, nba0, nba1);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   const int nb4 = fa.on ? fin_adam_blocks(PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W, 1024, 2) : 0;
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + nb4), dim3(1024), 0, s, slabs, C * nchunk,

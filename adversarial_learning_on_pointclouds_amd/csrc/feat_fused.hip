@@ -68,6 +68,20 @@ struct MlpLds2 {
 // per-wave form it needs more than 256 VGPRs)
 template <int TPW, bool FOLD>
 constexpr bool kMlpWaveStage = TPW == 2 && !FOLD;
+
+// bf16 mode's x3 store: eight staged f32 (16-B aligned) rounded to bf16 (nearest
+// even, the rounding k_conv4_max applied to the f32 x3 before) as one 16-B
+// nontemporal store
+__device__ __forceinline__ void store_bf16x8(__bf16* dst, const float* src) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(src), b = *reinterpret_cast<const f32x4*>(src + 4);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = (__bf16)a[j];
+    o[j + 4] = (__bf16)b[j];
+  }
+  __builtin_nontemporal_store(__builtin_bit_cast(f32x4, o), reinterpret_cast<f32x4*>(dst));
+}
 template <int TPW, bool FOLD>
 using MlpLds = std::conditional_t<kMlpWaveStage<TPW, FOLD>, MlpLds2, MlpLds1>;
 
@@ -188,6 +202,15 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
   auto store_x3 = [&](int stile, int u0, int u1) {
     const int sc = stile / T, sp0 = (stile % T) * PM_P;
     const float* xw = reinterpret_cast<const float*>(smem + offsetof(MlpLds2, x3w)) + wave * PM_P * 32;
+    if constexpr (NP3 == 1) {  // bf16 mode: half the pieces, eight channels each
+      __bf16* xb = reinterpret_cast<__bf16*>(x3g) + ((size_t)sc * N + sp0) * 128 + 32 * wave;
+#pragma unroll
+      for (int u = u0 / 2; u < u1 / 2; ++u) {
+        const int e = lane + 64 * u, row = e >> 2, c8 = e & 3;
+        if (sp0 + row < N) store_bf16x8(xb + (size_t)row * 128 + 8 * c8, &xw[row * 32 + 8 * c8]);
+      }
+      return;
+    }
     float* xg = x3g + ((size_t)sc * N + sp0) * 128 + 32 * wave;
 #pragma unroll
     for (int u = u0; u < u1; ++u) {
@@ -302,6 +325,14 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
           L.x3[(32 * pt + acc_row(i, lane)) * X3S + 32 * wave + r] = v > 0.f ? v : 0.f;
         }
       __syncthreads();
+      if constexpr (NP3 == 1) {  // bf16 mode: 16-B stores of eight channels
+        __bf16* xb = reinterpret_cast<__bf16*>(x3g) + ((size_t)c * N + p0) * 128;
+#pragma unroll
+        for (int u = 0; u < PM_P * 16 / PM_T; ++u) {
+          const int e = tid + PM_T * u, row = e >> 4, c8 = e & 15;
+          if (p0 + row < N) store_bf16x8(xb + (size_t)row * 128 + 8 * c8, &L.x3[row * X3S + 8 * c8]);
+        }
+      } else {
       float* xg = x3g + ((size_t)c * N + p0) * 128;
 #pragma unroll
       for (int u = 0; u < PM_P * 32 / PM_T; ++u) {
@@ -309,6 +340,7 @@ k_point_mlp(const float* __restrict__ pts_a, const float* __restrict__ pts_b, in
         if (p0 + row < N)
           __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&L.x3[row * X3S + 4 * c4]),
                                       reinterpret_cast<f32x4*>(xg + (size_t)row * 128 + 4 * c4));
+      }
       }
       }
       STAMP(7 + 5 * it);
@@ -471,7 +503,11 @@ __device__ __forceinline__ void pair_merge(int n1, int u1, int n2, int u2, int& 
 // same staged tiles; group 1 hands its top-2 to group 0 through LDS before the
 // exact re-evaluation.  Still two waves per SIMD (a lone wave gets half the
 // throughput: 4-wave workgroups measured slower).
-template <int NP4, bool G2>
+// XB (bf16 mode only): x3 arrives as bf16 (k_point_mlp<1>'s store, the same
+// rounding this kernel applies to an f32 x3), so the staging is a copy: half
+// the bytes and none of the conversion the channel-block workgroups of a cloud
+// would each redo.
+template <int NP4, bool G2, bool XB = false>
 __global__ void __launch_bounds__(C4_T)
 k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
             const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
@@ -498,15 +534,24 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   const int grp = G2 ? wave >> 2 : 0;     // G2: wave group = unit of each step
   constexpr int CB = G2 ? C4_CB / 2 : C4_CB;
   const int o = cb * CB + 32 * wblk + r;  // this lane's output channel
+  static_assert(!XB || NP4 == 1, "a bf16 x3 is bf16 mode's");
   const float* xc = x3g + (size_t)c * N * 128;
+  const __bf16* xcb = reinterpret_cast<const __bf16*>(x3g) + (size_t)c * N * 128;
   const int S = (N + C4_P - 1) / C4_P;
 
   // staging map: thread = (row tid >> 3, 16 consecutive k at 16 (tid & 7));
   // rows past the cloud re-read its last row (screening masks them)
   const int srow = tid >> 3, sk = 16 * (tid & 7);
   f32x4 stg[4];
+  bf16x8 stgb[2];  // XB
   auto stage_load = [&](int s) {
     const int p = min(s * C4_P + srow, N - 1);
+    if constexpr (XB) {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(xcb + (size_t)p * 128 + sk);
+      stgb[0] = src[0];
+      stgb[1] = src[1];
+      return;
+    }
     const f32x4* src = reinterpret_cast<const f32x4*>(xc + (size_t)p * 128 + sk);
 #pragma unroll
     for (int j = 0; j < 4; ++j) stg[j] = src[j];
@@ -519,6 +564,12 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     }
   };
   auto stage_write = [&](int buf) {  // split the staged f32 rows into bf16 hi / lo
+    if constexpr (XB) {
+      bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf][0][srow * C4_SB + sk]);
+      dh[0] = stgb[0];
+      dh[1] = stgb[1];
+      return;
+    }
     bf16x8 hi[2], lo[2];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -658,7 +709,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         // screening below the MFMAs, next to its only use)
         asm volatile("" ::"v"(k1), "v"(k2));
       }
-      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
+      if (!XB && (PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
 #pragma unroll
         for (int j = 4 * kb; j < 4 * kb + 4; ++j) {
           const float v = stg[j >> 2][j & 3];
@@ -674,8 +725,8 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) {  // the next step's tile (buffer free since the barrier)
         bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][srow * C4_SB + sk]);
         bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][srow * C4_SB + sk]);
-        dh[0] = shi[0];
-        dh[1] = shi[1];
+        dh[0] = XB ? stgb[0] : shi[0];
+        dh[1] = XB ? stgb[1] : shi[1];
         if constexpr (NP4 == 3) {
           dl[0] = slo[0];
           dl[1] = slo[1];
@@ -953,6 +1004,12 @@ static int feat_fwd_attrs() {
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(C4Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, false, NP4 == 1>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(C4Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, true, NP4 == 1>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(C4Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(MlpLds<2, false>)) != hipSuccess ||
@@ -974,8 +1031,8 @@ static int feat_fwd_attrs() {
 }
 
 // k_conv4_max alone over a given x3 (C x N x 128): the second launch of the
-// feature forward
-template <int NP3, int NP4>
+// feature forward.  XB: x3 is bf16 (bf16 mode's k_point_mlp store)
+template <int NP3, int NP4, bool XB = false>
 static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, const float* b4,
                                float* gmax, int32_t* gidx, hipStream_t s, uint64_t* stamps,
                                int relu = 0) {
@@ -987,10 +1044,10 @@ static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, c
 #define PCADV_C4_G2_MAXC 63  // A/B builds: the largest cloud count run in the two-group form
 #endif
   if (C <= PCADV_C4_G2_MAXC && !stamps)
-    hipLaunchKernelGGL((k_conv4_max<NP4, true>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
+    hipLaunchKernelGGL((k_conv4_max<NP4, true, XB>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
                        sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
   else
-    hipLaunchKernelGGL((k_conv4_max<NP4, false>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
+    hipLaunchKernelGGL((k_conv4_max<NP4, false, XB>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
                        sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
   PC_HIP_CHECK_LAUNCH("k_conv4_max");
   return PCADV_OK;
@@ -1017,14 +1074,17 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
   hipLaunchKernelGGL(kern, grid, dim3(PM_T), lds, s, pts_a, pts_b, split, N, T, ntiles,
                      w1, b1, w2, b2, w3, b3, x3, inc_counter, mlp_stamps, gf);
   PC_HIP_CHECK_LAUNCH("k_point_mlp");
-  return launch_conv4_max_np<NP3, NP4>(x3, C, N, w4, b4, gmax, gidx, s, stamps);
+  // bf16 mode: k_point_mlp<1> stored x3 as bf16
+  return launch_conv4_max_np<NP3, NP4, NP3 == 1>(x3, C, N, w4, b4, gmax, gidx, s, stamps);
 }
 
 int launch_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4, float* gmax,
                      int32_t* gidx, hipStream_t s, int precision, int relu) {
   PC_REQUIRE(C > 0 && N > 0, "conv4_max: bad shape C=%d N=%d", C, N);
-  PC_REQUIRE(precision == 0 || precision == 1, "conv4_max: precision %d (0 fp32, 1 bf16)",
-             precision);
+  PC_REQUIRE(precision >= 0 && precision <= 2,
+             "conv4_max: precision %d (0 fp32, 1 bf16, 2 bf16 over a bf16 x3)", precision);
+  if (precision == 2)
+    return launch_conv4_max_np<1, 1, true>(x3, C, N, w4, b4, gmax, gidx, s, nullptr, relu);
   if (precision == 1)
     return launch_conv4_max_np<1, 1>(x3, C, N, w4, b4, gmax, gidx, s, nullptr, relu);
   return launch_conv4_max_np<6, 3>(x3, C, N, w4, b4, gmax, gidx, s, nullptr, relu);

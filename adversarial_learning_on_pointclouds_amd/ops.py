@@ -46,7 +46,8 @@ PRECISIONS = {"fp32": 0, "bf16": 1}
 
 def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4, precision="fp32"):
     """pts (C, N, 3) -> gmax (C, 1024), gidx (C, 1024) int32, x3 (C, N, 128).
-    precision "bf16": conv3 / conv4 on bf16-rounded operands (pcadv_feat_fwd_bf16)."""
+    precision "bf16": conv3 / conv4 on bf16-rounded operands (pcadv_feat_fwd_bf16);
+    x3 comes back as torch.bfloat16 (the form conv4 and the backward read)."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}")
     lib = _lib.load()
@@ -59,7 +60,8 @@ def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4, precision="fp32"):
           _req(_mat(w3), "conv3.weight", (128, 64)), _req(b3, "conv3.bias", (128,)),
           _req(_mat(w4), "conv4.weight", (1024, 128)), _req(b4, "conv4.bias", (1024,))]
     dev = pts.device
-    x3 = torch.empty(C, N, 128, device=dev)
+    x3 = torch.empty(C, N, 128, device=dev,
+                     dtype=torch.bfloat16 if precision == "bf16" else torch.float32)
     gmax = torch.empty(C, 1024, device=dev)
     gidx = torch.empty(C, 1024, device=dev, dtype=torch.int32)
     nbytes = lib.pcadv_feat_fwd_workspace_bytes(C, N)
@@ -73,11 +75,19 @@ def feat_fwd(pts, w1, b1, w2, b2, w3, b3, w4, b4, precision="fp32"):
 def conv4_max(x3, w4, b4, precision="fp32", out=None):
     """conv4 + max over points of given conv3 activations x3 (C, N, 128) ->
     gmax (C, 1024), gidx (C, 1024) int32: pcadv_feat_fwd's second launch alone
-    (pcadv_conv4_max).  out: optional (gmax, gidx) to write into."""
+    (pcadv_conv4_max).  A bf16 x3 (feat_fwd's bf16 mode) takes precision
+    "bf16" (code 2: the in-step form).  out: optional (gmax, gidx) to write into."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}")
     lib = _lib.load()
-    _req(x3, "x3")
+    code = PRECISIONS[precision]
+    if isinstance(x3, torch.Tensor) and x3.dtype == torch.bfloat16:
+        if precision != "bf16":
+            raise TypeError("x3: a bf16 x3 is bf16 mode's (precision='bf16')")
+        _req(x3, "x3", dtype=torch.bfloat16)
+        code = 2
+    else:
+        _req(x3, "x3")
     if x3.dim() != 3 or x3.shape[2] != 128:
         raise ValueError(f"x3: expected (C, N, 128), got {tuple(x3.shape)}")
     C, N, _ = x3.shape
@@ -90,13 +100,16 @@ def conv4_max(x3, w4, b4, precision="fp32", out=None):
     _req(gmax, "gmax", (C, 1024))
     _req(gidx, "gidx", (C, 1024), torch.int32)
     check(lib.pcadv_conv4_max(ptr(x3), C, N, ptr(w), ptr(b4), ptr(gmax), ptr(gidx),
-                              PRECISIONS[precision], stream_ptr()), "pcadv_conv4_max")
+                              code, stream_ptr()), "pcadv_conv4_max")
     return gmax, gidx
 
 
 def feat_bwd(dgmax, gidx, pts, w1, b1, w2, b2, w3, w4, x3):
-    """Gradients of (conv1..conv4) weights and biases given dL/dgmax."""
+    """Gradients of (conv1..conv4) weights and biases given dL/dgmax.  A bf16
+    x3 (feat_fwd's bf16 mode) is widened to f32 first."""
     lib = _lib.load()
+    if isinstance(x3, torch.Tensor) and x3.dtype == torch.bfloat16:
+        x3 = x3.float()
     C, N, _ = pts.shape
     _req(dgmax, "dgmax", (C, 1024))
     _req(gidx, "gidx", (C, 1024), torch.int32)

@@ -434,8 +434,9 @@ def feat_roofline(pts_all, fw, prec, traffic_pattern=None, mfma_cfg=None):
     np3, np4 = (6, 3) if prec == "fp32" else (1, 1)  # bf16 products per f32 product
     issued4 = np4 * f4
     issued_pair = f12 * (BF16_PEAK / F32_PEAK) + np3 * f3 + np4 * f4
-    alg_bytes4 = C * Np * 128 * 4 + 1024 * 128 * 4 + C * 1024 * 8
-    alg_bytes_pair = C * Np * (3 + 128) * 4 + C * Np * 128 * 4 + C * 1024 * 8
+    xe = 4 if prec == "fp32" else 2  # bytes per x3 element (bf16 mode stores it in bf16)
+    alg_bytes4 = C * Np * 128 * xe + 1024 * 128 * 4 + C * 1024 * 8
+    alg_bytes_pair = C * Np * 3 * 4 + 2 * C * Np * 128 * xe + C * 1024 * 8
     traffic4, src = _pmc_traffic(traffic_pattern or "none", (f"pcadv::k_conv4_max<{np4}",),
                                  traffic_pattern is not None)
     traffic_pair, _ = _pmc_traffic(traffic_pattern or "none",

@@ -109,18 +109,21 @@ int pcadv_feat_fwd(const float* pts, int C, int N,
  * multiply bf16-rounded operands with f32 accumulation (one MFMA product each);
  * gmax is the winner's bf16-product value (low 6 bits of its screening key
  * dropped), gidx its point (first index on equal keys).  conv1/conv2 stay f32
- * (the backward's recompute of x1/x2 is bitwise). */
+ * (the backward's recompute of x1/x2 is bitwise).  x3 is stored as bf16
+ * [C][N][128] (2 bytes per element, the rounding conv4 applies to it; ABI
+ * version 10): pcadv_feat_bwd takes it widened to f32. */
 int pcadv_feat_fwd_bf16(const float* pts, int C, int N,
                         const float* w1, const float* b1, const float* w2, const float* b2,
                         const float* w3, const float* b3, const float* w4, const float* b4,
-                        float* x3, float* gmax, int32_t* gidx,
+                        void* x3, float* gmax, int32_t* gidx,
                         void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* The second launch of pcadv_feat_fwd alone: conv4 (128 -> 1024, no ReLU) +
  * torch.max over the points (models/pointnet.py:128-130) of given conv3
  * activations x3 [C][N][128] -> gmax, gidx [C][1024]; precision 0 = f32-level
- * (as pcadv_feat_fwd), 1 = bf16 (as pcadv_feat_fwd_bf16). */
-int pcadv_conv4_max(const float* x3, int C, int N, const float* w4, const float* b4,
+ * (as pcadv_feat_fwd), 1 = bf16 over an f32 x3, 2 = bf16 over a bf16 x3 (as
+ * pcadv_feat_fwd_bf16 runs it on the x3 it stores; ABI version 10). */
+int pcadv_conv4_max(const void* x3, int C, int N, const float* w4, const float* b4,
                     float* gmax, int32_t* gidx, int precision, hipStream_t stream);
 
 /* Bytes of workspace pcadv_feat_bwd needs for C clouds of N points. */
@@ -547,8 +550,9 @@ typedef struct pcadv_adv_args {
    *     pcadv_cls_step takes 0 or 3 (ABI 9: its head on given features). */
   int part;
   /* feature forward precision: 0 = f32-level (default), 1 = bf16 (as
-   * pcadv_feat_fwd_bf16; the head, the discriminator and every backward stay
-   * f32).  ABI version 5. */
+   * pcadv_feat_fwd_bf16, x3 kept in bf16 for the feature backward; the head,
+   * the discriminator and every backward stay f32 arithmetic).  ABI version 5;
+   * the bf16 x3 since version 10. */
   int precision;
   /* Data parallelism (ABI version 6): rank rng_rank of rng_world (<= 1: one
    * process) holding GT rows [rank B, rank B + B) and no-GT rows [rank B,

@@ -143,7 +143,9 @@ def point_mlp_fwd(pts, p, prefix="feat.", precision="fp32"):
     """relu(conv1), relu(conv2), relu(conv3) as per-point matvecs
     (models/pointnet.py:115-116,127).  pts: (B, N, 3).  precision "bf16" (the
     build's bf16 mode, not a reference behaviour): conv3's inputs and weights
-    rounded to bf16, the products summed exactly (f64) and rounded to f32."""
+    rounded to bf16, the products summed exactly (f64) and rounded to f32, and
+    the activation x3 kept in bf16 (rounded once more: what conv4 and the
+    backward read)."""
     def layer(x, i):
         w = _w(p, f"{prefix}conv{i}.weight")
         if precision == "bf16" and i == 3:
@@ -155,6 +157,8 @@ def point_mlp_fwd(pts, p, prefix="feat.", precision="fp32"):
     x1 = layer(pts, 1)
     x2 = layer(x1, 2)
     x3 = layer(x2, 3)
+    if precision == "bf16":
+        x3 = bf16_round(x3)
     return x1, x2, x3
 
 

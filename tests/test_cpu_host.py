@@ -25,7 +25,7 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, s
     assert sorted(_lib.SIGNATURES) == syms  # nothing bound that the header does not declare
-    assert lib.pcadv_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.pcadv_abi_version() == _lib.ABI_VERSION == 10
 
 
 def test_layout_matches_header_enums():
