@@ -6,6 +6,10 @@
 
 #include "common.h"
 
+#ifndef PCADV_CLS_PRESORT
+#define PCADV_CLS_PRESORT 1  // A/B builds: 0 = the cls step's chunks sort their own hits
+#endif
+
 namespace pcadv {
 
 static thread_local char g_err[512] = "";
@@ -488,7 +492,7 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
   // and fc3's input gradient, stored as fc2's dz (k_cls_head)
   PC_TRY(launch_cls_head(w.h2, w.mask, a->drop_p, G + PCADV_G_FC3_W, G + PCADV_G_FC3_B, a->labels,
                          B, a->lambda_cls, logits, w.dlogits, w.dh2, w.rowloss, s,
-                         ext ? nullptr : w.gidx, C, N, ext ? nullptr : w.sortrec));
+                         ext ? nullptr : w.gidx, C, N, ext || !PCADV_CLS_PRESORT ? nullptr : w.sortrec));
   {
     // fc2's backward; fc3's weight gradient and the CE batch mean ride along
     LinBwdExtra ex{};
@@ -520,8 +524,9 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                          gG + PCADV_G_CONV1_W, gG + PCADV_G_CONV1_B, gG + PCADV_G_CONV2_W,
                          gG + PCADV_G_CONV2_B, gG + PCADV_G_CONV3_W, gG + PCADV_G_CONV3_B,
                          gG + PCADV_G_CONV4_W, gG + PCADV_G_CONV4_B, w.feat_ws, w.feat_ws_bytes,
-                         s, nullptr, a->apply_adam ? &fa : nullptr, w.sortrec,
-                         epi_on ? &epi : nullptr, a->precision == 1);
+                         s, nullptr, a->apply_adam ? &fa : nullptr,
+                         PCADV_CLS_PRESORT ? w.sortrec : nullptr, epi_on ? &epi : nullptr,
+                         a->precision == 1);
 }
 
 }  // namespace pcadv

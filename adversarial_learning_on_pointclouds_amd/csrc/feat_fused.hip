@@ -506,9 +506,20 @@ __device__ __forceinline__ void pair_merge(int n1, int u1, int n2, int u2, int& 
 // XB (bf16 mode only): x3 arrives as bf16 (k_point_mlp<1>'s store, the same
 // rounding this kernel applies to an f32 x3), so the staging is a copy: half
 // the bytes and none of the conversion the channel-block workgroups of a cloud
-// would each redo.
+// would each redo.  With G2, XB workgroups run FOUR wave groups (16 waves,
+// 128-point steps, units 4 s + grp): the bf16 staging fits twice the rows in
+// the same LDS, W4 needs no lo fragments, and half as many step barriers are
+// shared by twice the waves.
+#ifndef PCADV_C4_G4
+#define PCADV_C4_G4 1  // A/B builds: 0 = XB workgroups keep two wave groups
+#endif
+template <int NP4, bool G2, bool XB>
+constexpr int c4_groups() { return G2 ? (XB && PCADV_C4_G4 ? 4 : 2) : 1; }
+template <int NP4, bool G2, bool XB>
+constexpr int c4_threads() { return c4_groups<NP4, G2, XB>() == 4 ? 2 * C4_T : C4_T; }
+
 template <int NP4, bool G2, bool XB = false>
-__global__ void __launch_bounds__(C4_T)
+__global__ void __launch_bounds__((c4_threads<NP4, G2, XB>()))
 k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
             const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
             uint64_t* __restrict__ stamps, int relu) {
@@ -530,6 +541,8 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  constexpr int NGRP = c4_groups<NP4, G2, XB>();
+  constexpr int P = G2 ? 32 * NGRP : C4_P;  // points per step
   const int wblk = G2 ? wave & 3 : wave;  // 32-channel block of this wave
   const int grp = G2 ? wave >> 2 : 0;     // G2: wave group = unit of each step
   constexpr int CB = G2 ? C4_CB / 2 : C4_CB;
@@ -537,7 +550,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   static_assert(!XB || NP4 == 1, "a bf16 x3 is bf16 mode's");
   const float* xc = x3g + (size_t)c * N * 128;
   const __bf16* xcb = reinterpret_cast<const __bf16*>(x3g) + (size_t)c * N * 128;
-  const int S = (N + C4_P - 1) / C4_P;
+  const int S = (N + P - 1) / P;
 
   // staging map: thread = (row tid >> 3, 16 consecutive k at 16 (tid & 7));
   // rows past the cloud re-read its last row (screening masks them)
@@ -545,7 +558,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   f32x4 stg[4];
   bf16x8 stgb[2];  // XB
   auto stage_load = [&](int s) {
-    const int p = min(s * C4_P + srow, N - 1);
+    const int p = min(s * P + srow, N - 1);
     if constexpr (XB) {
       const bf16x8* src = reinterpret_cast<const bf16x8*>(xcb + (size_t)p * 128 + sk);
       stgb[0] = src[0];
@@ -594,17 +607,25 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   // each lane takes k = 16 kb + 8 h .. + 8 of its channel, split to bf16 hi / lo
   bf16x8 bh[8], bl[8];
   {
+    // four groups: group 0's waves stage the four channel blocks, every wave
+    // reads its block's rows after a workgroup barrier
     const float* wsrc = w4 + (size_t)(cb * CB + 32 * wblk) * 128;
-    float* wl = L.w[wave];
+    float* wl = L.w[NGRP == 4 ? wblk : wave];
+    if (NGRP != 4 || grp == 0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = 4 * (lane + 64 * i);  // float index in the 32 x 128 block
-      *reinterpret_cast<f32x4*>(wl + (e >> 7) * C4_WS + (e & 127)) =
-          *reinterpret_cast<const f32x4*>(wsrc + e);
+      for (int i = 0; i < 16; ++i) {
+        const int e = 4 * (lane + 64 * i);  // float index in the 32 x 128 block
+        *reinterpret_cast<f32x4*>(wl + (e >> 7) * C4_WS + (e & 127)) =
+            *reinterpret_cast<const f32x4*>(wsrc + e);
+      }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (NGRP == 4) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     const float* wrow = wl + r * C4_WS + 8 * h;
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
@@ -669,7 +690,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     const int buf = s & 1;
     const __bf16* xh = &L.x[buf][0][(32 * pt + r) * C4_SB + 8 * h];
     const __bf16* xl = &L.x[buf][1][(32 * pt + r) * C4_SB + 8 * h];
-    const int uprev = G2 ? 2 * s + pt - 2 : 2 * s + pt - 1;
+    const int uprev = G2 ? NGRP * s + pt - NGRP : 2 * s + pt - 1;
     int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
     bf16x8 fa[3][2];  // A fragments, a 3-deep register ring: [k-block % 3][hi, lo]
     auto frag = [&](int kb) {
@@ -784,7 +805,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   }
   if constexpr (G2) {  // this wave's last unit
     int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
-    const int ul = 2 * (S - 1) + grp;
+    const int ul = NGRP * (S - 1) + grp;
     if ((S - 1) & 1) screen_unit(accB, ul, T_{}, 0, 8, k1, k2, k3);
     else screen_unit(accA, ul, T_{}, 0, 8, k1, k2, k3);
     cert_merge(k1, k2, k3);
@@ -847,12 +868,13 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       v2 = nv2;
       a2 = na2;
     }
-    if constexpr (G2) {  // group 1's top-2 of each channel into group 0's
-      float* xv = L.w[0];  // free: the point loop's last barrier has passed
-      int* xi = reinterpret_cast<int*>(L.w[1]);
+    if constexpr (G2) {  // groups 1.. hand their top-2 of each channel to group 0
       const int slot = 32 * wblk + r;  // lanes r and r + 32 hold the same pair
+      // free: the point loop's last barrier has passed (256 slots per group)
+      float* xv = L.w[0] + 256 * (grp > 0 ? grp - 1 : 0);
+      int* xi = reinterpret_cast<int*>(L.w[1]) + 256 * (grp > 0 ? grp - 1 : 0);
       float* x3v = L.w[2];
-      if (grp == 1 && h == 0) {
+      if (grp > 0 && h == 0) {
         xv[2 * slot] = v1;
         xv[2 * slot + 1] = v2;
         xi[2 * slot] = a1;
@@ -860,15 +882,15 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         if constexpr (PCADV_C4_CERT && NP4 == 3) x3v[slot] = cert_v3;
       }
       __syncthreads();
-      if (grp == 1) return;
+      if (grp > 0) return;
       if constexpr (PCADV_C4_CERT && NP4 == 3) {
         const float g1 = xv[2 * slot], g2 = xv[2 * slot + 1];
         cert_v3 = fmaxf(fmaxf(cert_v3, x3v[slot]), fmaxf(fminf(v1, g2), fminf(v2, g1)));
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const float v = xv[2 * slot + q];
-        const int p = xi[2 * slot + q];
+      for (int q = 0; q < 2 * (NGRP - 1); ++q) {  // group 1's pair, then group 2's, ...
+        const float v = xv[256 * (q >> 1) + 2 * slot + (q & 1)];
+        const int p = xi[256 * (q >> 1) + 2 * slot + (q & 1)];
         const bool a = ranks_before(v, p, v1, a1);
         const bool b = !a && ranks_before(v, p, v2, a2);
         const float nv2 = a ? v1 : (b ? v : v2);
@@ -1044,7 +1066,8 @@ static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, c
 #define PCADV_C4_G2_MAXC 63  // A/B builds: the largest cloud count run in the two-group form
 #endif
   if (C <= PCADV_C4_G2_MAXC && !stamps)
-    hipLaunchKernelGGL((k_conv4_max<NP4, true, XB>), dim3(C * (2 * C4_O / C4_CB)), dim3(C4_T),
+    hipLaunchKernelGGL((k_conv4_max<NP4, true, XB>), dim3(C * (2 * C4_O / C4_CB)),
+                       dim3(c4_threads<NP4, true, XB>()),
                        sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
   else
     hipLaunchKernelGGL((k_conv4_max<NP4, false, XB>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
