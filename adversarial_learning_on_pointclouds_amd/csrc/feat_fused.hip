@@ -379,7 +379,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int C4_WS = 132;  // f32 row stride of the prologue's W4 staging (conflict-free b128 reads)
 union C4Lds {
-  alignas(16) __bf16 x[2][2][C4_P * C4_SB];  // x3 tiles [buffer][hi, lo]
+  alignas(16) __bf16 x[2][2][2 * C4_P * C4_SB];  // x3 tiles [buffer][hi, lo], up to 128 rows
   alignas(16) float w[8][32 * C4_WS];        // prologue only: each wave's 32 rows of W4
 };
 
@@ -518,7 +518,12 @@ constexpr int c4_groups() { return G2 ? (XB && PCADV_C4_G4 ? 4 : 2) : 1; }
 template <int NP4, bool G2, bool XB>
 constexpr int c4_threads() { return c4_groups<NP4, G2, XB>() == 4 ? 2 * C4_T : C4_T; }
 
-template <int NP4, bool G2, bool XB = false>
+// P128 (the 256-channel form, N % 128 == 0): 128-point steps, four units per
+// wave and step, two staged rows per thread: half the step barriers.
+#ifndef PCADV_C4_P128
+#define PCADV_C4_P128 1  // A/B builds: 0 = 64-point steps throughout
+#endif
+template <int NP4, bool G2, bool XB = false, bool P128 = false>
 __global__ void __launch_bounds__((c4_threads<NP4, G2, XB>()))
 k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict__ w4,
             const float* __restrict__ b4, float* __restrict__ gmax, int32_t* __restrict__ gidx,
@@ -542,7 +547,10 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   constexpr int NGRP = c4_groups<NP4, G2, XB>();
-  constexpr int P = G2 ? 32 * NGRP : C4_P;  // points per step
+  static_assert(!(P128 && G2), "P128 is the 256-channel form's");
+  constexpr int UPS = G2 ? 1 : (P128 ? 4 : 2);  // units per wave and step
+  constexpr int P = G2 ? 32 * NGRP : 32 * UPS;  // points per step
+  constexpr int RPT = P * 8 / c4_threads<NP4, G2, XB>();  // staged rows per thread (1, or 2 at P128)
   const int wblk = G2 ? wave & 3 : wave;  // 32-channel block of this wave
   const int grp = G2 ? wave >> 2 : 0;     // G2: wave group = unit of each step
   constexpr int CB = G2 ? C4_CB / 2 : C4_CB;
@@ -555,19 +563,22 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
   // staging map: thread = (row tid >> 3, 16 consecutive k at 16 (tid & 7));
   // rows past the cloud re-read its last row (screening masks them)
   const int srow = tid >> 3, sk = 16 * (tid & 7);
-  f32x4 stg[4];
-  bf16x8 stgb[2];  // XB
+  f32x4 stg[4 * RPT];
+  bf16x8 stgb[2 * RPT];  // XB
   auto stage_load = [&](int s) {
-    const int p = min(s * P + srow, N - 1);
-    if constexpr (XB) {
-      const bf16x8* src = reinterpret_cast<const bf16x8*>(xcb + (size_t)p * 128 + sk);
-      stgb[0] = src[0];
-      stgb[1] = src[1];
-      return;
-    }
-    const f32x4* src = reinterpret_cast<const f32x4*>(xc + (size_t)p * 128 + sk);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) stg[j] = src[j];
+    for (int q = 0; q < RPT; ++q) {
+      const int p = min(s * P + srow + 64 * q, N - 1);
+      if constexpr (XB) {
+        const bf16x8* src = reinterpret_cast<const bf16x8*>(xcb + (size_t)p * 128 + sk);
+        stgb[2 * q] = src[0];
+        stgb[2 * q + 1] = src[1];
+      } else {
+        const f32x4* src = reinterpret_cast<const f32x4*>(xc + (size_t)p * 128 + sk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) stg[4 * q + j] = src[j];
+      }
+    }
   };
   float cert_ss = 0.f, cert_xn2 = 0.f;  // PCADV_C4_CERT >= 2: max_p ||x_p||^2 of the cloud
   auto cert_row_done = [&]() {
@@ -577,28 +588,30 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     }
   };
   auto stage_write = [&](int buf) {  // split the staged f32 rows into bf16 hi / lo
-    if constexpr (XB) {
-      bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf][0][srow * C4_SB + sk]);
-      dh[0] = stgb[0];
-      dh[1] = stgb[1];
-      return;
-    }
-    bf16x8 hi[2], lo[2];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float v = stg[j >> 2][j & 3];
-      if constexpr (PCADV_C4_CERT >= 2) cert_ss = fmaf(v, v, cert_ss);
-      const __bf16 hb = (__bf16)v;
-      hi[j >> 3][j & 7] = hb;
-      lo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
-    }
-    bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf][0][srow * C4_SB + sk]);
-    bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf][1][srow * C4_SB + sk]);
-    dh[0] = hi[0];
-    dh[1] = hi[1];
-    if constexpr (NP4 == 3) {
-      dl[0] = lo[0];
-      dl[1] = lo[1];
+    for (int q = 0; q < RPT; ++q) {
+      bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf][0][(srow + 64 * q) * C4_SB + sk]);
+      bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf][1][(srow + 64 * q) * C4_SB + sk]);
+      if constexpr (XB) {
+        dh[0] = stgb[2 * q];
+        dh[1] = stgb[2 * q + 1];
+        continue;
+      }
+      bf16x8 hi[2], lo[2];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float v = stg[4 * q + (j >> 2)][j & 3];
+        if constexpr (PCADV_C4_CERT >= 2) cert_ss = fmaf(v, v, cert_ss);
+        const __bf16 hb = (__bf16)v;
+        hi[j >> 3][j & 7] = hb;
+        lo[j >> 3][j & 7] = (__bf16)(v - (float)hb);
+      }
+      dh[0] = hi[0];
+      dh[1] = hi[1];
+      if constexpr (NP4 == 3) {
+        dl[0] = lo[0];
+        dl[1] = lo[1];
+      }
     }
   };
   stage_load(0);
@@ -690,7 +703,10 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     const int buf = s & 1;
     const __bf16* xh = &L.x[buf][0][(32 * pt + r) * C4_SB + 8 * h];
     const __bf16* xl = &L.x[buf][1][(32 * pt + r) * C4_SB + 8 * h];
-    const int uprev = G2 ? NGRP * s + pt - NGRP : 2 * s + pt - 1;
+    const int uprev = G2 ? NGRP * s + pt - NGRP : UPS * s + pt - 1;
+    // this unit's share of the staging: row q = pt of the thread's rows (G2: its one row)
+    const bool stg_turn = G2 || pt < RPT;
+    const int q = G2 ? 0 : (pt < RPT ? pt : 0);
     int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
     bf16x8 fa[3][2];  // A fragments, a 3-deep register ring: [k-block % 3][hi, lo]
     auto frag = [&](int kb) {
@@ -718,22 +734,35 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       } else if constexpr (decltype(SCREEN)::value && !(PCADV_C4_DIAG & 1)) {
         // 16 values over k-blocks 1..7 (2,2,2,2,2,3,3); none in k-block 0, so the
         // previous unit's MFMAs have retired before the asm reads them
+        // (tools/check_asm_hazards.py checks the distance in the ISA)
         using IC = std::integral_constant<int, 0>;
-        if (kb == 1) screen_fast(prev, IC{}, std::integral_constant<int, 2>{}, k1, k2, k3);
-        if (kb == 2) screen_fast(prev, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
-        if (kb == 3) screen_fast(prev, std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
-        if (kb == 4) screen_fast(prev, std::integral_constant<int, 6>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
-        if (kb == 5) screen_fast(prev, std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
-        if (kb == 6) screen_fast(prev, std::integral_constant<int, 10>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
-        if (kb == 7) screen_fast(prev, std::integral_constant<int, 13>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+        if constexpr (NP4 == 3 || !P128) {
+          if (kb == 1) screen_fast(prev, IC{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+          if (kb == 2) screen_fast(prev, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+          if (kb == 3) screen_fast(prev, std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+          if (kb == 4) screen_fast(prev, std::integral_constant<int, 6>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+          if (kb == 5) screen_fast(prev, std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+          if (kb == 6) screen_fast(prev, std::integral_constant<int, 10>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+          if (kb == 7) screen_fast(prev, std::integral_constant<int, 13>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+        } else {
+          // bf16 mode's P128 form: one MFMA per k-block and back-to-back units,
+          // so k-blocks 0 and 1 stand between the previous unit's last MFMA
+          // and the first read
+          if (kb == 2) screen_fast(prev, IC{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+          if (kb == 3) screen_fast(prev, std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+          if (kb == 4) screen_fast(prev, std::integral_constant<int, 6>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+          if (kb == 5) screen_fast(prev, std::integral_constant<int, 9>{}, std::integral_constant<int, 3>{}, k1, k2, k3);
+          if (kb == 6) screen_fast(prev, std::integral_constant<int, 12>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+          if (kb == 7) screen_fast(prev, std::integral_constant<int, 14>{}, std::integral_constant<int, 2>{}, k1, k2, k3);
+        }
         // pin the keys to this region (otherwise the IR passes sink the whole
         // screening below the MFMAs, next to its only use)
         asm volatile("" ::"v"(k1), "v"(k2));
       }
-      if (!XB && (PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
+      if (!XB && (PCADV_C4_DIAG & 2) == 0 && stg_turn && kb < 4) {  // split the staged f32 rows into bf16 hi / lo, 4 per k-block
 #pragma unroll
         for (int j = 4 * kb; j < 4 * kb + 4; ++j) {
-          const float v = stg[j >> 2][j & 3];
+          const float v = stg[4 * q + (j >> 2)][j & 3];
           if constexpr (PCADV_C4_CERT >= 2) cert_ss = fmaf(v, v, cert_ss);
           const __bf16 hb = (__bf16)v;
           shi[j >> 3][j & 7] = hb;
@@ -743,11 +772,11 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
         if constexpr (NP4 == 3) asm volatile("" ::"v"(shi[kb >> 1]), "v"(slo[kb >> 1]));
         else asm volatile("" ::"v"(shi[kb >> 1]));
       }
-      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) {  // the next step's tile (buffer free since the barrier)
-        bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][srow * C4_SB + sk]);
-        bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][srow * C4_SB + sk]);
-        dh[0] = XB ? stgb[0] : shi[0];
-        dh[1] = XB ? stgb[1] : shi[1];
+      if ((PCADV_C4_DIAG & 2) == 0 && stg_turn && kb == 4) {  // the next step's tile (buffer free since the barrier)
+        bf16x8* dh = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][0][(srow + 64 * q) * C4_SB + sk]);
+        bf16x8* dl = reinterpret_cast<bf16x8*>(&L.x[buf ^ 1][1][(srow + 64 * q) * C4_SB + sk]);
+        dh[0] = XB ? stgb[2 * q] : shi[0];
+        dh[1] = XB ? stgb[2 * q + 1] : shi[1];
         if constexpr (NP4 == 3) {
           dl[0] = slo[0];
           dl[1] = slo[1];
@@ -755,7 +784,7 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
       }
       // tile s + 2 into the staging registers just freed (clamped: past the
       // end it re-reads the last row): 1.5 units ahead of its conversion
-      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == 0) && kb == 4) stage_load(s + 2);
+      if ((PCADV_C4_DIAG & 2) == 0 && (G2 || pt == RPT - 1) && kb == 4) stage_load(s + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (decltype(SCREEN)::value) {
@@ -773,6 +802,21 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     for (int s = 1; s < S; ++s) {
       if (s & 1) unit(s, grp, accB, accA, T_{}, F_{});
       else unit(s, grp, accA, accB, T_{}, F_{});
+      __syncthreads();
+    }
+  } else if constexpr (P128) {
+    // N % 128 == 0: every unit of every step is full, so only the last unit's
+    // screen (after the loop) is masked
+    unit(0, 0, accA, accB, F_{}, F_{});
+    unit(0, 1, accB, accA, T_{}, F_{});
+    unit(0, 2, accA, accB, T_{}, F_{});
+    unit(0, 3, accB, accA, T_{}, F_{});
+    __syncthreads();
+    for (int s = 1; s < S; ++s) {
+      unit(s, 0, accA, accB, T_{}, F_{});
+      unit(s, 1, accB, accA, T_{}, F_{});
+      unit(s, 2, accA, accB, T_{}, F_{});
+      unit(s, 3, accB, accA, T_{}, F_{});
       __syncthreads();
     }
   } else {
@@ -812,9 +856,9 @@ k_conv4_max(const float* __restrict__ x3g, int C, int N, const float* __restrict
     pair_merge<NP4 == 3>(k1, ul, k2, ul, r1, t1, r2, t2);
   } else {  // the last unit
     int k1 = KEY_NONE, k2 = KEY_NONE, k3 = KEY_NONE;
-    screen_unit(accB, 2 * S - 1, T_{}, 0, 8, k1, k2, k3);
+    screen_unit(accB, UPS * S - 1, T_{}, 0, 8, k1, k2, k3);
     cert_merge(k1, k2, k3);
-    pair_merge<NP4 == 3>(k1, 2 * S - 1, k2, 2 * S - 1, r1, t1, r2, t2);
+    pair_merge<NP4 == 3>(k1, UPS * S - 1, k2, UPS * S - 1, r1, t1, r2, t2);
   }
   STAMP(2);
 
@@ -1032,6 +1076,12 @@ static int feat_fwd_attrs() {
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, true, NP4 == 1>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(C4Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, false, false, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(C4Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(k_conv4_max<NP4, false, NP4 == 1, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(C4Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(k_point_mlp<NP3, 2, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(MlpLds<2, false>)) != hipSuccess ||
@@ -1068,6 +1118,9 @@ static int launch_conv4_max_np(const float* x3, int C, int N, const float* w4, c
   if (C <= PCADV_C4_G2_MAXC && !stamps)
     hipLaunchKernelGGL((k_conv4_max<NP4, true, XB>), dim3(C * (2 * C4_O / C4_CB)),
                        dim3(c4_threads<NP4, true, XB>()),
+                       sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
+  else if (PCADV_C4_P128 && N % 128 == 0 && !stamps)
+    hipLaunchKernelGGL((k_conv4_max<NP4, false, XB, true>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
                        sizeof(C4Lds), s, x3, C, N, w4, b4, gmax, gidx, stamps, relu);
   else
     hipLaunchKernelGGL((k_conv4_max<NP4, false, XB>), dim3(C * (C4_O / C4_CB)), dim3(C4_T),
