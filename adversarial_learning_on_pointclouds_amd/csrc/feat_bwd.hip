@@ -816,6 +816,11 @@ __device__ void reduce_slabs_block(int blk, float (*part)[64], const float* __re
 // chunks read W4 until they end).  The dW4 gather and the other Adam work rode
 // along k_feat_bwd_chunk.
 constexpr int FIN_NRED = (SLAB + FIN_COLS - 1) / FIN_COLS;
+#ifndef PCADV_FIN_W4_SPREAD
+#define PCADV_FIN_W4_SPREAD 1  // A/B builds: 0 = conv4's Adam on the fewest blocks (two float4 per thread)
+#endif
+constexpr int FIN_W4_V4 = PCADV_FIN_W4_SPREAD ? 1 : 2;
+constexpr int FIN_CUS = 256;  // MI355X compute units
 __global__ void __launch_bounds__(1024)
 k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float* db1, float* dw2,
                   float* db2, float* dw3, float* db3, FinAdam fa, int nb4, IterEpi epi) {
@@ -829,7 +834,7 @@ k_feat_bwd_finish(const float* __restrict__ slabs, int nslabs, float* dw1, float
     reduce_slabs_block(blk, part, slabs, nslabs, dw1, db1, dw2, db2, dw3, db3, fa);
   } else {
     constexpr int64_t W4 = PCADV_G_CONV4_W, N4 = PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W;
-    adam_range<1024, 2>(blk - FIN_NRED, nb4, fa.gp + W4, fa.gm + W4, fa.gv + W4, fa.gg + W4, N4,
+    adam_range<1024, FIN_W4_V4>(blk - FIN_NRED, nb4, fa.gp + W4, fa.gm + W4, fa.gv + W4, fa.gg + W4, N4,
                         fa.lr_g, fa);
   }
 }
@@ -892,7 +897,13 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
                      pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps, sortrec, C,
                      dw4, db4, fa, nba0, nba1);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
-  const int nb4 = fa.on ? fin_adam_blocks(PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W, 1024, 2) : 0;
+  // conv4's Adam spread over the CUs the slab reduction leaves free (one
+  // float4 per thread), so no workgroup moves more than a reduction block does
+  int nb4 = 0;
+  if (fa.on) {
+    nb4 = fin_adam_blocks(PCADV_G_CONV4_B + PCADV_C4 - PCADV_G_CONV4_W, 1024, FIN_W4_V4);
+    if (PCADV_FIN_W4_SPREAD && nb4 < FIN_CUS - FIN_NRED) nb4 = FIN_CUS - FIN_NRED;
+  }
   hipLaunchKernelGGL(k_feat_bwd_finish, dim3(FIN_NRED + nb4), dim3(1024), 0, s, slabs, C * nchunk,
                      dw1, db1, dw2, db2, dw3, db3, fa, nb4, epi ? *epi : IterEpi{});
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_finish");
