@@ -202,12 +202,23 @@ static StepWs carve(int B, int N, char* base) {
 // Adam fused into the feature backward's finishing launch (apply_adam): G's
 // conv1..conv4 as their gradients are formed there, the rest of G and all of D
 // in extra blocks of the same launch (their gradients are final by then).
-static FinAdam fused_adam(const pcadv_adv_args* a, bool with_d) {
+// The fused Adam of a whole step is split by where each gradient becomes
+// final: fc2, fc3 and all of D before fc1's backward launch (their update rides
+// along it: early = true), fc1 before the chunk launch (its trailing
+// workgroups), conv1..conv4 in the finishing launch.
+#ifndef PCADV_EARLY_ADAM
+#define PCADV_EARLY_ADAM 0  // A/B builds: 1 = fc2, fc3 and D ride along fc1's backward (measured slower)
+#endif
+// whole: the chunk launch's share when no fc1 backward ran in this call (part 2)
+static FinAdam fused_adam(const pcadv_adv_args* a, bool with_d, bool early = false,
+                          bool whole = false) {
+  const bool split = PCADV_EARLY_ADAM && !whole;
   FinAdam f{};
   f.on = 1;
   f.gp = a->g_param; f.gm = a->g_m; f.gv = a->g_v; f.gg = a->g_grad;
-  f.g_rest0 = PCADV_G_FC1_W;
-  f.g_n = PCADV_G_NUMEL;
+  f.g_rest0 = split && early ? PCADV_G_FC2_W : PCADV_G_FC1_W;
+  f.g_n = split && !early ? PCADV_G_FC2_W : PCADV_G_NUMEL;
+  with_d = with_d && (!split || early);
   if (with_d) {
     f.dp = a->d_param; f.dm = a->d_m; f.dv = a->d_v; f.dg = a->d_grad;
     f.d_n = PCADV_D_NUMEL;
@@ -290,7 +301,7 @@ static int adv_step(const pcadv_adv_args* a, hipStream_t s) {
   //      optimizer_D.step() (:558-559) fused into its finishing launch --------
   PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v && a->d_param && a->d_m && a->d_v),
              "adv_step: Adam buffers");
-  const FinAdam fa = fused_adam(a, true);
+  const FinAdam fa = fused_adam(a, true, false, a->part == 2);
   IterEpi epi;
   bool epi_on;
   PC_TRY(step_epilogue(a, &epi, &epi_on));
@@ -427,9 +438,18 @@ static int adv_head_part(const pcadv_adv_args* a, hipStream_t s, const StepWs& w
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,
                              C, 256, 512, s, &ex));
   }
-  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, gmax,
-                           G + PCADV_G_FC1_W, dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
-                           C, 512, 1024, s));
+  {
+    // fc2, fc3 and D are final: their Adam (optimizer.step / optimizer_D.step,
+    // :558-559) rides along fc1's backward
+    LinBwdExtra ex{};
+    if (a->apply_adam && PCADV_EARLY_ADAM) {
+      PC_REQUIRE(a->g_m && a->g_v && a->d_param && a->d_m && a->d_v, "adv_step: Adam buffers");
+      ex.adam = fused_adam(a, true, true);
+    }
+    PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, gmax,
+                             G + PCADV_G_FC1_W, dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
+                             C, 512, 1024, s, &ex));
+  }
   return PCADV_OK;
 }
 
@@ -508,9 +528,16 @@ static int cls_step(const pcadv_adv_args* a, hipStream_t s) {
                              G + PCADV_G_FC2_W, w.dh1, gG + PCADV_G_FC2_W, gG + PCADV_G_FC2_B, C,
                              C, 256, 512, s, &ex));
   }
-  PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, gmax,
-                           G + PCADV_G_FC1_W, dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
-                           C, 512, 1024, s));
+  {
+    LinBwdExtra ex{};  // fc2 and fc3 are final: their Adam rides along fc1's backward
+    if (a->apply_adam && !ext && PCADV_EARLY_ADAM) {
+      PC_REQUIRE(a->g_m && a->g_v, "cls_step: Adam moments");
+      ex.adam = fused_adam(a, false, true);
+    }
+    PC_TRY(launch_linear_bwd(w.dh1, nullptr, PCADV_ACT_NONE, nullptr, nullptr, 0, 0.f, gmax,
+                             G + PCADV_G_FC1_W, dgmax, gG + PCADV_G_FC1_W, gG + PCADV_G_FC1_B, C,
+                             C, 512, 1024, s, &ex));
+  }
   if (ext) return PCADV_OK;
   // feature backward; Adam (generator only) fused into its finishing launch
   PC_REQUIRE(!a->apply_adam || (a->g_m && a->g_v), "cls_step: Adam moments");

@@ -287,6 +287,10 @@ struct LinBwdExtra {
   const float* chain_w;
   float* chain_out;
   int chain_row0, chain_n;
+  // Adam over parameters whose gradients are final before this launch, in
+  // trailing blocks (adam.on): the generator's [g_rest0, g_n) and the
+  // discriminator's [0, d_n) of adam's flat buffers
+  FinAdam adam;
 };
 int launch_linear_bwd(const float* dy, const float* y, int act, const float* mask,
                       const int32_t* step, uint64_t seed, float p, const float* x, const float* w,

@@ -408,7 +408,37 @@ struct BwdExtra {
   const float* red_src;
   float* red_dst;
   int red_n, red_cnt, red_ld;
+  FinAdam adam;
+  int nba_g, nba_d;  // Adam blocks over the generator's range, then the discriminator
 };
+
+// Adam over n floats of (p, m, v, g) on blocks [0, nb): one float4 per thread
+// and pass, every load of a pass issued before its updates (adam_elem: the
+// arithmetic of every other Adam of the library, so bitwise theirs)
+__device__ void adam_span(int b, int nb, float* p, float* m, float* v, const float* g, int64_t n,
+                          const AdamHp& h) {
+  const int64_t n4 = n / 4, stride = (int64_t)nb * blockDim.x;
+  for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 p4 = reinterpret_cast<const f32x4*>(p)[i], m4 = reinterpret_cast<const f32x4*>(m)[i];
+    f32x4 v4 = reinterpret_cast<const f32x4*>(v)[i];
+    const f32x4 g4 = reinterpret_cast<const f32x4*>(g)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pp = p4[e], mm = m4[e], vv = v4[e];
+      adam_elem(pp, g4[e], mm, vv, h);
+      p4[e] = pp;
+      m4[e] = mm;
+      v4[e] = vv;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = p4;
+    reinterpret_cast<f32x4*>(m)[i] = m4;
+    reinterpret_cast<f32x4*>(v)[i] = v4;
+  }
+  if (b == 0 && (int64_t)threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    adam_elem(p[i], g[i], m[i], v[i], h);
+  }
+}
 
 // The weight-gradient blocks of a launch: the block-level LDS-staged form
 // (wgrad.h) where the layer allows it, else one tile per wave.
@@ -469,11 +499,27 @@ k_linear_bwd(GemmArgs g, int S, int L, int nbx, int nwt, BwdExtra ex, int blk0, 
     }
     b -= ex.job[i].tiles;
   }
-  const int j = b * 64 * S + threadIdx.x;
-  if (j < ex.red_n) {
-    float acc = 0.f;
-    for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_ld + j];
-    ex.red_dst[j] = acc;
+  const int nred = ex.red_n > 0 ? (ex.red_n + 64 * S - 1) / (64 * S) : 0;
+  if (b < nred) {
+    const int j = b * 64 * S + threadIdx.x;
+    if (j < ex.red_n) {
+      float acc = 0.f;
+      for (int s = 0; s < ex.red_cnt; ++s) acc += ex.red_src[(size_t)s * ex.red_ld + j];
+      ex.red_dst[j] = acc;
+    }
+    LSTAMP(g, 3);
+    return;
+  }
+  b -= nred;
+  // Adam of the parameters whose gradients were final before this launch
+  const FinAdam& fa = ex.adam;
+  if (b < ex.nba_g) {
+    const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_g);
+    adam_span(b, ex.nba_g, fa.gp + fa.g_rest0, fa.gm + fa.g_rest0, fa.gv + fa.g_rest0,
+              fa.gg + fa.g_rest0, fa.g_n - fa.g_rest0, h);
+  } else if (b - ex.nba_g < ex.nba_d) {
+    const AdamHp h = adam_hp(fa.step_count, fa.step_offset, fa.b1, fa.b2, fa.eps, fa.lr_d);
+    adam_span(b - ex.nba_g, ex.nba_d, fa.dp, fa.dm, fa.dv, fa.dg, fa.d_n, h);
   }
   LSTAMP(g, 3);
 }
@@ -612,6 +658,17 @@ int launch_linear_bwd(const float* dy, const float* y, int act, const float* mas
       ex.red_cnt = extra->red_cnt;
       ex.red_ld = extra->red_ld ? extra->red_ld : extra->red_n;
       nbe += (ex.red_n + 64 * S - 1) / (64 * S);
+    }
+    if (extra->adam.on) {
+      const FinAdam& fa = extra->adam;
+      PC_REQUIRE(fa.gp && fa.gm && fa.gv && fa.gg && fa.step_count && fa.g_n >= fa.g_rest0 &&
+                     fa.g_rest0 % 4 == 0 && (fa.d_n == 0 || (fa.dp && fa.dm && fa.dv && fa.dg)),
+                 "linear_bwd: bad Adam ranges");
+      ex.adam = fa;
+      const int64_t per = (int64_t)64 * S * 4;  // floats per block and pass
+      ex.nba_g = (int)((fa.g_n - fa.g_rest0 + per - 1) / per);
+      ex.nba_d = (int)((fa.d_n + per - 1) / per);
+      nbe += ex.nba_g + ex.nba_d;
     }
   }
   if (nbx + nbw + nbe == 0) return PCADV_OK;
