@@ -1142,7 +1142,10 @@ static int launch_feat_fwd_np(const float* pts_a, const float* pts_b, int split,
   uint64_t* mlp_stamps = stamps ? stamps + (size_t)C * (C4_O / C4_CB) * 16 : nullptr;
   // one tile per workgroup when two would give fewer than two workgroups per
   // CU (512); the diagnostic stamps layout assumes two
-  const bool one = ntiles < 1024 && !stamps;
+#ifndef PCADV_MLP_ONE_BELOW
+#define PCADV_MLP_ONE_BELOW 1024  // A/B builds: the tile count below which one tile per workgroup runs
+#endif
+  const bool one = ntiles < PCADV_MLP_ONE_BELOW && !stamps;
   const dim3 grid(one ? ntiles : (ntiles + 1) / 2);
   auto kern = one ? (gf.n ? k_point_mlp<NP3, 1, true> : k_point_mlp<NP3, 1, false>)
                   : (gf.n ? k_point_mlp<NP3, 2, true> : k_point_mlp<NP3, 2, false>);
