@@ -415,9 +415,12 @@ class AdvTrainStep:
     # ------------------------------------------------------------------
     def saved_x3(self):
         """conv3 activations of the last step, (2B, N, 128) view of the workspace
-        (first region of the carve in csrc/capi.hip)."""
+        (first region of the carve in csrc/capi.hip): float32, or bfloat16 in
+        bf16 mode (the form the feature backward read)."""
         C, N = 2 * self.B, self.N
         n = C * N * 128
+        if self.precision == 1:
+            return self.workspace[:2 * n].view(torch.bfloat16).view(C, N, 128)
         return self.workspace[:4 * n].view(torch.float32).view(C, N, 128)
 
     def sync_optimizer_state(self):

@@ -465,6 +465,52 @@ def test_adv_step_large_batch_vs_oracle(B, N):
         assert_grad_close(p.grad.cpu().numpy(), gD[nm], nm)
 
 
+def test_adv_step_bf16_mode_same_activation():
+    """run_training's iteration in bf16 mode (AdvTrainStep(precision="bf16"),
+    B=32 + 32, N=1024): the 64-cloud forms of the bf16 x3 (k_conv4_max's
+    128-point steps over it, the feature backward's ReLU mask and dW4 rows from
+    it, the D Adam riding the chunk launch).  Every generator gradient strictly
+    against the oracle's backward on the step's own bf16 activations, pooled
+    features and argmax (as test_cls_step_bf16_full_size_vs_oracle), with the
+    adversarial term through the oracle's discriminator on those features."""
+    B, N = 32, 1024
+    model = _load(pc.PointNetCls(k=40), onp.make_params(onp.cls_spec(40), seed=5))
+    D = onp.make_params(onp.disc_spec(40, 1), seed=6, init="xavier")
+    model_D = _load(pc.DeepConvDiscNet(40, 1), D)
+    step = AdvTrainStep(model, model_D, B, N, seed=0, precision="bf16")
+    G = onp.make_params(onp.cls_spec(40), seed=5)
+    rng = np.random.default_rng(1500)
+    pg = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    lab = rng.integers(0, 40, B)
+    pn = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    m1 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    m2 = (rng.random((B, 256)) >= 0.3).astype(np.float32)
+    y1 = rng.uniform(0.7, 1.05, (B, 1)).astype(np.float32)
+    y2 = rng.uniform(0.0, 0.305, (B, 1)).astype(np.float32)
+    step(_t(pg), _t(lab, torch.int64), _t(pn), masks=(_t(m1), _t(m2)), soft=(_t(y1), _t(y2)),
+         apply_adam=False)
+    x3s = step.saved_x3()
+    assert x3s.dtype == torch.bfloat16
+    gmax, gidx, x3 = ops.feat_fwd(_t(np.concatenate([pg, pn])), *_feat_weights(G), precision="bf16")
+    assert torch.equal(x3, x3s)  # the step's own forward
+    gmax, gidx, x3 = gmax.cpu().numpy(), gidx.cpu().numpy().astype(np.int64), x3.float().cpu().numpy()
+    F32 = np.float32
+    _, _, c_gt = onp.cls_forward(G, pg, m1, precision="bf16")
+    _, _, c_ng = onp.cls_forward(G, pn, m2, precision="bf16")
+    lg, hg = onp.head_fwd(gmax[:B], G, m1)
+    _, dce = onp.cross_entropy(lg, lab)
+    ln, hn = onp.head_fwd(gmax[B:], G, m2)
+    lsm_ng = onp.log_softmax(ln)
+    d_ng, acts_ng = onp.disc_forward(D, lsm_ng)
+    _, dadv = onp.bce_with_logits(d_ng, np.ones_like(d_ng))
+    _, dlsm = onp.disc_backward(D, acts_ng, F32(0.001) * dadv, need_params=False)
+    dlog_ng = onp.log_softmax_bwd(lsm_ng, dlsm)
+    ga = onp.cls_backward(G, dict(c_gt, x3=x3[:B], am=gidx[:B], gmax=gmax[:B], head=hg), dce)
+    gb = onp.cls_backward(G, dict(c_ng, x3=x3[B:], am=gidx[B:], gmax=gmax[B:], head=hn), dlog_ng)
+    for nm, p in model.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), (ga[nm] + gb[nm]).astype(F32), nm, 1e-4, 1e-5)
+
+
 def test_cls_step_large_batch_vs_oracle():
     """configs[1]'s step at B=160: fc1..fc3's weight gradients over 160 rows."""
     B, N = 160, 64
