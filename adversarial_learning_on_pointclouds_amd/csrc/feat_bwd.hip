@@ -75,9 +75,6 @@ static_assert(FS_PCH == BW_PCH && FS_MAXO == BW_MAXO && FS_T == BW_T, "feat_sort
 #ifndef PCADV_FIN_ADAM_V4
 #define PCADV_FIN_ADAM_V4 4
 #endif
-#ifndef PCADV_CHUNK_ORDER
-#define PCADV_CHUNK_ORDER 0  // A/B builds: 1 = long chunks, trailing items, short chunks (measured slower)
-#endif
 #ifndef PCADV_TRAIL_ADAM_FIRST
 #define PCADV_TRAIL_ADAM_FIRST 0
 #endif
@@ -228,69 +225,19 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
                  const float* __restrict__ w3, const float* __restrict__ w4,
                  const float* __restrict__ x3, float* __restrict__ slabs, uint64_t* stamps,
                  const int* __restrict__ sortrec, int nclouds, float* __restrict__ dw4,
-                 float* __restrict__ db4, FinAdam fa, int nb_adam0, int nb_adam1,
-                 const int* __restrict__ nact_all) {
+                 float* __restrict__ db4, FinAdam fa, int nb_adam0, int nb_adam1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // Workgroups past the chunks: work that needs nothing from this launch,
+  // Workgroup rows past the clouds: work that needs nothing from this launch,
   // the dW4 / db4 gather and the Adam update of the parameters whose gradients
-  // are final before it (G from fc1 on, D; not W4, which the chunks read).
-  // Plain order: chunk (blockIdx.x, cloud blockIdx.y), the trailing items in
-  // the rows past the clouds, dispatched last.  With nact_all (the hit sort's
-  // active-row counts, <= 1024 chunks): the chunks with two or more row
-  // batches first, then the trailing items (memory-bound: the long chunks'
-  // f32 MFMA phases share their CUs with them instead of with other chunks),
-  // then the one-batch chunks; every chunk still writes its own slab, so the
-  // results do not depend on the order.
-  const int nch = (int)gridDim.x, nrec = nclouds * nch;
-  int c = (int)blockIdx.y, chunk = (int)blockIdx.x;
-  int tb = (int)blockIdx.y >= nclouds ? ((int)blockIdx.y - nclouds) * nch + (int)blockIdx.x : -1;
-  if (PRE && nact_all) {
-    int* ms = reinterpret_cast<int*>(smem);  // [16] per-wave long counts, [16] the pick
-    const int t = threadIdx.x, ln = t & 63, wv = t >> 6;
-    const int f = (int)blockIdx.y * nch + (int)blockIdx.x;
-    const int ntr = nch * (int)gridDim.y - nrec;
-    const bool v0 = t < nrec, v1 = t + BW_T < nrec;
-    const bool l0 = v0 && nact_all[t] > BW_RB, l1 = v1 && nact_all[t + BW_T] > BW_RB;
-    const uint64_t m0 = __ballot(l0), m1 = __ballot(l1);
-    if (ln == 0) {
-      ms[wv] = __popcll(m0);
-      ms[BW_T / 64 + wv] = __popcll(m1);
-    }
-    __syncthreads();
-    int base0 = 0, base1 = 0, nlong = 0;
-#pragma unroll
-    for (int k = 0; k < 2 * BW_T / 64; ++k) {
-      const int v = ms[k];
-      base0 += k < wv ? v : 0;
-      base1 += k < BW_T / 64 + wv ? v : 0;
-      nlong += v;
-    }
-    const uint64_t below = (1ull << ln) - 1ull;
-    const int r0 = base0 + __popcll(m0 & below), r1 = base1 + __popcll(m1 & below);
-    const int kind = f < nlong ? 0 : (f < nlong + ntr ? 1 : 2);
-    const int idx = kind == 0 ? f : (kind == 1 ? f - nlong : f - nlong - ntr);
-    if (kind == 0) {
-      if (l0 && r0 == idx) ms[16] = t;
-      if (l1 && r1 == idx) ms[16] = t + BW_T;
-    } else if (kind == 2) {  // one-batch chunks before record r: r - (long ones before r)
-      if (v0 && !l0 && t - r0 == idx) ms[16] = t;
-      if (v1 && !l1 && t + BW_T - r1 == idx) ms[16] = t + BW_T;
-    }
-    __syncthreads();
-    // uniform: kept in scalar registers (the chunk's code needs every VGPR)
-    const int pick = __builtin_amdgcn_readfirstlane(ms[16]);
-    __syncthreads();  // the LDS is the chunk's or the trailing item's from here
-    const int kd = __builtin_amdgcn_readfirstlane(kind), ix = __builtin_amdgcn_readfirstlane(idx);
-    tb = kd == 1 ? ix : -1;
-    c = kd == 1 ? 0 : pick / nch;
-    chunk = kd == 1 ? 0 : pick % nch;
-  }
-  if (tb >= 0) {
+  // are final before it (G from fc1 on, D; not W4, which the chunks read).  They are
+  // dispatched last, so they take the CU slots of the chunks that finish first
+  // while the two-batch chunks run on.
+  if ((int)blockIdx.y >= nclouds) {
 #ifdef PCADV_STAMPS
     const size_t wg_ = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     if (!stamps && threadIdx.x == 0 && wg_ < 1024) g_chunk_stamps[wg_][0] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int b = tb;
+    const int b = ((int)blockIdx.y - nclouds) * (int)gridDim.x + (int)blockIdx.x;
     constexpr int NDW4 = BW_MAXO / (BW_T / 64 / DW4_WPC);
     const int nad = nb_adam0 + nb_adam1;
     const bool is_dw4 = PCADV_TRAIL_ADAM_FIRST ? (b >= nad && b - nad < NDW4) : b < NDW4;
@@ -326,7 +273,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 #endif
   BSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int p0 = chunk * BW_PCH;
+  const int c = blockIdx.y, chunk = blockIdx.x, p0 = chunk * BW_PCH;
   const float* pts = c < split ? pts_a + (size_t)c * N * 3 : pts_b + (size_t)(c - split) * N * 3;
 
   // wave -> (row tile rt, column tile ct) of the 32 x 64 dX2 / dX1 outputs;
@@ -353,7 +300,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
   if constexpr (PRE) {
     // ---- 1-3 done ahead (feat_sort.h): one round of loads, the fixed-size
     //      record and this cloud's pooled gradients, then g of each sorted hit
-    const int* rec = sortrec + ((size_t)c * nch + chunk) * FS_REC;
+    const int* rec = sortrec + ((size_t)c * gridDim.x + chunk) * FS_REC;
     int so_v[2];
     float dg_v[2];
 #pragma unroll
@@ -764,7 +711,7 @@ k_feat_bwd_chunk(const float* __restrict__ dg, const int32_t* __restrict__ gidx,
 
   // ---- 4. write this workgroup's slab ----------------------------------------
   const int r32 = lane & 31;
-  float* slab = slabs + ((size_t)c * nch + chunk) * SLAB;
+  float* slab = slabs + ((size_t)c * gridDim.x + chunk) * SLAB;
   {
     const int ot = wave >> 1, it = wave & 1;
 #pragma unroll
@@ -946,14 +893,9 @@ int launch_feat_bwd(const float* dg, const int32_t* gidx, const float* pts_a, co
   const int arows = (NDW4 + nba0 + nba1 + nchunk - 1) / nchunk;
   auto kern = sortrec ? (x3_bf16 ? k_feat_bwd_chunk<true, true> : k_feat_bwd_chunk<true, false>)
                       : (x3_bf16 ? k_feat_bwd_chunk<false, true> : k_feat_bwd_chunk<false, false>);
-  // the sort's per-chunk nact follows its records (feat_sort.h); the ordered
-  // dispatch scans them two per thread
-  const int* nact_all = sortrec && PCADV_CHUNK_ORDER && C * nchunk <= 2 * BW_T && !stamps
-                            ? sortrec + (size_t)C * nchunk * FS_REC
-                            : nullptr;
   hipLaunchKernelGGL(kern, dim3(nchunk, C + arows), dim3(BW_T), sizeof(BwdLds), s, dg, gidx, O,
                      pts_a, pts_b, split, N, w1, b1, w2, b2, w3, w4, x3, slabs, stamps, sortrec, C,
-                     dw4, db4, fa, nba0, nba1, nact_all);
+                     dw4, db4, fa, nba0, nba1);
   PC_HIP_CHECK_LAUNCH("k_feat_bwd_chunk");
   // conv4's Adam spread over the CUs the slab reduction leaves free (one
   // float4 per thread), so no workgroup moves more than a reduction block does

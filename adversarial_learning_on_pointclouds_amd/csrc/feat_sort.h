@@ -7,9 +7,7 @@
 // Per (cloud c, 128-point chunk): the channels o whose argmax gidx[c][o] falls
 // in the chunk ("hits"), grouped by row (point) in increasing row order and by
 // o inside a row; the active rows (rows with hits) in increasing order, and
-// the first hit of each.  After the C x nch records, one int per record: its
-// nact again (feat_sort_nact), so the chunk launch can order its chunks by
-// length with one coalesced load.  Record layout (ints, FS_REC per chunk):
+// the first hit of each.  Record layout (ints, FS_REC per chunk):
 //   [0] nact, [1] nhits, [FSR_ROWS + s] row of active slot s (s < nact),
 //   [FSR_HOFF + s] first hit of slot s (s <= nact; [nact] = nhits),
 //   [FSR_SO + j] o of hit j (j < nhits).
@@ -36,8 +34,7 @@ struct SortLds {
 // reaches the same barriers; valid = false: barriers only).  gidx_c: the
 // cloud's argmax row [O]; p0: the chunk's first point.
 __device__ __forceinline__ void chunk_sort(const int32_t* __restrict__ gidx_c, int O, int p0, int t,
-                                           bool valid, SortLds& L, int* __restrict__ rec,
-                                           int* __restrict__ nact_out) {
+                                           bool valid, SortLds& L, int* __restrict__ rec) {
   const int lane = t & 63, wave = t >> 6;
   int ga[2];  // the argmax rows, loaded before the counters are cleared
 #pragma unroll
@@ -90,7 +87,6 @@ __device__ __forceinline__ void chunk_sort(const int32_t* __restrict__ gidx_c, i
       const int nact = L.wact[0] + L.wact[1], nhits = L.wsum[0] + L.wsum[1];
       rec[0] = nact;
       rec[1] = nhits;
-      *nact_out = nact;
       rec[FSR_HOFF + nact] = nhits;
     }
   }

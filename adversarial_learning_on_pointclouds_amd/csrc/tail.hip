@@ -338,7 +338,7 @@ k_disc_tail(const float* __restrict__ d3, int B, const float* __restrict__ w4,
     SortLds& S = reinterpret_cast<SortLds*>(smem)[half];
     const bool valid = cc < C;
     chunk_sort(gidx + (size_t)(valid ? cc : 0) * FS_MAXO, FS_MAXO, ch * FS_PCH, tid % FS_T, valid,
-               S, sortrec + (size_t)id * FS_REC, sortrec + (size_t)C * nch * FS_REC + id);
+               S, sortrec + (size_t)id * FS_REC);
     return;
   }
   TSTAMP(1, 0);
@@ -753,7 +753,7 @@ k_cls_head(const float* __restrict__ h2, const float* __restrict__ drop_mask, fl
     SortLds& S = reinterpret_cast<SortLds*>(smem)[half];
     const bool valid = cc < C;
     chunk_sort(gidx + (size_t)(valid ? cc : 0) * FS_MAXO, FS_MAXO, ch * FS_PCH, tid % FS_T, valid,
-               S, sortrec + (size_t)id * FS_REC, sortrec + (size_t)C * nch * FS_REC + id);
+               S, sortrec + (size_t)id * FS_REC);
     return;
   }
   ClsHeadLds& L = *reinterpret_cast<ClsHeadLds*>(smem);
@@ -867,7 +867,7 @@ int launch_cls_head(const float* h2, const float* drop_mask, float drop_p, const
   return PCADV_OK;
 }
 
-size_t feat_sort_record_ints(int C, int N) { return (size_t)C * ((N + FS_PCH - 1) / FS_PCH) * (FS_REC + 1); }
+size_t feat_sort_record_ints(int C, int N) { return (size_t)C * ((N + FS_PCH - 1) / FS_PCH) * FS_REC; }
 
 // sortrec (optional): also run the feature backward's hit sort over the C
 // clouds' argmax gidx [C][1024] into sortrec (feat_sort_record_ints(C, N))
